@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""Benchmark: clouds/s of NDT preprocessing + NDTNetSegmentation forward.
+
+Metric (BASELINE.json): "clouds/sec NDT preprocess+PointNet fwd, 100k pts ->
+1000 NDs, batch=16".  One step = one batch of 16 synthetic 100k-point clouds
+(SURVEY §8d generator U, float32, resident in HBM before timing) through
+``ndt_preprocessing`` (voxel-size bisection, per-voxel ND, KL prune) and the
+eval-mode ``NDTNetSegmentation(point_dim=3, num_classes=28, feature_dim=768)``
+forward -- the path tools/train.py:67-69 runs each iteration.
+
+Multi-GPU (torchrun, one process per GPU): every rank processes its own batch
+of 16 clouds (weak scaling, no collective on the data path -- SURVEY §8e);
+value = all clouds / max-over-ranks time.
+
+The JSON line carries
+  roofline     -- the dominant kernel stage, achieved vs MI355X peak
+  cpu_baseline -- the CPU oracle (sequential C port of the reference core) +
+                  torch fp32 CPU forward, timed on a bounded sample (rank 0, N=1)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "ndt-net_amd"))
+
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+FP32_MFMA_PEAK_TF = 157.3   # MI355X_MICROARCH.md: FP32 matrix 157.3 TF (dense)
+
+
+def pointnet_flops_per_cloud(n: int, F: int, C: int) -> float:
+    """2 x the Conv1d/Linear MACs NDTNetSegmentation executes per cloud."""
+    pt = (3 * 64 + 64 * 128 + 128 * 1024) + 12 * 64 + (64 * 64 + 64 * 128 + 128 * 1024) \
+        + 64 * 128 + 128 * F + (64 + F) * 512 + 512 * 256 + 256 * 128 + 128 * (C + 1)
+    fc = (1024 * 512 + 512 * 256 + 256 * 9) + (1024 * 512 + 512 * 256 + 256 * 4096)
+    return 2.0 * (pt * n + fc)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--points", type=int, default=100_000)
+    ap.add_argument("--nds", type=int, default=1000)
+    ap.add_argument("--kind", default="U", choices=["U", "L"])
+    ap.add_argument("--feature-dim", type=int, default=768)
+    ap.add_argument("--classes", type=int, default=28)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=8.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from ndnet.models.ndtnet import NDTNetSegmentation
+    from ndnet.models import pointnet_hip
+    from ndnet.preprocessing.ndtnet_preprocessing import ndt_preprocessing, get_plan
+    from ndnet.synthetic import make_batch
+    from ndnet import _lib
+
+    B, n, k, F, C = args.batch, args.points, args.nds, args.feature_dim, args.classes
+    pts = torch.from_numpy(make_batch(args.kind, B, n, seed0=rank * B)).to(dev)
+    torch.manual_seed(1234)
+    model = NDTNetSegmentation(3, C, F).to(dev).eval()
+    with torch.no_grad():
+        for m in model.modules():  # non-trivial BN statistics
+            if isinstance(m, torch.nn.BatchNorm1d):
+                m.running_mean.uniform_(-0.2, 0.2)
+                m.running_var.uniform_(0.5, 1.5)
+
+    def step():
+        p, c, _ = ndt_preprocessing(k, pts)
+        return model(p, c)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            out = step()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = step()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    total_clouds = world * B * args.steps
+    value = total_clouds / elapsed
+    stats = get_plan(B, n, k, -1, dev).host_stats()
+    assert all(s.rc == 0 for s in stats), [s.rc for s in stats]
+    assert torch.isfinite(out).all()
+
+    # ---- stage timing (HIP events on the stream the kernels run on) ----
+    plan = get_plan(B, n, k, -1, dev)
+    _lib.lib().ndnet_ndt_set_timing(plan.handle, 1)
+    stage_names = ["reset+limits", "bisection (15 launches)", "dense ids", "chunk sort", "welford", "kl+prune"]
+    stage_ms = np.zeros(6)
+    fwd_ms = 0.0
+    reps = max(3, min(args.steps, 10))
+    with torch.no_grad():
+        for _ in range(reps):
+            p, c, _ = ndt_preprocessing(k, pts)
+            ms = np.zeros(6, np.float32)
+            _lib.lib().ndnet_ndt_stage_ms(plan.handle, ms.ctypes.data)
+            stage_ms += ms
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            model(p, c)
+            e1.record()
+            e1.synchronize()
+            fwd_ms += e0.elapsed_time(e1)
+    _lib.lib().ndnet_ndt_set_timing(plan.handle, 0)
+    stage_ms /= reps
+    fwd_ms /= reps
+    ndt_ms = float(stage_ms.sum())
+    hip_fwd = pointnet_hip.available()
+    # dominant stage -> roofline entry
+    flops = pointnet_flops_per_cloud(k, F, C) * B
+    ndt_bytes = (24.0 * n + 48.0 * k) * B  # fp64 xyz read once + fp32 12-D write
+    if fwd_ms >= stage_ms.max():
+        achieved = flops / (fwd_ms * 1e-3) / 1e12
+        roofline = {"kernel": "NDTNetSegmentation forward" + (" (HIP MFMA)" if hip_fwd else " (torch)"),
+                    "bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                    "frac": round(achieved / FP32_MFMA_PEAK_TF, 4), "traffic": None,
+                    "algorithmic": f"{flops / 1e9:.2f} GFLOP per batch of {B}", "ms": round(fwd_ms, 4)}
+    else:
+        i = int(stage_ms.argmax())
+        achieved = ndt_bytes / (stage_ms[i] * 1e-3) / 1e9
+        roofline = {"kernel": f"ndt {stage_names[i]}", "bound": "hbm", "achieved": round(achieved, 2),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                    "traffic": None, "algorithmic": f"{ndt_bytes / 1e6:.2f} MB per batch of {B} (24N+48k per cloud)",
+                    "ms": round(float(stage_ms[i]), 4)}
+
+    # ---- CPU baseline: sequential oracle port + torch CPU forward, bounded sample ----
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle as O
+        host = pts.cpu().numpy()
+        t_ndt, done = 0.0, 0
+        budget = args.cpu_baseline_seconds * 0.6
+        while done < B and t_ndt < budget:
+            t1 = time.perf_counter()
+            O.run(host[done].astype(np.float64), k)
+            t_ndt += time.perf_counter() - t1
+            done += 1
+        cpu_model = NDTNetSegmentation(3, C, F).eval()
+        cpu_model.load_state_dict({kk: v.cpu() for kk, v in model.state_dict().items()})
+        pc = torch.randn(1, k, 3)
+        cc = torch.randn(1, k, 9)
+        t_fwd, fdone = 0.0, 0
+        with torch.no_grad():
+            while fdone < 4 and t_fwd < args.cpu_baseline_seconds * 0.4:
+                t1 = time.perf_counter()
+                cpu_model.forward_torch(pc, cc)
+                t_fwd += time.perf_counter() - t1
+                fdone += 1
+        per_cloud = t_ndt / done + t_fwd / fdone
+        cpu = {"value": round(1.0 / per_cloud, 3), "unit": "clouds/s", "cores": torch.get_num_threads(),
+               "kind": "port",
+               "sample": f"{done} clouds through oracle/ndt_oracle.c (1 thread, {t_ndt / done * 1e3:.1f} ms/cloud) "
+                         f"+ {fdone} single-cloud torch fp32 CPU forwards ({torch.get_num_threads()} threads, "
+                         f"{t_fwd / fdone * 1e3:.1f} ms/cloud)"}
+
+    if rank == 0:
+        line = {
+            "metric": "clouds/sec NDT preprocess+PointNet fwd, 100k pts->1000 NDs, batch=16",
+            "value": round(value, 2),
+            "unit": "clouds/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64 (NDT core) + fp32 (PointNet)",
+            "data": f"synthetic {args.kind} clouds (SURVEY 8d), random-init weights",
+            "config": {"workload": f"batch {B} x {n} pts -> {k} NDs, NDTNetSegmentation F={F} C={C} eval",
+                       "global_batch": B * world, "points": n, "nds": k, "parallelism": f"dp{world} (clouds sharded)"},
+            "stages_ms": {nm: round(float(v), 4) for nm, v in zip(stage_names, stage_ms)} | {"pointnet_fwd": round(fwd_ms, 4)},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,156 @@
+/*
+ * ndnet_amd.h -- C ABI of libndnet_amd.so, the MI355X (gfx950) NDT path.
+ *
+ * Two groups of entry points:
+ *
+ * 1. The reference's own ABI (core_legacy/include/ndnet_core/ndt.h:59-116 and
+ *    kullback_leibler.h:74), same names, argument order, meaning and return
+ *    codes, host pointers in and out.  The reference's ctypes wrapper
+ *    (ndnet/preprocessing/ndt_legacy.py:28-43) binds these unchanged once its
+ *    library path points at libndnet_amd.so.  The ND and KL
+ *    handles are opaque, as they already are to the reference's Python side
+ *    (ndt_legacy.py:5-25 declares `__fields__`, so ctypes never sees a field).
+ *
+ * 2. A batched device API for B clouds resident in HBM (no PCIe in the hot
+ *    path): plan once, run many times on a HIP stream.  The run functions do
+ *    no allocation and no synchronisation, so they can be captured in a graph.
+ *
+ * Return codes: the reference's (0 success; -1 voxel table allocation /
+ * capacity; -3 "Reached maximum number of iterations!"; prune: -1 "desired >
+ * valid", -2 "Reached the end of the divergences array!") plus
+ * NDNET_ERR_* for API misuse and HIP failures.  Nothing aborts.
+ */
+#ifndef NDNET_AMD_H_
+#define NDNET_AMD_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NDNET_OK 0
+#define NDNET_ERR_ARG (-20)  /* bad argument (NULL, zero size, unsupported point_dim) */
+#define NDNET_ERR_HIP (-21)  /* HIP runtime failure; message on stderr */
+#define NDNET_PRUNE_POISON (-8) /* a prune walk reached a list entry the reference never wrote */
+
+/* Per-cloud outcome of a batched run; written on the device. */
+typedef struct ndnet_ndt_stats {
+  int32_t rc;          /* ndt_downsample return code for this cloud */
+  int32_t prune_rc;    /* prune_nds return code of the last prune level */
+  uint32_t iters;      /* estimate passes of the voxel-size bisection */
+  uint32_t len[3];     /* voxel grid of the accepted (or last tried) size */
+  double offset[3];
+  double voxel_size;
+  uint64_t num_nds;    /* occupied voxels at the accepted size */
+  uint64_t num_valid;  /* NDs left after the prune */
+  uint64_t num_kl;     /* live divergence-list length after the prune */
+  uint64_t num_events; /* divergence entries created */
+  uint64_t num_out;    /* surviving NDs (rows written = min(num_out, k)) */
+} ndnet_ndt_stats;
+
+/* ---------------------------------------------------------------------------
+ * 1. Reference ABI (host pointers).
+ * ------------------------------------------------------------------------ */
+
+/* Replaces ndt_downsample (ndt.h:100-110, ndt.c:119-222).  point_dim must be 3
+ * (the reference's workers hard-code a stride of 3, normal_distributions.c:47).
+ * out_pc/out_cov/out_classes hold num_desired_points rows; out_classes may be
+ * NULL; classes may be NULL (unlabelled).  *nd_array and *kl_divergences
+ * receive opaque handles for prune_nds / to_point_cloud / free_*. */
+int ndt_downsample(double *point_cloud, unsigned short point_dim, unsigned long num_points,
+                   unsigned int *len_x, unsigned int *len_y, unsigned int *len_z,
+                   double *offset_x, double *offset_y, double *offset_z,
+                   double *voxel_size,
+                   unsigned short *classes, unsigned short num_classes,
+                   unsigned long num_desired_points,
+                   double *downsampled_point_cloud, unsigned long *num_downsampled_points,
+                   double *covariances,
+                   unsigned short *downsampled_classes,
+                   void **nd_array, unsigned long *num_valid_nds,
+                   void **kl_divergences, unsigned long *num_kl_divergences);
+
+/* Replaces prune_nds (ndt.h:59-62, ndt.c:28-73): prunes the retained list of a
+ * handle to num_desired_nds, with the reference's walk, bound check and
+ * left shift. */
+int prune_nds(void *nd_array,
+              unsigned int len_x, unsigned int len_y, unsigned int len_z,
+              unsigned long num_desired_nds, unsigned long *num_valid_nds,
+              void *kl_divergences, unsigned long *num_kl_divergences);
+
+/* Replaces to_point_cloud (ndt.h:76-82, ndt.c:75-117): surviving NDs in
+ * ascending voxel order.  Writes at most the row count of the last
+ * downsample/prune (the reference has no capacity argument and overruns its
+ * buffers when a prune fails); *num_points receives the survivor count. */
+int to_point_cloud(void *nd_array,
+                   unsigned int len_x, unsigned int len_y, unsigned int len_z,
+                   double offset_x, double offset_y, double offset_z,
+                   double voxel_size,
+                   double *point_cloud, unsigned long *num_points,
+                   double *covariances,
+                   unsigned short *classes);
+
+/* Replaces free_nds (ndt.h:116) and free_kl_divergences (kullback_leibler.h:74).
+ * NULL is accepted (the reference dereferences it after a failed search). */
+void free_nds(void *nd_array, unsigned long num_nds);
+void free_kl_divergences(void *kl_divergences);
+
+/* ---------------------------------------------------------------------------
+ * 2. Batched device API (the ndt_preprocessing hot path,
+ *    ndnet/preprocessing/ndtnet_preprocessing.py:6-73).
+ * ------------------------------------------------------------------------ */
+
+/* Allocates the device workspace for `batch` clouds of `num_points` points
+ * downsampled to `num_desired` NDs.  num_classes >= 0 enables labelled runs
+ * (class histograms of num_classes + 1 bins); -1 disables them.
+ * voxel_capacity bounds the voxels of any grid the bisection visits (0: 2^22);
+ * a grid beyond it fails that cloud with rc -1, as the reference's malloc
+ * would. */
+int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, int num_classes,
+                          uint64_t voxel_capacity, void **plan);
+void ndnet_ndt_plan_destroy(void *plan);
+
+/* d_points: [batch][num_points][3] float32 on the device (the tensor
+ * ndt_preprocessing receives).  d_labels: [batch][num_points] int32 class ids
+ * or NULL.  d_out: [batch][num_desired][12] float32 = mean(3) | covariance(9)
+ * row-major, nan_to_num applied (ndtnet_preprocessing.py:66-67), zero rows
+ * past the survivors.  d_out_classes: [batch][num_desired][num_classes+1]
+ * one-hot or NULL.  d_stats: [batch] device array or NULL.  stream: a
+ * hipStream_t (NULL = default stream). */
+int ndnet_ndt_run(void *plan, void *stream, const float *d_points, const int32_t *d_labels, float *d_out,
+                  float *d_out_classes, ndnet_ndt_stats *d_stats);
+
+/* Same on float64 points, with float64 outputs as the reference's
+ * ndt_downsample writes them: d_out_points [batch][k][3], d_out_covariances
+ * [batch][k][9], d_out_classes [batch][k] (any may be NULL), and optionally
+ * the float32 [batch][k][12] block. */
+int ndnet_ndt_run_f64(void *plan, void *stream, const double *d_points, const int32_t *d_labels,
+                      double *d_out_points, double *d_out_covariances, uint16_t *d_out_classes, float *d_out,
+                      ndnet_ndt_stats *d_stats);
+
+/* A further prune level of every cloud of the last run (NDT_Sampler.prune,
+ * ndt_legacy.py:173-240): outputs sized [batch][num_desired][...]. */
+int ndnet_ndt_prune(void *plan, void *stream, uint64_t num_desired, float *d_out, float *d_out_classes,
+                    double *d_out_points, double *d_out_covariances, uint16_t *d_out_classes16,
+                    ndnet_ndt_stats *d_stats);
+
+/* Stage timing with HIP events on the run's stream (bench.py): after
+ * ndnet_ndt_set_timing(plan, 1), each run records events around its stages;
+ * ndnet_ndt_stage_ms fills ms[6] = reset+limits, 15 bisection passes, dense
+ * ids, chunk sort, Welford, KL+prune of the last run (synchronises). */
+int ndnet_ndt_set_timing(void *plan, int enable);
+int ndnet_ndt_stage_ms(void *plan, float *ms);
+
+/* Host copies of one cloud's intermediates after a run (parity tests). */
+int ndnet_ndt_debug_dump(void *plan, int cloud, uint32_t *nd_n, double *nd_mean, double *nd_cov_pre,
+                         double *nd_cov_post, uint32_t *vox, double *ord_val, uint32_t *ord_p, uint32_t *ord_q,
+                         double *guesses, uint32_t *counts, uint32_t *iters, uint8_t *alive);
+
+/* Library identification (no GPU needed). */
+const char *ndnet_amd_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NDNET_AMD_H_ */

@@ -1,0 +1,221 @@
+// Device-side arithmetic of the NDT path (gfx950).  Every function here performs
+// the same IEEE double operations, in the same order, as the reference C core
+// on x86-64 without FMA; the translation unit is compiled with
+// -ffp-contract=off so no multiply-add is fused.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define NDNET_FN __device__ static inline
+#define NDNET_TABQ __constant__
+#include "ndt_log.h"
+
+namespace ndnet {
+
+constexpr uint32_t kInvalid = 0xffffffffu;
+constexpr int kWorkers = 8;          // NUM_PCL_WORKERS, normal_distributions.h:39
+constexpr int kMaxIters = 15;        // MAX_GUESS_ITERATIONS, ndt.h:43
+constexpr double kMinGuess = 0.01;   // ndt.h:41
+constexpr double kMaxGuess = 30.0;   // ndt.h:42
+constexpr double kUpper = 0.2;       // DOWNSAMPLE_UPPER_THRESHOLD, ndt.h:38
+constexpr double kDblMin = 2.2250738585072014e-308;
+constexpr double kDblMax = 1.7976931348623157e308;
+
+// Order-preserving map of a double onto u64 (NaN excluded by the callers).
+NDNET_FN uint64_t ord_key(double x) {
+  uint64_t u = ndnet_dbits(x);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+NDNET_FN double ord_unkey(uint64_t k) {
+  return ndnet_bitsd((k >> 63) ? (k & 0x7fffffffffffffffull) : ~k);
+}
+
+// (unsigned int) floor(x) as x86-64 gcc lowers it (cvttsd2si to 64 bits, low
+// half kept): NaN and |x| >= 2^63 give 0.  voxel.c:89-91.
+NDNET_FN uint32_t floor_to_u32(double f) {
+  if (!(f > -9.2233720368547758e18 && f < 9.2233720368547758e18)) return 0u;
+  return (uint32_t)(uint64_t)(int64_t)f;
+}
+
+// One axis of metric_to_voxel_space (voxel.c:89-91): floor((p - off) / vs).
+// The quotient is first estimated with a multiply by 1/vs; only when that
+// estimate lies within a few ulps of an integer is the correctly rounded
+// division performed, so the floor always equals the reference's.
+NDNET_FN uint32_t axis_index(double p, double off, double vs, double inv_vs) {
+  const double d = p - off;
+  const double qa = d * inv_vs;
+  const double f = floor(qa);
+  const double r = qa - f;
+  const double tol = fabs(qa) * 0x1p-46 + 0x1p-60;
+  if (r > tol && r < 1.0 - tol) return floor_to_u32(f);
+  return floor_to_u32(floor(d / vs));
+}
+
+// voxel.c:83-103 + 177-189.  Returns kInvalid when the point is out of grid.
+NDNET_FN uint32_t voxel_key(double x, double y, double z, const double* off, const uint32_t* len, double vs,
+                            double inv_vs) {
+  const uint32_t vx = axis_index(x, off[0], vs, inv_vs);
+  const uint32_t vy = axis_index(y, off[1], vs, inv_vs);
+  const uint32_t vz = axis_index(z, off[2], vs, inv_vs);
+  if (vx >= len[0] || vy >= len[1] || vz >= len[2]) return kInvalid;
+  return vz * len[0] * len[1] + vy * len[0] + vx;
+}
+
+// Welford state of one voxel (normal_distributions.h:41-51, class handled apart).
+struct Welford {
+  double mean[3];
+  double m2[3];
+  double cov[9];
+  uint64_t n;
+};
+
+NDNET_FN void welford_init(Welford& w) {
+  for (int j = 0; j < 3; j++) { w.mean[j] = 0.0; w.m2[j] = 0.0; }
+  for (int j = 0; j < 9; j++) w.cov[j] = 0.0;
+  w.n = 0;
+}
+
+// normal_distributions.c:75-104, one sample.
+NDNET_FN void welford_update(Welford& w, const double* x) {
+  w.n++;
+  const double n = (double)w.n;
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    const double old = w.mean[j];
+    w.mean[j] = w.mean[j] + (x[j] - w.mean[j]) / n;
+    w.m2[j] = w.m2[j] + (x[j] - old) * (x[j] - w.mean[j]);
+    double v = w.m2[j] / n;
+    w.cov[j * 3 + j] = (v != v) ? 0.0 : v;
+#pragma unroll
+    for (int k = j + 1; k < 3; k++) {
+      double c = w.cov[j * 3 + k] + (x[j] - w.mean[j]) * (x[k] - w.mean[k]) / n;
+      c = (c != c) ? 0.0 : c;
+      w.cov[j * 3 + k] = c;
+      w.cov[k * 3 + j] = c;
+    }
+  }
+}
+
+// gsl_linalg_LU_decomp for a 3x3 (GSL 2.7: LU_decomp_L2 via LU_decomp_L3):
+// per column, first max |a| as pivot (cblas idamax), full row swap, scale the
+// sub-column by 1/a_jj (divide when |a_jj| < DBL_MIN), rank-1 update
+// a_ic += a_jc * (-a_ij).  perm/signum from the pivot sequence.
+NDNET_FN void lu3(double* A, uint32_t& perm_packed, int& signum) {
+  int ipiv[3];
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    double mx = 0.0;
+    int r = 0;
+#pragma unroll
+    for (int i = j; i < 3; i++) {
+      const double a = fabs(A[i * 3 + j]);
+      if (a > mx) { mx = a; r = i - j; }
+    }
+    const int jp = j + r;
+    ipiv[j] = jp;
+    if (jp != j) {
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        const double t = A[j * 3 + c];
+        A[j * 3 + c] = A[jp * 3 + c];
+        A[jp * 3 + c] = t;
+      }
+    }
+    if (j < 2) {
+      const double ajj = A[j * 3 + j];
+      if (fabs(ajj) >= kDblMin) {
+        const double s = 1.0 / ajj;
+#pragma unroll
+        for (int i = j + 1; i < 3; i++) A[i * 3 + j] = s * A[i * 3 + j];
+      } else {
+#pragma unroll
+        for (int i = j + 1; i < 3; i++) A[i * 3 + j] = A[i * 3 + j] / ajj;
+      }
+#pragma unroll
+      for (int i = j + 1; i < 3; i++) {
+        const double t = -1.0 * A[i * 3 + j];
+#pragma unroll
+        for (int c = j + 1; c < 3; c++) A[i * 3 + c] = A[i * 3 + c] + A[j * 3 + c] * t;
+      }
+    }
+  }
+  int p[3] = {0, 1, 2};
+  int s = 1;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const int pi = ipiv[i];
+    if (p[i] != p[pi]) {
+      const int t = p[i];
+      p[i] = p[pi];
+      p[pi] = t;
+      s = -s;
+    }
+  }
+  perm_packed = (uint32_t)p[0] | ((uint32_t)p[1] << 2) | ((uint32_t)p[2] << 4);
+  signum = s;
+}
+
+NDNET_FN double lu3_det(const double* LU, int signum) {
+  double d = (double)signum;
+  d = d * LU[0];
+  d = d * LU[4];
+  d = d * LU[8];
+  return d;
+}
+
+NDNET_FN int lu3_sgndet(const double* LU, int signum) {
+  int s = signum;
+  for (int i = 0; i < 3; i++) {
+    const double u = LU[i * 4];
+    if (u < 0) s = -s;
+    else if (u == 0) return 0;
+  }
+  return s;
+}
+
+// Inverse from LU, column by column (P e_j, unit-lower forward, upper back
+// substitution in gslcblas dtrsv order).
+NDNET_FN void lu3_invert(const double* LU, uint32_t perm_packed, double* inv) {
+  int perm[3] = {(int)(perm_packed & 3), (int)((perm_packed >> 2) & 3), (int)((perm_packed >> 4) & 3)};
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    double x0 = (perm[0] == j) ? 1.0 : 0.0;
+    double x1 = (perm[1] == j) ? 1.0 : 0.0;
+    double x2 = (perm[2] == j) ? 1.0 : 0.0;
+    x1 = x1 - LU[3] * x0;
+    x2 = x2 - LU[6] * x0;
+    x2 = x2 - LU[7] * x1;
+    x2 = x2 / LU[8];
+    x1 = x1 - LU[5] * x2;
+    x1 = x1 / LU[4];
+    double t = x0 - LU[1] * x1;
+    t = t - LU[2] * x2;
+    x0 = t / LU[0];
+    inv[0 * 3 + j] = x0;
+    inv[1 * 3 + j] = x1;
+    inv[2 * 3 + j] = x2;
+  }
+}
+
+// kullback_leibler.c:98-115 given both operands already decomposed:
+// 0.5 * (0 + tr(inv_q * LU_p) - log(det_q / det_p) - 3), the trace summed as
+// gslcblas dgemm does (C zeroed, skip zero A entries, k ascending).
+NDNET_FN double kl_score(const double* LUp, const double* LUq, uint32_t perm_q, double det_p, double det_q) {
+  double inv[9];
+  lu3_invert(LUq, perm_q, inv);
+  double tr = 0.0;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    double c = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const double t = 1.0 * inv[i * 3 + k];
+      if (t != 0.0) c = c + t * LUp[k * 3 + i];
+    }
+    tr = tr + c;
+  }
+  const double first = 0.0;
+  return 0.5 * (((first + tr) - ndnet_log(det_q / det_p)) - 3.0);
+}
+
+}  // namespace ndnet

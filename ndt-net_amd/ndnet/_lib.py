@@ -1,0 +1,110 @@
+"""Loader of lib/libndnet_amd.so (the HIP path) with its C-ABI signatures.
+
+The library is built in-tree (``make -C ndt-net_amd`` or
+``__graft_entry__.build()``).  There is no fallback: when the library is
+missing or no GPU is visible the product entry points raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  -- load torch's HIP runtime first so the library binds to it
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+LIB_PATH = os.path.join(ROOT, "lib", "libndnet_amd.so")
+
+NDNET_OK = 0
+NDNET_ERR_ARG = -20
+NDNET_ERR_HIP = -21
+
+
+class NdtStats(ctypes.Structure):
+    """ndnet_ndt_stats (include/ndnet_amd.h)."""
+    _fields_ = [
+        ("rc", ctypes.c_int32),
+        ("prune_rc", ctypes.c_int32),
+        ("iters", ctypes.c_uint32),
+        ("len", ctypes.c_uint32 * 3),
+        ("offset", ctypes.c_double * 3),
+        ("voxel_size", ctypes.c_double),
+        ("num_nds", ctypes.c_uint64),
+        ("num_valid", ctypes.c_uint64),
+        ("num_kl", ctypes.c_uint64),
+        ("num_events", ctypes.c_uint64),
+        ("num_out", ctypes.c_uint64),
+    ]
+
+
+STATS_BYTES = ctypes.sizeof(NdtStats)
+assert STATS_BYTES == 96
+
+_lib = None
+
+_P = ctypes.c_void_p
+_U64 = ctypes.c_uint64
+_I = ctypes.c_int
+_UL = ctypes.c_ulong
+_PUL = ctypes.POINTER(ctypes.c_ulong)
+_PU = ctypes.POINTER(ctypes.c_uint)
+_PD = ctypes.POINTER(ctypes.c_double)
+_PUS = ctypes.POINTER(ctypes.c_ushort)
+
+EXPORTS = {
+    # reference ABI (core_legacy/include/ndnet_core/ndt.h, kullback_leibler.h)
+    "ndt_downsample": (_I, [_PD, ctypes.c_ushort, _UL, _PU, _PU, _PU, _PD, _PD, _PD, _PD, _PUS, ctypes.c_ushort,
+                            _UL, _PD, _PUL, _PD, _PUS, ctypes.POINTER(_P), _PUL, ctypes.POINTER(_P), _PUL]),
+    "prune_nds": (_I, [_P, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint, _UL, _PUL, _P, _PUL]),
+    "to_point_cloud": (_I, [_P, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint, ctypes.c_double, ctypes.c_double,
+                            ctypes.c_double, ctypes.c_double, _PD, _PUL, _PD, _PUS]),
+    "free_nds": (None, [_P, _UL]),
+    "free_kl_divergences": (None, [_P]),
+    # batched device API
+    "ndnet_ndt_plan_create": (_I, [_I, _U64, _U64, _I, _U64, ctypes.POINTER(_P)]),
+    "ndnet_ndt_plan_destroy": (None, [_P]),
+    "ndnet_ndt_run": (_I, [_P, _P, _P, _P, _P, _P, _P]),
+    "ndnet_ndt_run_f64": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "ndnet_ndt_prune": (_I, [_P, _P, _U64, _P, _P, _P, _P, _P, _P]),
+    "ndnet_ndt_debug_dump": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "ndnet_ndt_set_timing": (_I, [_P, _I]),
+    "ndnet_ndt_stage_ms": (_I, [_P, _P]),
+    "ndnet_amd_version": (ctypes.c_char_p, []),
+}
+
+
+def lib() -> ctypes.CDLL:
+    """The loaded library; raises if it was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C {ROOT}` "
+                               "(there is no CPU fallback)")
+        _lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in EXPORTS.items():
+            fn = getattr(_lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        for name, (res, args) in POINTNET_EXPORTS.items():
+            if hasattr(_lib, name):
+                fn = getattr(_lib, name)
+                fn.restype = res
+                fn.argtypes = args
+    return _lib
+
+
+POINTNET_EXPORTS: dict = {}
+
+
+def require_gpu() -> None:
+    if not torch.cuda.is_available():
+        raise RuntimeError("ndnet_amd needs a ROCm GPU (gfx950); none is visible and there is no CPU fallback")
+
+
+def check(rc: int, what: str) -> None:
+    if rc != NDNET_OK:
+        raise RuntimeError(f"{what} failed with code {rc}")
+
+
+def stream_ptr(device: torch.device | None = None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,148 @@
+"""NDTNet: PointNet over 12-D normal distributions (mean | flattened covariance).
+
+Module tree and parameter names follow the reference
+(ndnet/models/ndtnet.py:7-243) so its ``state_dict`` checkpoints
+(tools/train.py:186-194) load unchanged:
+
+    NDTNetSegmentation
+      feature_extractor: NDTNet
+        conv1/conv2/conv3 (+bn1..3), t1: TNet(3), t2: TNet(64)
+      conv1..conv4, bn1..bn3
+
+Two forward paths:
+  * eval mode on a gfx950 GPU -> the fused HIP kernels of
+    lib/libndnet_amd.so (``ndnet.models.pointnet_hip``): BatchNorm folded into
+    the 1x1 convolutions, FP32 MFMA GEMMs over (points x channels), global
+    max-pool fused into the producing GEMM.
+  * anything else (training, autograd, CPU) -> the PyTorch composition below,
+    which is also the fp32 reference the kernels are tested against.
+"""
+from __future__ import annotations
+
+from enum import Enum
+
+import torch
+from torch import nn
+
+
+def _conv(cin: int, cout: int) -> nn.Conv1d:
+    return nn.Conv1d(cin, cout, 1)
+
+
+class TNet(nn.Module):
+    """Predicts a ``in_dim x in_dim`` transform (reference ndtnet.py:7-62)."""
+
+    def __init__(self, in_dim: int = 64) -> None:
+        super().__init__()
+        self.in_dim = in_dim
+        self.conv1, self.conv2, self.conv3 = _conv(in_dim, 64), _conv(64, 128), _conv(128, 1024)
+        self.fc1, self.fc2, self.fc3 = nn.Linear(1024, 512), nn.Linear(512, 256), nn.Linear(256, in_dim * in_dim)
+        self.relu = nn.ReLU()
+        self.bn1, self.bn2, self.bn3 = nn.BatchNorm1d(64), nn.BatchNorm1d(128), nn.BatchNorm1d(1024)
+        self.bn4, self.bn5 = nn.BatchNorm1d(512), nn.BatchNorm1d(256)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        # pointwise MLP with BN+ReLU, max over points, FC head, + identity
+        for conv, bn in ((self.conv1, self.bn1), (self.conv2, self.bn2), (self.conv3, self.bn3)):
+            x = self.relu(bn(conv(x)))
+        g = x.amax(dim=2)
+        g = self.relu(self.bn4(self.fc1(g)))
+        g = self.relu(self.bn5(self.fc2(g)))
+        t = self.fc3(g) + torch.eye(self.in_dim, device=g.device, dtype=g.dtype).reshape(1, -1)
+        return t.view(-1, self.in_dim, self.in_dim)
+
+
+class NDTNet(nn.Module):
+    """Feature extractor (reference ndtnet.py:65-164)."""
+
+    class AdditionalFeatures(Enum):
+        NONE = "none"
+        COVARIANCES = "covariances"
+        FEATURE_VECTOR = "feature_vector"
+
+    def __init__(self, point_dim: int = 3, feature_dim: int = 768,
+                 extra_type: "NDTNet.AdditionalFeatures" = AdditionalFeatures.COVARIANCES) -> None:
+        super().__init__()
+        self.point_dim = point_dim
+        self.feature_dim = feature_dim
+        extra = {
+            NDTNet.AdditionalFeatures.COVARIANCES: point_dim ** 2,
+            NDTNet.AdditionalFeatures.FEATURE_VECTOR: feature_dim + point_dim ** 2,
+            NDTNet.AdditionalFeatures.NONE: 0,
+        }
+        self.extra_dim = extra.get(extra_type, 0)
+        self.conv1 = _conv(point_dim + self.extra_dim, 64)
+        self.conv2 = _conv(64, 128)
+        self.conv3 = _conv(128, feature_dim)
+        self.bn1, self.bn2, self.bn3 = nn.BatchNorm1d(64), nn.BatchNorm1d(128), nn.BatchNorm1d(feature_dim)
+        self.t1 = TNet(in_dim=point_dim)
+        self.t2 = TNet(in_dim=64)
+
+    def forward(self, points: torch.Tensor, extra: torch.Tensor):
+        """points [B,N,3], extra [B,N,9] -> (features [B,F,N], x_t2 [B,64,N])."""
+        B, N, _ = points.shape
+        d = self.point_dim
+        xyz = points.transpose(1, 2)                      # [B,3,N]
+        t = self.t1(xyz)                                  # [B,3,3]
+        xyz = torch.bmm(t, xyz)                           # t . p
+        cov = torch.matmul(t.unsqueeze(1), extra.reshape(B, N, d, d)).reshape(B, N, d * d)  # t . C (left only)
+        x = torch.cat((xyz.transpose(1, 2), cov), dim=2).transpose(1, 2)  # [B,12,N]
+        x = self.bn1(self.conv1(x))                       # no ReLU (reference ndtnet.py:149)
+        t2 = self.t2(x)                                   # [B,64,64]
+        x = torch.bmm(x.transpose(1, 2), t2).transpose(1, 2)  # x^T t2
+        x_t2 = x
+        x = self.bn2(self.conv2(x))
+        x = self.bn3(self.conv3(x))
+        return x, x_t2
+
+
+class NDTNetClassification(nn.Module):
+    """Global classifier head (reference ndtnet.py:166-196)."""
+
+    def __init__(self, point_dim: int = 3, num_classes: int = 512, feature_dim: int = 768) -> None:
+        super().__init__()
+        self.point_dim, self.num_classes, self.feature_dim = point_dim, num_classes, feature_dim
+        self.feature_extractor = NDTNet(point_dim, feature_dim=feature_dim)
+        self.conv1, self.conv2, self.conv3 = _conv(feature_dim, 512), _conv(512, 256), _conv(256, num_classes)
+
+    def forward(self, points: torch.Tensor, covariances: torch.Tensor) -> torch.Tensor:
+        x, _ = self.feature_extractor(points, covariances)
+        x = x.amax(dim=2, keepdim=True)
+        x = torch.relu(self.conv1(x))
+        x = torch.relu(self.conv2(x))
+        return torch.softmax(self.conv3(x), dim=1)
+
+
+class NDTNetSegmentation(nn.Module):
+    """Per-ND segmentation (reference ndtnet.py:198-243): log-probs [B,N,C+1]."""
+
+    def __init__(self, point_dim: int = 3, num_classes: int = 16, feature_dim: int = 1024) -> None:
+        super().__init__()
+        self.point_dim, self.num_classes, self.feature_dim = point_dim, num_classes, feature_dim
+        self.feature_extractor = NDTNet(point_dim, feature_dim=feature_dim)
+        self.conv1 = _conv(feature_dim + 64, 512)
+        self.conv2 = _conv(512, 256)
+        self.conv3 = _conv(256, 128)
+        self.conv4 = _conv(128, num_classes + 1)
+        self.bn1, self.bn2, self.bn3 = nn.BatchNorm1d(512), nn.BatchNorm1d(256), nn.BatchNorm1d(128)
+        self._hip = None  # folded-weight cache of the HIP path
+
+    def forward_torch(self, points: torch.Tensor, covariances: torch.Tensor) -> torch.Tensor:
+        x, x_t2 = self.feature_extractor(points, covariances)
+        g = x.amax(dim=2, keepdim=True).expand(-1, -1, x_t2.shape[2])
+        x = torch.cat((x_t2, g), dim=1)
+        for conv, bn in ((self.conv1, self.bn1), (self.conv2, self.bn2), (self.conv3, self.bn3)):
+            x = torch.relu(bn(conv(x)))
+        x = torch.nn.functional.log_softmax(self.conv4(x), dim=1)
+        return x.transpose(2, 1)
+
+    def forward(self, points: torch.Tensor, covariances: torch.Tensor) -> torch.Tensor:
+        if not self.training and points.is_cuda and self.point_dim == 3:
+            from . import pointnet_hip
+            if pointnet_hip.available():
+                return pointnet_hip.segmentation_forward(self, points, covariances)
+        return self.forward_torch(points, covariances)
+
+    def train(self, mode: bool = True):
+        self._hip = None  # weights may change; re-fold on the next eval forward
+        return super().train(mode)

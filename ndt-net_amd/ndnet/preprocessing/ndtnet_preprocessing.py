@@ -1,0 +1,140 @@
+"""Batched NDT preprocessing on the GPU.
+
+Drop-in for ``ndnet.preprocessing.ndtnet_preprocessing.ndt_preprocessing``
+(reference ndnet/preprocessing/ndtnet_preprocessing.py:6-73).  The reference
+loops over the batch on the host, copies each cloud to the CPU as float64,
+runs the C core and copies the result back; here the whole batch stays in HBM
+and one call of ``ndnet_ndt_run`` (include/ndnet_amd.h) processes every cloud.
+Results are bit-identical to the reference core's single-worker schedule
+(SURVEY §8c), cast to float32 and passed through ``nan_to_num`` as the
+reference does (ndtnet_preprocessing.py:66-69).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import torch
+
+from .. import _lib
+
+
+class NdtPlan:
+    """Device workspace for one (batch, points, NDs, classes) shape."""
+
+    def __init__(self, batch: int, num_points: int, num_nds: int, num_classes: int = -1,
+                 voxel_capacity: int = 0, device: torch.device | None = None):
+        _lib.require_gpu()
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.batch, self.num_points, self.num_nds, self.num_classes = batch, num_points, num_nds, num_classes
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            rc = _lib.lib().ndnet_ndt_plan_create(batch, num_points, num_nds, num_classes, voxel_capacity,
+                                                  ctypes.byref(h))
+        _lib.check(rc, "ndnet_ndt_plan_create")
+        self.handle = h
+        self.stats = torch.zeros((batch, _lib.STATS_BYTES), dtype=torch.uint8, device=self.device)
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                with torch.cuda.device(self.device):
+                    _lib.lib().ndnet_ndt_plan_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+    def run(self, points: torch.Tensor, labels: Optional[torch.Tensor], out: torch.Tensor,
+            out_classes: Optional[torch.Tensor]) -> None:
+        assert points.is_contiguous() and points.dtype == torch.float32 and points.device == self.device
+        assert out.is_contiguous() and out.shape == (self.batch, self.num_nds, 12)
+        st = _lib.stream_ptr(self.device)
+        rc = _lib.lib().ndnet_ndt_run(
+            self.handle, st, points.data_ptr(),
+            labels.data_ptr() if labels is not None else None,
+            out.data_ptr(),
+            out_classes.data_ptr() if out_classes is not None else None,
+            self.stats.data_ptr())
+        _lib.check(rc, "ndnet_ndt_run")
+
+    def prune(self, num_nds: int, out: torch.Tensor, out_classes: Optional[torch.Tensor] = None) -> None:
+        st = _lib.stream_ptr(self.device)
+        rc = _lib.lib().ndnet_ndt_prune(self.handle, st, num_nds, out.data_ptr(),
+                                        out_classes.data_ptr() if out_classes is not None else None,
+                                        None, None, None, self.stats.data_ptr())
+        _lib.check(rc, "ndnet_ndt_prune")
+
+    def host_stats(self) -> list:
+        raw = self.stats.cpu().numpy().tobytes()
+        return [_lib.NdtStats.from_buffer_copy(raw, i * _lib.STATS_BYTES) for i in range(self.batch)]
+
+
+_plans: dict = {}
+
+
+def get_plan(batch: int, num_points: int, num_nds: int, num_classes: int, device: torch.device) -> NdtPlan:
+    key = (batch, num_points, num_nds, num_classes, device)
+    p = _plans.get(key)
+    if p is None:
+        p = NdtPlan(batch, num_points, num_nds, num_classes, device=device)
+        _plans[key] = p
+    return p
+
+
+def ndt_preprocessing(num_nds: int, points: torch.Tensor, classes: torch.Tensor = None,
+                      num_classes: int = None) -> Tuple[torch.Tensor, torch.Tensor, Optional[torch.Tensor]]:
+    """Downsample a batch of clouds to ``num_nds`` normal distributions.
+
+    Args:
+        num_nds: NDs per cloud (the reference's ``n_desired_nds``).
+        points: ``[B, N, 3]`` float tensor (any device; computed on the GPU).
+        classes: optional ``[B, N, num_classes + 1]`` one-hot labels.
+        num_classes: number of classes (labels take ``num_classes + 1`` values).
+
+    Returns:
+        ``(points [B, num_nds, 3], covariances [B, num_nds, 9], classes one-hot
+        [B, num_nds, num_classes + 1] or None)`` float32 on ``points.device``.
+        The first two are views of one ``[B, num_nds, 12]`` block, the layout
+        the NDTNet kernels read.
+    """
+    _lib.require_gpu()
+    src_device = points.device
+    dev = src_device if src_device.type == "cuda" else torch.device("cuda", torch.cuda.current_device())
+    pts = points.to(device=dev, dtype=torch.float32).contiguous()
+    B, N, D = pts.shape
+    if D != 3:
+        raise ValueError(f"points must be [B, N, 3], got {tuple(pts.shape)}")
+    labelled = classes is not None
+    if labelled and num_classes is None:
+        raise ValueError("num_classes is required with classes")
+    ncls = int(num_classes) if labelled else -1
+    plan = get_plan(B, N, int(num_nds), ncls, dev)
+    out = torch.empty((B, num_nds, 12), dtype=torch.float32, device=dev)
+    out_cls = None
+    labels = None
+    if labelled:
+        # argmax of the one-hot labels, as ndtnet_preprocessing.py:34 does per cloud
+        labels = torch.argmax(classes.to(dev), dim=2).to(torch.int32).contiguous()
+        out_cls = torch.empty((B, num_nds, ncls + 1), dtype=torch.float32, device=dev)
+    plan.run(pts, labels, out, out_cls)
+    ndt_preprocessing.last_plan = plan
+    if src_device != dev:
+        out = out.to(src_device)
+        out_cls = out_cls.to(src_device) if out_cls is not None else None
+    return out[..., :3], out[..., 3:], out_cls
+
+
+ndt_preprocessing.last_plan = None
+
+
+def ndt_preprocessing_packed(num_nds: int, points: torch.Tensor) -> torch.Tensor:
+    """The unlabelled path returning the ``[B, num_nds, 12]`` block itself."""
+    p, _, _ = ndt_preprocessing(num_nds, points)
+    return p.as_strided((p.shape[0], p.shape[1], 12), (p.shape[1] * 12, 12, 1))
+
+
+def last_stats() -> list:
+    """Per-cloud ``ndnet_ndt_stats`` of the last ``ndt_preprocessing`` call."""
+    plan = ndt_preprocessing.last_plan
+    return plan.host_stats() if plan is not None else []

@@ -1,0 +1,43 @@
+"""The C-ABI library loads and exports every symbol include/ndnet_amd.h declares
+(CPU: nothing is called that needs a GPU)."""
+import ctypes
+import os
+import re
+
+from conftest import REPO
+
+
+def declared_symbols():
+    src = open(os.path.join(REPO, "include", "ndnet_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b([a-z_][a-z0-9_]*)\s*\(", src)) - {"defined"})
+
+
+def test_library_exports_header():
+    from ndnet import _lib
+    lib = _lib.lib()
+    syms = declared_symbols()
+    assert "ndt_downsample" in syms and "ndnet_ndt_run" in syms
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert b"gfx950" in lib.ndnet_amd_version()
+
+
+def test_python_bindings_cover_header():
+    from ndnet import _lib
+    assert set(declared_symbols()) <= set(_lib.EXPORTS) | set(_lib.POINTNET_EXPORTS)
+
+
+def test_code_object_targets_gfx950():
+    so = os.path.join(REPO, "ndt-net_amd", "lib", "libndnet_amd.so")
+    data = open(so, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data  # the offload bundle holds a gfx950 code object
+
+
+def test_product_does_not_import_oracle():
+    pkg = os.path.join(REPO, "ndt-net_amd")
+    for root, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".cpp", ".h")):
+                txt = open(os.path.join(root, f)).read()
+                assert "import oracle" not in txt and "liboracle" not in txt, f

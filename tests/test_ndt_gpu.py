@@ -1,0 +1,194 @@
+"""Parity of the HIP NDT path with the CPU oracle and the reference fixtures.
+
+Bar: bit-exact for integer/index results (grid, counts, dense order, KL list
+order, kept set) and for every double the reference computes (means,
+covariances, KL scores: the kernels perform the same IEEE operations);
+float32 rows equal the oracle's after the same cast + nan_to_num.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+FIXTURES = ["ndt_U4096_k256_s0.npz", "ndt_U4096_k256_s1.npz", "ndt_L4096_k256_s0.npz", "ndt_L4096_k256_s1.npz",
+            "ndt_U2003_k128_s7.npz"]
+
+
+def _run_plan(points_b: np.ndarray, k: int, labels_b=None, num_classes=-1):
+    import torch
+    from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
+    B, n, _ = points_b.shape
+    plan = NdtPlan(B, n, k, num_classes)
+    pts = torch.from_numpy(np.ascontiguousarray(points_b, dtype=np.float32)).cuda()
+    lbl = None if labels_b is None else torch.from_numpy(labels_b.astype(np.int32)).cuda()
+    out = torch.empty((B, k, 12), dtype=torch.float32, device="cuda")
+    out_cls = None if labels_b is None else torch.empty((B, k, num_classes + 1), dtype=torch.float32, device="cuda")
+    plan.run(pts, lbl, out, out_cls)
+    torch.cuda.synchronize()
+    return plan, out.cpu().numpy(), (None if out_cls is None else out_cls.cpu().numpy())
+
+
+def _dump(plan, cloud: int, nd: int, ne: int):
+    from ndnet import _lib
+    d = dict(nd_n=np.zeros(nd, np.uint32), nd_mean=np.zeros((nd, 3)), nd_cov_pre=np.zeros((nd, 9)),
+             nd_cov_post=np.zeros((nd, 9)), vox=np.zeros(nd, np.uint32), ord_val=np.zeros(max(ne, 1)),
+             ord_p=np.zeros(max(ne, 1), np.uint32), ord_q=np.zeros(max(ne, 1), np.uint32),
+             guesses=np.zeros(16), counts=np.zeros(16, np.uint32), alive=np.zeros(nd, np.uint8))
+    iters = ctypes.c_uint32(0)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    rc = _lib.lib().ndnet_ndt_debug_dump(plan.handle, cloud, p(d["nd_n"]), p(d["nd_mean"]), p(d["nd_cov_pre"]),
+                                         p(d["nd_cov_post"]), p(d["vox"]), p(d["ord_val"]), p(d["ord_p"]),
+                                         p(d["ord_q"]), p(d["guesses"]), p(d["counts"]), ctypes.byref(iters),
+                                         p(d["alive"]))
+    assert rc == 0
+    d["iters"] = iters.value
+    return d
+
+
+def _f32_rows(pc64, cov64, k):
+    rows = np.zeros((k, 12), np.float32)
+    rows[:, :3] = np.nan_to_num(pc64.astype(np.float32), nan=0.0, posinf=0.0, neginf=0.0)
+    rows[:, 3:] = np.nan_to_num(cov64.astype(np.float32), nan=0.0, posinf=0.0, neginf=0.0)
+    return rows
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_stages_match_reference_and_oracle(name):
+    z = golden(name)
+    k = int(z["k"])
+    ncls = int(z["num_classes"])
+    plan, out, out_cls = _run_plan(z["points"][None], k, z["labels"][None], ncls)
+    st = plan.host_stats()[0]
+    assert st.rc == 0 and st.prune_rc == int(z["orc_prune_rc"])
+    # bisection: every guess and count of the reference's own estimate stage
+    occ = np.nonzero(z["ref_count"])[0]
+    nd = len(occ)
+    d = _dump(plan, 0, nd, int(st.num_events))
+    assert d["iters"] == len(z["ref_guesses"])
+    assert np.array_equal(d["guesses"][:d["iters"]], z["ref_guesses"])
+    assert np.array_equal(d["counts"][:d["iters"]], z["ref_counts"])
+    assert tuple(st.len) == tuple(z["ref_len"]) and st.voxel_size == float(z["ref_voxel_size"])
+    # per-ND state at the accepted size, dense ids in ascending voxel order
+    assert st.num_nds == nd
+    assert np.array_equal(d["vox"], occ)
+    assert np.array_equal(d["nd_n"], z["ref_count"][occ])
+    assert np.array_equal(d["nd_mean"], z["ref_mean"][occ])
+    assert np.array_equal(d["nd_cov_pre"], z["ref_cov"][occ])
+    # KL list in the reference's insertion order (oracle), prune, mutated covariances
+    dense = -np.ones(len(z["ref_count"]), np.int64)
+    dense[occ] = np.arange(nd)
+    E = len(z["orc_ord_div"])
+    assert st.num_events == E
+    assert np.array_equal(d["ord_val"][:E], z["orc_ord_div"], equal_nan=True)
+    assert np.array_equal(d["ord_p"][:E], dense[z["orc_ord_p"]])
+    assert np.array_equal(d["ord_q"][:E], dense[z["orc_ord_q"]])
+    assert np.array_equal(d["nd_cov_post"], z["orc_cov_post"][occ], equal_nan=True)
+    assert np.array_equal(d["alive"], z["orc_kept"][occ])
+    assert st.num_out == int(z["orc_nout"]) and st.num_valid == int(z["orc_num_valid"])
+    # rows as ndt_preprocessing returns them
+    assert np.array_equal(out[0], _f32_rows(z["orc_out_pc"], z["orc_out_cov"], k))
+    onehot = np.zeros((k, ncls + 1), np.float32)
+    onehot[np.arange(k), z["orc_out_cls"]] = 1.0
+    assert np.array_equal(out_cls[0], onehot)
+
+
+def test_reference_driver_fixture():
+    """Rows the reference's own ndt_preprocessing produced (over the oracle ABI)."""
+    import torch
+    from ndnet.preprocessing.ndtnet_preprocessing import ndt_preprocessing
+    z = golden("preproc_B3_k256.npz")
+    p, c, cl = ndt_preprocessing(int(z["k"]), torch.from_numpy(z["points"]).cuda())
+    assert cl is None
+    assert np.array_equal(p.cpu().numpy(), z["out_points"])
+    assert np.array_equal(c.cpu().numpy(), z["out_covs"])
+
+
+@pytest.mark.parametrize("kind", ["U", "L"])
+def test_full_size_batch(kind):
+    """C2: 16 x 100k -> 1000, every cloud against the oracle."""
+    import torch
+    import oracle as O
+    from ndnet.preprocessing.ndtnet_preprocessing import ndt_preprocessing, last_stats
+    from ndnet.synthetic import make_batch
+    B, n, k = 16, 100_000, 1000
+    pts = make_batch(kind, B, n)
+    p, c, _ = ndt_preprocessing(k, torch.from_numpy(pts).cuda())
+    p, c = p.cpu().numpy(), c.cpu().numpy()
+    stats = last_stats()
+    for b in range(B):
+        pc, cov, r = O.downsample_f32(pts[b], k)
+        assert stats[b].rc == r.rc == 0
+        assert stats[b].num_events == len(r.ord_div)
+        assert np.array_equal(p[b], pc), f"cloud {b} means"
+        assert np.array_equal(c[b], cov), f"cloud {b} covariances"
+
+
+def test_mixed_batch_equals_single_runs():
+    import torch
+    from ndnet.preprocessing.ndtnet_preprocessing import ndt_preprocessing
+    names = FIXTURES[:4]
+    pts = np.stack([golden(nm)["points"] for nm in names])
+    p, c, _ = ndt_preprocessing(256, torch.from_numpy(pts).cuda())
+    for b, nm in enumerate(names):
+        z = golden(nm)
+        rows = _f32_rows(z["orc_out_pc"], z["orc_out_cov"], 256)
+        assert np.array_equal(p[b].cpu().numpy(), rows[:, :3])
+        assert np.array_equal(c[b].cpu().numpy(), rows[:, 3:])
+
+
+def test_edge_clouds():
+    """A failed search (z constant and positive: a 0-length axis puts every
+    point out of grid), and a cloud whose extent is exactly one first-pass
+    voxel, so a reference worker abandons the rest of its chunk at the point on
+    the grid maximum (float64 path: the extent is not float32-representable)."""
+    import torch
+    import oracle as O
+    from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
+    from ndnet.preprocessing.ndt_legacy import NDT_Sampler
+    rng = np.random.default_rng(5)
+    n, k = 4101, 200
+    flat = rng.uniform(-5, 5, (n, 3)).astype(np.float32)
+    flat[:, 2] = 1.5
+    plan = NdtPlan(1, n, k, -1)
+    out = torch.full((1, k, 12), 7.0, dtype=torch.float32, device="cuda")
+    plan.run(torch.from_numpy(flat[None]).cuda(), None, out, None)
+    torch.cuda.synchronize()
+    st = plan.host_stats()[0]
+    r = O.run(flat.astype(np.float64), k)
+    assert st.rc == r.rc == -3 and st.iters == 15
+    assert not out.any().item()
+    # abandoned chunks
+    a = rng.uniform(0.0, 14.995, (n, 3))
+    a[17] = [14.995, 3.0, 3.0]
+    a[1000] = [0.0, 0.0, 0.0]
+    assert (a[:, 0].max() - a[:, 0].min()) / 14.995 == 1.0
+    s = NDT_Sampler(a)
+    pc, cov, _ = s.downsample(k)
+    ref = O.LegacyChain(a)
+    pc2, cov2 = ref.downsample(k)
+    assert np.array_equal(pc, pc2) and np.array_equal(cov, cov2, equal_nan=True)
+    s.cleanup()
+    ref.cleanup()
+
+
+def test_legacy_sampler_multilevel():
+    """NDT_Sampler.downsample(k) -> prune(k2) -> prune(k3) (config 5's levels)
+    against the oracle's implementation of the same reference ABI calls."""
+    import oracle as O
+    from ndnet.preprocessing.ndt_legacy import NDT_Sampler
+    from ndnet.synthetic import uniform_cloud, lidar_cloud
+    for cloud in (uniform_cloud(30_000, 3), lidar_cloud(30_000, 4)):
+        pts = cloud.astype(np.float64)
+        s = NDT_Sampler(pts)
+        levels = [s.downsample(600), s.prune(300), s.prune(150)]
+        ref = O.LegacyChain(pts)
+        expect = [ref.downsample(600), ref.prune(300), ref.prune(150)]
+        for (p1, c1, _), (p2, c2) in zip(levels, expect):
+            assert np.array_equal(p1, p2)
+            assert np.array_equal(c1, c2, equal_nan=True)
+        s.cleanup()
+        ref.cleanup()
