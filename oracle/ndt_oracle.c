@@ -427,6 +427,7 @@ static int orc_prune(orc_nd* nds, uint64_t k, uint64_t* num_valid, orc_kl* kl, u
   uint64_t idx = 0;
   for (uint64_t i = 0; i < to_remove; idx++) {
     if (idx >= *nkl) return -2;
+    if (kl[idx].p == NULL) return -8; /* an entry never written (the reference reads garbage) */
     if (kl[idx].p->n == 0) continue;
     kl[idx].p->n = 0;
     (*num_valid)--;
@@ -470,7 +471,7 @@ int orc_run(const double* pc, uint64_t n, const uint16_t* cls, int ncls, uint64_
             uint8_t* vox_kept, uint64_t ecap, double* ev_div, int64_t* ev_p, int64_t* ev_q, int32_t* ev_rc,
             double* ord_div, int64_t* ord_p, int64_t* ord_q, uint64_t* nvox, uint64_t* nev, uint64_t* nord,
             int* prune_rc, uint64_t* num_valid_out, double* out_pc, double* out_cov, uint16_t* out_cls,
-            uint64_t* nout) {
+            uint64_t* nout, double* post_div, int64_t* post_p, int64_t* post_q, uint64_t* post_nkl) {
   orc_nd* nds = NULL;
   *nvox = *nev = *nord = *nout = 0;
   int rc = orc_search_impl(pc, 3, n, cls, ncls, k, s, &nds);
@@ -488,7 +489,7 @@ int orc_run(const double* pc, uint64_t n, const uint16_t* cls, int ncls, uint64_
     memcpy(vox_cov_pre + 9 * v, nds[v].cov, 72);
     vox_cls[v] = nds[v].cls;
   }
-  orc_kl* kl = (orc_kl*)malloc((V ? V : 1) * 6 * sizeof(orc_kl));
+  orc_kl* kl = (orc_kl*)calloc((V ? V : 1) * 6, sizeof(orc_kl)); /* p == NULL marks never-written entries */
   uint64_t num_valid = 0, nkl = 0;
   orc_kl_all(nds, s->len, &num_valid, kl, &nkl, ev_div, ev_p, ev_q, ev_rc, nev);
   for (uint64_t i = 0; i < nkl; i++) {
@@ -499,6 +500,13 @@ int orc_run(const double* pc, uint64_t n, const uint16_t* cls, int ncls, uint64_
   *nord = nkl;
   *prune_rc = orc_prune(nds, k, &num_valid, kl, &nkl, 6 * V);
   *num_valid_out = num_valid;
+  /* the physical list after the prune's left shift, first *nord entries */
+  for (uint64_t i = 0; i < *nord; i++) {
+    post_div[i] = kl[i].div;
+    post_p[i] = kl[i].p ? kl[i].p - nds : -1;
+    post_q[i] = kl[i].q ? kl[i].q - nds : -1;
+  }
+  *post_nkl = nkl;
   for (uint64_t v = 0; v < V; v++) {
     memcpy(vox_cov_post + 9 * v, nds[v].cov, 72);
     vox_kept[v] = nds[v].n > 0;

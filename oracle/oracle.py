@@ -135,6 +135,10 @@ class RunResult:
     out_cov: np.ndarray = field(default=None)
     out_cls: np.ndarray = field(default=None)
     nout: int = 0
+    post_div: np.ndarray = field(default=None)
+    post_p: np.ndarray = field(default=None)
+    post_q: np.ndarray = field(default=None)
+    post_nkl: int = 0
 
 
 def run(points: np.ndarray, k: int, classes: np.ndarray | None = None, num_classes: int = 0,
@@ -166,8 +170,11 @@ def run(points: np.ndarray, k: int, classes: np.ndarray | None = None, num_class
     r.out_pc = np.zeros((k, 3))
     r.out_cov = np.zeros((k, 9))
     r.out_cls = np.zeros(k, np.uint16)
+    r.post_div = np.zeros(ecap)
+    r.post_p = np.zeros(ecap, np.int64)
+    r.post_q = np.zeros(ecap, np.int64)
     s = _SearchT()
-    nvox, nev, nord, nout, nvalid = (_U64(0) for _ in range(5))
+    nvox, nev, nord, nout, nvalid, pnkl = (_U64(0) for _ in range(6))
     prc = ctypes.c_int(0)
     rc = lib().orc_run(
         _ptr(pts), _U64(n), _ptr(cls), ctypes.c_int(num_classes), _U64(k), ctypes.byref(s), _U64(vcap),
@@ -175,13 +182,15 @@ def run(points: np.ndarray, k: int, classes: np.ndarray | None = None, num_class
         _ptr(r.vox_kept), _U64(ecap), _ptr(r.ev_div), _ptr(r.ev_p), _ptr(r.ev_q), _ptr(r.ev_rc),
         _ptr(r.ord_div), _ptr(r.ord_p), _ptr(r.ord_q), ctypes.byref(nvox), ctypes.byref(nev), ctypes.byref(nord),
         ctypes.byref(prc), ctypes.byref(nvalid), _ptr(r.out_pc), _ptr(r.out_cov), _ptr(r.out_cls),
-        ctypes.byref(nout))
+        ctypes.byref(nout), _ptr(r.post_div), _ptr(r.post_p), _ptr(r.post_q), ctypes.byref(pnkl))
     r.rc = rc
     r.search = _search_result(s)
     e = nev.value
     r.ev_div, r.ev_p, r.ev_q, r.ev_rc = r.ev_div[:e], r.ev_p[:e], r.ev_q[:e], r.ev_rc[:e]
     o = nord.value
     r.ord_div, r.ord_p, r.ord_q = r.ord_div[:o], r.ord_p[:o], r.ord_q[:o]
+    r.post_div, r.post_p, r.post_q = r.post_div[:o], r.post_p[:o], r.post_q[:o]
+    r.post_nkl = pnkl.value
     r.prune_rc = prc.value
     r.num_valid = nvalid.value
     r.nout = nout.value

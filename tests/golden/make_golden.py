@@ -104,6 +104,7 @@ def ndt_fixtures() -> None:
             ref_count=cnt, ref_mean=mean, ref_cov=cov, ref_cls=cls,
             orc_ev_div=r.ev_div, orc_ev_p=r.ev_p, orc_ev_q=r.ev_q, orc_ev_rc=r.ev_rc,
             orc_ord_div=r.ord_div, orc_ord_p=r.ord_p, orc_ord_q=r.ord_q,
+            orc_post_div=r.post_div, orc_post_p=r.post_p, orc_post_q=r.post_q, orc_post_nkl=r.post_nkl,
             orc_cov_post=r.vox_cov_post, orc_kept=r.vox_kept, orc_prune_rc=r.prune_rc, orc_num_valid=r.num_valid,
             orc_out_pc=r.out_pc, orc_out_cov=r.out_cov, orc_out_cls=r.out_cls, orc_nout=r.nout,
             orc_glibc_kept=rl.vox_kept, orc_glibc_out_cov=rl.out_cov)

@@ -79,13 +79,16 @@ def test_stages_match_reference_and_oracle(name):
     assert np.array_equal(d["nd_mean"], z["ref_mean"][occ])
     assert np.array_equal(d["nd_cov_pre"], z["ref_cov"][occ])
     # KL list in the reference's insertion order (oracle), prune, mutated covariances
-    dense = -np.ones(len(z["ref_count"]), np.int64)
+    dense = -np.ones(len(z["ref_count"]) + 1, np.int64)
     dense[occ] = np.arange(nd)
+    dense[-1] = 0xFFFFFFFF  # index -1: an entry the reference never wrote (poison)
     E = len(z["orc_ord_div"])
-    assert st.num_events == E
-    assert np.array_equal(d["ord_val"][:E], z["orc_ord_div"], equal_nan=True)
-    assert np.array_equal(d["ord_p"][:E], dense[z["orc_ord_p"]])
-    assert np.array_equal(d["ord_q"][:E], dense[z["orc_ord_q"]])
+    assert st.num_events == E and st.num_kl == int(z["orc_post_nkl"])
+    # the retained list after the level-1 prune's left shift (ndt.c:69-72)
+    live = z["orc_post_p"] >= 0
+    assert np.array_equal(d["ord_val"][:E][live], z["orc_post_div"][live], equal_nan=True)
+    assert np.array_equal(d["ord_p"][:E], dense[z["orc_post_p"]])
+    assert np.array_equal(d["ord_q"][:E], dense[z["orc_post_q"]])
     assert np.array_equal(d["nd_cov_post"], z["orc_cov_post"][occ], equal_nan=True)
     assert np.array_equal(d["alive"], z["orc_kept"][occ])
     assert st.num_out == int(z["orc_nout"]) and st.num_valid == int(z["orc_num_valid"])
