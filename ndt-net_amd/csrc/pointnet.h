@@ -1,2 +1,36 @@
-// PointNet (NDTNetSegmentation) forward kernels: see pointnet_kernels.hip.
+// NDTNetSegmentation forward (eval mode) on gfx950: argument blocks of the
+// fused point-MLP kernel (pointnet_kernels.hip).  Layer weights are stored
+// transposed, W^T[K][N] row-major (K input channels x N output channels),
+// with BatchNorm folded in and K padded to a multiple of 4, N to 16.
 #pragma once
+#include <stdint.h>
+
+#define NDNET_PN_MAX_LAYERS 5
+
+typedef struct ndnet_pn_layer {
+  const float* wT;        // [K][N] (+ cloud * w_cloud_stride)
+  int64_t w_cloud_stride; // 0 for shared weights, K*N for per-cloud folded weights
+  const float* bias;      // [N] (+ cloud * bias_cloud_stride)
+  int64_t bias_cloud_stride;
+  int32_t K, N;           // padded sizes
+  int32_t relu;
+  int32_t pad_;
+} ndnet_pn_layer;
+
+// mode: 0 = max-pool the last layer over points into gmax[cloud][N]
+//       1 = log-softmax over the first `out_cols` channels of the last layer,
+//           written to out[cloud][point][out_cols]
+typedef struct ndnet_pn_chain {
+  const float* x;         // [B][num_points][x_ld] input rows
+  int32_t x_ld;           // floats per input row (12)
+  int32_t in_cols;        // columns of x the first layer reads (3 or 12); the rest of K is zero
+  int32_t num_points;
+  int32_t num_layers;
+  ndnet_pn_layer L[NDNET_PN_MAX_LAYERS];
+  int32_t mode;
+  int32_t out_cols;
+  float* gmax;            // mode 0: [B][gmax_ld], pre-set to -inf
+  int32_t gmax_ld;
+  int32_t max_width;      // widest stored activation (LDS sizing)
+  float* out;             // mode 1
+} ndnet_pn_chain;

@@ -1,0 +1,98 @@
+"""NDTNetSegmentation: the reference module tree and numerics (CPU), and the
+HIP MFMA forward against torch fp32 (GPU).
+
+Tolerance: |log-prob difference| <= 1e-4 absolute (SURVEY §8d, FP32 mode);
+the kernels compute in fp32 with a different summation order and with the
+BatchNorms and the t1/t2 transforms folded into the weights."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from model_init import deterministic_state
+
+TOL = 1e-4
+
+
+def _model(F, C, device="cpu"):
+    from ndnet.models.ndtnet import NDTNetSegmentation
+    m = NDTNetSegmentation(3, C, F)
+    m.load_state_dict(deterministic_state(m.state_dict()))
+    return m.to(device).eval()
+
+
+@pytest.mark.parametrize("name", ["ndtnet_seg_F768_C28.npz", "ndtnet_seg_F64_C5.npz"])
+def test_torch_forward_matches_reference_fixture(name):
+    z = golden(name)
+    m = _model(int(z["feature_dim"]), int(z["num_classes"]))
+    p, c = torch.from_numpy(z["points"]), torch.from_numpy(z["covs"])
+    with torch.no_grad():
+        assert np.array_equal(m(p, c).numpy(), z["out_eval"])       # CPU -> torch path
+        m.train()
+        assert np.array_equal(m(p, c).numpy(), z["out_train"])      # batch-statistics BN
+
+
+def test_state_dict_keys_match_reference_layout():
+    m = _model(768, 28)
+    keys = set(m.state_dict())
+    for k in ["feature_extractor.t1.conv1.weight", "feature_extractor.t2.fc3.bias", "feature_extractor.bn3.running_var",
+              "conv4.weight", "bn3.num_batches_tracked"]:
+        assert k in keys
+    assert sum(p.numel() for p in m.parameters()) == 3_366_822  # reference NDTNetSegmentation(3, 28, 768)
+
+
+@pytest.mark.parametrize("name", ["ndtnet_seg_F768_C28.npz", "ndtnet_seg_F64_C5.npz"])
+def test_folded_algebra_cpu(name):
+    """The HIP path's folding (BN, t1, t2, split seg head), evaluated with torch ops."""
+    from ndnet.models import pointnet_hip as ph
+    z = golden(name)
+    m = _model(int(z["feature_dim"]), int(z["num_classes"]))
+    with torch.no_grad():
+        out = ph.segmentation_forward(m, torch.from_numpy(z["points"]), torch.from_numpy(z["covs"]),
+                                      chain=ph._chain_torch)
+    assert np.abs(out.numpy() - z["out_eval"]).max() < TOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["ndtnet_seg_F768_C28.npz", "ndtnet_seg_F64_C5.npz"])
+def test_hip_forward_matches_reference_fixture(name):
+    from ndnet.models import pointnet_hip as ph
+    assert ph.available(), "the HIP forward must be built (no silent fallback)"
+    z = golden(name)
+    m = _model(int(z["feature_dim"]), int(z["num_classes"]), "cuda")
+    with torch.no_grad():
+        out = m(torch.from_numpy(z["points"]).cuda(), torch.from_numpy(z["covs"]).cuda()).cpu().numpy()
+    assert np.abs(out - z["out_eval"]).max() < TOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,N", [(16, 1000), (3, 77), (1, 31)])
+def test_hip_forward_matches_torch_fp32(B, N):
+    """Full-size C3 shape plus ragged point counts (tails of the 32-point tiles)."""
+    from ndnet.models import pointnet_hip as ph
+    m = _model(768, 28, "cuda")
+    g = torch.Generator(device="cuda").manual_seed(B * 1000 + N)
+    p = torch.rand((B, N, 3), device="cuda", generator=g) * 20 - 10
+    c = torch.randn((B, N, 9), device="cuda", generator=g)
+    with torch.no_grad():
+        out = m(p, c)
+        ref = m.forward_torch(p, c)
+        emu = ph.segmentation_forward(m, p, c, chain=ph._chain_torch)
+    assert out.shape == (B, N, 29)
+    assert (out - ref).abs().max().item() < TOL
+    assert (out - emu).abs().max().item() < TOL
+    assert torch.equal(out.argmax(-1), ref.argmax(-1)) or (out.argmax(-1) != ref.argmax(-1)).float().mean() < 1e-3
+
+
+@pytest.mark.gpu
+def test_hip_forward_on_ndt_rows():
+    """End to end: ndt_preprocessing rows (views of one [B,k,12] block) into the model."""
+    from ndnet.preprocessing.ndtnet_preprocessing import ndt_preprocessing
+    from ndnet.synthetic import make_batch
+    m = _model(768, 28, "cuda")
+    pts = torch.from_numpy(make_batch("L", 4, 20_000)).cuda()
+    p, c, _ = ndt_preprocessing(500, pts)
+    with torch.no_grad():
+        out = m(p, c)
+        ref = m.forward_torch(p.contiguous(), c.contiguous())
+    assert (out - ref).abs().max().item() < TOL
