@@ -116,7 +116,7 @@ def main() -> None:
     # ---- stage timing (HIP events on the stream the kernels run on) ----
     plan = get_plan(B, n, k, -1, dev)
     _lib.lib().ndnet_ndt_set_timing(plan.handle, 1)
-    stage_names = ["reset+limits", "bisection (15 launches)", "dense ids", "chunk sort", "welford", "kl+prune"]
+    stage_names = ["reset+limits", "bisection (15 launches)", "dense ids", "binning", "welford", "kl (chains+events+order+prune)"]
     stage_ms = np.zeros(6)
     fwd_ms = 0.0
     reps = max(3, min(args.steps, 10))

@@ -37,12 +37,12 @@ using namespace ndnet;
 
 namespace {
 
-constexpr int kChunk = 4096;         // points per k_chunk_sort workgroup
-constexpr int kChunkThreads = 1024;
 constexpr int kPassThreads = 256;    // threads per search workgroup
-constexpr int kPassPPT = 16;         // points per thread per search workgroup
+constexpr int kPassPPT = 4;          // points per thread per search workgroup
 constexpr int kPassPts = kPassThreads * kPassPPT;
-constexpr int kHashSlots = 8192;     // LDS dedup table of a search workgroup
+constexpr int kHashSlots = 2048;     // LDS dedup table of a search workgroup (>= kBitsWords)
+constexpr int kBitsCap = 32768;      // grids up to this many voxels count through bitmaps
+constexpr int kBitsWords = kBitsCap / 32;
 constexpr int kKLThreads = 1024;
 constexpr int kSortLds = 8192;       // largest event sort kept in LDS
 
@@ -61,6 +61,7 @@ struct CloudCtl {
   uint32_t epoch;
   uint32_t stamp;
   uint32_t accepted_stamp;
+  uint32_t acc_mode;     // occupancy of the accepted pass: 0/1 bitmap buffer, 2 stamps
   uint32_t count;
   uint32_t arrive;
   uint32_t nbad;
@@ -87,7 +88,7 @@ struct Plan {
   uint64_t vcap;       // voxels per cloud the stamp / dense tables hold
   uint32_t ndcap;      // max accepted NDs per cloud = floor(1.2 k) + 1
   uint32_t ecap;       // 6 * ndcap
-  uint32_t nchunks;    // k_chunk_sort chunks per cloud
+  uint32_t nbins;      // 1024-point binning chunks per cloud
   uint32_t G;          // search workgroups per cloud
   int in_f64;          // input element type of the last run
   uint64_t calls;      // runs issued (mirrors the device epoch)
@@ -98,9 +99,13 @@ struct Plan {
   uint32_t* stamps;    // [B][vcap]
   uint32_t* dense_of;  // [B][vcap]
   uint32_t* vox;       // [B][ndcap] linear index of dense id
-  void* chunk_pts;     // [B][nchunks][kChunk] double[3]
-  uint16_t* chunk_lbl; // [B][nchunks][kChunk]
-  uint2* chunk_tab;    // [B][nchunks][ndcap] (start, count)
+  uint32_t* gbits;     // [B][2][kBitsWords] occupancy bitmaps of small-grid passes
+  uint32_t* pkeys;     // [B][n] voxel key of every point in the latest pass
+  uint32_t* did;       // [B][n] dense id of every point in the accepted pass
+  uint32_t* bin_cnt;   // [B][nbins][ndcap] per-chunk histograms -> offsets
+  uint32_t* nd_base;   // [B][ndcap]
+  void* nd_pts;        // [B][n][3] points grouped by ND (input element type)
+  uint16_t* nd_lbl;    // [B][n]
   uint32_t* nd_n;      // [B][ndcap]
   double* nd_mean;     // [B][ndcap][3]
   double* nd_cov;      // [B][ndcap][9] pre-KL
@@ -134,7 +139,7 @@ struct Plan {
 
 // ------------------------------------------------------------------ helpers
 
-__device__ inline uint32_t hash32(uint32_t k) { return (k * 2654435761u) >> (32 - 13); }
+__device__ inline uint32_t hash32(uint32_t k) { return (k * 2654435761u) >> (32 - 11); }
 
 template <typename T>
 __device__ inline void load_point(const T* pts, uint64_t i, double* x) {
@@ -246,21 +251,40 @@ __device__ inline void set_guess(CloudCtl& c, double guess, uint64_t vcap) {
   }
 }
 
+constexpr int kLimPPT = 16;        // flat coordinates per thread in k_limits
+
+// Bounding box (pointclouds.c:40-66) over every point, the n % 8 tail
+// included.  Coordinates are read as a flat, coalesced stream; element f is
+// axis f % 3.
 template <typename T>
-__global__ void k_limits(const T* __restrict__ pts, CloudCtl* ctl, uint64_t n, uint32_t G, uint64_t vcap) {
+__global__ void __launch_bounds__(256) k_limits(const T* __restrict__ pts, CloudCtl* ctl, uint32_t* gbits_all,
+                                                uint64_t n, uint32_t G, uint64_t vcap) {
   const int b = blockIdx.y;
   const T* p = pts + (uint64_t)b * n * 3;
+  const uint64_t nf = 3 * n;
   double mx[3] = {kDblMin, kDblMin, kDblMin}, mn[3] = {kDblMax, kDblMax, kDblMax};
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)G * blockDim.x) {
-    double x[3];
-    load_point(p, i, x);
-    for (int a = 0; a < 3; a++) {
-      mx[a] = x[a] > mx[a] ? x[a] : mx[a];  // maxf(point, cur), pointclouds.c:28-30
-      mn[a] = x[a] < mn[a] ? x[a] : mn[a];
+  const uint64_t f0 = (uint64_t)blockIdx.x * 256 * kLimPPT + threadIdx.x;
+  T v[kLimPPT];
+#pragma unroll
+  for (int j = 0; j < kLimPPT; j++) {
+    const uint64_t f = f0 + 256 * j;
+    v[j] = f < nf ? p[f] : T(0);
+  }
+#pragma unroll
+  for (int j = 0; j < kLimPPT; j++) {
+    const uint64_t f = f0 + 256 * j;
+    if (f >= nf) continue;
+    const uint32_t a = (uint32_t)(f % 3);
+    const double x = (double)v[j];
+#pragma unroll
+    for (int ax = 0; ax < 3; ax++) {
+      // maxf(point, cur) / minf(point, cur): a NaN coordinate never wins
+      mx[ax] = (a == (uint32_t)ax && x > mx[ax]) ? x : mx[ax];
+      mn[ax] = (a == (uint32_t)ax && x < mn[ax]) ? x : mn[ax];
     }
   }
-  // wave reduce on order keys
   unsigned long long kmx[3], kmn[3];
+#pragma unroll
   for (int a = 0; a < 3; a++) {
     kmx[a] = ord_key(mx[a]);
     kmn[a] = ord_key(mn[a]);
@@ -278,6 +302,7 @@ __global__ void k_limits(const T* __restrict__ pts, CloudCtl* ctl, uint64_t n, u
       atomicMin(&c.limkey[3 + a], kmn[a]);
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   __shared__ uint32_t last;
   if (threadIdx.x == 0) {
@@ -286,57 +311,44 @@ __global__ void k_limits(const T* __restrict__ pts, CloudCtl* ctl, uint64_t n, u
     last = (t == G - 1);
   }
   __syncthreads();
-  if (!last || threadIdx.x != 0) return;
+  if (!last) return;
   __atomic_thread_fence(__ATOMIC_ACQUIRE);
-  for (int a = 0; a < 6; a++)
-    c.lim[a] = ord_unkey(__hip_atomic_load(&c.limkey[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  c.arrive = 0;
-  c.lo = kMinGuess;
-  c.hi = kMaxGuess;
-  set_guess(c, (kMaxGuess - kMinGuess) / 2.0, vcap);  // ndt.c:136
+  if (threadIdx.x == 0) {
+    for (int a = 0; a < 6; a++)
+      c.lim[a] = ord_unkey(__hip_atomic_load(&c.limkey[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    c.arrive = 0;
+    c.lo = kMinGuess;
+    c.hi = kMaxGuess;
+    set_guess(c, (kMaxGuess - kMinGuess) / 2.0, vcap);  // ndt.c:136
+  }
+  __syncthreads();
+  if (c.state == kSearching && c.V <= (uint64_t)kBitsCap) {  // clear pass 0's occupancy bitmap
+    uint32_t* gb = gbits_all + (uint64_t)b * 2 * kBitsWords;
+    for (uint32_t w = threadIdx.x; w < (uint32_t)((c.V + 31) / 32); w += blockDim.x) gb[w] = 0;
+  }
 }
 
-// Distinct-voxel counting of one bisection pass for the points [start, end)
-// of one cloud.  Returns this thread's number of newly stamped voxels.
-template <typename T>
-__device__ inline uint32_t mark_points(const T* p, uint64_t start, uint64_t end, uint64_t chunk, const CloudCtl& c,
-                                       uint32_t* stamps, uint32_t stamp, uint32_t* table, bool track_bad,
-                                       uint32_t* bad_out, const uint32_t* cutoff) {
-  const double vs = c.guess;
-  const double inv_vs = 1.0 / vs;
-  uint32_t fresh = 0;
-  for (uint64_t i = start + threadIdx.x; i < end; i += blockDim.x) {
-    if (cutoff && i >= cutoff[i / chunk]) continue;
-    double x[3];
-    load_point(p, i, x);
-    const uint32_t key = voxel_key(x[0], x[1], x[2], c.off, c.len, vs, inv_vs);
-    if (key == kInvalid) {
-      if (track_bad) atomicMin(&bad_out[i / chunk], (uint32_t)i);
-      continue;
-    }
-    if (table) {
-      // LDS dedup: only the thread that inserts a key touches the global stamp
-      uint32_t h = hash32(key);
-      bool mine = false;
-      for (int probe = 0; probe < kHashSlots; probe++) {
-        uint32_t cur = table[h];
-        if (cur == key) break;
-        if (cur == kInvalid) {
-          uint32_t old = atomicCAS(&table[h], kInvalid, key);
-          if (old == kInvalid) { mine = true; break; }
-          if (old == key) break;
-        }
-        h = (h + 1) & (kHashSlots - 1);
+// Large-grid path of a pass: dedup keys in an LDS hash table; the thread that
+// inserts a key flips the voxel's global stamp.  Returns the new voxels.
+__device__ inline uint32_t stamp_key(uint32_t key, uint32_t* table, uint32_t* stamps, uint32_t stamp) {
+  if (table) {
+    uint32_t h = hash32(key);
+    bool mine = false;
+    for (int probe = 0; probe < kHashSlots; probe++) {
+      const uint32_t cur = table[h];
+      if (cur == key) break;
+      if (cur == kInvalid) {
+        const uint32_t old = atomicCAS(&table[h], kInvalid, key);
+        if (old == kInvalid) { mine = true; break; }
+        if (old == key) break;
       }
-      if (!mine) continue;
+      h = (h + 1) & (kHashSlots - 1);
     }
-    uint32_t* s = stamps + key;
-    if (__hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != stamp) {
-      uint32_t old = atomicExch(s, stamp);
-      fresh += (old != stamp);
-    }
+    if (!mine) return 0;
   }
-  return fresh;
+  uint32_t* s = stamps + key;
+  if (__hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == stamp) return 0;
+  return atomicExch(s, stamp) != stamp;
 }
 
 __device__ inline uint32_t block_sum_u32(uint32_t v, uint32_t* scratch) {
@@ -346,7 +358,7 @@ __device__ inline uint32_t block_sum_u32(uint32_t v, uint32_t* scratch) {
 }
 
 // Bisection decision of ndt.c:168-187 after a pass counted `count` NDs.
-__device__ inline void finish_pass(CloudCtl& c, uint32_t count, uint64_t k, uint64_t vcap) {
+__device__ inline void finish_pass(CloudCtl& c, uint32_t count, uint64_t k, uint64_t vcap, uint32_t mode) {
   c.guesses[c.iter] = c.guess;
   c.counts[c.iter] = count;
   if ((double)count > (double)k * (1 + kUpper)) {
@@ -358,6 +370,7 @@ __device__ inline void finish_pass(CloudCtl& c, uint32_t count, uint64_t k, uint
     c.vs = c.guess;
     c.num_nds = count;
     c.accepted_stamp = c.stamp;
+    c.acc_mode = mode;
     c.iter++;
     return;
   }
@@ -374,33 +387,78 @@ __device__ inline void finish_pass(CloudCtl& c, uint32_t count, uint64_t k, uint
   set_guess(c, g, vcap);
 }
 
+// One bisection pass (estimate_ndt's occupancy, normal_distributions.c:38-60
+// + ndt.c:158-176) over kPassPts points of one cloud per workgroup.  The
+// points are staged through LDS with coalesced loads; each point's voxel key
+// is kept (keys_all) for the binning of the accepted pass.  Small grids
+// (V <= kBitsCap) count distinct voxels with an LDS bitmap per workgroup
+// merged by one global atomicOr per word; larger grids use per-voxel stamps.
 template <typename T>
 __global__ void __launch_bounds__(kPassThreads) k_search_pass(const T* __restrict__ pts, CloudCtl* ctl,
-                                                              uint32_t* stamps_all, uint64_t n, uint64_t k,
-                                                              uint32_t G, uint64_t vcap) {
+                                                              uint32_t* stamps_all, uint32_t* gbits_all,
+                                                              uint32_t* keys_all, uint64_t n, uint64_t k, uint32_t G,
+                                                              uint64_t vcap) {
   const int b = blockIdx.y;
   CloudCtl& c = ctl[b];
   if (__hip_atomic_load(&c.state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != kSearching) return;
-  __shared__ uint32_t table[kHashSlots];
+  __shared__ T sp[3 * kPassPts];
+  __shared__ uint32_t table[kHashSlots];  // LDS bitmap (small grids) or hash table
   __shared__ uint32_t scratch[16];
   __shared__ uint32_t last;
-  for (int i = threadIdx.x; i < kHashSlots; i += blockDim.x) table[i] = kInvalid;
-  __syncthreads();
   const uint64_t chunk = n / kWorkers;       // pcl_worker range, normal_distributions.c:34-35
   const uint64_t n8 = chunk * kWorkers;      // the n % 8 tail is never estimated
   const T* p = pts + (uint64_t)b * n * 3;
   uint32_t* stamps = stamps_all + (uint64_t)b * vcap;
   const uint32_t stamp = c.stamp;
+  const uint32_t parity = c.iter & 1u;
+  uint32_t* gbits = gbits_all + ((uint64_t)b * 2 + parity) * kBitsWords;
+  const bool small = c.V <= (uint64_t)kBitsCap;
+  const uint32_t words = small ? (uint32_t)((c.V + 31) / 32) : 0u;
   const uint64_t start = (uint64_t)blockIdx.x * kPassPts;
-  const uint64_t end = start + kPassPts < n8 ? start + kPassPts : n8;
+  const uint32_t cnt = start < n8 ? (uint32_t)(n8 - start < (uint64_t)kPassPts ? n8 - start : kPassPts) : 0u;
+#pragma unroll
+  for (int j = 0; j < 3 * kPassPPT; j++) {
+    const uint32_t f = threadIdx.x + kPassThreads * j;
+    if (f < 3 * cnt) sp[f] = p[3 * start + f];
+  }
+  if (small) {
+    for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) table[w] = 0;
+  } else {
+    for (int i = threadIdx.x; i < kHashSlots; i += blockDim.x) table[i] = kInvalid;
+  }
+  __syncthreads();
+  const double vs = c.guess, inv_vs = 1.0 / vs;
   uint32_t fresh = 0;
-  if (start < end)
-    fresh = mark_points(p, start, end, chunk, c, stamps, stamp, table, true, c.first_bad, nullptr);
+#pragma unroll
+  for (int q = 0; q < kPassPPT; q++) {
+    const uint32_t il = threadIdx.x + kPassThreads * q;
+    if (il >= cnt) continue;
+    const uint64_t i = start + il;
+    const uint32_t key = voxel_key((double)sp[3 * il], (double)sp[3 * il + 1], (double)sp[3 * il + 2], c.off, c.len,
+                                   vs, inv_vs);
+    keys_all[(uint64_t)b * n + i] = key;
+    if (key == kInvalid) {
+      atomicMin(&c.first_bad[i / chunk], (uint32_t)i);
+    } else if (small) {
+      atomicOr(&table[key >> 5], 1u << (key & 31));
+    } else {
+      fresh += stamp_key(key, table, stamps, stamp);
+    }
+  }
+  if (small) {
+    __syncthreads();
+    for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) {
+      const uint32_t bits = table[w];
+      if (bits) fresh += __popc(bits & ~atomicOr(&gbits[w], bits));
+    }
+  }
   fresh = block_sum_u32(fresh, scratch);
+  if (threadIdx.x == 0 && fresh) atomicAdd(&c.count, fresh);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   if (threadIdx.x == 0) {
-    if (fresh) atomicAdd(&c.count, fresh);
     __atomic_thread_fence(__ATOMIC_RELEASE);
-    uint32_t t = __hip_atomic_fetch_add(&c.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t t = __hip_atomic_fetch_add(&c.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     last = (t == G - 1);
   }
   __syncthreads();
@@ -420,11 +478,18 @@ __global__ void __launch_bounds__(kPassThreads) k_search_pass(const T* __restric
   }
   __syncthreads();
   uint32_t count;
+  uint32_t mode = small ? parity : 2u;
   if (any_bad) {
     const uint32_t stamp2 = c.epoch * 32u + 16u + c.iter;
-    uint32_t f = mark_points(p, 0, n8, chunk, c, stamps, stamp2, nullptr, false, nullptr, cut);
+    uint32_t f = 0;
+    for (uint64_t i = threadIdx.x; i < n8; i += blockDim.x) {
+      if (i >= cut[i / chunk]) continue;
+      const uint32_t key = keys_all[(uint64_t)b * n + i];
+      if (key != kInvalid) f += stamp_key(key, nullptr, stamps, stamp2);
+    }
     count = block_sum_u32(f, scratch);
     if (threadIdx.x == 0) c.stamp = stamp2;
+    mode = 2u;
   } else {
     count = __hip_atomic_load(&c.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -432,22 +497,54 @@ __global__ void __launch_bounds__(kPassThreads) k_search_pass(const T* __restric
   if (threadIdx.x == 0) {
     c.count = 0;
     c.arrive = 0;
-    finish_pass(c, count, k, vcap);
+    finish_pass(c, count, k, vcap, mode);
+  }
+  __syncthreads();
+  if (c.state == kSearching && c.V <= (uint64_t)kBitsCap) {  // clear the next pass's bitmap
+    uint32_t* gb = gbits_all + ((uint64_t)b * 2 + (c.iter & 1u)) * kBitsWords;
+    for (uint32_t w = threadIdx.x; w < (uint32_t)((c.V + 31) / 32); w += blockDim.x) gb[w] = 0;
   }
 }
 
 // Occupied voxels of the accepted grid -> dense ids in ascending linear order.
-__global__ void __launch_bounds__(1024) k_dense(CloudCtl* ctl, const uint32_t* stamps_all, uint32_t* dense_all,
-                                                uint32_t* vox_all, uint64_t vcap, uint32_t ndcap) {
+__global__ void __launch_bounds__(1024) k_dense(CloudCtl* ctl, const uint32_t* stamps_all,
+                                                const uint32_t* gbits_all, uint32_t* dense_all, uint32_t* vox_all,
+                                                uint64_t vcap, uint32_t ndcap) {
   const int b = blockIdx.x;
   const CloudCtl& c = ctl[b];
   if (c.state != kAccepted) return;
   __shared__ uint32_t scratch[16];
-  const uint32_t* st = stamps_all + (uint64_t)b * vcap;
   uint32_t* dense = dense_all + (uint64_t)b * vcap;
   uint32_t* vox = vox_all + (uint64_t)b * ndcap;
-  const uint32_t stamp = c.accepted_stamp;
   const uint64_t V = c.V;
+  if (c.acc_mode < 2) {  // the pass's occupancy bitmap: one word per thread
+    const uint32_t* gb = gbits_all + ((uint64_t)b * 2 + c.acc_mode) * kBitsWords;
+    const uint32_t words = (uint32_t)((V + 31) / 32);
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < words; base += blockDim.x) {
+      const uint32_t w = base + threadIdx.x;
+      const uint32_t bits = w < words ? gb[w] : 0u;
+      uint32_t tot;
+      uint32_t d = carry + block_excl_scan((uint32_t)__popc(bits), 0u, AddU32(), scratch, tot);
+      if (w < words) {
+        for (int j = 0; j < 32; j++) {
+          const uint64_t v = 32ull * w + j;
+          if (v >= V) break;
+          if ((bits >> j) & 1u) {
+            dense[v] = d;
+            if (d < ndcap) vox[d] = (uint32_t)v;
+            d++;
+          } else {
+            dense[v] = kInvalid;
+          }
+        }
+      }
+      carry += tot;
+    }
+    return;
+  }
+  const uint32_t* st = stamps_all + (uint64_t)b * vcap;
+  const uint32_t stamp = c.accepted_stamp;
   uint32_t carry = 0;
   for (uint64_t base = 0; base < V; base += blockDim.x) {
     const uint64_t v = base + threadIdx.x;
@@ -463,44 +560,102 @@ __global__ void __launch_bounds__(1024) k_dense(CloudCtl* ctl, const uint32_t* s
   }
 }
 
-// Per chunk of kChunk points: dense id of each point (kInvalid when the
-// reference would not estimate it), stable sort by (dense id, index) in LDS,
-// then the sorted coordinates and a (start, count) table per dense id.
-template <typename T>
-__global__ void __launch_bounds__(kChunkThreads) k_chunk_sort(const T* __restrict__ pts, const int32_t* __restrict__ lbl,
-                                                              const CloudCtl* ctl, const uint32_t* dense_all,
-                                                              double* cpts_all, uint16_t* clbl_all, uint2* ctab_all,
-                                                              uint64_t n, uint64_t vcap, uint32_t ndcap,
-                                                              uint32_t nchunks) {
+// --- binning of the accepted pass: points grouped by ND, in index order ---
+//
+// k_bin_count   per 1024-point chunk: dense id of every point the reference
+//               estimates (kInvalid past a worker's cut-off or the n % 8 tail)
+//               and the chunk's histogram over NDs
+// k_bin_offsets per ND: its base (prefix over NDs) and its start within every
+//               chunk (prefix over chunks): a stable counting sort
+// k_bin_scatter per chunk: stable rank within the chunk (LDS bitonic sort of
+//               (id, index)), points written to their ND's contiguous run
+constexpr int kBinPts = 1024;
+constexpr int kBinThreads = 256;
+
+__global__ void __launch_bounds__(kBinThreads) k_bin_count(const CloudCtl* ctl, const uint32_t* __restrict__ keys_all,
+                                                           const uint32_t* __restrict__ dense_all, uint32_t* did_all,
+                                                           uint32_t* counts_all, uint64_t n, uint64_t vcap,
+                                                           uint32_t ndcap, uint32_t nbins) {
   const int b = blockIdx.y, ch = blockIdx.x;
   const CloudCtl& c = ctl[b];
   if (c.state != kAccepted) return;
-  __shared__ uint32_t skey[kChunk];
-  const uint64_t chunk = n / kWorkers;
-  const uint64_t n8 = chunk * kWorkers;
-  const T* p = pts + (uint64_t)b * n * 3;
+  extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+  const uint32_t nd = c.num_nds;
+  for (uint32_t d = threadIdx.x; d < nd; d += blockDim.x) hist[d] = 0;
+  __syncthreads();
+  const uint64_t chunk = n / kWorkers, n8 = chunk * kWorkers;
   const uint32_t* dense = dense_all + (uint64_t)b * vcap;
-  const double vs = c.vs, inv_vs = 1.0 / vs;
-  const uint64_t base = (uint64_t)ch * kChunk;
-  for (int t = threadIdx.x; t < kChunk; t += blockDim.x) {
-    const uint64_t i = base + t;
-    uint32_t key = kInvalid;
+  const uint64_t base = (uint64_t)ch * kBinPts;
+#pragma unroll
+  for (int q = 0; q < kBinPts / kBinThreads; q++) {
+    const uint64_t i = base + threadIdx.x + kBinThreads * q;
+    if (i >= n) continue;
+    uint32_t d = kInvalid;
     if (i < n8 && i < c.first_bad[i / chunk]) {
-      double x[3];
-      load_point(p, i, x);
-      const uint32_t lin = voxel_key(x[0], x[1], x[2], c.off, c.len, vs, inv_vs);
-      if (lin != kInvalid) {
-        const uint32_t d = dense[lin];
-        if (d != kInvalid) key = (d << 12) | (uint32_t)t;
-      }
+      const uint32_t key = keys_all[(uint64_t)b * n + i];
+      if (key != kInvalid) d = dense[key];
     }
-    skey[t] = key;
+    did_all[(uint64_t)b * n + i] = d;
+    if (d != kInvalid) atomicAdd(&hist[d], 1u);
   }
   __syncthreads();
-  // bitonic sort, ascending (keys are unique except kInvalid padding)
-  for (int size = 2; size <= kChunk; size <<= 1) {
+  uint32_t* row = counts_all + ((uint64_t)b * nbins + ch) * ndcap;
+  for (uint32_t d = threadIdx.x; d < nd; d += blockDim.x) row[d] = hist[d];
+}
+
+__global__ void __launch_bounds__(1024) k_bin_offsets(const CloudCtl* ctl, uint32_t* counts_all, uint32_t* nd_n,
+                                                      uint32_t* nd_base, uint32_t ndcap, uint32_t nbins) {
+  const int b = blockIdx.x;
+  const CloudCtl& c = ctl[b];
+  if (c.state != kAccepted) return;
+  __shared__ uint32_t scratch[16];
+  const uint32_t nd = c.num_nds;
+  uint32_t* cnt = counts_all + (uint64_t)b * nbins * ndcap;
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < nd; base += blockDim.x) {
+    const uint32_t d = base + threadIdx.x;
+    uint32_t tot_d = 0;
+    if (d < nd)
+      for (uint32_t ch = 0; ch < nbins; ch++) tot_d += cnt[(uint64_t)ch * ndcap + d];
+    uint32_t tot;
+    const uint32_t start = carry + block_excl_scan(tot_d, 0u, AddU32(), scratch, tot);
+    if (d < nd) {
+      nd_n[(uint64_t)b * ndcap + d] = tot_d;
+      nd_base[(uint64_t)b * ndcap + d] = start;
+      uint32_t run = start;
+      for (uint32_t ch = 0; ch < nbins; ch++) {
+        const uint32_t x = cnt[(uint64_t)ch * ndcap + d];
+        cnt[(uint64_t)ch * ndcap + d] = run;
+        run += x;
+      }
+    }
+    carry += tot;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBinThreads) k_bin_scatter(const T* __restrict__ pts, const int32_t* __restrict__ lbl,
+                                                             const CloudCtl* ctl, const uint32_t* __restrict__ did_all,
+                                                             const uint32_t* __restrict__ offs_all, T* nd_pts,
+                                                             uint16_t* nd_lbl, uint64_t n, uint32_t ndcap,
+                                                             uint32_t nbins) {
+  const int b = blockIdx.y, ch = blockIdx.x;
+  const CloudCtl& c = ctl[b];
+  if (c.state != kAccepted) return;
+  __shared__ uint32_t skey[kBinPts];
+  __shared__ uint32_t scratch[16];
+  const uint64_t base = (uint64_t)ch * kBinPts;
+#pragma unroll
+  for (int q = 0; q < kBinPts / kBinThreads; q++) {
+    const uint32_t t = threadIdx.x + kBinThreads * q;
+    const uint64_t i = base + t;
+    const uint32_t d = i < n ? did_all[(uint64_t)b * n + i] : kInvalid;
+    skey[t] = d == kInvalid ? kInvalid : (d << 10) | t;
+  }
+  __syncthreads();
+  for (int size = 2; size <= kBinPts; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int t = threadIdx.x; t < kChunk / 2; t += blockDim.x) {
+      for (int t = threadIdx.x; t < kBinPts / 2; t += blockDim.x) {
         const int lo = 2 * t - (t & (stride - 1));
         const int hi = lo + stride;
         const bool up = (lo & size) == 0;
@@ -510,71 +665,85 @@ __global__ void __launch_bounds__(kChunkThreads) k_chunk_sort(const T* __restric
       __syncthreads();
     }
   }
-  uint2* tab = ctab_all + ((uint64_t)b * nchunks + ch) * ndcap;
-  const uint32_t nd = c.num_nds;
-  for (uint32_t d = threadIdx.x; d < nd; d += blockDim.x) tab[d] = make_uint2(0, 0);
-  __syncthreads();
-  double* cp = cpts_all + ((uint64_t)b * nchunks + ch) * kChunk * 3;
-  uint16_t* cl = clbl_all ? clbl_all + ((uint64_t)b * nchunks + ch) * kChunk : nullptr;
-  for (int s = threadIdx.x; s < kChunk; s += blockDim.x) {
+  // rank within the run of equal ids: position - first position of the run
+  const uint32_t* offs = offs_all + ((uint64_t)b * nbins + ch) * ndcap;
+  const T* p = pts + (uint64_t)b * n * 3;
+  uint32_t run_carry = 0;
+#pragma unroll
+  for (int q = 0; q < kBinPts / kBinThreads; q++) {
+    const uint32_t s = threadIdx.x + kBinThreads * q;  // consecutive per pass: a block scan of run starts
     const uint32_t key = skey[s];
+    const bool head = key != kInvalid && (s == 0 || (skey[s - 1] >> 10) != (key >> 10));
+    uint32_t tot;
+    // max-scan of run heads via an exclusive scan of (head ? s : 0) with max
+    uint32_t hs = head ? s + 1 : 0u;
+    uint32_t x = wave_incl_scan(hs, [](uint32_t a, uint32_t bb) { return a > bb ? a : bb; });
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 63) scratch[wid] = x;
+    __syncthreads();
+    uint32_t pre = run_carry;
+    for (int w2 = 0; w2 < wid; w2++) pre = pre > scratch[w2] ? pre : scratch[w2];
+    tot = run_carry;
+    for (int w2 = 0; w2 < (int)(blockDim.x >> 6); w2++) tot = tot > scratch[w2] ? tot : scratch[w2];
+    __syncthreads();
+    const uint32_t head_pos = (x > pre ? x : pre) - 1;  // last run head at or before s
+    run_carry = tot;
     if (key == kInvalid) continue;
-    const uint32_t d = key >> 12, t = key & 0xfff;
-    double x[3];
-    load_point(p, base + t, x);
-    cp[3 * s + 0] = x[0];
-    cp[3 * s + 1] = x[1];
-    cp[3 * s + 2] = x[2];
-    if (cl) cl[s] = (uint16_t)lbl[(uint64_t)b * n + base + t];
-    if (s == 0 || (skey[s - 1] >> 12) != d) tab[d].x = (uint32_t)s;  // run start
-  }
-  __syncthreads();
-  for (int s = threadIdx.x; s < kChunk; s += blockDim.x) {
-    const uint32_t key = skey[s];
-    if (key == kInvalid) continue;
-    const uint32_t d = key >> 12;
-    const bool run_end = (s + 1 == kChunk) || skey[s + 1] == kInvalid || (skey[s + 1] >> 12) != d;
-    if (run_end) tab[d].y = (uint32_t)s + 1 - tab[d].x;
+    const uint32_t d = key >> 10, t = key & 1023;
+    const uint32_t dst = offs[d] + (s - head_pos);
+    const uint64_t i = base + t;
+    T* o = nd_pts + ((uint64_t)b * n + dst) * 3;
+    o[0] = p[3 * i + 0];
+    o[1] = p[3 * i + 1];
+    o[2] = p[3 * i + 2];
+    if (nd_lbl) nd_lbl[(uint64_t)b * n + dst] = (uint16_t)lbl[(uint64_t)b * n + i];
   }
 }
 
-// One lane per ND: sequential Welford over its points in index order.
-__global__ void __launch_bounds__(256) k_welford(const CloudCtl* ctl, const double* __restrict__ cpts_all,
-                                                 const uint16_t* __restrict__ clbl_all, const uint2* __restrict__ ctab_all,
-                                                 uint32_t* nd_n, double* nd_mean, double* nd_cov, uint16_t* nd_cls,
-                                                 uint32_t* hist_all, int ncls, uint32_t ndcap, uint32_t nchunks) {
+// One lane per ND: sequential Welford over its contiguous, index-ordered points
+// (normal_distributions.c:75-121), bit-exact; loads run 8 points ahead.
+template <typename T>
+__global__ void __launch_bounds__(256) k_welford(const CloudCtl* ctl, const T* __restrict__ nd_pts,
+                                                 const uint16_t* __restrict__ nd_lbl, const uint32_t* nd_n,
+                                                 const uint32_t* nd_base, double* nd_mean, double* nd_cov,
+                                                 uint16_t* nd_cls, uint32_t* hist_all, int ncls, uint64_t n,
+                                                 uint32_t ndcap) {
   const int b = blockIdx.y;
   const CloudCtl& c = ctl[b];
   if (c.state != kAccepted) return;
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= c.num_nds) return;
+  const uint64_t o = (uint64_t)b * ndcap + d;
+  const uint32_t cnt = nd_n[o];
+  const T* q = nd_pts + ((uint64_t)b * n + nd_base[o]) * 3;
   Welford w;
   welford_init(w);
-  const uint64_t cb = (uint64_t)b * nchunks;
-  uint32_t* hist = clbl_all ? hist_all + ((uint64_t)b * ndcap + d) * (uint32_t)(ncls + 1) : nullptr;
-  if (hist)
-    for (int j = 0; j <= ncls; j++) hist[j] = 0;
-  for (uint32_t ch = 0; ch < nchunks; ch++) {
-    const uint2 se = ctab_all[(cb + ch) * ndcap + d];
-    const double* cp = cpts_all + (cb + ch) * kChunk * 3;
-    for (uint32_t j = 0; j < se.y; j++) {
-      double x[3];
-      x[0] = cp[3 * (se.x + j) + 0];
-      x[1] = cp[3 * (se.x + j) + 1];
-      x[2] = cp[3 * (se.x + j) + 2];
-      welford_update(w, x);
-      if (hist) {
-        const uint32_t l = clbl_all[(cb + ch) * kChunk + se.x + j];
-        if (l <= (uint32_t)ncls) hist[l]++;
+  constexpr int U = 8;
+  T cur[3 * U], nxt[3 * U];
+#pragma unroll
+  for (int j = 0; j < 3 * U; j++) cur[j] = (uint32_t)j < 3 * cnt ? q[j] : T(0);
+  for (uint32_t s = 0; s < cnt; s += U) {
+#pragma unroll
+    for (int j = 0; j < 3 * U; j++) nxt[j] = 3 * (s + U) + j < 3 * cnt ? q[3 * (s + U) + j] : T(0);
+#pragma unroll
+    for (int j = 0; j < U; j++) {
+      if (s + j < cnt) {
+        const double x[3] = {(double)cur[3 * j], (double)cur[3 * j + 1], (double)cur[3 * j + 2]};
+        welford_update(w, x);
       }
     }
+#pragma unroll
+    for (int j = 0; j < 3 * U; j++) cur[j] = nxt[j];
   }
-  const uint64_t o = (uint64_t)b * ndcap + d;
-  nd_n[o] = (uint32_t)w.n;
   for (int j = 0; j < 3; j++) nd_mean[3 * o + j] = w.mean[j];
   for (int j = 0; j < 9; j++) nd_cov[9 * o + j] = w.cov[j];
   uint16_t cls = 0;
-  if (hist) {  // first index of the max count (normal_distributions.c:107-121)
+  if (nd_lbl) {  // class histogram, first index of the max (normal_distributions.c:107-121)
+    uint32_t* hist = hist_all + o * (uint32_t)(ncls + 1);
+    for (int j = 0; j <= ncls; j++) hist[j] = 0;
+    const uint16_t* l = nd_lbl + (uint64_t)b * n + nd_base[o];
+    for (uint32_t s = 0; s < cnt; s++)
+      if (l[s] <= (uint32_t)ncls) hist[l[s]]++;
     uint32_t best = 0;
     for (int j = 0; j <= ncls; j++)
       if (hist[j] > best) { best = hist[j]; cls = (uint16_t)j; }
@@ -838,6 +1007,114 @@ __device__ void pad_class_rows(const KLArgs& A, int b, uint64_t k) {
   for (uint64_t r = c.num_out + threadIdx.x; r < k; r += blockDim.x) A.out_cls[w * ((uint64_t)b * k + r)] = 1.0f;
 }
 
+// Event order of one ND's in-place LU chain: the mutating events
+// it takes part in, by ascending key 6 * dense(v) + d.  Neighbours below it
+// (Z-, Y-, X-: smaller linear index) come first, as q; then its own six
+// directions, as p; then the neighbours above (X+, Y+, Z+), as q.  So the
+// chain position of an event is a popcount over a 12-slot mask:
+//   slot 0 Z-(q), 1 Y-(q), 2 X-(q), 3..8 own d = 0..5 (p), 9 X+(q), 10 Y+(q), 11 Z+(q)
+__device__ inline uint32_t chain_mask(uint32_t e) {  // e: 6 eligible-direction bits
+  return ((e >> 5) & 1u) | (((e >> 3) & 1u) << 1) | (((e >> 1) & 1u) << 2) | ((e & 0x3fu) << 3) |
+         ((e & 1u) << 9) | (((e >> 2) & 1u) << 10) | (((e >> 4) & 1u) << 11);
+}
+__device__ inline uint32_t qslot_of_dir(uint32_t d) {  // q-slot of the neighbour in direction d
+  return (0x0b1a29u >> (4 * d)) & 0xfu;  // {d0: 9, d1: 2, d2: 10, d3: 1, d4: 11, d5: 0}
+}
+
+// Neighbours, chain masks and LU chains, one lane per ND.
+__global__ void __launch_bounds__(256) k_kl_chains(KLArgs A) {
+  const int b = blockIdx.y;
+  const CloudCtl& c = A.ctl[b];
+  if (c.state != kAccepted) return;
+  const uint32_t nd = c.num_nds;
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= nd) return;
+  const uint64_t ob = (uint64_t)b * A.ndcap;
+  const uint32_t* dense = A.dense_all + (uint64_t)b * A.vcap;
+  const uint32_t* vn = A.nd_n + ob;
+  const uint32_t lx = c.len[0], ly = c.len[1], lz = c.len[2];
+  const uint32_t lin = A.vox_all[ob + u];
+  const uint32_t z = lin / (lx * ly), y = (lin % (lx * ly)) / lx, x = lin % lx;
+  const uint32_t nu = vn[u];
+  uint32_t elig = 0;
+#pragma unroll
+  for (int d = 0; d < 6; d++) {
+    // voxel.c:116-175, directions X+, X-, Y+, Y-, Z+, Z-
+    const uint32_t xx = x + (d == 0 ? 1u : d == 1 ? ~0u : 0u);
+    const uint32_t yy = y + (d == 2 ? 1u : d == 3 ? ~0u : 0u);
+    const uint32_t zz = z + (d == 4 ? 1u : d == 5 ? ~0u : 0u);
+    int32_t w = -1;
+    if (xx < lx && yy < ly && zz < lz) {
+      const uint32_t dn = dense[zz * lx * ly + yy * lx + xx];
+      if (dn != kInvalid) w = (int32_t)dn;
+    }
+    A.nb_all[6 * ob + 6 * u + d] = w;
+    if (w >= 0 && nu > 1 && vn[w] > 1) elig |= 1u << d;
+  }
+  const uint32_t mask = chain_mask(elig);
+  const int T = __popc(mask);
+  double S[9];
+#pragma unroll
+  for (int j = 0; j < 9; j++) S[j] = A.nd_cov[9 * (ob + u) + j];
+  double* chain = A.chain_all + 108 * (ob + u);
+  uint32_t* ps = A.chain_ps_all + 12 * (ob + u);
+  for (int t = 0; t < T; t++) {
+    uint32_t perm;
+    int sg;
+    lu3(S, perm, sg);
+#pragma unroll
+    for (int j = 0; j < 9; j++) chain[9 * t + j] = S[j];
+    ps[t] = perm | (sg < 0 ? 0x100u : 0u);
+  }
+  A.nkeys_all[ob + u] = mask;
+#pragma unroll
+  for (int j = 0; j < 9; j++) A.nd_cov_post[9 * (ob + u) + j] = S[j];
+}
+
+// KL score of every (voxel, direction) slot (kullback_leibler.c:28-127, 141-180).
+__global__ void __launch_bounds__(256) k_kl_events(KLArgs A) {
+  const int b = blockIdx.y;
+  const CloudCtl& c = A.ctl[b];
+  if (c.state != kAccepted) return;
+  const uint32_t nd = c.num_nds;
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= 6 * nd) return;
+  const uint64_t ob = (uint64_t)b * A.ndcap, eb = (uint64_t)b * A.ecap;
+  const uint32_t u = s / 6, d = s % 6;
+  const uint32_t* vn = A.nd_n + ob;
+  const int32_t w = A.nb_all[6 * ob + s];
+  uint32_t flag = 0;
+  double val = 0.0;
+  if (w >= 0) {
+    if (vn[u] <= 1 || vn[w] <= 1) {
+      flag = 1;  // kl_divergence returns -1 with div 0 and the entry is kept
+    } else {
+      const uint32_t mu = A.nkeys_all[ob + u], mw = A.nkeys_all[ob + (uint32_t)w];
+      const int rp = __popc(mu & ((1u << (3 + d)) - 1u));
+      const int rq = __popc(mw & ((1u << qslot_of_dir(d ^ 1u)) - 1u));
+      const double* LUp = A.chain_all + 108 * (ob + u) + 9 * rp;
+      const double* LUq = A.chain_all + 108 * (ob + (uint32_t)w) + 9 * rq;
+      const uint32_t psp = A.chain_ps_all[12 * (ob + u) + rp], psq = A.chain_ps_all[12 * (ob + (uint32_t)w) + rq];
+      const int sp = (psp & 0x100) ? -1 : 1, sq = (psq & 0x100) ? -1 : 1;
+      double Lp[9], Lq[9];
+#pragma unroll
+      for (int j = 0; j < 9; j++) {
+        Lp[j] = LUp[j];
+        Lq[j] = LUq[j];
+      }
+      const double pd = lu3_det(Lp, sp), qd = lu3_det(Lq, sq);
+      if (!(pd == 0 || qd == 0) && lu3_sgndet(Lp, sp) != 0 && lu3_sgndet(Lq, sq) != 0) {
+        flag = 1;
+        val = kl_score(Lp, Lq, psq & 0x3f, pd, qd);
+      }
+    }
+  }
+  A.slot_val_all[eb + s] = val;
+  A.slot_flag_all[eb + s] = flag;
+}
+
+// The reference's insertion order, the prune and the output rows: one
+// workgroup per cloud.
 __global__ void __launch_bounds__(kKLThreads) k_kl(KLArgs A) {
   const int b = blockIdx.x;
   CloudCtl& c = A.ctl[b];
@@ -855,99 +1132,10 @@ __global__ void __launch_bounds__(kKLThreads) k_kl(KLArgs A) {
   }
   const uint32_t nd = c.num_nds;
   const uint64_t ob = (uint64_t)b * A.ndcap, eb = (uint64_t)b * A.ecap;
-  const uint32_t* vox = A.vox_all + ob;
-  const uint32_t* dense = A.dense_all + (uint64_t)b * A.vcap;
-  const uint32_t* vn = A.nd_n + ob;
-  int32_t* nb = A.nb_all + 6 * ob;
-  uint32_t* keys = A.keys_all + 12 * ob;
-  uint32_t* nkeys = A.nkeys_all + ob;
-  double* chain = A.chain_all + 108 * ob;
-  uint32_t* chain_ps = A.chain_ps_all + 12 * ob;
-  const uint32_t lx = c.len[0], ly = c.len[1], lz = c.len[2];
-  // -- neighbours (voxel.c:116-175, directions X+,X-,Y+,Y-,Z+,Z-)
-  for (uint32_t u = threadIdx.x; u < nd; u += blockDim.x) {
-    const uint32_t lin = vox[u];
-    const uint32_t z = lin / (lx * ly), y = (lin % (lx * ly)) / lx, x = lin % lx;
-    const int dx[6] = {1, -1, 0, 0, 0, 0}, dy[6] = {0, 0, 1, -1, 0, 0}, dz[6] = {0, 0, 0, 0, 1, -1};
-    for (int d = 0; d < 6; d++) {
-      const uint32_t xx = x + (uint32_t)dx[d], yy = y + (uint32_t)dy[d], zz = z + (uint32_t)dz[d];
-      int32_t w = -1;
-      if (xx < lx && yy < ly && zz < lz) {
-        const uint32_t dn = dense[zz * lx * ly + yy * lx + xx];
-        if (dn != kInvalid) w = (int32_t)dn;
-      }
-      nb[6 * u + d] = w;
-    }
-  }
-  __syncthreads();
-  // -- per ND: the sorted keys (6 v + d) of the mutating events it takes part in,
-  //    and its chain of in-place LU factorisations
-  for (uint32_t u = threadIdx.x; u < nd; u += blockDim.x) {
-    uint32_t kk[12];
-    int T = 0;
-    const uint32_t nu = vn[u];
-    if (nu > 1) {
-      for (int d = 0; d < 6; d++) {
-        const int32_t w = nb[6 * u + d];
-        if (w < 0 || vn[w] <= 1) continue;
-        kk[T++] = 6 * u + d;                 // u as p
-        kk[T++] = 6 * (uint32_t)w + (d ^ 1); // u as q of w's opposite direction
-      }
-    }
-    for (int i = 1; i < T; i++) {  // insertion sort
-      const uint32_t v = kk[i];
-      int j = i - 1;
-      while (j >= 0 && kk[j] > v) { kk[j + 1] = kk[j]; j--; }
-      kk[j + 1] = v;
-    }
-    double S[9];
-    for (int j = 0; j < 9; j++) S[j] = A.nd_cov[9 * (ob + u) + j];
-    for (int t = 0; t < T; t++) {
-      uint32_t perm;
-      int sg;
-      lu3(S, perm, sg);
-      for (int j = 0; j < 9; j++) chain[108 * u + 9 * t + j] = S[j];
-      chain_ps[12 * u + t] = perm | (sg < 0 ? 0x100u : 0u);
-      keys[12 * u + t] = kk[t];
-    }
-    nkeys[u] = (uint32_t)T;
-    for (int j = 0; j < 9; j++) A.nd_cov_post[9 * (ob + u) + j] = S[j];
-  }
-  __syncthreads();
-  // -- events, one per (voxel, direction) slot (kullback_leibler.c:141-180)
-  double* slot_val = A.slot_val_all + eb;
-  uint32_t* slot_flag = A.slot_flag_all + eb;
+  const int32_t* nb = A.nb_all + 6 * ob;
+  const double* slot_val = A.slot_val_all + eb;
+  const uint32_t* slot_flag = A.slot_flag_all + eb;
   const uint32_t nslots = 6 * nd;
-  for (uint32_t s = threadIdx.x; s < nslots; s += blockDim.x) {
-    const uint32_t u = s / 6, d = s % 6;
-    const int32_t w = nb[6 * u + d];
-    uint32_t flag = 0;
-    double val = 0.0;
-    if (w >= 0) {
-      if (vn[u] <= 1 || vn[w] <= 1) {
-        flag = 1;  // kl_divergence returns -1 with div 0 and the entry is kept
-      } else {
-        const uint32_t key = 6 * u + d;
-        int rp = 0, rq = 0;
-        while (keys[12 * u + rp] != key) rp++;
-        while (keys[12 * (uint32_t)w + rq] != key) rq++;
-        const double* LUp = chain + 108 * u + 9 * rp;
-        const double* LUq = chain + 108 * (uint32_t)w + 9 * rq;
-        const uint32_t psp = chain_ps[12 * u + rp], psq = chain_ps[12 * (uint32_t)w + rq];
-        const int sp = (psp & 0x100) ? -1 : 1, sq = (psq & 0x100) ? -1 : 1;
-        double Lp[9], Lq[9];
-        for (int j = 0; j < 9; j++) { Lp[j] = LUp[j]; Lq[j] = LUq[j]; }
-        const double pd = lu3_det(Lp, sp), qd = lu3_det(Lq, sq);
-        if (!(pd == 0 || qd == 0) && lu3_sgndet(Lp, sp) != 0 && lu3_sgndet(Lq, sq) != 0) {
-          flag = 1;
-          val = kl_score(Lp, Lq, psq & 0x3f, pd, qd);
-        }
-      }
-    }
-    slot_val[s] = val;
-    slot_flag[s] = flag;
-  }
-  __syncthreads();
   // -- compaction into enumeration order; NaN-skipping exclusive prefix min
   double* ev_val = A.ev_val_all + eb;
   uint32_t* ev_p = A.ev_p_all + eb;
@@ -1126,7 +1314,8 @@ static void plan_free(Plan* P) {
   if (!P) return;
   if (P->timing)
     for (int i = 0; i < 7; i++) (void)hipEventDestroy(P->ev[i]);
-  void* bufs[] = {P->ctl, P->stamps, P->dense_of, P->vox, P->chunk_pts, P->chunk_lbl, P->chunk_tab, P->nd_n,
+  void* bufs[] = {P->ctl, P->stamps, P->dense_of, P->vox, P->gbits, P->pkeys, P->did, P->bin_cnt, P->nd_base,
+                  P->nd_pts, P->nd_lbl, P->nd_n,
                   P->nd_mean, P->nd_cov, P->nd_cov_post, P->nd_cls, P->hist, P->nb, P->keys, P->nkeys,
                   P->chain, P->chain_ps, P->slot_val, P->slot_flag, P->ev_val, P->ev_p, P->ev_q, P->ev_min,
                   P->sort_key, P->sort_idx, P->nan_list, P->nan_pos, P->ord_val, P->ord_p, P->ord_q,
@@ -1192,27 +1381,33 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
   if (lbl && P->ncls < 0) return NDNET_ERR_ARG;
   if (P->timing) HIPCHK(hipEventRecord(P->ev[0], st));
   k_reset<<<(B + 63) / 64, 64, 0, st>>>(P->ctl, B);
-  const uint32_t Gl = (uint32_t)((n + 4095) / 4096);
+  const uint32_t Gl = (uint32_t)((3 * n + 256 * kLimPPT - 1) / (256 * kLimPPT));
   // stamps are epoch * 32 + pass; the device epoch wraps to 1 after 2^26 - 1 calls
   if (++P->calls % ((1u << 26) - 1) == 0)
     HIPCHK(hipMemsetAsync(P->stamps, 0, (size_t)B * P->vcap * sizeof(uint32_t), st));
-  k_limits<T><<<dim3(Gl, B), 256, 0, st>>>(pts, P->ctl, n, Gl, P->vcap);
+  k_limits<T><<<dim3(Gl, B), 256, 0, st>>>(pts, P->ctl, P->gbits, n, Gl, P->vcap);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[1], st));
   for (int it = 0; it < kMaxIters; it++)
-    k_search_pass<T><<<dim3(P->G, B), kPassThreads, 0, st>>>(pts, P->ctl, P->stamps, n, P->k, P->G, P->vcap);
+    k_search_pass<T><<<dim3(P->G, B), kPassThreads, 0, st>>>(pts, P->ctl, P->stamps, P->gbits, P->pkeys, n, P->k,
+                                                              P->G, P->vcap);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[2], st));
-  k_dense<<<B, 1024, 0, st>>>(P->ctl, P->stamps, P->dense_of, P->vox, P->vcap, P->ndcap);
+  k_dense<<<B, 1024, 0, st>>>(P->ctl, P->stamps, P->gbits, P->dense_of, P->vox, P->vcap, P->ndcap);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[3], st));
-  k_chunk_sort<T><<<dim3(P->nchunks, B), kChunkThreads, 0, st>>>(
-      pts, lbl, P->ctl, P->dense_of, (double*)P->chunk_pts, lbl ? P->chunk_lbl : nullptr, P->chunk_tab, n, P->vcap,
-      P->ndcap, P->nchunks);
+  k_bin_count<<<dim3(P->nbins, B), kBinThreads, P->ndcap * sizeof(uint32_t), st>>>(
+      P->ctl, P->pkeys, P->dense_of, P->did, P->bin_cnt, n, P->vcap, P->ndcap, P->nbins);
+  k_bin_offsets<<<B, 1024, 0, st>>>(P->ctl, P->bin_cnt, P->nd_n, P->nd_base, P->ndcap, P->nbins);
+  k_bin_scatter<T><<<dim3(P->nbins, B), kBinThreads, 0, st>>>(pts, lbl, P->ctl, P->did, P->bin_cnt,
+                                                               (T*)P->nd_pts, lbl ? P->nd_lbl : nullptr, n,
+                                                               P->ndcap, P->nbins);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[4], st));
-  k_welford<<<dim3((P->ndcap + 255) / 256, B), 256, 0, st>>>(P->ctl, (const double*)P->chunk_pts,
-                                                              lbl ? P->chunk_lbl : nullptr, P->chunk_tab, P->nd_n,
-                                                              P->nd_mean, P->nd_cov, P->nd_cls, P->hist, P->ncls,
-                                                              P->ndcap, P->nchunks);
+  k_welford<T><<<dim3((P->ndcap + 255) / 256, B), 256, 0, st>>>(P->ctl, (const T*)P->nd_pts,
+                                                                  lbl ? P->nd_lbl : nullptr, P->nd_n, P->nd_base,
+                                                                  P->nd_mean, P->nd_cov, P->nd_cls, P->hist, P->ncls,
+                                                                  n, P->ndcap);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[5], st));
   KLArgs A = kl_args(P, P->k, out, out_cls, pc64, cov64, cls16);
+  k_kl_chains<<<dim3((P->ndcap + 255) / 256, B), 256, 0, st>>>(A);
+  k_kl_events<<<dim3((6 * P->ndcap + 255) / 256, B), 256, 0, st>>>(A);
   k_kl<<<B, kKLThreads, kl_lds_bytes(), st>>>(A);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[6], st));
   if (stats_dst)
@@ -1245,15 +1440,15 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   uint32_t sc = 1;
   while (sc < P->ecap) sc <<= 1;
   P->sortcap = sc;
-  P->nchunks = (uint32_t)((num_points + kChunk - 1) / kChunk);
+  P->nbins = (uint32_t)((num_points + kBinPts - 1) / kBinPts);
   const uint64_t n8 = (num_points / kWorkers) * kWorkers;
   P->G = (uint32_t)((n8 + kPassPts - 1) / kPassPts);
   if (P->G == 0) P->G = 1;
-  if (P->ndcap >= (1u << 20)) {  // dense ids share a 32-bit sort key with a 12-bit chunk index
+  if (P->ndcap > 16384) {  // per-chunk ND histograms live in LDS (k_bin_count)
     delete P;
     return NDNET_ERR_ARG;
   }
-  const size_t B = (size_t)batch, nd = P->ndcap, ec = P->ecap, nc = P->nchunks;
+  const size_t B = (size_t)batch, nd = P->ndcap, ec = P->ecap, nbn = P->nbins, n = num_points;
   const int nb = num_classes >= 0 ? num_classes + 1 : 1;
   hipError_t e = hipSuccess;
 #define A_(ptr, cnt) \
@@ -1262,9 +1457,13 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   A_(stamps, B * P->vcap);
   A_(dense_of, B * P->vcap);
   A_(vox, B * nd);
-  if (e == hipSuccess) e = hipMalloc(&P->chunk_pts, B * nc * kChunk * 3 * sizeof(double));
-  A_(chunk_lbl, num_classes >= 0 ? B * nc * kChunk : 1);
-  A_(chunk_tab, B * nc * nd);
+  A_(gbits, B * 2 * kBitsWords);
+  A_(pkeys, B * n);
+  A_(did, B * n);
+  A_(bin_cnt, B * nbn * nd);
+  A_(nd_base, B * nd);
+  if (e == hipSuccess) e = hipMalloc(&P->nd_pts, B * n * 3 * sizeof(double));
+  A_(nd_lbl, num_classes >= 0 ? B * n : 1);
   A_(nd_n, B * nd);
   A_(nd_mean, B * nd * 3);
   A_(nd_cov, B * nd * 9);
@@ -1299,6 +1498,8 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   if (e == hipSuccess) e = hipMemset(P->d_stats, 0, B * sizeof(ndnet_ndt_stats));
   if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_kl, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                (int)kl_lds_bytes());
+  if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_bin_count, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)(16384 * sizeof(uint32_t)));
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     fprintf(stderr, "ndnet_amd: plan allocation failed: %s\n", hipGetErrorString(e));
