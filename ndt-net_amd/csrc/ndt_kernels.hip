@@ -181,6 +181,27 @@ __device__ inline T block_excl_scan(T v, T identity, Op op, T* scratch, T& total
   return op(pre, excl_w);
 }
 
+// Exclusive block scan over ITEMS consecutive elements per thread (one
+// barrier round for blockDim * ITEMS elements).  v[j] becomes the exclusive
+// prefix of element j within the round; total is the round's reduction.
+template <int ITEMS, typename T, typename Op>
+__device__ inline void block_scan_items(T (&v)[ITEMS], T identity, Op op, T* scratch, T& total) {
+  T local = identity;
+#pragma unroll
+  for (int j = 0; j < ITEMS; j++) {
+    const T x = v[j];
+    v[j] = local;
+    local = op(local, x);
+  }
+  const T ex = block_excl_scan(local, identity, op, scratch, total);
+#pragma unroll
+  for (int j = 0; j < ITEMS; j++) v[j] = op(ex, v[j]);
+}
+
+struct AddU64 {
+  __device__ unsigned long long operator()(unsigned long long a, unsigned long long b) const { return a + b; }
+};
+
 struct AddU32 {
   __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; }
 };
@@ -251,6 +272,16 @@ __device__ inline void set_guess(CloudCtl& c, double guess, uint64_t vcap) {
   }
 }
 
+// Workgroup arrival ticket of a cloud: true for the last of G arrivals.
+// Everything the workgroups hand to the last one (counts, cut-offs, bitmap
+// and stamp words) is written with device-scope atomics, which the caller has
+// drained (s_waitcnt vmcnt(0) in every wave before the barrier), so the
+// ticket needs no release fence (an L2 write-back per workgroup), and the last
+// workgroup reads those words with atomic loads, so it needs no acquire.
+__device__ inline bool arrive_ticket(uint32_t* arrive, uint32_t G) {
+  return __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
+}
+
 constexpr int kLimPPT = 16;        // flat coordinates per thread in k_limits
 
 // Bounding box (pointclouds.c:40-66) over every point, the n % 8 tail
@@ -270,11 +301,12 @@ __global__ void __launch_bounds__(256) k_limits(const T* __restrict__ pts, Cloud
     const uint64_t f = f0 + 256 * j;
     v[j] = f < nf ? p[f] : T(0);
   }
+  const uint32_t a0 = (uint32_t)(f0 % 3);  // 256 = 1 (mod 3): element j is axis (a0 + j) % 3
 #pragma unroll
   for (int j = 0; j < kLimPPT; j++) {
     const uint64_t f = f0 + 256 * j;
     if (f >= nf) continue;
-    const uint32_t a = (uint32_t)(f % 3);
+    const uint32_t a = (a0 + j) % 3;
     const double x = (double)v[j];
 #pragma unroll
     for (int ax = 0; ax < 3; ax++) {
@@ -305,14 +337,9 @@ __global__ void __launch_bounds__(256) k_limits(const T* __restrict__ pts, Cloud
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   __shared__ uint32_t last;
-  if (threadIdx.x == 0) {
-    __atomic_thread_fence(__ATOMIC_RELEASE);
-    uint32_t t = __hip_atomic_fetch_add(&c.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    last = (t == G - 1);
-  }
+  if (threadIdx.x == 0) last = arrive_ticket(&c.arrive, G);
   __syncthreads();
   if (!last) return;
-  __atomic_thread_fence(__ATOMIC_ACQUIRE);
   if (threadIdx.x == 0) {
     for (int a = 0; a < 6; a++)
       c.lim[a] = ord_unkey(__hip_atomic_load(&c.limkey[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -456,14 +483,9 @@ __global__ void __launch_bounds__(kPassThreads) k_search_pass(const T* __restric
   if (threadIdx.x == 0 && fresh) atomicAdd(&c.count, fresh);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __atomic_thread_fence(__ATOMIC_RELEASE);
-    const uint32_t t = __hip_atomic_fetch_add(&c.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    last = (t == G - 1);
-  }
+  if (threadIdx.x == 0) last = arrive_ticket(&c.arrive, G);
   __syncthreads();
   if (!last) return;
-  __atomic_thread_fence(__ATOMIC_ACQUIRE);
   // Last workgroup of this cloud.  If some point fell outside the grid, its
   // reference worker abandoned the rest of its chunk (normal_distributions.c
   // :47-52): recount with those cut-offs (rare: needs dim/vs integral).
@@ -484,7 +506,9 @@ __global__ void __launch_bounds__(kPassThreads) k_search_pass(const T* __restric
     uint32_t f = 0;
     for (uint64_t i = threadIdx.x; i < n8; i += blockDim.x) {
       if (i >= cut[i / chunk]) continue;
-      const uint32_t key = keys_all[(uint64_t)b * n + i];
+      double x[3];
+      load_point(p, i, x);
+      const uint32_t key = voxel_key(x[0], x[1], x[2], c.off, c.len, vs, inv_vs);
       if (key != kInvalid) f += stamp_key(key, nullptr, stamps, stamp2);
     }
     count = block_sum_u32(f, scratch);
@@ -570,6 +594,7 @@ __global__ void __launch_bounds__(1024) k_dense(CloudCtl* ctl, const uint32_t* s
 // k_bin_scatter per chunk: stable rank within the chunk (LDS bitonic sort of
 //               (id, index)), points written to their ND's contiguous run
 constexpr int kBinPts = 1024;
+constexpr int kNdSlack = 64;  // points of padding after the last cloud's ND runs
 constexpr int kBinThreads = 256;
 
 __global__ void __launch_bounds__(kBinThreads) k_bin_count(const CloudCtl* ctl, const uint32_t* __restrict__ keys_all,
@@ -615,15 +640,35 @@ __global__ void __launch_bounds__(1024) k_bin_offsets(const CloudCtl* ctl, uint3
   for (uint32_t base = 0; base < nd; base += blockDim.x) {
     const uint32_t d = base + threadIdx.x;
     uint32_t tot_d = 0;
-    if (d < nd)
-      for (uint32_t ch = 0; ch < nbins; ch++) tot_d += cnt[(uint64_t)ch * ndcap + d];
+    if (d < nd) {
+      uint32_t part[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      uint32_t ch = 0;
+      for (; ch + 8 <= nbins; ch += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) part[j] += cnt[(uint64_t)(ch + j) * ndcap + d];
+      }
+      for (; ch < nbins; ch++) part[0] += cnt[(uint64_t)ch * ndcap + d];
+#pragma unroll
+      for (int j = 0; j < 8; j++) tot_d += part[j];
+    }
     uint32_t tot;
     const uint32_t start = carry + block_excl_scan(tot_d, 0u, AddU32(), scratch, tot);
     if (d < nd) {
       nd_n[(uint64_t)b * ndcap + d] = tot_d;
       nd_base[(uint64_t)b * ndcap + d] = start;
       uint32_t run = start;
-      for (uint32_t ch = 0; ch < nbins; ch++) {
+      uint32_t ch = 0;
+      for (; ch + 8 <= nbins; ch += 8) {
+        uint32_t x[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) x[j] = cnt[(uint64_t)(ch + j) * ndcap + d];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          cnt[(uint64_t)(ch + j) * ndcap + d] = run;
+          run += x[j];
+        }
+      }
+      for (; ch < nbins; ch++) {
         const uint32_t x = cnt[(uint64_t)ch * ndcap + d];
         cnt[(uint64_t)ch * ndcap + d] = run;
         run += x;
@@ -720,11 +765,14 @@ __global__ void __launch_bounds__(256) k_welford(const CloudCtl* ctl, const T* _
   welford_init(w);
   constexpr int U = 8;
   T cur[3 * U], nxt[3 * U];
+  // nd_pts carries kNdSlack points of padding, so these loads run unconditionally
+  // past a run's end (a predicated load would branch and wait on every element)
 #pragma unroll
-  for (int j = 0; j < 3 * U; j++) cur[j] = (uint32_t)j < 3 * cnt ? q[j] : T(0);
+  for (int j = 0; j < 3 * U; j++) cur[j] = q[j];
   for (uint32_t s = 0; s < cnt; s += U) {
+    const T* qn = q + 3 * (s + U < cnt ? s + U : s);
 #pragma unroll
-    for (int j = 0; j < 3 * U; j++) nxt[j] = 3 * (s + U) + j < 3 * cnt ? q[3 * (s + U) + j] : T(0);
+    for (int j = 0; j < 3 * U; j++) nxt[j] = qn[j];
 #pragma unroll
     for (int j = 0; j < U; j++) {
       if (s + j < cnt) {
@@ -845,22 +893,36 @@ __device__ void prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t* s_u
     // walk order: the c-th first (1-based) at position f_c is killed iff
     // f_c < nkl0 - (c-1) for it and for every earlier first.
     uint32_t carry = 0;
-    for (uint32_t base = 0; base < nkl0; base += blockDim.x) {
-      const uint32_t i = base + threadIdx.x;
-      uint32_t isf = 0;
-      if (i < nkl0) {
-        const uint32_t pp = op[i];
-        isf = (pp != kInvalid && alive[pp] && first[pp] == i);
+    constexpr int IT = 8;
+    for (uint32_t base = 0; base < nkl0; base += blockDim.x * IT) {
+      const uint32_t i0 = base + threadIdx.x * IT;
+      uint32_t isf[IT];
+#pragma unroll
+      for (int j = 0; j < IT; j++) {
+        const uint32_t i = i0 + j;
+        isf[j] = 0;
+        if (i < nkl0) {
+          const uint32_t pp = op[i];
+          isf[j] = (pp != kInvalid && alive[pp] && first[pp] == i);
+        }
       }
+      uint32_t pre[IT];
+#pragma unroll
+      for (int j = 0; j < IT; j++) pre[j] = isf[j];
       uint32_t tot;
-      const uint32_t ex = block_excl_scan(isf, 0u, AddU32(), scratch, tot);
-      if (isf) {
-        const uint32_t cth = carry + ex + 1;
-        tmp[i] = cth;
-        if (cth <= to_remove && i >= nkl0 - (cth - 1)) atomicMin(&s_failc, cth);
-        if (cth == to_remove) s_kpos = i;
-      } else if (i < nkl0) {
-        tmp[i] = 0;
+      block_scan_items(pre, 0u, AddU32(), scratch, tot);
+#pragma unroll
+      for (int j = 0; j < IT; j++) {
+        const uint32_t i = i0 + j;
+        if (i >= nkl0) continue;
+        if (isf[j]) {
+          const uint32_t cth = carry + pre[j] + 1;
+          tmp[i] = cth;
+          if (cth <= to_remove && i >= nkl0 - (cth - 1)) atomicMin(&s_failc, cth);
+          if (cth == to_remove) s_kpos = i;
+        } else {
+          tmp[i] = 0;
+        }
       }
       carry += tot;
     }
@@ -897,19 +959,24 @@ __device__ void prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t* s_u
       double* ov = A.ord_val_all + eb;
       uint32_t* oq = A.ord_q_all + eb;
       uint32_t* opw = A.ord_p_all + eb;
-      // gather into registers in passes, then write (in-place left shift)
-      for (uint32_t base = 0; base < nkl1; base += blockDim.x) {
-        const uint32_t i = base + threadIdx.x;
-        double v = 0;
-        uint32_t pq = kInvalid, qq = kInvalid;
-        if (i < nkl1) {
-          const uint32_t src = i + shift;
-          if (src < c.num_phys) { v = ov[src]; pq = opw[src]; qq = oq[src]; }
-        }
-        __syncthreads();
-        if (i < nkl1) { ov[i] = v; opw[i] = pq; oq[i] = qq; }
-        __syncthreads();
+      // in-place left shift through the event arrays (free once the list is built)
+      double* tv = A.ev_val_all + eb;
+      uint32_t* tp = A.ev_p_all + eb;
+      uint32_t* tq = A.ev_q_all + eb;
+      for (uint32_t i = threadIdx.x; i < nkl1; i += blockDim.x) {
+        const uint32_t src = i + shift;
+        const bool ok = src < c.num_phys;  // past it: entries the reference never wrote
+        tv[i] = ok ? ov[src] : 0.0;
+        tp[i] = ok ? opw[src] : kInvalid;
+        tq[i] = ok ? oq[src] : kInvalid;
       }
+      __syncthreads();
+      for (uint32_t i = threadIdx.x; i < nkl1; i += blockDim.x) {
+        ov[i] = tv[i];
+        opw[i] = tp[i];
+        oq[i] = tq[i];
+      }
+      __syncthreads();
       if (threadIdx.x == 0) c.num_kl = nkl1;
     } else if (threadIdx.x == 0) {
       c.num_kl = nkl0 - kills;
@@ -921,24 +988,32 @@ __device__ void prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t* s_u
   const uint64_t kout = k;
   const uint32_t* vn = A.nd_n + ob;
   uint32_t carry = 0;
-  for (uint32_t base = 0; base < nd; base += blockDim.x) {
-    const uint32_t u = base + threadIdx.x;
-    const uint32_t live = (u < nd) && alive[u];
+  constexpr int IT = 8;
+  for (uint32_t base = 0; base < nd; base += blockDim.x * IT) {
+    const uint32_t u0 = base + threadIdx.x * IT;
+    uint32_t row[IT];
+#pragma unroll
+    for (int j = 0; j < IT; j++) row[j] = (u0 + j < nd) && alive[u0 + j];
     uint32_t tot;
-    const uint32_t row = carry + block_excl_scan(live, 0u, AddU32(), scratch, tot);
-    if (live && row < kout) {
-      const uint64_t o = (uint64_t)b * kout + row;
+    block_scan_items(row, 0u, AddU32(), scratch, tot);
+#pragma unroll
+    for (int j = 0; j < IT; j++) {
+      const uint32_t u = u0 + j;
+      if (u >= nd || !alive[u]) continue;
+      const uint32_t rw = carry + row[j];
+      if (rw >= kout) continue;
+      const uint64_t o = (uint64_t)b * kout + rw;
       const double* m = A.nd_mean + 3 * (ob + u);
       const double* cv = A.nd_cov_post + 9 * (ob + u);
       if (A.out) {
         float* r = A.out + 12 * o;
-        for (int j = 0; j < 3; j++) {
-          const float f = (float)m[j];
-          r[j] = isfinite(f) ? f : 0.0f;  // nan_to_num(nan=0, posinf=0, neginf=0)
+        for (int q = 0; q < 3; q++) {
+          const float f = (float)m[q];
+          r[q] = isfinite(f) ? f : 0.0f;  // nan_to_num(nan=0, posinf=0, neginf=0)
         }
-        for (int j = 0; j < 9; j++) {
-          const float f = (float)cv[j];
-          r[3 + j] = isfinite(f) ? f : 0.0f;
+        for (int q = 0; q < 9; q++) {
+          const float f = (float)cv[q];
+          r[3 + q] = isfinite(f) ? f : 0.0f;
         }
       }
       if (A.out_cls) {
@@ -946,8 +1021,8 @@ __device__ void prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t* s_u
         r[A.nd_cls[ob + u]] = 1.0f;
       }
       if (A.out_pc64) {
-        for (int j = 0; j < 3; j++) A.out_pc64[3 * o + j] = m[j];
-        for (int j = 0; j < 9; j++) A.out_cov64[9 * o + j] = cv[j];
+        for (int q = 0; q < 3; q++) A.out_pc64[3 * o + q] = m[q];
+        for (int q = 0; q < 9; q++) A.out_cov64[9 * o + q] = cv[q];
       }
       if (A.out_cls16) A.out_cls16[o] = A.nd_cls[ob + u];
     }
@@ -1136,88 +1211,76 @@ __global__ void __launch_bounds__(kKLThreads) k_kl(KLArgs A) {
   const double* slot_val = A.slot_val_all + eb;
   const uint32_t* slot_flag = A.slot_flag_all + eb;
   const uint32_t nslots = 6 * nd;
-  // -- compaction into enumeration order; NaN-skipping exclusive prefix min
+  // -- one pass over the slots (enumeration order): event index, non-NaN rank,
+  //    NaN rank and the NaN-skipping exclusive prefix min of the values
   double* ev_val = A.ev_val_all + eb;
   uint32_t* ev_p = A.ev_p_all + eb;
   uint32_t* ev_q = A.ev_q_all + eb;
-  uint32_t E = 0;
-  {
-    uint32_t carry = 0;
-    for (uint32_t base = 0; base < nslots; base += blockDim.x) {
-      const uint32_t s = base + threadIdx.x;
-      const uint32_t f = s < nslots ? slot_flag[s] : 0u;
-      uint32_t tot;
-      const uint32_t e = carry + block_excl_scan(f, 0u, AddU32(), s_u32, tot);
-      if (f) {
-        ev_val[e] = slot_val[s];
-        ev_p[e] = s / 6;
-        ev_q[e] = (uint32_t)nb[s];
-      }
-      carry += tot;
-    }
-    E = carry;
-  }
-  __syncthreads();
   double* ev_min = A.ev_min_all + eb;
   uint32_t* nan_list = A.nan_list_all + eb;
   uint32_t* nan_pos = A.nan_pos_all + eb;
+  __shared__ unsigned long long s_u64[16];
+  // the sort buffers: LDS when the non-NaN events fit (bounded by the slots)
+  uint32_t sortcap_needed = 1;
+  while (sortcap_needed < nslots) sortcap_needed <<= 1;
   unsigned long long* skey;
   uint32_t* sidx;
-  uint32_t NN = 0, NNaN = 0;
-  {
-    // count non-NaN first to size the sort
-    uint32_t carry = 0, carry_nan = 0;
-    double mcarry = __builtin_inf();
-    const bool fits = true;
-    (void)fits;
-    for (uint32_t base = 0; base < E; base += blockDim.x) {
-      const uint32_t e = base + threadIdx.x;
-      const double v = e < E ? ev_val[e] : 0.0;
-      const bool isn = e < E && v != v;
-      const uint32_t nn = (e < E && !isn) ? 1u : 0u;
-      uint32_t tot;
-      (void)block_excl_scan(nn, 0u, AddU32(), s_u32, tot);
-      double mt;
-      const double mv = (e < E && !isn) ? v : __builtin_inf();
-      const double mex = block_excl_scan(mv, __builtin_inf(), MinF64(), s_f64, mt);
-      if (e < E) ev_min[e] = MinF64()(mcarry, mex);
-      mcarry = MinF64()(mcarry, mt);
-      carry += tot;
-      uint32_t totn;
-      const uint32_t jn = carry_nan + block_excl_scan(isn ? 1u : 0u, 0u, AddU32(), s_u32, totn);
-      if (isn) nan_list[jn] = e;
-      carry_nan += totn;
-    }
-    NN = carry;
-    NNaN = carry_nan;
-  }
-  uint32_t sortn = 1;
-  while (sortn < NN) sortn <<= 1;
-  if (sortn <= (uint32_t)kSortLds) {
+  if (sortcap_needed <= (uint32_t)kSortLds) {
     skey = reinterpret_cast<unsigned long long*>(dyn);
     sidx = reinterpret_cast<uint32_t*>(dyn + 8 * kSortLds);
   } else {
     skey = A.sort_key_all + (uint64_t)b * A.sortcap;
     sidx = A.sort_idx_all + (uint64_t)b * A.sortcap;
   }
-  {
-    uint32_t carry = 0;
-    for (uint32_t base = 0; base < E; base += blockDim.x) {
-      const uint32_t e = base + threadIdx.x;
-      const double v = e < E ? ev_val[e] : 0.0;
-      const uint32_t nn = (e < E && v == v) ? 1u : 0u;
-      uint32_t tot;
-      const uint32_t r = carry + block_excl_scan(nn, 0u, AddU32(), s_u32, tot);
-      if (nn) {
-        skey[r] = ~ord_key(v);  // ascending key == descending value
-        sidx[r] = e;
+  constexpr int IT = 8;
+  unsigned long long cnt_carry = 0;  // (non-NaN count << 32) | NaN count
+  double min_carry = __builtin_inf();
+  for (uint32_t base = 0; base < nslots; base += blockDim.x * IT) {
+    const uint32_t s0 = base + threadIdx.x * IT;
+    double val[IT];
+    unsigned long long cnt[IT];
+    double mv[IT];
+#pragma unroll
+    for (int j = 0; j < IT; j++) {
+      const uint32_t sl = s0 + j;
+      const bool f = sl < nslots && slot_flag[sl];
+      val[j] = f ? slot_val[sl] : 0.0;
+      const bool isn = f && val[j] != val[j];
+      cnt[j] = f ? (isn ? 1ull : (1ull << 32)) : 0ull;
+      mv[j] = (f && !isn) ? val[j] : __builtin_inf();
+    }
+    unsigned long long ctot;
+    double mtot;
+    block_scan_items(cnt, 0ull, AddU64(), s_u64, ctot);
+    block_scan_items(mv, __builtin_inf(), MinF64(), s_f64, mtot);
+#pragma unroll
+    for (int j = 0; j < IT; j++) {
+      const uint32_t sl = s0 + j;
+      if (sl >= nslots || !slot_flag[sl]) continue;
+      const unsigned long long c2 = cnt_carry + cnt[j];
+      const uint32_t rnn = (uint32_t)(c2 >> 32), rnan = (uint32_t)c2;
+      const uint32_t e = rnn + rnan;
+      ev_val[e] = val[j];
+      ev_p[e] = sl / 6;
+      ev_q[e] = (uint32_t)nb[sl];
+      ev_min[e] = MinF64()(min_carry, mv[j]);
+      if (val[j] == val[j]) {
+        skey[rnn] = ~ord_key(val[j]);  // ascending key == descending value
+        sidx[rnn] = e;
+      } else {
+        nan_list[rnan] = e;
       }
-      carry += tot;
     }
-    for (uint32_t r = NN + threadIdx.x; r < sortn; r += blockDim.x) {
-      skey[r] = ~0ull;
-      sidx[r] = kInvalid;
-    }
+    cnt_carry += ctot;
+    min_carry = MinF64()(min_carry, mtot);
+  }
+  const uint32_t NN = (uint32_t)(cnt_carry >> 32), NNaN = (uint32_t)cnt_carry;
+  const uint32_t E = NN + NNaN;
+  uint32_t sortn = 1;
+  while (sortn < NN) sortn <<= 1;
+  for (uint32_t r = NN + threadIdx.x; r < sortn; r += blockDim.x) {
+    skey[r] = ~0ull;
+    sidx[r] = kInvalid;
   }
   __syncthreads();
   bitonic_pairs(skey, sidx, sortn);
@@ -1462,7 +1525,7 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   A_(did, B * n);
   A_(bin_cnt, B * nbn * nd);
   A_(nd_base, B * nd);
-  if (e == hipSuccess) e = hipMalloc(&P->nd_pts, B * n * 3 * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc(&P->nd_pts, (B * n + kNdSlack) * 3 * sizeof(double));
   A_(nd_lbl, num_classes >= 0 ? B * n : 1);
   A_(nd_n, B * nd);
   A_(nd_mean, B * nd * 3);
