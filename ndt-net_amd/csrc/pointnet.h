@@ -8,13 +8,13 @@
 #define NDNET_PN_MAX_LAYERS 5
 
 typedef struct ndnet_pn_layer {
-  const float* wT;        // [K][N] (+ cloud * w_cloud_stride)
-  int64_t w_cloud_stride; // 0 for shared weights, K*N for per-cloud folded weights
+  const float* wT;        // [K][ldw] (+ cloud * w_cloud_stride), 16-byte aligned
+  int64_t w_cloud_stride; // 0 for shared weights, else the per-cloud stride of folded weights
   const float* bias;      // [N] (+ cloud * bias_cloud_stride)
   int64_t bias_cloud_stride;
-  int32_t K, N;           // padded sizes
+  int32_t K, N;           // padded sizes: K % 4 == 0, N % 32 == 0
   int32_t relu;
-  int32_t pad_;
+  int32_t ldw;            // row stride of wT in floats (>= N, % 4 == 0)
 } ndnet_pn_layer;
 
 // mode: 0 = max-pool the last layer over points into gmax[cloud][N]
@@ -31,6 +31,7 @@ typedef struct ndnet_pn_chain {
   int32_t out_cols;
   float* gmax;            // mode 0: [B][gmax_ld], pre-set to -inf
   int32_t gmax_ld;
-  int32_t max_width;      // widest stored activation (LDS sizing)
+  int32_t max_width;      // widest activation of LDS region 0 (the input, layers 1, 3, ... outputs)
+  int32_t max_width2;     // widest activation of LDS region 1 (layers 0, 2, ... outputs)
   float* out;             // mode 1
 } ndnet_pn_chain;

@@ -11,10 +11,14 @@
 // ends either in a max-pool over points (fused into the last GEMM's
 // epilogue, one float atomic max per channel per tile) or in log-softmax.
 //
-// Tile geometry: 32 points (two 16-row MFMA blocks) x all output channels;
-// 4 waves split the 16-column blocks of each layer, 8 blocks at a time
-// (2 x 8 accumulators of 4 floats); the weight fragments for k-step s+1 are
-// loaded while the MFMAs of k-step s issue.
+// Tile geometry: 32 points = two 16-row MFMA blocks; the 4 waves are 2 row
+// blocks x 2 column halves of a 256-column chunk (8 accumulator blocks of
+// 16x16 each).  Weights stream through LDS in 16-row K-slabs of the chunk,
+// loaded with 16-byte global loads by all 256 threads, double-buffered: the
+// next slab's loads are issued into registers before the current slab's MFMAs
+// and written to LDS after them.  Activations live in two LDS regions sized
+// for the widest (input, output) pair of the chain, so the 512-wide seg-head
+// layer fits beside its 256-wide successor.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -24,9 +28,13 @@
 
 namespace {
 
-constexpr int kP = 32;        // points per workgroup
-constexpr int kThreads = 256; // 4 waves
-constexpr int kCBG = 8;       // 16-column blocks per wave per pass
+constexpr int kP = 32;          // points per workgroup
+constexpr int kThreads = 256;   // 4 waves
+constexpr int kNC = 256;        // columns per chunk
+constexpr int kKS = 16;         // K rows per weight slab
+constexpr int kSlabPitch = kNC + 16;  // floats per slab row (breaks the 2-way bank conflict)
+constexpr int kSlabFloats = kKS * kSlabPitch;
+constexpr int kSlabVecs = kKS * kNC / 4 / kThreads;  // float4 loads per thread per slab (4)
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -36,114 +44,135 @@ __device__ inline void atomic_max_f32(float* addr, float v) {
   else atomicMin(reinterpret_cast<unsigned int*>(addr), __float_as_uint(v));
 }
 
+// Loads this thread's share of slab rows [ks, ks + kr) x columns [c0, c0 + nc)
+// of W^T (row stride ldw) into registers.
+__device__ inline void slab_load(f32x4 (&r)[kSlabVecs], const float* __restrict__ wT, int ldw, int ks, int kr, int c0,
+                                 int nc) {
+  const int vpr = nc / 4;  // float4 per slab row
+#pragma unroll
+  for (int v = 0; v < kSlabVecs; v++) {
+    const int e = threadIdx.x + kThreads * v;
+    const int row = e / (kNC / 4), col4 = e % (kNC / 4);
+    if (row < kr && col4 < vpr)
+      r[v] = *reinterpret_cast<const f32x4*>(wT + (int64_t)(ks + row) * ldw + c0 + 4 * col4);
+    else
+      r[v] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+__device__ inline void slab_store(const f32x4 (&r)[kSlabVecs], float* slab) {
+#pragma unroll
+  for (int v = 0; v < kSlabVecs; v++) {
+    const int e = threadIdx.x + kThreads * v;
+    const int row = e / (kNC / 4), col4 = e % (kNC / 4);
+    *reinterpret_cast<f32x4*>(slab + row * kSlabPitch + 4 * col4) = r[v];
+  }
+}
+
 __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int b = blockIdx.y;
   const int p0 = blockIdx.x * kP;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int pitch = A.max_width + 1;  // odd: a column read by 16 lanes hits 16 banks
-  float* bufs[2] = {smem, smem + kP * pitch};
+  const int wr = wave >> 1;  // row block
+  const int wc = wave & 1;   // column half
+  const int kq = lane >> 4;  // k row of the A/B fragments
+  const int cl = lane & 15;  // row (A) / column (B, C) of the fragments
+  // LDS: activation region 0 | region 1 | two weight slabs
+  float* act[2] = {smem, smem + kP * (A.max_width + 1)};
+  const int pitch0 = A.max_width + 1, pitch1 = A.max_width2 + 1;
+  float* slabs = smem + kP * (pitch0 + pitch1);
   const int K0 = A.L[0].K;
   for (int e = threadIdx.x; e < kP * K0; e += kThreads) {
     const int r = e / K0, c = e % K0;
     const int p = p0 + r;
     float v = 0.0f;
     if (p < A.num_points && c < A.in_cols) v = A.x[((int64_t)b * A.num_points + p) * A.x_ld + c];
-    bufs[0][r * pitch + c] = v;
+    act[0][r * pitch0 + c] = v;
   }
   __syncthreads();
-  const int kr = lane >> 4;   // k row of the A/B fragments
-  const int cl = lane & 15;   // row (A) / column (B, C) of the fragments
-  int cur = 0;
   for (int l = 0; l < A.num_layers; l++) {
     const ndnet_pn_layer L = A.L[l];
     const float* __restrict__ wT = L.wT + (int64_t)b * L.w_cloud_stride;
     const float* __restrict__ bias = L.bias + (int64_t)b * L.bias_cloud_stride;
-    const int K = L.K, N = L.N, ncb = N / 16;
+    const int K = L.K, N = L.N, ldw = L.ldw;
     const bool last = (l == A.num_layers - 1);
-    const float* in = bufs[cur];
-    float* outb = bufs[cur ^ 1];
-    for (int g0 = wave; g0 < ncb; g0 += 4 * kCBG) {
-      f32x4 acc[2][kCBG];
+    const float* in = act[l & 1];
+    const int pin = (l & 1) ? pitch1 : pitch0;
+    float* outb = act[(l + 1) & 1];
+    const int pout = ((l + 1) & 1) ? pitch1 : pitch0;
+    const int nslab = (K + kKS - 1) / kKS;
+    for (int c0 = 0; c0 < N; c0 += kNC) {
+      const int nc = N - c0 < kNC ? N - c0 : kNC;
+      const int half = nc / 2;
+      const int nblk = half / 16;  // accumulator blocks of this wave (<= 8)
+      const int cw = wc * half;    // first column of this wave within the chunk
+      f32x4 acc[8];
 #pragma unroll
-      for (int j = 0; j < kCBG; j++) {
-        acc[0][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        acc[1][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-      float bw[kCBG], bn[kCBG];
+      for (int j = 0; j < 8; j++) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 stage[kSlabVecs];
+      slab_load(stage, wT, ldw, 0, K < kKS ? K : kKS, c0, nc);
+      slab_store(stage, slabs);
+      __syncthreads();
+      for (int s = 0; s < nslab; s++) {
+        const float* slab = slabs + (s & 1) * kSlabFloats;
+        const int ks = s * kKS;
+        const int kr = K - ks < kKS ? K - ks : kKS;
+        const bool more = s + 1 < nslab;
+        if (more) slab_load(stage, wT, ldw, ks + kKS, K - ks - kKS < kKS ? K - ks - kKS : kKS, c0, nc);
+        for (int kk = 0; kk < kr; kk += 4) {
+          const float a = in[(16 * wr + cl) * pin + ks + kk + kq];
+          const float* brow = slab + (kk + kq) * kSlabPitch + cw + cl;
 #pragma unroll
-      for (int j = 0; j < kCBG; j++) {
-        const int cb = g0 + 4 * j;
-        bw[j] = cb < ncb ? wT[(int64_t)kr * N + cb * 16 + cl] : 0.0f;
-      }
-      for (int k = 0; k < K; k += 4) {
-        const float a0 = in[cl * pitch + k + kr];
-        const float a1 = in[(16 + cl) * pitch + k + kr];
-        const bool more = k + 4 < K;
-#pragma unroll
-        for (int j = 0; j < kCBG; j++) {
-          const int cb = g0 + 4 * j;
-          bn[j] = (more && cb < ncb) ? wT[(int64_t)(k + 4 + kr) * N + cb * 16 + cl] : 0.0f;
+          for (int j = 0; j < 8; j++)
+            if (j < nblk) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, brow[16 * j], acc[j], 0, 0, 0);
         }
-#pragma unroll
-        for (int j = 0; j < kCBG; j++) {
-          if (g0 + 4 * j < ncb) {
-            acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bw[j], acc[0][j], 0, 0, 0);
-            acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bw[j], acc[1][j], 0, 0, 0);
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < kCBG; j++) bw[j] = bn[j];
+        if (more) slab_store(stage, slabs + ((s + 1) & 1) * kSlabFloats);
+        __syncthreads();
       }
-      // epilogue: C[row = 16 rb + 4 (lane >> 4) + r][col = lane & 15]
+      // epilogue: C[row = 16 wr + 4 kq + r][col = c0 + cw + 16 j + cl]
 #pragma unroll
-      for (int j = 0; j < kCBG; j++) {
-        const int cb = g0 + 4 * j;
-        if (cb >= ncb) continue;
-        const int ch = cb * 16 + cl;
+      for (int j = 0; j < 8; j++) {
+        if (j >= nblk) continue;
+        const int ch = c0 + cw + 16 * j + cl;
         const float bv = bias[ch];
         if (last && A.mode == 0) {
           float m = -INFINITY;
 #pragma unroll
-          for (int rb = 0; rb < 2; rb++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-              float v = acc[rb][j][r] + bv;
-              if (L.relu) v = fmaxf(v, 0.0f);
-              const int row = 16 * rb + 4 * kr + r;
-              if (p0 + row < A.num_points) m = fmaxf(m, v);
-            }
+          for (int r = 0; r < 4; r++) {
+            float v = acc[j][r] + bv;
+            if (L.relu) v = fmaxf(v, 0.0f);
+            if (p0 + 16 * wr + 4 * kq + r < A.num_points) m = fmaxf(m, v);
+          }
           m = fmaxf(m, __shfl_xor(m, 16, 64));
           m = fmaxf(m, __shfl_xor(m, 32, 64));
           if (lane < 16) atomic_max_f32(A.gmax + (int64_t)b * A.gmax_ld + ch, m);
         } else {
 #pragma unroll
-          for (int rb = 0; rb < 2; rb++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-              float v = acc[rb][j][r] + bv;
-              if (L.relu) v = fmaxf(v, 0.0f);
-              outb[(16 * rb + 4 * kr + r) * pitch + ch] = v;
-            }
+          for (int r = 0; r < 4; r++) {
+            float v = acc[j][r] + bv;
+            if (L.relu) v = fmaxf(v, 0.0f);
+            outb[(16 * wr + 4 * kq + r) * pout + ch] = v;
+          }
         }
       }
     }
     __syncthreads();
-    cur ^= 1;
   }
   if (A.mode == 1) {  // log_softmax over channels (ndtnet.py:239), [B][N][C+1] layout
-    const float* lg = bufs[cur];
+    const float* lg = act[A.num_layers & 1];
+    const int pl = (A.num_layers & 1) ? pitch1 : pitch0;
     for (int r = threadIdx.x; r < kP; r += kThreads) {
       const int p = p0 + r;
       if (p >= A.num_points) continue;
       float m = -INFINITY;
-      for (int c = 0; c < A.out_cols; c++) m = fmaxf(m, lg[r * pitch + c]);
+      for (int c = 0; c < A.out_cols; c++) m = fmaxf(m, lg[r * pl + c]);
       float s = 0.0f;
-      for (int c = 0; c < A.out_cols; c++) s += expf(lg[r * pitch + c] - m);
+      for (int c = 0; c < A.out_cols; c++) s += expf(lg[r * pl + c] - m);
       const float ls = logf(s);
       float* o = A.out + ((int64_t)b * A.num_points + p) * A.out_cols;
-      for (int c = 0; c < A.out_cols; c++) o[c] = (lg[r * pitch + c] - m) - ls;
+      for (int c = 0; c < A.out_cols; c++) o[c] = (lg[r * pl + c] - m) - ls;
     }
   }
 }
@@ -155,13 +184,17 @@ extern "C" {
 // One fused point-MLP chain over `batch` clouds on `stream` (see pointnet.h).
 int ndnet_pn_chain_run(const ndnet_pn_chain* args, int batch, void* stream) {
   if (!args || batch <= 0 || args->num_layers < 1 || args->num_layers > NDNET_PN_MAX_LAYERS) return -20;
-  if (args->L[0].K > args->max_width) return -20;
+  // activation regions: layer l reads region l & 1 and writes region (l + 1) & 1
+  int w[2] = {args->L[0].K, 0};
   for (int l = 0; l < args->num_layers; l++) {
+    const ndnet_pn_layer& L = args->L[l];
+    if (L.K % 4 || L.N % 32 || L.ldw % 4 || L.ldw < L.N) return -20;
+    if (l > 0 && L.K > w[l & 1]) return -20;
     const bool stored = l + 1 < args->num_layers || args->mode == 1;
-    if (args->L[l].K % 4 || args->L[l].N % 16) return -20;
-    if (stored && args->L[l].N > args->max_width) return -20;
+    if (stored && L.N > w[(l + 1) & 1]) w[(l + 1) & 1] = L.N;
   }
-  const size_t lds = (size_t)2 * kP * (args->max_width + 1) * sizeof(float);
+  if (args->max_width < w[0] || args->max_width2 < w[1]) return -20;
+  const size_t lds = sizeof(float) * ((size_t)kP * (args->max_width + 1 + args->max_width2 + 1) + 2 * kSlabFloats);
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)k_pn_chain, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=

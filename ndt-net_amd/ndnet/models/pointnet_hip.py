@@ -32,14 +32,15 @@ MAX_LAYERS = 5
 class _Layer(ctypes.Structure):
     _fields_ = [("wT", ctypes.c_void_p), ("w_cloud_stride", ctypes.c_int64), ("bias", ctypes.c_void_p),
                 ("bias_cloud_stride", ctypes.c_int64), ("K", ctypes.c_int32), ("N", ctypes.c_int32),
-                ("relu", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+                ("relu", ctypes.c_int32), ("ldw", ctypes.c_int32)]
 
 
 class _Chain(ctypes.Structure):
     _fields_ = [("x", ctypes.c_void_p), ("x_ld", ctypes.c_int32), ("in_cols", ctypes.c_int32),
                 ("num_points", ctypes.c_int32), ("num_layers", ctypes.c_int32), ("L", _Layer * MAX_LAYERS),
                 ("mode", ctypes.c_int32), ("out_cols", ctypes.c_int32), ("gmax", ctypes.c_void_p),
-                ("gmax_ld", ctypes.c_int32), ("max_width", ctypes.c_int32), ("out", ctypes.c_void_p)]
+                ("gmax_ld", ctypes.c_int32), ("max_width", ctypes.c_int32), ("max_width2", ctypes.c_int32),
+                ("out", ctypes.c_void_p)]
 
 
 _lib.POINTNET_EXPORTS["ndnet_pn_chain_run"] = (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p])
@@ -111,14 +112,29 @@ class _Folded:
                       (_wT(t1["w3"], 128, 1024), t1["b3"])]
             self.B_tail = [(_wT(t2["w1"], 64, 64), t2["b1"]), (_wT(t2["w2"], 64, 128), t2["b2"]),
                            (_wT(t2["w3"], 128, 1024), t2["b3"])]
-            self.C_tail = (_wT(self.c3w, 128, _pad(F, 16)), _bpad(self.c3b, _pad(F, 16)))
+            self.C_tail = (_wT(self.c3w, 128, _pad(F, 32)), _bpad(self.c3b, _pad(F, 32)))
             self.s1a = self.s1w[:, :64].contiguous()      # acts on x_t2
             self.s1bT = self.s1w[:, 64:].t().contiguous()  # [F, 512], acts on g3
             self.D_tail = [(_wT(self.s2w, 512, 256), self.s2b), (_wT(self.s3w, 256, 128), self.s3b),
-                           (_wT(self.s4w, 128, _pad(self.C1, 16)), _bpad(self.s4b, _pad(self.C1, 16)))]
+                           (_wT(self.s4w, 128, _pad(self.C1, 32)), _bpad(self.s4b, _pad(self.C1, 32)))]
             self.c1wT = self.c1w.t().contiguous()         # [12, 64]
             self.c2wT = self.c2w.t().contiguous()         # [64, 128]
             self.s1aT = self.s1a.t().contiguous()         # [64, 512]
+            # x_t2 = t2^T x1 feeds conv2 and the seg head: one bmm t2 @ [W2^T | Ws1a^T]
+            self.t2_rhs = torch.cat((self.c2wT, self.s1aT), dim=1).contiguous()  # [64, 640]
+            # conv1 of the t1-transformed input: (W1 M(t1))^T = sum_ac t1[a,c] E_ac^T W1^T,
+            # M(t1) = blockdiag(t1, kron(t1, I3)) (p' = t1 p, C' = t1 C)
+            dev = self.c1wT.device
+            E = torch.zeros((9, 12, 12), device=dev)
+            for a in range(3):
+                for c in range(3):
+                    E[3 * a + c, a, c] = 1.0
+                    for j in range(3):
+                        E[3 * a + c, 3 + 3 * a + j, 3 + 3 * c + j] = 1.0
+            self.t1_basis = torch.matmul(E.transpose(1, 2), self.c1wT).reshape(9, 12 * 64).contiguous()
+            # the identity the TNet heads add (ndtnet.py:59), folded into fc3's bias
+            self.t1["c3"] = self.t1["c3"] + torch.eye(3, device=dev).reshape(-1)
+            self.t2["c3"] = self.t2["c3"] + torch.eye(64, device=dev).reshape(-1)
 
 
 def _signature(m) -> tuple:
@@ -126,38 +142,37 @@ def _signature(m) -> tuple:
 
 
 def _fc_head(g: torch.Tensor, t: dict, dim: int) -> torch.Tensor:
-    h = torch.relu(torch.addmm(t["c1"], g, t["f1"].t()))
-    h = torch.relu(torch.addmm(t["c2"], h, t["f2"].t()))
-    out = torch.addmm(t["c3"], h, t["f3"].t())
-    out = out + torch.eye(dim, device=g.device, dtype=g.dtype).reshape(1, -1)
-    return out.view(-1, dim, dim)
+    """TNet FC head (ndtnet.py:53-60); the identity is folded into t["c3"]."""
+    h = torch.addmm(t["c1"], g, t["f1"].t()).relu_()
+    h = torch.addmm(t["c2"], h, t["f2"].t()).relu_()
+    return torch.addmm(t["c3"], h, t["f3"].t()).view(-1, dim, dim)
 
 
 def _chain_gpu(x: torch.Tensor, n: int, in_cols: int, layers, relus, mode: int, gmax=None, out=None, out_cols=0,
                per_cloud=()) -> None:
     ch = _Chain()
     ch.x = x.data_ptr()
-    ch.x_ld = x.shape[-1]
+    ch.x_ld = x.stride(1)
     ch.in_cols = in_cols
     ch.num_points = n
     ch.num_layers = len(layers)
-    width = layers[0][0].shape[-2]  # K of the first layer
+    widths = [layers[0][0].shape[-2], 4]  # LDS regions: layer l reads l & 1, writes (l + 1) & 1
     for i, (w, b) in enumerate(layers):
         L = ch.L[i]
-        pc = i in per_cloud
         L.wT = w.data_ptr()
         L.K, L.N = w.shape[-2], w.shape[-1]
-        L.w_cloud_stride = L.K * L.N if pc and w.dim() == 3 else 0
+        L.ldw = w.stride(-2)
+        L.w_cloud_stride = w.stride(0) if (i in per_cloud and w.dim() == 3) else 0
         L.bias = b.data_ptr()
-        L.bias_cloud_stride = b.shape[-1] if b.dim() == 2 else 0
+        L.bias_cloud_stride = b.stride(0) if b.dim() == 2 else 0
         L.relu = relus[i]
         if i + 1 < len(layers) or mode == 1:
-            width = max(width, L.N)
+            widths[(i + 1) & 1] = max(widths[(i + 1) & 1], L.N)
     ch.mode = mode
     ch.out_cols = out_cols
     ch.gmax = gmax.data_ptr() if gmax is not None else None
-    ch.gmax_ld = gmax.shape[-1] if gmax is not None else 0
-    ch.max_width = width
+    ch.gmax_ld = gmax.stride(0) if gmax is not None else 0
+    ch.max_width, ch.max_width2 = widths
     ch.out = out.data_ptr() if out is not None else None
     rc = _lib.lib().ndnet_pn_chain_run(ctypes.byref(ch), x.shape[0], _lib.stream_ptr(x.device))
     _lib.check(rc, "ndnet_pn_chain_run")
@@ -197,31 +212,23 @@ def segmentation_forward(model, points: torch.Tensor, covariances: torch.Tensor,
     else:
         x = torch.cat((points, covariances), dim=2).float().contiguous()
     del base
-    neg_inf = float("-inf")
-    # A: TNet(3)
-    g1 = torch.zeros((B, 1024), dtype=torch.float32, device=dev)  # post-ReLU max >= 0
-    _chain(x, N, 3, W.A, (1, 1, 1), 0, gmax=g1)
-    t1 = _fc_head(g1, W.t1, 3)                                      # [B,3,3]
-    # x' = M x with M = blockdiag(t1, kron(t1, I3)); conv1 folded: W1 M
-    eye3 = torch.eye(3, device=dev)
-    M = torch.zeros((B, 12, 12), device=dev)
-    M[:, :3, :3] = t1
-    M[:, 3:, 3:] = torch.einsum("bik,jl->bijkl", t1, eye3).reshape(B, 9, 9)
-    w1T = torch.matmul(M.transpose(1, 2), W.c1wT)                   # [B,12,64] = (W1 M)^T
-    # B: conv1 (+t1) then TNet(64)
-    g2 = torch.zeros((B, 1024), dtype=torch.float32, device=dev)
-    layersB = [(w1T, W.c1b)] + W.B_tail
-    _chain(x, N, 12, layersB, (0, 1, 1, 1), 0, gmax=g2, per_cloud=(0,))
-    t2 = _fc_head(g2, W.t2, 64)                                     # [B,64,64]
-    # C: x_t2 = t2^T x1 folded into conv2: (W2 t2^T)^T = t2 W2^T
-    w2T = torch.matmul(t2, W.c2wT)                                  # [B,64,128]
+    # the three max-pooled vectors, -inf before the atomic maxima (ReLU'd maxima are >= 0)
     Fp = W.C_tail[0].shape[1]
-    g3 = torch.full((B, Fp), neg_inf, dtype=torch.float32, device=dev)
+    gbuf = torch.full((B, 2048 + Fp), float("-inf"), dtype=torch.float32, device=dev)
+    g1, g2, g3 = gbuf[:, :1024], gbuf[:, 1024:2048], gbuf[:, 2048:]
+    # A: TNet(3)
+    _chain(x, N, 3, W.A, (1, 1, 1), 0, gmax=g1)
+    t1 = _fc_head(g1, W.t1, 3)                                        # [B,3,3]
+    w1T = torch.matmul(t1.reshape(B, 9), W.t1_basis).view(B, 12, 64)  # (W1 M(t1))^T
+    # B: conv1 (+t1) then TNet(64)
+    _chain(x, N, 12, [(w1T, W.c1b)] + W.B_tail, (0, 1, 1, 1), 0, gmax=g2, per_cloud=(0,))
+    t2 = _fc_head(g2, W.t2, 64)                                       # [B,64,64]
+    t2w = torch.matmul(t2, W.t2_rhs)                                  # [B,64,640]
+    w2T, sT = t2w[:, :, :128], t2w[:, :, 128:]                        # conv2, seg conv1[:, :64]; t2 folded
+    # C: conv2, conv3, max over points
     _chain(x, N, 12, [(w1T, W.c1b), (w2T, W.c2b), W.C_tail], (0, 0, 0), 0, gmax=g3, per_cloud=(0, 1))
-    g3 = g3[:, : W.F]
-    # D: seg head; per-cloud bias W[:,64:] g3 + b; x_t2 term folded: t2 Wa^T
-    sT = torch.matmul(t2, W.s1aT)                                   # [B,64,512]
-    cvec = torch.addmm(W.s1b, g3, W.s1bT)                           # [B,512]
+    # D: seg head; the broadcast global feature enters as a per-cloud bias
+    cvec = torch.addmm(W.s1b, g3[:, : W.F], W.s1bT)                   # [B,512]
     out = torch.empty((B, N, W.C1), dtype=torch.float32, device=dev)
     _chain(x, N, 12, [(w1T, W.c1b), (sT, cvec)] + W.D_tail, (0, 1, 1, 1, 0), 1, out=out, out_cols=W.C1,
            per_cloud=(0, 1))
