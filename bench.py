@@ -43,6 +43,17 @@ def pointnet_flops_per_cloud(n: int, F: int, C: int) -> float:
     return 2.0 * (pt * n + fc)
 
 
+def chain_flops_per_point(F: int, C: int) -> tuple:
+    """Algorithmic FLOPs per point of the four k_pn_chain launches: each layer
+    counted once at its unpadded size (the kernels' recomputation of conv1 /
+    conv2 in later chains and the zero padding are overhead, not counted)."""
+    a = 3 * 64 + 64 * 128 + 128 * 1024
+    b = 12 * 64 + 64 * 64 + 64 * 128 + 128 * 1024
+    c = 64 * 128 + 128 * F
+    d = 64 * 512 + 512 * 256 + 256 * 128 + 128 * (C + 1)
+    return tuple(2.0 * v for v in (a, b, c, d))
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -56,6 +67,7 @@ def main() -> None:
     ap.add_argument("--classes", type=int, default=28)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="launch kernels from Python each step (no HIP graph)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -84,9 +96,18 @@ def main() -> None:
                 m.running_mean.uniform_(-0.2, 0.2)
                 m.running_var.uniform_(0.5, 1.5)
 
-    def step():
+    def eager_step():
         p, c, _ = ndt_preprocessing(k, pts)
         return model(p, c)
+
+    if args.eager:
+        step = eager_step
+    else:
+        # the same kernels, launched from one captured HIP graph per step
+        from ndnet.pipeline import GraphedSegmentation
+        graphed = GraphedSegmentation(model, k, B, n, device=dev)
+        graphed.points.copy_(pts)
+        step = graphed.replay
 
     with torch.no_grad():
         for _ in range(args.warmup):
@@ -120,6 +141,7 @@ def main() -> None:
     stage_ms = np.zeros(6)
     fwd_ms = 0.0
     reps = max(3, min(args.steps, 10))
+    pointnet_hip.chain_timing = []
     with torch.no_grad():
         for _ in range(reps):
             p, c, _ = ndt_preprocessing(k, pts)
@@ -135,17 +157,26 @@ def main() -> None:
     _lib.lib().ndnet_ndt_set_timing(plan.handle, 0)
     stage_ms /= reps
     fwd_ms /= reps
+    chain_ms = np.zeros(4)
+    for i, e0, e1 in pointnet_hip.chain_timing:
+        chain_ms[i] += e0.elapsed_time(e1) / reps
+    pointnet_hip.chain_timing = None
     ndt_ms = float(stage_ms.sum())
     hip_fwd = pointnet_hip.available()
     # dominant stage -> roofline entry
     flops = pointnet_flops_per_cloud(k, F, C) * B
     ndt_bytes = (24.0 * n + 48.0 * k) * B  # fp64 xyz read once + fp32 12-D write
-    if fwd_ms >= stage_ms.max():
-        achieved = flops / (fwd_ms * 1e-3) / 1e12
-        roofline = {"kernel": "NDTNetSegmentation forward" + (" (HIP MFMA)" if hip_fwd else " (torch)"),
-                    "bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
+    cflops = np.array(chain_flops_per_point(F, C)) * k * B
+    ci = int(chain_ms.argmax())
+    if hip_fwd and chain_ms[ci] >= stage_ms.max():
+        achieved = cflops[ci] / (chain_ms[ci] * 1e-3) / 1e12
+        roofline = {"kernel": f"k_pn_chain {pointnet_hip.CHAIN_NAMES[ci]}", "bound": "mfma",
+                    "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
                     "frac": round(achieved / FP32_MFMA_PEAK_TF, 4), "traffic": None,
-                    "algorithmic": f"{flops / 1e9:.2f} GFLOP per batch of {B}", "ms": round(fwd_ms, 4)}
+                    "algorithmic": f"{cflops[ci] / 1e9:.3f} GFLOP per launch ({B} clouds x {k} points)",
+                    "ms": round(float(chain_ms[ci]), 4),
+                    "all_chains": {"ms": [round(float(v), 4) for v in chain_ms],
+                                   "tflops": [round(float(f / (t * 1e-3) / 1e12), 2) for f, t in zip(cflops, chain_ms)]}}
     else:
         i = int(stage_ms.argmax())
         achieved = ndt_bytes / (stage_ms[i] * 1e-3) / 1e9
@@ -200,6 +231,7 @@ def main() -> None:
             "dtype": "f64 (NDT core) + fp32 (PointNet)",
             "data": f"synthetic {args.kind} clouds (SURVEY 8d), random-init weights",
             "config": {"workload": f"batch {B} x {n} pts -> {k} NDs, NDTNetSegmentation F={F} C={C} eval",
+                       "launch": "eager" if args.eager else "hip graph (ndnet.pipeline.GraphedSegmentation)",
                        "global_batch": B * world, "points": n, "nds": k, "parallelism": f"dp{world} (clouds sharded)"},
             "stages_ms": {nm: round(float(v), 4) for nm, v in zip(stage_names, stage_ms)} | {"pointnet_fwd": round(fwd_ms, 4)},
             "roofline": roofline,

@@ -138,13 +138,24 @@ int ndnet_ndt_prune(void *plan, void *stream, uint64_t num_desired, float *d_out
  * ndnet_ndt_set_timing(plan, 1), each run records events around its stages;
  * ndnet_ndt_stage_ms fills ms[6] = reset+limits, 15 bisection passes, dense
  * ids, chunk sort, Welford, KL+prune of the last run (synchronises). */
-int ndnet_ndt_set_timing(void *plan, int enable);
+int ndnet_ndt_set_timing(void *plan, int enable);  /* 0 off, 1 stage events, 2 + k_kl phase stamps */
 int ndnet_ndt_stage_ms(void *plan, float *ms);
 
 /* Host copies of one cloud's intermediates after a run (parity tests). */
 int ndnet_ndt_debug_dump(void *plan, int cloud, uint32_t *nd_n, double *nd_mean, double *nd_cov_pre,
                          double *nd_cov_post, uint32_t *vox, double *ord_val, uint32_t *ord_p, uint32_t *ord_q,
                          double *guesses, uint32_t *counts, uint32_t *iters, uint8_t *alive);
+
+/* Sets every cloud's stamp epoch (synchronises).  The epoch advances once per
+ * run and wraps after 2^26 - 1 runs, when the device clears the stale voxel
+ * stamps itself; tests use this to reach the wrap. */
+int ndnet_ndt_debug_set_epoch(void *plan, uint32_t epoch);
+
+/* k_kl phase stamps of the last run at timing level 2: marks[cloud * 16 + i],
+ * 100 MHz s_memrealtime ticks (0 start, 1 outputs zeroed, 2 event count,
+ * 5 list initialised, 6 first occurrences, 7 walk scan, 8 kills, 9 shift,
+ * 10 rows emitted, 11 end; 3 and 4 unused); synchronises. */
+int ndnet_ndt_debug_kl_marks(void *plan, unsigned long long *marks);
 
 /* Library identification (no GPU needed). */
 const char *ndnet_amd_version(void);

@@ -44,7 +44,9 @@ constexpr int kHashSlots = 2048;     // LDS dedup table of a search workgroup (>
 constexpr int kBitsCap = 32768;      // grids up to this many voxels count through bitmaps
 constexpr int kBitsWords = kBitsCap / 32;
 constexpr int kKLThreads = 1024;
-constexpr int kSortLds = 8192;       // largest event sort kept in LDS
+constexpr int kChunk = 256;          // slots per chunk of the chip-wide event sort
+constexpr int kMergeLdsChunks = 34;  // k_kl_merge stages score + NaN keys in LDS up to this many chunks (136 KB)
+constexpr int kMaxChunks = 6 * 16384 / kChunk;  // ndcap <= 16384
 
 enum State : uint32_t { kSearching = 0, kAccepted = 1, kFailed = 2 };
 
@@ -78,6 +80,7 @@ struct CloudCtl {
   int32_t prune_rc;
   uint32_t num_out;
   uint32_t last_k;
+  uint32_t clear_stamps; // the epoch wrapped this run: k_limits zeroes the cloud's stamps
 };
 
 struct Plan {
@@ -91,9 +94,11 @@ struct Plan {
   uint32_t nbins;      // 1024-point binning chunks per cloud
   uint32_t G;          // search workgroups per cloud
   int in_f64;          // input element type of the last run
-  uint64_t calls;      // runs issued (mirrors the device epoch)
-  int timing;          // record stage events
+  uint64_t calls;      // runs issued from the host (graph replays not counted)
+  int timing;          // 0 off, 1 stage events, 2 + k_kl phase marks
+  int ev_created;
   hipEvent_t ev[8];
+  unsigned long long* kl_marks;  // [B][16] s_memrealtime stamps (timing level 2)
   // device buffers
   CloudCtl* ctl;
   uint32_t* stamps;    // [B][vcap]
@@ -125,15 +130,20 @@ struct Plan {
   double* ev_min;      // [B][ecap] exclusive prefix min (NaN-skipping)
   unsigned long long* sort_key;  // [B][sortcap]
   uint32_t* sort_idx;  // [B][sortcap]
-  uint32_t* nan_list;  // [B][ecap]
-  uint32_t* nan_pos;   // [B][ecap]
+  uint32_t* nan_list;  // [B][ecap] NaN slots per chunk (chunk * kChunk + j)
+  unsigned long long* nan_key;  // [B][ecap] NaN keys, contiguous in slot order
+  uint32_t* nan_slot;  // [B][ecap] their slots
+  uint32_t* chunk_nanbase;  // [B][nchunk] NaN events in earlier chunks
   double* ord_val;     // [B][ecap] the retained list (physical array)
   uint32_t* ord_p;     // [B][ecap]
   uint32_t* ord_q;     // [B][ecap]
   uint32_t* first_occ; // [B][ndcap]
   uint32_t* tmp_u32;   // [B][ecap] scratch
   uint8_t* alive;      // [B][ndcap]
-  uint32_t sortcap;
+  uint32_t sortcap;    // chunked sort arrays per cloud: roundup(ecap, kChunk)
+  uint32_t nchunk;     // kChunk-slot chunks per cloud (max)
+  uint32_t* chunk_cnt; // [B][nchunk] (non-NaN count << 16) | NaN count
+  double* chunk_min;   // [B][nchunk] min non-NaN value of the chunk (+inf if none)
   ndnet_ndt_stats* d_stats;  // [B] device copy of the stats
 };
 
@@ -232,7 +242,14 @@ __global__ void k_reset(CloudCtl* ctl, int B) {
   if (b >= B) return;
   CloudCtl& c = ctl[b];
   c.epoch = c.epoch + 1;
-  if (c.epoch >= (1u << 26)) c.epoch = 1;  // stamps are epoch*32 + pass
+  // stamps are epoch*32 + pass; on a wrap the stale stamps are cleared on the
+  // device (k_limits), so a captured graph replayed any number of times stays
+  // correct without host bookkeeping
+  c.clear_stamps = 0;
+  if (c.epoch >= (1u << 26)) {
+    c.epoch = 1;
+    c.clear_stamps = 1;
+  }
   for (int a = 0; a < 3; a++) {
     c.limkey[a] = ord_key(kDblMin);      // max starts at DBL_MIN (pointclouds.c:44-46)
     c.limkey[3 + a] = ord_key(kDblMax);  // min starts at DBL_MAX
@@ -289,8 +306,12 @@ constexpr int kLimPPT = 16;        // flat coordinates per thread in k_limits
 // axis f % 3.
 template <typename T>
 __global__ void __launch_bounds__(256) k_limits(const T* __restrict__ pts, CloudCtl* ctl, uint32_t* gbits_all,
-                                                uint64_t n, uint32_t G, uint64_t vcap) {
+                                                uint32_t* stamps, uint64_t n, uint32_t G, uint64_t vcap) {
   const int b = blockIdx.y;
+  if (ctl[b].clear_stamps) {  // epoch wrap (k_reset): rare, cost irrelevant
+    uint32_t* sb = stamps + (uint64_t)b * vcap;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < vcap; i += (uint64_t)G * 256) sb[i] = 0;
+  }
   const T* p = pts + (uint64_t)b * n * 3;
   const uint64_t nf = 3 * n;
   double mx[3] = {kDblMin, kDblMin, kDblMin}, mn[3] = {kDblMax, kDblMax, kDblMax};
@@ -800,27 +821,14 @@ __global__ void __launch_bounds__(256) k_welford(const CloudCtl* ctl, const T* _
 }
 
 // Bitonic sort of (key, idx) pairs ascending, n a power of two, within one workgroup.
-__device__ void bitonic_pairs(unsigned long long* key, uint32_t* idx, uint32_t n) {
-  for (uint32_t size = 2; size <= n; size <<= 1) {
-    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-      for (uint32_t t = threadIdx.x; t < n / 2; t += blockDim.x) {
-        const uint32_t lo = 2 * t - (t & (stride - 1));
-        const uint32_t hi = lo + stride;
-        const bool up = (lo & size) == 0;
-        const unsigned long long ka = key[lo], kb = key[hi];
-        const uint32_t ia = idx[lo], ib = idx[hi];
-        const bool gt = ka > kb || (ka == kb && ia > ib);
-        if (gt == up) {
-          key[lo] = kb; key[hi] = ka;
-          idx[lo] = ib; idx[hi] = ia;
-        }
-      }
-      __syncthreads();
-    }
-  }
-}
+// phase stamp of k_kl (timing level 2): 100 MHz constant clock
+#define KL_MARK(i)                                                                   \
+  do {                                                                               \
+    if (A.marks && threadIdx.x == 0) A.marks[(uint64_t)b * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 
 struct KLArgs {
+  unsigned long long* marks;  // [B][16] phase stamps of k_kl, or null
   CloudCtl* ctl;
   const uint32_t* dense_all;
   const uint32_t* vox_all;
@@ -843,7 +851,9 @@ struct KLArgs {
   unsigned long long* sort_key_all;
   uint32_t* sort_idx_all;
   uint32_t* nan_list_all;
-  uint32_t* nan_pos_all;
+  unsigned long long* nan_key_all;
+  uint32_t* nan_slot_all;
+  uint32_t* chunk_nanbase;
   double* ord_val_all;
   uint32_t* ord_p_all;
   uint32_t* ord_q_all;
@@ -857,7 +867,9 @@ struct KLArgs {
   uint16_t* out_cls16;   // [B][k] or null
   ndnet_ndt_stats* stats;
   uint64_t vcap;
-  uint32_t ndcap, ecap, sortcap;
+  uint32_t ndcap, ecap, sortcap, nchunk;
+  uint32_t* chunk_cnt;
+  double* chunk_min;
   uint64_t k;
   int ncls;
 };
@@ -890,6 +902,7 @@ __device__ void prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t* s_u
       if (alive[pp]) atomicMin(&first[pp], i);
     }
     __syncthreads();
+    KL_MARK(6);
     // walk order: the c-th first (1-based) at position f_c is killed iff
     // f_c < nkl0 - (c-1) for it and for every earlier first.
     uint32_t carry = 0;
@@ -927,6 +940,7 @@ __device__ void prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t* s_u
       carry += tot;
     }
     __syncthreads();
+    KL_MARK(7);
     const uint32_t F = carry;
     uint32_t failc = s_failc;
     if (failc == kInvalid && F < to_remove) failc = F + 1;  // the walk runs off the end
@@ -948,6 +962,7 @@ __device__ void prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t* s_u
       }
     }
     __syncthreads();
+    KL_MARK(8);
     kills = s_kills;
     if (poisoned) rc = -8;
     else if (kills < to_remove) rc = -2;  // "Reached the end of the divergences array!"
@@ -984,6 +999,7 @@ __device__ void prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t* s_u
     if (threadIdx.x == 0) c.num_valid = nv0 - kills;
   }
   __syncthreads();
+  KL_MARK(9);
   // output rows: survivors in ascending voxel order
   const uint64_t kout = k;
   const uint32_t* vn = A.nd_n + ob;
@@ -1030,6 +1046,7 @@ __device__ void prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t* s_u
   }
   (void)vn;
   __syncthreads();
+  KL_MARK(10);
   if (threadIdx.x == 0) {
     c.prune_rc = rc;
     c.num_out = carry;
@@ -1188,15 +1205,294 @@ __global__ void __launch_bounds__(256) k_kl_events(KLArgs A) {
   A.slot_flag_all[eb + s] = flag;
 }
 
-// The reference's insertion order, the prune and the output rows: one
-// workgroup per cloud.
+// ---- the reference's insertion order as one chip-wide sort ----
+//
+// kl_divergences inserts every event into a list kept in descending order,
+// a tie going after the entries already there; a NaN score compares false
+// with everything and lands after the entries x with x > m or x == m
+// inserted earlier, m being the minimum non-NaN score inserted before it.
+// Both rules are one total order on composite keys (key, slot):
+//   non-NaN event at slot s with score v:   (~ord(v), s)
+//   NaN event at slot s:                    (~ord(m_s), s), m_s the NaN-skipping
+//                                           exclusive prefix min over slots
+// (ascending key = descending score; slot order is the insertion order).  For
+// a NaN t and a non-NaN x, t precedes x exactly when x is not among the p_t
+// entries ahead of t; two NaNs keep slot order because m_s is non-increasing.
+// -0.0 is keyed as +0.0 (the reference compares with >, where they are equal).
+//
+// k_kl_rank_chunks sorts each kChunk-slot chunk (rank by counting in LDS);
+// k_kl_merge gives every event its global position: its rank in its chunk
+// plus, per other chunk, a binary search.  Chunks cover ordered, disjoint slot
+// ranges, so a tie against a chunk below counts and against a chunk above
+// does not, and the searches need only the 64-bit keys.
+
+__device__ inline unsigned long long score_key(double v) { return ~ord_key(v + 0.0); }
+
+__global__ void __launch_bounds__(kChunk) k_kl_rank_chunks(KLArgs A) {
+  const int b = blockIdx.y;
+  const CloudCtl& c = A.ctl[b];
+  if (c.state != kAccepted) return;
+  const uint32_t nslots = 6 * c.num_nds;
+  const uint32_t ch = blockIdx.x;
+  if (ch * kChunk >= nslots) return;
+  const uint64_t eb = (uint64_t)b * A.ecap, kb = (uint64_t)b * A.sortcap + (uint64_t)ch * kChunk;
+  const uint32_t t = threadIdx.x;
+  const uint32_t sl = ch * kChunk + t;
+  const bool f = sl < nslots && A.slot_flag_all[eb + sl];
+  const double v = f ? A.slot_val_all[eb + sl] : 0.0;
+  const bool isn = f && v != v;
+  const bool num = f && !isn;
+  const unsigned long long key = num ? score_key(v) : ~0ull;
+  __shared__ unsigned long long s_key[kChunk];
+  __shared__ double s_f64[16];
+  __shared__ uint32_t s_u32[16];
+  s_key[t] = key;
+  double pm[1] = {num ? v : __builtin_inf()};
+  uint32_t cnt[1] = {(uint32_t)isn | ((uint32_t)num << 16)};
+  double mtot;
+  uint32_t ctot;
+  block_scan_items(pm, __builtin_inf(), MinF64(), s_f64, mtot);
+  block_scan_items(cnt, 0u, AddU32(), s_u32, ctot);
+  __syncthreads();
+  // rank in the chunk: keys below, then equal keys at lower slots
+  uint32_t r = 0;
+#pragma unroll 8
+  for (uint32_t j = 0; j < (uint32_t)kChunk; j++) {
+    const unsigned long long kj = s_key[j];
+    r += (kj < key) | ((kj == key) & (j < t));
+  }
+  A.sort_key_all[kb + r] = key;  // positions past the chunk's scores hold ~0
+  A.sort_idx_all[kb + r] = sl;
+  if (isn) {
+    const uint32_t j = cnt[0] & 0xffffu;
+    A.nan_list_all[eb + ch * kChunk + j] = sl;
+    A.ev_min_all[eb + ch * kChunk + j] = pm[0];
+  }
+  if (t == 0) {
+    A.chunk_cnt[(uint64_t)b * A.nchunk + ch] = ctot;
+    A.chunk_min[(uint64_t)b * A.nchunk + ch] = mtot;
+  }
+}
+
+// NaN keys need the min over all earlier chunks: one pass writes every NaN
+// event's key and slot contiguously in slot order (a sorted sequence: keys
+// non-decreasing, slots increasing) and the per-chunk NaN bases.
+__global__ void __launch_bounds__(kChunk) k_kl_nan_keys(KLArgs A) {
+  const int b = blockIdx.y;
+  const CloudCtl& c = A.ctl[b];
+  if (c.state != kAccepted) return;
+  const uint32_t nch = (6 * c.num_nds + kChunk - 1) / kChunk;
+  const uint32_t ch = blockIdx.x;
+  if (ch >= nch) return;
+  const uint32_t t = threadIdx.x;
+  const uint64_t eb = (uint64_t)b * A.ecap, cb = (uint64_t)b * A.nchunk;
+  constexpr int ITC = (kMaxChunks + kChunk - 1) / kChunk;
+  __shared__ double s_f64[16];
+  __shared__ uint32_t s_u32[16];
+  __shared__ uint32_t s_base;
+  __shared__ double s_carry;
+  uint32_t nanb[ITC];
+  double cmin[ITC];
+#pragma unroll
+  for (int i = 0; i < ITC; i++) {
+    const uint32_t c2 = t * ITC + i;
+    nanb[i] = c2 < nch ? (A.chunk_cnt[cb + c2] & 0xffffu) : 0u;
+    cmin[i] = c2 < nch ? A.chunk_min[cb + c2] : __builtin_inf();
+  }
+  uint32_t nan_total;
+  double min_total;
+  block_scan_items(nanb, 0u, AddU32(), s_u32, nan_total);
+  block_scan_items(cmin, __builtin_inf(), MinF64(), s_f64, min_total);
+#pragma unroll
+  for (int i = 0; i < ITC; i++) {
+    const uint32_t c2 = t * ITC + i;
+    if (c2 == ch) {
+      s_base = nanb[i];
+      s_carry = cmin[i];
+    }
+    if (ch == 0 && c2 < nch) A.chunk_nanbase[cb + c2] = nanb[i];
+  }
+  __syncthreads();
+  const uint32_t nn = A.chunk_cnt[cb + ch] & 0xffffu;
+  if (t < nn) {
+    const uint32_t o = ch * kChunk + t;
+    A.nan_key_all[eb + s_base + t] = score_key(MinF64()(s_carry, A.ev_min_all[eb + o]));
+    A.nan_slot_all[eb + s_base + t] = A.nan_list_all[eb + o];
+  }
+}
+
+// #entries of a sorted, ~0-padded kChunk-key run ahead of x: keys <= x (le)
+// or keys < x; four runs searched together (eight halving probes each).
+template <typename KP>
+__device__ inline void count_before4(KP K, const uint32_t (&run)[4], unsigned long long x, const bool (&le)[4],
+                                     uint32_t (&base)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; q++) base[q] = 0;
+#pragma unroll
+  for (uint32_t half = kChunk / 2; half >= 1; half >>= 1) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const unsigned long long k = K[run[q] * kChunk + base[q] + half - 1];
+      base[q] += (le[q] ? k <= x : k < x) ? half : 0u;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const unsigned long long k = K[run[q] * kChunk + base[q]];
+    base[q] += (le[q] ? k <= x : k < x) ? 1u : 0u;
+  }
+}
+
+// #entries of the sorted K[lo, hi) with key <= x (le) or < x.
+template <typename KP>
+__device__ inline uint32_t count_sorted(KP K, uint32_t lo, uint32_t hi, unsigned long long x, bool le) {
+  const uint32_t lo0 = lo;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    const unsigned long long k = K[mid];
+    if (le ? k <= x : k < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo - lo0;
+}
+
+// #entries (K[i], S[i]), i < n, preceding (x, s) (keys and slots both sorted).
+template <typename KP, typename SP>
+__device__ inline uint32_t count_composite(KP K, SP S, uint32_t n, unsigned long long x, uint32_t s) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    const unsigned long long k = K[mid];
+    if (k < x || (k == x && S[mid] < s)) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+constexpr int kMergeRuns = 4;  // chunks merged per k_kl_merge workgroup (1024 threads)
+
+template <bool kLds>
+__global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
+  const int b = blockIdx.y;
+  const CloudCtl& c = A.ctl[b];
+  if (c.state != kAccepted) return;
+  const uint32_t nch = (6 * c.num_nds + kChunk - 1) / kChunk;
+  if (blockIdx.x * kMergeRuns >= nch) return;
+  const uint64_t eb = (uint64_t)b * A.ecap, kb = (uint64_t)b * A.sortcap, cb = (uint64_t)b * A.nchunk;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lc = tid / kChunk, t = tid % kChunk;
+  const uint32_t ch = blockIdx.x * kMergeRuns + lc;
+  extern __shared__ __attribute__((aligned(16))) unsigned long long dynk[];
+  __shared__ uint32_t s_cnt[kMaxChunks];
+  __shared__ uint32_t s_nb[kMaxChunks + 1];
+  __shared__ uint32_t s_own_num_slot[kMergeRuns][kChunk];
+  __shared__ uint32_t s_own_nan_slot[kMergeRuns][kChunk];
+  for (uint32_t c2 = tid; c2 < nch; c2 += blockDim.x) {
+    s_cnt[c2] = A.chunk_cnt[cb + c2];
+    s_nb[c2] = A.chunk_nanbase[cb + c2];
+  }
+  if (tid == 0) s_nb[nch] = A.chunk_nanbase[cb + nch - 1] + (A.chunk_cnt[cb + nch - 1] & 0xffffu);  // NaN total
+  const unsigned long long* gK = A.sort_key_all + kb;
+  const unsigned long long* gN = A.nan_key_all + eb;
+  if (ch < nch) s_own_num_slot[lc][t] = A.sort_idx_all[kb + ch * kChunk + t];
+  __syncthreads();
+  const uint32_t nnan_tot = s_nb[nch];
+  const uint32_t cc = ch < nch ? s_cnt[ch] : 0u;
+  const uint32_t nnum = cc >> 16, nnan = cc & 0xffffu;
+  const uint32_t nb0 = ch < nch ? s_nb[ch] : 0u;
+  if (t < nnan) s_own_nan_slot[lc][t] = A.nan_slot_all[eb + nb0 + t];
+  unsigned long long* lK = dynk;
+  unsigned long long* lN = dynk + (uint64_t)nch * kChunk;
+  if (kLds) {  // stage the score runs and the NaN keys, eight 16-byte loads in flight per thread
+    const uint32_t nv = nch * kChunk / 2;
+    const ulonglong2* src = reinterpret_cast<const ulonglong2*>(gK);
+    ulonglong2* dst = reinterpret_cast<ulonglong2*>(lK);
+    constexpr int U = 8;
+    for (uint32_t i0 = 0; i0 < nv; i0 += U * blockDim.x) {
+      ulonglong2 v[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint32_t i = i0 + u * blockDim.x + tid;
+        v[u] = src[i < nv ? i : 0];
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint32_t i = i0 + u * blockDim.x + tid;
+        if (i < nv) dst[i] = v[u];
+      }
+    }
+    for (uint32_t i0 = 0; i0 < nnan_tot; i0 += U * blockDim.x) {
+      unsigned long long v[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint32_t i = i0 + u * blockDim.x + tid;
+        v[u] = gN[i < nnan_tot ? i : 0];
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint32_t i = i0 + u * blockDim.x + tid;
+        if (i < nnan_tot) lN[i] = v[u];
+      }
+    }
+  }
+  __syncthreads();
+  if (ch >= nch) return;
+  const bool is_num = t < nnum;
+  if (!is_num && t >= nnum + nnan) return;
+  const uint32_t* own_num_slot = s_own_num_slot[lc];
+  const uint32_t* own_nan_slot = s_own_nan_slot[lc];
+  auto body = [&](auto K, auto N) {
+    uint32_t sl;
+    unsigned long long x;
+    uint32_t pos;
+    if (is_num) {
+      x = K[ch * kChunk + t];
+      sl = own_num_slot[t];
+      pos = t;
+      // NaN events ahead: earlier chunks (key <= x), this chunk (composite), later chunks (key < x)
+      if (nnan_tot) {
+        pos += count_sorted(N, 0, nb0, x, true);
+        pos += count_composite(N + nb0, own_nan_slot, nnan, x, sl);
+        pos += count_sorted(N, nb0 + nnan, nnan_tot, x, false);
+      }
+    } else {
+      const uint32_t j = t - nnum;
+      x = N[nb0 + j];
+      sl = own_nan_slot[j];
+      // scores of its own chunk ahead of it, then every earlier NaN
+      pos = count_composite(K + ch * kChunk, own_num_slot, nnum, x, sl) + nb0 + j;
+    }
+    // scores of the other chunks ahead of it, four runs per pass
+    for (uint32_t c0 = 0; c0 < nch; c0 += 4) {
+      uint32_t run[4], add[4];
+      bool le[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t c2 = c0 + q;
+        run[q] = (c2 < nch && c2 != ch) ? c2 : ch;  // own run: masked below
+        le[q] = c2 < ch;
+      }
+      count_before4(K, run, x, le, add);
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        if (c0 + q < nch && c0 + q != ch) pos += add[q];
+    }
+    A.ord_val_all[eb + pos] = A.slot_val_all[eb + sl];
+    A.ord_p_all[eb + pos] = sl / 6;
+    A.ord_q_all[eb + pos] = (uint32_t)A.nb_all[6 * (uint64_t)b * A.ndcap + sl];
+  };
+  if (kLds) body(static_cast<const unsigned long long*>(lK), static_cast<const unsigned long long*>(lN));
+  else body(gK, gN);
+}
+
+// Prune and output rows: one workgroup per cloud.
 __global__ void __launch_bounds__(kKLThreads) k_kl(KLArgs A) {
   const int b = blockIdx.x;
   CloudCtl& c = A.ctl[b];
-  __shared__ double s_f64[16];
   __shared__ uint32_t s_u32[16];
-  extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+  KL_MARK(0);
   zero_outputs(A, b, A.k);
+  KL_MARK(1);
   if (c.state != kAccepted) {
     if (threadIdx.x == 0) {
       c.num_out = 0;
@@ -1207,122 +1503,20 @@ __global__ void __launch_bounds__(kKLThreads) k_kl(KLArgs A) {
   }
   const uint32_t nd = c.num_nds;
   const uint64_t ob = (uint64_t)b * A.ndcap, eb = (uint64_t)b * A.ecap;
-  const int32_t* nb = A.nb_all + 6 * ob;
-  const double* slot_val = A.slot_val_all + eb;
-  const uint32_t* slot_flag = A.slot_flag_all + eb;
-  const uint32_t nslots = 6 * nd;
-  // -- one pass over the slots (enumeration order): event index, non-NaN rank,
-  //    NaN rank and the NaN-skipping exclusive prefix min of the values
-  double* ev_val = A.ev_val_all + eb;
-  uint32_t* ev_p = A.ev_p_all + eb;
-  uint32_t* ev_q = A.ev_q_all + eb;
-  double* ev_min = A.ev_min_all + eb;
-  uint32_t* nan_list = A.nan_list_all + eb;
-  uint32_t* nan_pos = A.nan_pos_all + eb;
-  __shared__ unsigned long long s_u64[16];
-  // the sort buffers: LDS when the non-NaN events fit (bounded by the slots)
-  uint32_t sortcap_needed = 1;
-  while (sortcap_needed < nslots) sortcap_needed <<= 1;
-  unsigned long long* skey;
-  uint32_t* sidx;
-  if (sortcap_needed <= (uint32_t)kSortLds) {
-    skey = reinterpret_cast<unsigned long long*>(dyn);
-    sidx = reinterpret_cast<uint32_t*>(dyn + 8 * kSortLds);
-  } else {
-    skey = A.sort_key_all + (uint64_t)b * A.sortcap;
-    sidx = A.sort_idx_all + (uint64_t)b * A.sortcap;
+  const uint32_t nch = (6 * nd + kChunk - 1) / kChunk;
+  // event count from the chunk counters
+  uint32_t e_part = 0;
+  for (uint32_t c2 = threadIdx.x; c2 < nch; c2 += blockDim.x) {
+    const uint32_t cc = A.chunk_cnt[(uint64_t)b * A.nchunk + c2];
+    e_part += (cc >> 16) + (cc & 0xffffu);
   }
-  constexpr int IT = 8;
-  unsigned long long cnt_carry = 0;  // (non-NaN count << 32) | NaN count
-  double min_carry = __builtin_inf();
-  for (uint32_t base = 0; base < nslots; base += blockDim.x * IT) {
-    const uint32_t s0 = base + threadIdx.x * IT;
-    double val[IT];
-    unsigned long long cnt[IT];
-    double mv[IT];
-#pragma unroll
-    for (int j = 0; j < IT; j++) {
-      const uint32_t sl = s0 + j;
-      const bool f = sl < nslots && slot_flag[sl];
-      val[j] = f ? slot_val[sl] : 0.0;
-      const bool isn = f && val[j] != val[j];
-      cnt[j] = f ? (isn ? 1ull : (1ull << 32)) : 0ull;
-      mv[j] = (f && !isn) ? val[j] : __builtin_inf();
-    }
-    unsigned long long ctot;
-    double mtot;
-    block_scan_items(cnt, 0ull, AddU64(), s_u64, ctot);
-    block_scan_items(mv, __builtin_inf(), MinF64(), s_f64, mtot);
-#pragma unroll
-    for (int j = 0; j < IT; j++) {
-      const uint32_t sl = s0 + j;
-      if (sl >= nslots || !slot_flag[sl]) continue;
-      const unsigned long long c2 = cnt_carry + cnt[j];
-      const uint32_t rnn = (uint32_t)(c2 >> 32), rnan = (uint32_t)c2;
-      const uint32_t e = rnn + rnan;
-      ev_val[e] = val[j];
-      ev_p[e] = sl / 6;
-      ev_q[e] = (uint32_t)nb[sl];
-      ev_min[e] = MinF64()(min_carry, mv[j]);
-      if (val[j] == val[j]) {
-        skey[rnn] = ~ord_key(val[j]);  // ascending key == descending value
-        sidx[rnn] = e;
-      } else {
-        nan_list[rnan] = e;
-      }
-    }
-    cnt_carry += ctot;
-    min_carry = MinF64()(min_carry, mtot);
-  }
-  const uint32_t NN = (uint32_t)(cnt_carry >> 32), NNaN = (uint32_t)cnt_carry;
-  const uint32_t E = NN + NNaN;
-  uint32_t sortn = 1;
-  while (sortn < NN) sortn <<= 1;
-  for (uint32_t r = NN + threadIdx.x; r < sortn; r += blockDim.x) {
-    skey[r] = ~0ull;
-    sidx[r] = kInvalid;
-  }
-  __syncthreads();
-  bitonic_pairs(skey, sidx, sortn);
-  // NaN event t sits after the non-NaN x with x > m_t, or x == m_t occurring
-  // before t: its insertion point in the sorted list.
-  for (uint32_t j = threadIdx.x; j < NNaN; j += blockDim.x) {
-    const uint32_t t = nan_list[j];
-    const unsigned long long km = ~ord_key(ev_min[t]);
-    uint32_t lo = 0, hi = NN;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      const bool before = skey[mid] < km || (skey[mid] == km && sidx[mid] < t);
-      if (before) lo = mid + 1;
-      else hi = mid;
-    }
-    nan_pos[j] = lo;
-  }
-  __syncthreads();
+  uint32_t ev[1] = {e_part};
+  uint32_t E;
+  block_scan_items(ev, 0u, AddU32(), s_u32, E);
+  KL_MARK(2);
   double* ov = A.ord_val_all + eb;
   uint32_t* opp = A.ord_p_all + eb;
   uint32_t* oq = A.ord_q_all + eb;
-  for (uint32_t r = threadIdx.x; r < NN; r += blockDim.x) {
-    // NaNs with insertion point <= r precede it (nan_pos is non-decreasing)
-    uint32_t lo = 0, hi = NNaN;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (nan_pos[mid] <= r) lo = mid + 1;
-      else hi = mid;
-    }
-    const uint32_t pos = r + lo;
-    const uint32_t e = sidx[r];
-    ov[pos] = ev_val[e];
-    opp[pos] = ev_p[e];
-    oq[pos] = ev_q[e];
-  }
-  for (uint32_t j = threadIdx.x; j < NNaN; j += blockDim.x) {
-    const uint32_t pos = nan_pos[j] + j;
-    const uint32_t e = nan_list[j];
-    ov[pos] = ev_val[e];
-    opp[pos] = ev_p[e];
-    oq[pos] = ev_q[e];
-  }
   // poison beyond the written list (the reference's uninitialised tail)
   for (uint32_t i = E + threadIdx.x; i < A.ecap; i += blockDim.x) {
     opp[i] = kInvalid;
@@ -1337,9 +1531,11 @@ __global__ void __launch_bounds__(kKLThreads) k_kl(KLArgs A) {
     c.num_valid = nd;
   }
   __syncthreads();
+  KL_MARK(5);
   prune_and_emit(A, b, A.k, s_u32, s_u32);
   pad_class_rows(A, b, A.k);
   if (threadIdx.x == 0) write_stats(A, b);
+  KL_MARK(11);
 }
 
 __global__ void __launch_bounds__(kKLThreads) k_prune(KLArgs A) {
@@ -1375,14 +1571,15 @@ static hipError_t alloc(T** p, size_t count) {
 
 static void plan_free(Plan* P) {
   if (!P) return;
-  if (P->timing)
+  if (P->ev_created)
     for (int i = 0; i < 7; i++) (void)hipEventDestroy(P->ev[i]);
+  if (P->kl_marks) (void)hipFree(P->kl_marks);
   void* bufs[] = {P->ctl, P->stamps, P->dense_of, P->vox, P->gbits, P->pkeys, P->did, P->bin_cnt, P->nd_base,
                   P->nd_pts, P->nd_lbl, P->nd_n,
                   P->nd_mean, P->nd_cov, P->nd_cov_post, P->nd_cls, P->hist, P->nb, P->keys, P->nkeys,
                   P->chain, P->chain_ps, P->slot_val, P->slot_flag, P->ev_val, P->ev_p, P->ev_q, P->ev_min,
-                  P->sort_key, P->sort_idx, P->nan_list, P->nan_pos, P->ord_val, P->ord_p, P->ord_q,
-                  P->first_occ, P->tmp_u32, P->alive, P->d_stats};
+                  P->sort_key, P->sort_idx, P->nan_list, P->nan_key, P->nan_slot, P->chunk_nanbase, P->ord_val, P->ord_p, P->ord_q,
+                  P->first_occ, P->tmp_u32, P->alive, P->d_stats, P->chunk_cnt, P->chunk_min};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete P;
@@ -1390,6 +1587,7 @@ static void plan_free(Plan* P) {
 
 static KLArgs kl_args(Plan* P, uint64_t k, float* out, float* out_cls, double* pc64, double* cov64, uint16_t* cls16) {
   KLArgs A;
+  A.marks = P->timing >= 2 ? P->kl_marks : nullptr;
   A.ctl = P->ctl;
   A.dense_all = P->dense_of;
   A.vox_all = P->vox;
@@ -1412,7 +1610,9 @@ static KLArgs kl_args(Plan* P, uint64_t k, float* out, float* out_cls, double* p
   A.sort_key_all = P->sort_key;
   A.sort_idx_all = P->sort_idx;
   A.nan_list_all = P->nan_list;
-  A.nan_pos_all = P->nan_pos;
+  A.nan_key_all = P->nan_key;
+  A.nan_slot_all = P->nan_slot;
+  A.chunk_nanbase = P->chunk_nanbase;
   A.ord_val_all = P->ord_val;
   A.ord_p_all = P->ord_p;
   A.ord_q_all = P->ord_q;
@@ -1429,12 +1629,15 @@ static KLArgs kl_args(Plan* P, uint64_t k, float* out, float* out_cls, double* p
   A.ndcap = P->ndcap;
   A.ecap = P->ecap;
   A.sortcap = P->sortcap;
+  A.nchunk = P->nchunk;
+  A.chunk_cnt = P->chunk_cnt;
+  A.chunk_min = P->chunk_min;
   A.k = k;
   A.ncls = P->ncls;
   return A;
 }
 
-static size_t kl_lds_bytes() { return (size_t)kSortLds * (8 + 4); }
+static size_t merge_lds_bytes(const Plan* P) { return 2 * (size_t)P->nchunk * kChunk * sizeof(unsigned long long); }
 
 template <typename T>
 static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, float* out, float* out_cls,
@@ -1445,10 +1648,8 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
   if (P->timing) HIPCHK(hipEventRecord(P->ev[0], st));
   k_reset<<<(B + 63) / 64, 64, 0, st>>>(P->ctl, B);
   const uint32_t Gl = (uint32_t)((3 * n + 256 * kLimPPT - 1) / (256 * kLimPPT));
-  // stamps are epoch * 32 + pass; the device epoch wraps to 1 after 2^26 - 1 calls
-  if (++P->calls % ((1u << 26) - 1) == 0)
-    HIPCHK(hipMemsetAsync(P->stamps, 0, (size_t)B * P->vcap * sizeof(uint32_t), st));
-  k_limits<T><<<dim3(Gl, B), 256, 0, st>>>(pts, P->ctl, P->gbits, n, Gl, P->vcap);
+  P->calls++;
+  k_limits<T><<<dim3(Gl, B), 256, 0, st>>>(pts, P->ctl, P->gbits, P->stamps, n, Gl, P->vcap);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[1], st));
   for (int it = 0; it < kMaxIters; it++)
     k_search_pass<T><<<dim3(P->G, B), kPassThreads, 0, st>>>(pts, P->ctl, P->stamps, P->gbits, P->pkeys, n, P->k,
@@ -1471,12 +1672,24 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
   KLArgs A = kl_args(P, P->k, out, out_cls, pc64, cov64, cls16);
   k_kl_chains<<<dim3((P->ndcap + 255) / 256, B), 256, 0, st>>>(A);
   k_kl_events<<<dim3((6 * P->ndcap + 255) / 256, B), 256, 0, st>>>(A);
-  k_kl<<<B, kKLThreads, kl_lds_bytes(), st>>>(A);
+  k_kl_rank_chunks<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
+  k_kl_nan_keys<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
+  const uint32_t mg = (P->nchunk + kMergeRuns - 1) / kMergeRuns;
+  if (P->nchunk <= (uint32_t)kMergeLdsChunks)
+    k_kl_merge<true><<<dim3(mg, B), kChunk * kMergeRuns, merge_lds_bytes(P), st>>>(A);
+  else
+    k_kl_merge<false><<<dim3(mg, B), kChunk * kMergeRuns, 0, st>>>(A);
+  k_kl<<<B, kKLThreads, 0, st>>>(A);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[6], st));
   if (stats_dst)
     HIPCHK(hipMemcpyAsync(stats_dst, P->d_stats, sizeof(ndnet_ndt_stats) * B, hipMemcpyDeviceToDevice, st));
   HIPCHK(hipGetLastError());
   return NDNET_OK;
+}
+
+__global__ void k_set_epoch(CloudCtl* ctl, int B, uint32_t epoch) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) ctl[b].epoch = epoch;
 }
 
 }  // namespace
@@ -1500,9 +1713,8 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   const double upper = (double)num_desired * (1 + 0.2);
   P->ndcap = (uint32_t)upper + 1;
   P->ecap = 6 * P->ndcap;
-  uint32_t sc = 1;
-  while (sc < P->ecap) sc <<= 1;
-  P->sortcap = sc;
+  P->nchunk = (P->ecap + kChunk - 1) / kChunk;
+  P->sortcap = P->nchunk * kChunk;
   P->nbins = (uint32_t)((num_points + kBinPts - 1) / kBinPts);
   const uint64_t n8 = (num_points / kWorkers) * kWorkers;
   P->G = (uint32_t)((n8 + kPassPts - 1) / kPassPts);
@@ -1547,20 +1759,25 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   A_(sort_key, B * P->sortcap);
   A_(sort_idx, B * P->sortcap);
   A_(nan_list, B * ec);
-  A_(nan_pos, B * ec);
+  A_(nan_key, B * ec);
+  A_(nan_slot, B * ec);
+  A_(chunk_nanbase, B * P->nchunk);
   A_(ord_val, B * ec);
   A_(ord_p, B * ec);
   A_(ord_q, B * ec);
   A_(first_occ, B * nd);
   A_(tmp_u32, B * ec);
   A_(alive, B * nd);
+  A_(chunk_cnt, B * P->nchunk);
+  A_(chunk_min, B * P->nchunk);
   A_(d_stats, B);
 #undef A_
   if (e == hipSuccess) e = hipMemset(P->ctl, 0, B * sizeof(CloudCtl));
   if (e == hipSuccess) e = hipMemset(P->stamps, 0, B * P->vcap * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(P->d_stats, 0, B * sizeof(ndnet_ndt_stats));
-  if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_kl, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               (int)kl_lds_bytes());
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_kl_merge<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(2 * kMergeLdsChunks * kChunk * sizeof(unsigned long long)));
   if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_bin_count, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                (int)(16384 * sizeof(uint32_t)));
   if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -1578,9 +1795,16 @@ void ndnet_ndt_plan_destroy(void* plan) { plan_free((Plan*)plan); }
 int ndnet_ndt_set_timing(void* plan, int enable) {
   Plan* P = (Plan*)plan;
   if (!P) return NDNET_ERR_ARG;
-  if (enable && !P->timing)
+  if (enable < 0 || enable > 2) return NDNET_ERR_ARG;
+  if (enable && !P->ev_created) {
     for (int i = 0; i < 7; i++) HIPCHK(hipEventCreate(&P->ev[i]));
-  P->timing = P->timing || enable;
+    P->ev_created = 1;
+  }
+  if (enable >= 2 && !P->kl_marks) {
+    HIPCHK(hipMalloc(&P->kl_marks, (size_t)P->B * 16 * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(P->kl_marks, 0, (size_t)P->B * 16 * sizeof(unsigned long long)));
+  }
+  P->timing = enable;
   return NDNET_OK;
 }
 
@@ -1627,6 +1851,24 @@ int ndnet_ndt_prune(void* plan, void* stream, uint64_t num_desired, float* d_out
 }
 
 // Stage dumps for the parity tests (host copies of one cloud's intermediates).
+int ndnet_ndt_debug_kl_marks(void* plan, unsigned long long* marks) {
+  Plan* P = (Plan*)plan;
+  if (!P || !marks || !P->kl_marks) return NDNET_ERR_ARG;
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(marks, P->kl_marks, (size_t)P->B * 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return NDNET_OK;
+}
+
+int ndnet_ndt_debug_set_epoch(void* plan, uint32_t epoch) {
+  Plan* P = (Plan*)plan;
+  if (!P || epoch >= (1u << 26)) return NDNET_ERR_ARG;
+  HIPCHK(hipDeviceSynchronize());
+  k_set_epoch<<<(P->B + 63) / 64, 64>>>(P->ctl, P->B, epoch);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipDeviceSynchronize());
+  return NDNET_OK;
+}
+
 int ndnet_ndt_debug_dump(void* plan, int cloud, uint32_t* nd_n, double* nd_mean, double* nd_cov_pre,
                          double* nd_cov_post, uint32_t* vox, double* ord_val, uint32_t* ord_p, uint32_t* ord_q,
                          double* guesses, uint32_t* counts, uint32_t* iters, uint8_t* alive) {

@@ -67,6 +67,8 @@ EXPORTS = {
     "ndnet_ndt_run_f64": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "ndnet_ndt_prune": (_I, [_P, _P, _U64, _P, _P, _P, _P, _P, _P]),
     "ndnet_ndt_debug_dump": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "ndnet_ndt_debug_set_epoch": (_I, [_P, ctypes.c_uint32]),
+    "ndnet_ndt_debug_kl_marks": (_I, [_P, _P]),
     "ndnet_ndt_set_timing": (_I, [_P, _I]),
     "ndnet_ndt_stage_ms": (_I, [_P, _P]),
     "ndnet_amd_version": (ctypes.c_char_p, []),

@@ -27,6 +27,11 @@ import torch
 from .. import _lib
 
 MAX_LAYERS = 5
+CHAIN_NAMES = ("A: TNet(3) 3-64-128-1024 + max", "B: conv1(t1) + TNet(64) 64-64-128-1024 + max",
+               "C: conv1, conv2(t2), conv3 + max", "D: seg head 64-512-256-128-(C+1) + log_softmax")
+
+# set to a list to collect (chain index, start event, end event) per chain launch
+chain_timing = None
 
 
 class _Layer(ctypes.Structure):
@@ -137,22 +142,28 @@ class _Folded:
             self.t2["c3"] = self.t2["c3"] + torch.eye(64, device=dev).reshape(-1)
 
 
-def _signature(m) -> tuple:
-    return tuple((t.data_ptr(), t._version) for t in list(m.parameters()) + list(m.buffers()))
+def _tensors(m) -> list:
+    return list(m.parameters()) + list(m.buffers())
 
 
-def _fc_head(g: torch.Tensor, t: dict, dim: int) -> torch.Tensor:
-    """TNet FC head (ndtnet.py:53-60); the identity is folded into t["c3"]."""
-    h = torch.addmm(t["c1"], g, t["f1"].t()).relu_()
-    h = torch.addmm(t["c2"], h, t["f2"].t()).relu_()
-    return torch.addmm(t["c3"], h, t["f3"].t()).view(-1, dim, dim)
+def _signature(tensors) -> tuple:
+    """Storage and in-place version of every weight: a change re-folds."""
+    return tuple((t.data_ptr(), t._version) for t in tensors)
 
 
-def _chain_gpu(x: torch.Tensor, n: int, in_cols: int, layers, relus, mode: int, gmax=None, out=None, out_cols=0,
-               per_cloud=()) -> None:
+def _fc_head(g: torch.Tensor, t: dict, dim: int, h1: torch.Tensor, h2: torch.Tensor, out: torch.Tensor):
+    """TNet FC head (ndtnet.py:53-60) into preallocated buffers; the identity is
+    folded into t["c3"]."""
+    torch.addmm(t["c1"], g, t["f1"].t(), out=h1).relu_()
+    torch.addmm(t["c2"], h1, t["f2"].t(), out=h2).relu_()
+    torch.addmm(t["c3"], h2, t["f3"].t(), out=out)
+    return out.view(-1, dim, dim)
+
+
+def _build_chain(n: int, in_cols: int, layers, relus, mode: int, gmax=None, out_cols=0, per_cloud=()) -> "_Chain":
+    """ctypes argument block of one ``ndnet_pn_chain_run`` (x / out set per call)."""
     ch = _Chain()
-    ch.x = x.data_ptr()
-    ch.x_ld = x.stride(1)
+    ch.x_ld = 12
     ch.in_cols = in_cols
     ch.num_points = n
     ch.num_layers = len(layers)
@@ -173,9 +184,20 @@ def _chain_gpu(x: torch.Tensor, n: int, in_cols: int, layers, relus, mode: int, 
     ch.gmax = gmax.data_ptr() if gmax is not None else None
     ch.gmax_ld = gmax.stride(0) if gmax is not None else 0
     ch.max_width, ch.max_width2 = widths
+    return ch
+
+
+def _run_chain(ch: "_Chain", x: torch.Tensor, out=None) -> None:
+    assert x.stride(1) == 12 and x.stride(2) == 1 and x.dtype == torch.float32
+    ch.x = x.data_ptr()
     ch.out = out.data_ptr() if out is not None else None
     rc = _lib.lib().ndnet_pn_chain_run(ctypes.byref(ch), x.shape[0], _lib.stream_ptr(x.device))
     _lib.check(rc, "ndnet_pn_chain_run")
+
+
+def _chain_gpu(x: torch.Tensor, n: int, in_cols: int, layers, relus, mode: int, gmax=None, out=None, out_cols=0,
+               per_cloud=()) -> None:
+    _run_chain(_build_chain(n, in_cols, layers, relus, mode, gmax, out_cols, per_cloud), x, out)
 
 
 def _chain_torch(x: torch.Tensor, n: int, in_cols: int, layers, relus, mode: int, gmax=None, out=None,
@@ -195,41 +217,94 @@ def _chain_torch(x: torch.Tensor, n: int, in_cols: int, layers, relus, mode: int
         out.copy_(torch.log_softmax(h[..., :out_cols], dim=2))
 
 
+class _Workspace:
+    """Per-(batch, points) intermediates and prebuilt chain argument blocks, so
+    an eval forward does no allocation but its output and no struct building."""
+
+    def __init__(self, W: _Folded, B: int, N: int, dev) -> None:
+        f32 = dict(dtype=torch.float32, device=dev)
+        Fp = W.C_tail[0].shape[1]
+        # the three max-pooled vectors, -inf before the atomic maxima (ReLU'd maxima are >= 0)
+        self.gbuf = torch.empty((B, 2048 + Fp), **f32)
+        self.g1, self.g2, self.g3 = self.gbuf[:, :1024], self.gbuf[:, 1024:2048], self.gbuf[:, 2048:]
+        self.h1, self.h2 = torch.empty((B, 512), **f32), torch.empty((B, 256), **f32)
+        self.t1, self.t2 = torch.empty((B, 9), **f32), torch.empty((B, 4096), **f32)
+        self.w1T = torch.empty((B, 12, 64), **f32)      # (W1 M(t1))^T per cloud
+        self.t2w = torch.empty((B, 64, 640), **f32)     # t2 @ [W2^T | Ws1a^T]
+        self.w2T, self.sT = self.t2w[:, :, :128], self.t2w[:, :, 128:]
+        self.cvec = torch.empty((B, 512), **f32)        # per-cloud bias of the seg head
+        self.specs = [
+            (3, W.A, (1, 1, 1), 0, dict(gmax=self.g1)),
+            (12, [(self.w1T, W.c1b)] + W.B_tail, (0, 1, 1, 1), 0, dict(gmax=self.g2, per_cloud=(0,))),
+            (12, [(self.w1T, W.c1b), (self.w2T, W.c2b), W.C_tail], (0, 0, 0), 0,
+             dict(gmax=self.g3, per_cloud=(0, 1))),
+            (12, [(self.w1T, W.c1b), (self.sT, self.cvec)] + W.D_tail, (0, 1, 1, 1, 0), 1,
+             dict(out_cols=W.C1, per_cloud=(0, 1))),
+        ]
+        self.N = N
+        self.structs = None
+
+    def chain(self, i: int, x: torch.Tensor, chain_fn=None, out=None) -> None:
+        in_cols, layers, relus, mode, kw = self.specs[i]
+        if chain_fn is not None:
+            kw = dict(kw)
+            if out is not None:
+                kw["out"] = out
+            chain_fn(x, self.N, in_cols, layers, relus, mode, **kw)
+            return
+        if self.structs is None:
+            self.structs = [_build_chain(self.N, s[0], s[1], s[2], s[3], **s[4]) for s in self.specs]
+        if chain_timing is not None:  # torch events on the launch stream (bench.py)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            _run_chain(self.structs[i], x, out)
+            e1.record()
+            chain_timing.append((i, e0, e1))
+        else:
+            _run_chain(self.structs[i], x, out)
+
+
+def _folded(model):
+    """The model's folded weights, re-folded when any weight changed."""
+    cache = model._hip
+    if cache is None:
+        tensors = _tensors(model)
+        cache = model._hip = {"tensors": tensors, "sig": None}
+    sig = _signature(cache["tensors"])
+    if cache["sig"] != sig:
+        cache.update(sig=sig, W=_Folded(model), ws={})
+    return cache
+
+
 def segmentation_forward(model, points: torch.Tensor, covariances: torch.Tensor, chain=None) -> torch.Tensor:
     """model(points [B,N,3], covariances [B,N,9]) -> log-probs [B,N,C+1], eval mode."""
-    _chain = chain or _chain_gpu
-    sig = _signature(model)
-    if model._hip is None or model._hip[0] != sig:
-        model._hip = (sig, _Folded(model))
-    W = model._hip[1]
+    cache = _folded(model)
+    W = cache["W"]
     B, N, _ = points.shape
     dev = points.device
+    key = (B, N, dev)
+    ws = cache["ws"].get(key)
+    if ws is None:
+        ws = cache["ws"][key] = _Workspace(W, B, N, dev)
     # one [B,N,12] block; ndt_preprocessing already returns views of one
-    base = points
     if (points.stride() == (N * 12, 12, 1) and covariances.stride() == (N * 12, 12, 1)
             and covariances.data_ptr() == points.data_ptr() + 12 and points.dtype == torch.float32):
         x = points.as_strided((B, N, 12), (N * 12, 12, 1))
     else:
         x = torch.cat((points, covariances), dim=2).float().contiguous()
-    del base
-    # the three max-pooled vectors, -inf before the atomic maxima (ReLU'd maxima are >= 0)
-    Fp = W.C_tail[0].shape[1]
-    gbuf = torch.full((B, 2048 + Fp), float("-inf"), dtype=torch.float32, device=dev)
-    g1, g2, g3 = gbuf[:, :1024], gbuf[:, 1024:2048], gbuf[:, 2048:]
+    ws.gbuf.fill_(float("-inf"))
     # A: TNet(3)
-    _chain(x, N, 3, W.A, (1, 1, 1), 0, gmax=g1)
-    t1 = _fc_head(g1, W.t1, 3)                                        # [B,3,3]
-    w1T = torch.matmul(t1.reshape(B, 9), W.t1_basis).view(B, 12, 64)  # (W1 M(t1))^T
+    ws.chain(0, x, chain)
+    t1 = _fc_head(ws.g1, W.t1, 3, ws.h1, ws.h2, ws.t1)                        # [B,3,3]
+    torch.matmul(t1.reshape(B, 9), W.t1_basis, out=ws.w1T.view(B, 12 * 64))  # (W1 M(t1))^T
     # B: conv1 (+t1) then TNet(64)
-    _chain(x, N, 12, [(w1T, W.c1b)] + W.B_tail, (0, 1, 1, 1), 0, gmax=g2, per_cloud=(0,))
-    t2 = _fc_head(g2, W.t2, 64)                                       # [B,64,64]
-    t2w = torch.matmul(t2, W.t2_rhs)                                  # [B,64,640]
-    w2T, sT = t2w[:, :, :128], t2w[:, :, 128:]                        # conv2, seg conv1[:, :64]; t2 folded
+    ws.chain(1, x, chain)
+    t2 = _fc_head(ws.g2, W.t2, 64, ws.h1, ws.h2, ws.t2)                       # [B,64,64]
+    torch.matmul(t2, W.t2_rhs, out=ws.t2w)        # conv2 and seg conv1[:, :64] with t2 folded in
     # C: conv2, conv3, max over points
-    _chain(x, N, 12, [(w1T, W.c1b), (w2T, W.c2b), W.C_tail], (0, 0, 0), 0, gmax=g3, per_cloud=(0, 1))
+    ws.chain(2, x, chain)
     # D: seg head; the broadcast global feature enters as a per-cloud bias
-    cvec = torch.addmm(W.s1b, g3[:, : W.F], W.s1bT)                   # [B,512]
+    torch.addmm(W.s1b, ws.g3[:, : W.F], W.s1bT, out=ws.cvec)
     out = torch.empty((B, N, W.C1), dtype=torch.float32, device=dev)
-    _chain(x, N, 12, [(w1T, W.c1b), (sT, cvec)] + W.D_tail, (0, 1, 1, 1, 0), 1, out=out, out_cols=W.C1,
-           per_cloud=(0, 1))
+    ws.chain(3, x, chain, out=out)
     return out

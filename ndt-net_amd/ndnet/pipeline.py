@@ -1,0 +1,82 @@
+"""NDT preprocessing + NDTNetSegmentation eval forward as one HIP graph.
+
+The reference runs ``ndt_preprocessing`` then ``model(points, covariances)``
+per batch (ndnet/train_segmentation.py / ndnet/models/ndtnet.py:218-243), with
+a host round trip per cloud in between.  Here both halves are GPU-resident
+and launch ~45 kernels per batch (17 NDT launches, 4 point-MLP chains, the
+per-cloud FC heads / weight folds); on a 1 ms step the host-side launch cost
+of that sequence is a large fraction of the step.  ``GraphedSegmentation``
+captures the whole sequence once into a HIP graph (``torch.cuda.CUDAGraph``
+is hipGraph on ROCm) and replays it: every kernel still runs on every step,
+only the host launch work is gone.
+
+Capture is legal because neither half synchronises or allocates device
+memory after its first (warm-up) call: the NDT plan and the forward's
+workspace are cached per shape, and the NDT stamp-epoch wrap is handled on
+the device (k_reset / k_limits), not by host bookkeeping.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _lib
+from .preprocessing.ndtnet_preprocessing import ndt_preprocessing, get_plan
+
+
+class GraphedSegmentation:
+    """Replays ``model(*ndt_preprocessing(num_nds, points)[:2])`` from a graph.
+
+    Args:
+        model: an ``NDTNetSegmentation`` in eval mode on a cuda device.  Its
+            weights are folded at capture time; after changing them, build a
+            new ``GraphedSegmentation``.
+        num_nds: NDs per cloud (the reference's ``n_desired_nds``).
+        batch, num_points: the static input shape ``[batch, num_points, 3]``.
+        warmup: eager runs before capture (plan / workspace creation, kernel
+            attribute setup).
+
+    ``points`` is the static float32 input buffer; ``__call__(new_points)``
+    copies into it, replays, and returns the static ``[B, num_nds, C+1]``
+    output buffer (overwritten by the next replay -- clone to keep it).
+    """
+
+    def __init__(self, model, num_nds: int, batch: int, num_points: int,
+                 device: Optional[torch.device] = None, warmup: int = 2) -> None:
+        _lib.require_gpu()
+        if model.training:
+            raise ValueError("GraphedSegmentation needs an eval-mode model")
+        dev = torch.device(device) if device is not None else next(model.parameters()).device
+        if dev.type != "cuda":
+            raise ValueError("GraphedSegmentation needs the model on a cuda device")
+        self.model, self.num_nds, self.device = model, int(num_nds), dev
+        self.points = torch.zeros((batch, num_points, 3), dtype=torch.float32, device=dev)
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.no_grad(), torch.cuda.stream(side):
+            for _ in range(max(1, warmup)):
+                self._step()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.no_grad(), torch.cuda.graph(self.graph):
+            self.out = self._step()
+        self.plan = get_plan(batch, num_points, self.num_nds, -1, dev)
+
+    def _step(self) -> torch.Tensor:
+        p, c, _ = ndt_preprocessing(self.num_nds, self.points)
+        return self.model(p, c)
+
+    def replay(self) -> torch.Tensor:
+        self.graph.replay()
+        return self.out
+
+    def __call__(self, points: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if points is not None:
+            self.points.copy_(points, non_blocking=True)
+        return self.replay()
+
+    def stats(self) -> list:
+        """Per-cloud ``ndnet_ndt_stats`` of the last replay (synchronises)."""
+        return self.plan.host_stats()

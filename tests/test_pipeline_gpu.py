@@ -1,0 +1,83 @@
+"""The graph-captured pipeline and the device-side stamp-epoch wrap.
+
+* ``GraphedSegmentation`` replays exactly the eager kernels, so its output is
+  bit-identical to ``model(*ndt_preprocessing(k, points)[:2])``.
+* The NDT plan's voxel stamps carry a 26-bit run epoch; when it wraps the
+  device clears the stale stamps itself (k_reset / k_limits), so results stay
+  identical across the wrap with no host bookkeeping (graph replays never run
+  host code).  The cloud is wide and sparse so the bisection's grids exceed
+  the bitmap capacity and run in stamp mode.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(F=64, C=5, seed=3):
+    import torch
+    from ndnet.models.ndtnet import NDTNetSegmentation
+    torch.manual_seed(seed)
+    m = NDTNetSegmentation(3, C, F).cuda().eval()
+    with torch.no_grad():
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm1d):
+                mod.running_mean.uniform_(-0.2, 0.2)
+                mod.running_var.uniform_(0.5, 1.5)
+    return m
+
+
+def test_graph_replay_matches_eager():
+    import torch
+    from ndnet.synthetic import make_batch
+    from ndnet.pipeline import GraphedSegmentation
+    from ndnet.preprocessing.ndtnet_preprocessing import ndt_preprocessing
+    B, n, k = 4, 20000, 256
+    m = _model()
+    pts = torch.from_numpy(make_batch("L", B, n, seed0=11)).cuda()
+    with torch.no_grad():
+        p, c, _ = ndt_preprocessing(k, pts)
+        eager = m(p, c).clone()
+    g = GraphedSegmentation(m, k, B, n)
+    out = g(pts).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(out, eager)
+    assert all(s.rc == 0 and s.prune_rc == 0 for s in g.stats())
+    # new input through the same graph
+    pts2 = torch.from_numpy(make_batch("U", B, n, seed0=23)).cuda()
+    with torch.no_grad():
+        p, c, _ = ndt_preprocessing(k, pts2)
+        eager2 = m(p, c).clone()
+    out2 = g(pts2).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(out2, eager2)
+    assert not torch.equal(out2, out)
+
+
+def test_epoch_wrap_clears_stamps():
+    import torch
+    from ndnet import _lib
+    from ndnet.preprocessing.ndtnet_preprocessing import ndt_preprocessing, get_plan
+    rng = np.random.default_rng(5)
+    B, n, k = 2, 20000, 500
+    # 60 clusters in an 800^3 box: ~500 occupied voxels on grids of ~10^5 voxels
+    # (oracle: 4 bisection passes, accepted grids 49x49x48 and 49x48x46)
+    centers = rng.uniform(0, 800, (B, 60, 3))
+    pick = rng.integers(0, 60, (B, n))
+    pts = (np.take_along_axis(centers, pick[..., None], 1) + rng.normal(0, 4.0, (B, n, 3))).astype(np.float32)
+    t = torch.from_numpy(pts).cuda()
+    p0, c0, _ = ndt_preprocessing(k, t)
+    first = torch.cat((p0, c0), 2).clone()
+    plan = get_plan(B, n, k, -1, t.device)
+    st0 = plan.host_stats()
+    assert all(s.rc == 0 for s in st0)
+    assert any(s.len[0] * s.len[1] * s.len[2] > 32768 for s in st0)  # stamp-mode grids
+    rc = _lib.lib().ndnet_ndt_debug_set_epoch(plan.handle, ctypes.c_uint32((1 << 26) - 2))
+    assert rc == 0
+    for _ in range(3):  # epochs 2^26 - 1, then the wrap to 1 (stale stamps of epoch 1 exist), then 2
+        p, c, _ = ndt_preprocessing(k, t)
+        assert torch.equal(torch.cat((p, c), 2), first)
+        st = plan.host_stats()
+        assert [s.iters for s in st] == [s.iters for s in st0]

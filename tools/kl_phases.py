@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Per-phase time inside k_kl (the one-workgroup-per-cloud insertion-order /
+prune / emit kernel) from its s_memrealtime stamps (timing level 2).
+
+    python tools/kl_phases.py [--batch 16 --points 100000 --nds 1000 --kind U]
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "ndt-net_amd"))
+
+from ndnet import _lib  # noqa: E402
+from ndnet.preprocessing.ndtnet_preprocessing import ndt_preprocessing, get_plan  # noqa: E402
+from ndnet.synthetic import make_batch  # noqa: E402
+
+# (from mark, to mark, phase); the event order itself is built before k_kl by
+# k_kl_rank_chunks / k_kl_merge (time those with rocprofv3 --kernel-trace)
+PHASES = [(0, 1, "zero outputs"), (1, 2, "event count"), (2, 5, "list init"), (5, 6, "first occurrences"),
+          (6, 7, "walk scan"), (7, 8, "kills"), (8, 9, "shift"), (9, 10, "rows emitted"), (10, 11, "end")]
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--batch", type=int, default=16)
+ap.add_argument("--points", type=int, default=100_000)
+ap.add_argument("--nds", type=int, default=1000)
+ap.add_argument("--kind", default="U")
+ap.add_argument("--reps", type=int, default=5)
+a = ap.parse_args()
+dev = torch.device("cuda", 0)
+pts = torch.from_numpy(make_batch(a.kind, a.batch, a.points, seed0=0)).to(dev)
+ndt_preprocessing(a.nds, pts)
+plan = get_plan(a.batch, a.points, a.nds, -1, dev)
+_lib.check(_lib.lib().ndnet_ndt_set_timing(plan.handle, 2), "set_timing")
+acc = np.zeros(len(PHASES))
+for _ in range(a.reps):
+    ndt_preprocessing(a.nds, pts)
+    m = np.zeros(a.batch * 16, np.uint64)
+    _lib.check(_lib.lib().ndnet_ndt_debug_kl_marks(plan.handle, m.ctypes.data), "kl_marks")
+    m = m.reshape(a.batch, 16).astype(np.float64)
+    acc += np.array([((m[:, j] - m[:, i]) * 0.01).mean() for i, j, _ in PHASES])  # 100 MHz ticks -> us
+_lib.lib().ndnet_ndt_set_timing(plan.handle, 0)
+acc /= a.reps
+for (_, _, nm), v in zip(PHASES, acc):
+    print(f"  {nm:20s} {v:8.2f} us")
+print(f"  {'total':20s} {acc.sum():8.2f} us (mean over clouds)")
