@@ -70,15 +70,11 @@ def main() -> None:
     ap.add_argument("--eager", action="store_true", help="launch kernels from Python each step (no HIP graph)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from ndnet import distributed as D
+    rank, local, world = D.world_from_env()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+    dist = D.init("nccl", dev)  # RCCL; used only for the barrier and the max-over-ranks time
 
     from ndnet.models.ndtnet import NDTNetSegmentation
     from ndnet.models import pointnet_hip
@@ -113,21 +109,16 @@ def main() -> None:
         for _ in range(args.warmup):
             out = step()
         torch.cuda.synchronize()
-        if dist:
-            dist.barrier()
+        D.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             out = step()
         torch.cuda.synchronize()
-        if dist:
-            dist.barrier()
+        D.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+    elapsed = D.max_over_ranks(elapsed)
     total_clouds = world * B * args.steps
     value = total_clouds / elapsed
     stats = get_plan(B, n, k, -1, dev).host_stats()
@@ -239,7 +230,7 @@ def main() -> None:
         }
         print(json.dumps(line))
     if dist:
-        dist.destroy_process_group()
+        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -1,9 +1,26 @@
-// NDTNetSegmentation forward (eval mode) on gfx950: argument blocks of the
-// fused point-MLP kernel (pointnet_kernels.hip).  Layer weights are stored
-// transposed, W^T[K][N] row-major (K input channels x N output channels),
-// with BatchNorm folded in and K padded to a multiple of 4, N to 16.
-#pragma once
+/*
+ * ndnet_pointnet.h -- C ABI of the fused point-MLP kernel of libndnet_amd.so
+ * (ndt-net_amd/csrc/pointnet_kernels.hip), the NDTNetSegmentation eval forward
+ * on gfx950.
+ *
+ * It replaces the per-point Conv1d(k=1) + BatchNorm1d + ReLU chains of
+ * ndnet/models/ndtnet.py:45-60 (TNet convs), :148-161 (NDTNet convs) and
+ * :233-241 (segmentation head), each of which the reference runs as separate
+ * torch ops with activations round-tripping through memory.  Host side:
+ * ndt-net_amd/ndnet/models/pointnet_hip.py (BatchNorm folding, per-cloud
+ * steps, the four chains A-D).
+ *
+ * Layer weights are stored transposed, W^T[K][N] row-major (K input channels x
+ * N output channels), with BatchNorm folded in, K padded to a multiple of 4
+ * and N to 32.
+ */
+#ifndef NDNET_POINTNET_H_
+#define NDNET_POINTNET_H_
 #include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
 
 #define NDNET_PN_MAX_LAYERS 5
 
@@ -35,3 +52,15 @@ typedef struct ndnet_pn_chain {
   int32_t max_width2;     // widest activation of LDS region 1 (layers 0, 2, ... outputs)
   float* out;             // mode 1
 } ndnet_pn_chain;
+
+/* Runs one chain over `batch` clouds on `stream` (a hipStream_t; NULL = default
+ * stream).  Returns 0, NDNET_ERR_ARG (-20) for an inconsistent argument block
+ * (layer sizes, LDS region widths) or NDNET_ERR_HIP (-21) on a launch failure.
+ * No allocation, no synchronisation: graph-capturable. */
+int ndnet_pn_chain_run(const ndnet_pn_chain *args, int batch, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NDNET_POINTNET_H_ */

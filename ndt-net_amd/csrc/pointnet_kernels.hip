@@ -24,7 +24,7 @@
 #include <stdint.h>
 #include <stdio.h>
 
-#include "pointnet.h"
+#include "../../include/ndnet_pointnet.h"
 
 namespace {
 

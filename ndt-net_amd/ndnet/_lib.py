@@ -88,14 +88,16 @@ def lib() -> ctypes.CDLL:
             fn.restype = res
             fn.argtypes = args
         for name, (res, args) in POINTNET_EXPORTS.items():
-            if hasattr(_lib, name):
-                fn = getattr(_lib, name)
-                fn.restype = res
-                fn.argtypes = args
+            fn = getattr(_lib, name)
+            fn.restype = res
+            fn.argtypes = args
     return _lib
 
 
-POINTNET_EXPORTS: dict = {}
+# include/ndnet_pointnet.h
+POINTNET_EXPORTS: dict = {
+    "ndnet_pn_chain_run": (_I, [_P, _I, _P]),
+}
 
 
 def require_gpu() -> None:

@@ -48,7 +48,6 @@ class _Chain(ctypes.Structure):
                 ("out", ctypes.c_void_p)]
 
 
-_lib.POINTNET_EXPORTS["ndnet_pn_chain_run"] = (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p])
 
 
 def available() -> bool:
