@@ -32,6 +32,8 @@ typedef struct ndnet_pn_layer {
   int32_t K, N;           // padded sizes: K % 4 == 0, N % 32 == 0
   int32_t relu;
   int32_t ldw;            // row stride of wT in floats (>= N, % 4 == 0)
+  int32_t fuse_next;      // 1: this layer's output is produced in 64-column chunks, each consumed at once
+                          // by the next layer (whose N <= 256) -- the activation never occupies LDS whole
 } ndnet_pn_layer;
 
 // mode: 0 = max-pool the last layer over points into gmax[cloud][N]
@@ -49,7 +51,8 @@ typedef struct ndnet_pn_chain {
   float* gmax;            // mode 0: [B][gmax_ld], pre-set to -inf
   int32_t gmax_ld;
   int32_t max_width;      // widest activation of LDS region 0 (the input, layers 1, 3, ... outputs)
-  int32_t max_width2;     // widest activation of LDS region 1 (layers 0, 2, ... outputs)
+  int32_t max_width2;     // widest activation of LDS region 1 (layers 0, 2, ... outputs); a fused
+                          // layer's output is not stored in either region
   float* out;             // mode 1
 } ndnet_pn_chain;
 

@@ -37,7 +37,7 @@ chain_timing = None
 class _Layer(ctypes.Structure):
     _fields_ = [("wT", ctypes.c_void_p), ("w_cloud_stride", ctypes.c_int64), ("bias", ctypes.c_void_p),
                 ("bias_cloud_stride", ctypes.c_int64), ("K", ctypes.c_int32), ("N", ctypes.c_int32),
-                ("relu", ctypes.c_int32), ("ldw", ctypes.c_int32)]
+                ("relu", ctypes.c_int32), ("ldw", ctypes.c_int32), ("fuse_next", ctypes.c_int32)]
 
 
 class _Chain(ctypes.Structure):
@@ -159,14 +159,19 @@ def _fc_head(g: torch.Tensor, t: dict, dim: int, h1: torch.Tensor, h2: torch.Ten
     return out.view(-1, dim, dim)
 
 
-def _build_chain(n: int, in_cols: int, layers, relus, mode: int, gmax=None, out_cols=0, per_cloud=()) -> "_Chain":
-    """ctypes argument block of one ``ndnet_pn_chain_run`` (x / out set per call)."""
+def _build_chain(n: int, in_cols: int, layers, relus, mode: int, gmax=None, out_cols=0, per_cloud=(),
+                 fuse=()) -> "_Chain":
+    """ctypes argument block of one ``ndnet_pn_chain_run`` (x / out set per call).
+    Layers in ``fuse`` are produced in 64-column chunks straight into the next
+    layer (include/ndnet_pointnet.h)."""
     ch = _Chain()
     ch.x_ld = 12
     ch.in_cols = in_cols
     ch.num_points = n
     ch.num_layers = len(layers)
-    widths = [layers[0][0].shape[-2], 4]  # LDS regions: layer l reads l & 1, writes (l + 1) & 1
+    # LDS regions: layer l reads l & 1, writes (l + 1) & 1; the input tile is
+    # zero-filled to a 16-column K-slab; a fused layer's output has no region
+    widths = [_pad(layers[0][0].shape[-2], 16), 4]
     for i, (w, b) in enumerate(layers):
         L = ch.L[i]
         L.wT = w.data_ptr()
@@ -176,6 +181,9 @@ def _build_chain(n: int, in_cols: int, layers, relus, mode: int, gmax=None, out_
         L.bias = b.data_ptr()
         L.bias_cloud_stride = b.stride(0) if b.dim() == 2 else 0
         L.relu = relus[i]
+        L.fuse_next = 1 if i in fuse else 0
+        if i in fuse:
+            continue
         if i + 1 < len(layers) or mode == 1:
             widths[(i + 1) & 1] = max(widths[(i + 1) & 1], L.N)
     ch.mode = mode
@@ -195,12 +203,12 @@ def _run_chain(ch: "_Chain", x: torch.Tensor, out=None) -> None:
 
 
 def _chain_gpu(x: torch.Tensor, n: int, in_cols: int, layers, relus, mode: int, gmax=None, out=None, out_cols=0,
-               per_cloud=()) -> None:
-    _run_chain(_build_chain(n, in_cols, layers, relus, mode, gmax, out_cols, per_cloud), x, out)
+               per_cloud=(), fuse=()) -> None:
+    _run_chain(_build_chain(n, in_cols, layers, relus, mode, gmax, out_cols, per_cloud, fuse), x, out)
 
 
 def _chain_torch(x: torch.Tensor, n: int, in_cols: int, layers, relus, mode: int, gmax=None, out=None,
-                 out_cols=0, per_cloud=()) -> None:
+                 out_cols=0, per_cloud=(), fuse=()) -> None:
     """What one ``ndnet_pn_chain_run`` computes, in torch ops (tests: checks the
     folding algebra on CPU and the kernel against it on the GPU)."""
     h = x[..., :in_cols].float()
@@ -237,8 +245,9 @@ class _Workspace:
             (12, [(self.w1T, W.c1b)] + W.B_tail, (0, 1, 1, 1), 0, dict(gmax=self.g2, per_cloud=(0,))),
             (12, [(self.w1T, W.c1b), (self.w2T, W.c2b), W.C_tail], (0, 0, 0), 0,
              dict(gmax=self.g3, per_cloud=(0, 1))),
+            # the 512-wide seg conv1 output feeds conv2 chunk by chunk (never stored whole)
             (12, [(self.w1T, W.c1b), (self.sT, self.cvec)] + W.D_tail, (0, 1, 1, 1, 0), 1,
-             dict(out_cols=W.C1, per_cloud=(0, 1))),
+             dict(out_cols=W.C1, per_cloud=(0, 1), fuse=(1,))),
         ]
         self.N = N
         self.structs = None

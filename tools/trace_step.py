@@ -20,7 +20,10 @@ def rows_from(path):
                        r.get("LDS_Block_Size", r.get("Lds_Size", "")), r.get("VGPR_Count", r.get("Arch_VGPR_Count", "")))
         return
     import sqlite3
-    db = sqlite3.connect(glob.glob(os.path.join(path, "*.db"))[0])
+    dbs = glob.glob(os.path.join(path, "*.db"))
+    if not dbs:
+        raise SystemExit(f"no kernel trace under {path}")
+    db = sqlite3.connect(dbs[0])
     for r in db.execute("select name, start, end, grid_x, workgroup_x, lds_size, vgpr_count from kernels"):
         yield r
 
