@@ -32,6 +32,7 @@ extern "C" {
 #define NDNET_OK 0
 #define NDNET_ERR_ARG (-20)  /* bad argument (NULL, zero size, unsupported point_dim) */
 #define NDNET_ERR_HIP (-21)  /* HIP runtime failure; message on stderr */
+#define NDNET_ERR_SYNC (-22) /* a cloud's workgroups did not meet within ~2 s (k_front barrier): the cloud fails */
 #define NDNET_PRUNE_POISON (-8) /* a prune walk reached a list entry the reference never wrote */
 
 /* Per-cloud outcome of a batched run; written on the device. */
@@ -110,6 +111,15 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
                           uint64_t voxel_capacity, void **plan);
 void ndnet_ndt_plan_destroy(void *plan);
 
+/* Launch path of a plan: 1 = one launch per stage (limits, 15 bisection
+ * passes, dense ids, three binning kernels), 2 = the fused front kernel
+ * k_front (limits through binning in one launch; needs every workgroup of a
+ * cloud resident, so only where the plan's shape allows it), 0 = 2 where
+ * allowed, else 1 (the default).  Both paths give identical results.
+ * ndnet_ndt_get_path returns the path in use. */
+int ndnet_ndt_set_path(void *plan, int path);
+int ndnet_ndt_get_path(void *plan);
+
 /* d_points: [batch][num_points][3] float32 on the device (the tensor
  * ndt_preprocessing receives).  d_labels: [batch][num_points] int32 class ids
  * or NULL.  d_out: [batch][num_desired][12] float32 = mean(3) | covariance(9)
@@ -156,6 +166,13 @@ int ndnet_ndt_debug_set_epoch(void *plan, uint32_t epoch);
  * 5 list initialised, 6 first occurrences, 7 walk scan, 8 kills, 9 shift,
  * 10 rows emitted, 11 end; 3 and 4 unused); synchronises. */
 int ndnet_ndt_debug_kl_marks(void *plan, unsigned long long *marks);
+
+/* k_front phase stamps of the last run at timing level 2 (workgroup 0 of each
+ * cloud): marks[cloud * 32 + i], 100 MHz ticks; 0 start, 1/2 limits barrier
+ * in/out, 3+2p/4+2p pass p barrier in/out (p < 7; later passes share 17/18),
+ * 20 accepted, 21 dense ids, 22 point NDs, 23/24 offsets barrier in/out,
+ * 25 offsets, 26 scattered; synchronises. */
+int ndnet_ndt_debug_front_marks(void *plan, unsigned long long *marks);
 
 /* Library identification (no GPU needed). */
 const char *ndnet_amd_version(void);

@@ -51,12 +51,38 @@ NDNET_FN uint32_t axis_index(double p, double off, double vs, double inv_vs) {
   return floor_to_u32(floor(d / vs));
 }
 
+// Fast path of one axis of metric_to_voxel_space: the floor of d * (1/vs)
+// where that product lies safely away from an integer and the floor fits an
+// int32 (then it equals the reference's floor of the division and its
+// unsigned conversion); *ok is false otherwise and the caller takes the
+// exact path.
+NDNET_FN uint32_t axis_index_fast(double p, double off, double inv_vs, bool& ok) {
+  const double d = p - off;
+  const double qa = d * inv_vs;
+  const double f = floor(qa);
+  const double r = qa - f;
+  const double tol = fabs(qa) * 0x1p-46 + 0x1p-60;
+  ok = r > tol && r < 1.0 - tol && f >= -2147483648.0 && f < 2147483648.0;
+  return (uint32_t)(int32_t)(ok ? f : 0.0);
+}
+
 // voxel.c:83-103 + 177-189.  Returns kInvalid when the point is out of grid.
+// The exact division runs behind a wave-uniform branch, only when some lane
+// of the wave needs it, so the common case issues no double division.
 NDNET_FN uint32_t voxel_key(double x, double y, double z, const double* off, const uint32_t* len, double vs,
                             double inv_vs) {
-  const uint32_t vx = axis_index(x, off[0], vs, inv_vs);
-  const uint32_t vy = axis_index(y, off[1], vs, inv_vs);
-  const uint32_t vz = axis_index(z, off[2], vs, inv_vs);
+  bool o0, o1, o2;
+  uint32_t vx = axis_index_fast(x, off[0], inv_vs, o0);
+  uint32_t vy = axis_index_fast(y, off[1], inv_vs, o1);
+  uint32_t vz = axis_index_fast(z, off[2], inv_vs, o2);
+  const bool ok = o0 && o1 && o2;
+  if (!__all(ok)) {
+    if (!ok) {
+      vx = axis_index(x, off[0], vs, inv_vs);
+      vy = axis_index(y, off[1], vs, inv_vs);
+      vz = axis_index(z, off[2], vs, inv_vs);
+    }
+  }
   if (vx >= len[0] || vy >= len[1] || vz >= len[2]) return kInvalid;
   return vz * len[0] * len[1] + vy * len[0] + vx;
 }

@@ -1,0 +1,718 @@
+// ndt_front.h -- k_front: the whole front of ndt_downsample in ONE launch.
+//
+// Included by ndt_kernels.hip inside its anonymous namespace (it uses
+// CloudCtl, voxel_key, the block scans and finish_pass from there).
+//
+// What it replaces, per cloud (reference: pointclouds.c:40-66 limits,
+// ndt.c:136-194 bisection over estimate_ndt's occupancy,
+// normal_distributions.c:28-175 voxel assignment in worker order):
+//   k_limits + 15 x k_search_pass + k_dense + k_bin_count + k_bin_offsets +
+//   k_bin_scatter  (19 launches, ~260 us at 16 x 100k points)
+//
+// Geometry: G workgroups of 1024 threads per cloud (blockIdx.x = g,
+// blockIdx.y = cloud), G * B <= CUs so every workgroup of a cloud is resident
+// at once (checked on the host; G = 1 needs no residency at all).  Workgroup
+// g owns `bpw` consecutive 1024-point bins; thread t holds point t of each of
+// its bins in registers for the whole bisection, so the points are read from
+// HBM once per run instead of once per pass.
+//
+// The G workgroups of a cloud meet at cloud barriers (one per phase): every
+// wave drains its write-through (sc1) stores / atomics, the workgroup
+// barriers, lane 0 adds to the cloud's counter and polls it with sc1 loads;
+// everything handed across the barrier is read back with sc1 loads
+// (MI355X_MICROARCH.md, inter-workgroup visibility, table row 1).  Each
+// workgroup applies the bisection rule itself to the same summed counts, so
+// no decision has to be broadcast.  A barrier that has not completed after
+// ~2 s fails the cloud (NDNET_ERR_SYNC) instead of hanging.
+//
+// Phases:
+//   0     limits: per-workgroup min/max keys -> [B][G][6], barrier, reduce
+//   pass  voxel key of every estimated point; distinct voxels through an LDS
+//         bitmap OR'd into the pass's global bitmap (V <= 32768), or an LDS
+//         hash + per-voxel stamps (larger grids); per-workgroup fresh counts
+//         -> record slots, barrier, sum, ndt.c:168-187.  A point out of the
+//         grid abandons the rest of its worker chunk (normal_distributions.c
+//         :47-52): on that rare pass the survivors are recounted.
+//   dense accepted occupancy -> dense ids in ascending voxel order
+//         (normal_distributions.c NDs are allocated per linear index); each
+//         workgroup writes its slice of dense_of / vox.
+//   bins  per point its ND; per bin a stable rank of the point among the
+//         bin's points of the same ND (one wave per bin: 64-key bitonic sort
+//         in registers, runs, an LDS cursor per ND); per-workgroup ND counts
+//         -> [B][G][ndcap], barrier, ND bases (scan over NDs) + the counts of
+//         earlier workgroups and bins, and every point written to its ND's
+//         contiguous run in index order -- the order the reference's
+//         1-worker schedule feeds each ND's Welford update.
+#pragma once
+
+constexpr int kFrontThreads = 1024;
+constexpr int kFrontWaves = kFrontThreads / 64;
+constexpr int kFrontR = 8;          // bins per workgroup whose points stay in registers
+constexpr int kFrontTable = 8192;   // LDS words: byte map of a small grid (32768 voxels) or hash slots
+constexpr int kFrontPhases = 40;    // record slots per cloud and run
+constexpr int kRecWords = 16;       // per-workgroup record: [0] count, [1] any bad, [2..9] first bad per worker
+constexpr int kPhDenseLarge = 36;
+constexpr int kBarStride = 16;      // u32 between the barrier counters of two clouds (64 B)
+constexpr int kNdtErrSync = -22;    // NDNET_ERR_SYNC
+static_assert(kFrontTable * 4 >= kBitsCap, "the byte map holds a whole small grid");
+
+struct FrontArgs {
+  CloudCtl* ctl;
+  const int32_t* lbl;           // [B][n] or null
+  uint32_t* stamps;             // [B][vcap]
+  uint32_t* gbits;              // [B][2][kBitsWords]
+  uint32_t* dense_of;           // [B][vcap]
+  uint32_t* vox;                // [B][ndcap]
+  uint32_t* nd_n;               // [B][ndcap]
+  uint32_t* nd_base;            // [B][ndcap]
+  void* nd_pts;                 // [B * n + slack][3] T
+  uint16_t* nd_lbl;             // [B][n] or null
+  unsigned long long* lims;     // [B][G][6]
+  uint32_t* rec;                // [B][kFrontPhases][G][kRecWords]
+  uint32_t* wgcnt;              // [B][G][ndcap]
+  uint32_t* bar;                // [B * kBarStride]
+  unsigned long long* marks;    // [B][32] phase stamps of workgroup 0 (timing level 2), or null
+  uint64_t n, k, vcap;
+  uint32_t ndcap, G, bpw;
+  uint32_t rbs;                 // points per rank bin (512 or 1024)
+};
+
+// The shared bisection state of one workgroup (every workgroup of a cloud
+// holds an identical copy).
+struct FrontState {
+  double lim[6];
+  double guess, lo, hi, vs;
+  double off[3];
+  uint32_t len[3];
+  uint64_t V;
+  uint32_t state, iter, stamp, mode, num_nds;
+  int32_t rc;
+  uint32_t cut[kWorkers];
+  uint32_t sync_no;
+  uint32_t ok;
+  uint32_t count;
+  uint32_t anybad;
+  unsigned long long limkey[6];
+};
+
+__device__ inline uint32_t ld_sc1(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void st_sc1(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// v of lane (lane ^ S), through DPP where the pattern allows (strides 1..8
+// stay inside a row), ds_swizzle for 16, ds_bpermute for 32.
+template <int S>
+__device__ inline uint32_t xor_lane(uint32_t v) {
+  const int x = (int)v;
+  if constexpr (S == 1) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  } else if constexpr (S == 2) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  } else if constexpr (S == 4) {
+    const int h = __builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, false);    // row_half_mirror: i ^ 7
+    return (uint32_t)__builtin_amdgcn_mov_dpp(h, 0x1B, 0xF, 0xF, false);  // quad_perm [3,2,1,0]: ^ 3
+  } else if constexpr (S == 8) {
+    const int h = __builtin_amdgcn_mov_dpp(x, 0x140, 0xF, 0xF, false);    // row_mirror: i ^ 15
+    return (uint32_t)__builtin_amdgcn_mov_dpp(h, 0x141, 0xF, 0xF, false); // row_half_mirror: ^ 7
+  } else if constexpr (S == 16) {
+    return (uint32_t)__builtin_amdgcn_ds_swizzle(x, 0x401F);              // bitmask mode, xor 16
+  } else {
+    return (uint32_t)__shfl_xor(x, 32, 64);
+  }
+}
+
+template <int S>
+__device__ inline unsigned long long xor_lane64(unsigned long long v) {
+  return (unsigned long long)xor_lane<S>((uint32_t)v) | ((unsigned long long)xor_lane<S>((uint32_t)(v >> 32)) << 32);
+}
+
+template <bool MAX>
+__device__ inline unsigned long long wave_minmax64(unsigned long long v) {
+  auto f = [](unsigned long long a, unsigned long long b) { return MAX ? (a > b ? a : b) : (a < b ? a : b); };
+  v = f(v, xor_lane64<1>(v));
+  v = f(v, xor_lane64<2>(v));
+  v = f(v, xor_lane64<4>(v));
+  v = f(v, xor_lane64<8>(v));
+  v = f(v, xor_lane64<16>(v));
+  v = f(v, xor_lane64<32>(v));
+  return v;
+}
+
+// Cloud barrier of the G workgroups of one cloud.  Returns false (and fails
+// the cloud) if the other workgroups did not arrive within ~2 s.
+__device__ inline bool cloud_sync(FrontState& s, uint32_t* bar, uint32_t G) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    s.sync_no++;
+    if (G > 1) {
+      const uint32_t target = G * s.sync_no;
+      __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (ld_sc1(bar) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 100 MHz clock: 2 s
+          s.ok = 0;
+          break;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  return s.ok != 0;
+}
+
+// Large-grid dedup: an LDS hash in front of the per-voxel stamps (bounded
+// probing; a full table falls through to the global stamp, which dedups too).
+__device__ inline uint32_t stamp_key_front(uint32_t key, uint32_t* table, uint32_t* stamps, uint32_t stamp) {
+  uint32_t h = (key * 2654435761u) >> (32 - 13);
+#pragma unroll 1
+  for (int probe = 0; probe < 32; probe++) {
+    const uint32_t cur = table[h];
+    if (cur == key) return 0;
+    if (cur == kInvalid) {
+      const uint32_t old = atomicCAS(&table[h], kInvalid, key);
+      if (old == kInvalid) break;
+      if (old == key) return 0;
+    }
+    h = (h + 1) & (kFrontTable - 1);
+  }
+  uint32_t* sp = stamps + key;
+  if (ld_sc1(sp) == stamp) return 0;
+  return atomicExch(sp, stamp) != stamp;
+}
+
+// 64 keys sorted ascending across the wave (bitonic network in registers).
+__device__ inline uint32_t wave_sort64(uint32_t key) {
+  const uint32_t lane = threadIdx.x & 63;
+#define NDNET_BITONIC(SIZE, STRIDE)                                             \
+  {                                                                             \
+    const uint32_t o = xor_lane<STRIDE>(key);                                   \
+    const bool up = (SIZE) == 64 || (lane & (SIZE)) == 0;                       \
+    const bool lower = (lane & (STRIDE)) == 0;                                  \
+    const uint32_t mn = key < o ? key : o, mx = key < o ? o : key;              \
+    key = (lower == up) ? mn : mx;                                              \
+  }
+  NDNET_BITONIC(2, 1)
+  NDNET_BITONIC(4, 2) NDNET_BITONIC(4, 1)
+  NDNET_BITONIC(8, 4) NDNET_BITONIC(8, 2) NDNET_BITONIC(8, 1)
+  NDNET_BITONIC(16, 8) NDNET_BITONIC(16, 4) NDNET_BITONIC(16, 2) NDNET_BITONIC(16, 1)
+  NDNET_BITONIC(32, 16) NDNET_BITONIC(32, 8) NDNET_BITONIC(32, 4) NDNET_BITONIC(32, 2) NDNET_BITONIC(32, 1)
+  NDNET_BITONIC(64, 32) NDNET_BITONIC(64, 16) NDNET_BITONIC(64, 8) NDNET_BITONIC(64, 4) NDNET_BITONIC(64, 2)
+  NDNET_BITONIC(64, 1)
+#undef NDNET_BITONIC
+  return key;
+}
+
+template <typename T>
+__device__ inline void front_point(const T* p, uint64_t i, T& x, T& y, T& z) {
+  x = p[3 * i + 0];
+  y = p[3 * i + 1];
+  z = p[3 * i + 2];
+}
+
+// phase stamp (s_memrealtime, 100 MHz) of workgroup 0 of the cloud
+#define FRONT_MARK(i)                                                                                     \
+  do {                                                                                                    \
+    if (A.marks && g == 0 && t == 0) A.marks[(uint64_t)b * 32 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
+template <typename T>
+__global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ pts, FrontArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t f_smem[];
+  __shared__ FrontState s;
+  __shared__ uint32_t scratch[32];
+  __shared__ uint32_t s_bad[kWorkers];
+  const int b = blockIdx.y;
+  const uint32_t g = blockIdx.x, G = A.G, bpw = A.bpw, rbs = A.rbs, nrb = bpw * (1024 / A.rbs);
+  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  CloudCtl& c = A.ctl[b];
+  const uint64_t n = A.n;
+  const uint64_t chunk = n / kWorkers, n8 = chunk * kWorkers;
+  const T* p = pts + (uint64_t)b * n * 3;
+  uint32_t* bar = A.bar + (uint64_t)b * kBarStride;
+  uint32_t* table = f_smem;                                   // kFrontTable words
+  uint8_t* bytemap = (uint8_t*)f_smem;                        // small grids: one byte per voxel
+  uint32_t* binfo = f_smem + kFrontTable;                     // [bpw][1024]: key, then did << 10 | rank
+  uint32_t* hist = binfo + (uint64_t)bpw * 1024;              // [nrb][ndcap]
+  uint32_t* stamps = A.stamps + (uint64_t)b * A.vcap;
+  const uint64_t bin0 = (uint64_t)g * bpw;
+  const uint32_t epoch = c.epoch;
+  FRONT_MARK(0);
+
+  if (t == 0) {
+    s.sync_no = 0;
+    s.ok = 1;
+    s.rc = 0;
+    for (int a = 0; a < 3; a++) {
+      s.limkey[a] = ord_key(kDblMin);      // max starts at DBL_MIN (pointclouds.c:44-46)
+      s.limkey[3 + a] = ord_key(kDblMax);  // min starts at DBL_MAX
+    }
+  }
+  if (c.clear_stamps) {  // epoch wrap (k_reset): rare, cost irrelevant
+    for (uint64_t v = (uint64_t)g * kFrontThreads + t; v < A.vcap; v += (uint64_t)G * kFrontThreads)
+      st_sc1(stamps + v, 0u);
+  }
+  // ---- phase 0: points into registers, bounding box over all n points ----
+  T px[kFrontR], py[kFrontR], pz[kFrontR];
+  // per-thread extremes in T (the double of a float is exact and ordered
+  // alike; NaN never wins, pointclouds.c maxf / minf)
+  T mx[3] = {-INFINITY, -INFINITY, -INFINITY}, mn[3] = {INFINITY, INFINITY, INFINITY};
+  auto lim_acc = [&](T x, T y, T z) {
+    const T v[3] = {x, y, z};
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      mx[a] = v[a] > mx[a] ? v[a] : mx[a];
+      mn[a] = v[a] < mn[a] ? v[a] : mn[a];
+    }
+  };
+#pragma unroll
+  for (int j = 0; j < kFrontR; j++) {
+    const uint64_t i = (bin0 + j) * 1024 + t;
+    if ((uint32_t)j < bpw && i < n) {
+      front_point(p, i, px[j], py[j], pz[j]);
+      lim_acc(px[j], py[j], pz[j]);
+    } else {
+      px[j] = py[j] = pz[j] = T(0);
+    }
+  }
+  for (uint32_t j = kFrontR; j < bpw; j++) {
+    const uint64_t i = (bin0 + j) * 1024 + t;
+    if (i < n) {
+      T x, y, z;
+      front_point(p, i, x, y, z);
+      lim_acc(x, y, z);
+    }
+  }
+  {
+    unsigned long long kk[6];
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      const double dx = (double)mx[a], dn = (double)mn[a];
+      kk[a] = wave_minmax64<true>(ord_key(dx > kDblMin ? dx : kDblMin));
+      kk[3 + a] = wave_minmax64<false>(ord_key(dn < kDblMax ? dn : kDblMax));
+    }
+    __syncthreads();  // s.limkey initialised
+    if (lane == 0) {
+      for (int a = 0; a < 3; a++) {
+        atomicMax(&s.limkey[a], kk[a]);
+        atomicMin(&s.limkey[3 + a], kk[3 + a]);
+      }
+    }
+  }
+  // zero pass 0's bitmap (my slice), write-through
+  {
+    uint32_t* gb = A.gbits + (uint64_t)b * 2 * kBitsWords;
+    for (uint32_t w = g * kFrontThreads + t; w < (uint32_t)kBitsWords; w += G * kFrontThreads) st_sc1(gb + w, 0u);
+  }
+  __syncthreads();
+  unsigned long long* lims = A.lims + (uint64_t)b * G * 6;
+  if (t < 6) __hip_atomic_store(lims + (uint64_t)g * 6 + t, s.limkey[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  FRONT_MARK(1);
+  if (!cloud_sync(s, bar, G)) goto fail;
+  FRONT_MARK(2);
+  if (t < 6) s.limkey[t] = t < 3 ? 0ull : ~0ull;
+  __syncthreads();
+  for (uint32_t e = t; e < 6 * G; e += kFrontThreads) {
+    const unsigned long long v = __hip_atomic_load(lims + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t a = e % 6;
+    if (a < 3) atomicMax(&s.limkey[a], v);
+    else atomicMin(&s.limkey[a], v);
+  }
+  __syncthreads();
+  if (t == 0) {
+    for (int a = 0; a < 6; a++) s.lim[a] = ord_unkey(s.limkey[a]);
+    s.lo = kMinGuess;
+    s.hi = kMaxGuess;
+    s.iter = 0;
+    s.state = kSearching;
+    s.guess = (kMaxGuess - kMinGuess) / 2.0;  // ndt.c:136
+  }
+  __syncthreads();
+
+  // ---- bisection passes ----
+  for (;;) {
+    // grid of this guess (voxel.c:61-81), identical in every workgroup
+    if (t == 0) {
+      uint64_t V = 1;
+      for (int a = 0; a < 3; a++) {
+        const double d = s.lim[a] - s.lim[3 + a];
+        const double q = ceil(d / s.guess);
+        int li;
+        if (q >= -2147483648.0 && q < 2147483648.0) li = (int)q;
+        else li = (int)0x80000000;  // x86 cvttsd2si overflow value
+        s.len[a] = (uint32_t)li;
+        s.off[a] = s.lim[3 + a];
+        V *= (uint64_t)s.len[a];
+      }
+      s.V = V;
+      s.stamp = epoch * 32u + s.iter;
+      if (V > A.vcap) {  // the reference's malloc of V NDs would be the failure point
+        s.state = kFailed;
+        s.rc = -1;
+        s.vs = s.guess;
+      }
+    }
+    __syncthreads();
+    if (s.state != kSearching) break;
+    const uint64_t V = s.V;
+    const bool small = V <= (uint64_t)kBitsCap;
+    const uint32_t words = small ? (uint32_t)((V + 31) / 32) : 0u;
+    const uint32_t parity = s.iter & 1u;
+    const uint32_t stamp = s.stamp;
+    uint32_t* gb = A.gbits + ((uint64_t)b * 2 + parity) * kBitsWords;
+    if (small) {
+      for (uint32_t w = t; w < 8 * words; w += kFrontThreads) table[w] = 0;
+    } else {
+      for (uint32_t w = t; w < (uint32_t)kFrontTable; w += kFrontThreads) table[w] = kInvalid;
+    }
+    if (t < (uint32_t)kWorkers) s_bad[t] = kInvalid;
+    __syncthreads();
+    if (s.iter == 1) FRONT_MARK(27);
+    const double vs = s.guess, inv_vs = 1.0 / vs;
+    double off[3] = {s.off[0], s.off[1], s.off[2]};
+    uint32_t len[3] = {s.len[0], s.len[1], s.len[2]};
+    uint32_t fresh = 0;
+    // key of every estimated point into binfo (the accepted pass's keys feed the binning)
+    auto visit = [&](uint32_t j, uint64_t i, T x, T y, T z) {
+      uint32_t key = kInvalid;
+      if (i < n8) {
+        key = voxel_key((double)x, (double)y, (double)z, off, len, vs, inv_vs);
+        if (key == kInvalid) atomicMin(&s_bad[i / chunk], (uint32_t)i);
+        else if (small) bytemap[key] = 1;
+        else fresh += stamp_key_front(key, table, stamps, stamp);
+      }
+      binfo[j * 1024 + t] = key;
+    };
+#pragma unroll
+    for (int j = 0; j < kFrontR; j++)
+      if ((uint32_t)j < bpw) visit(j, (bin0 + j) * 1024 + t, px[j], py[j], pz[j]);
+    for (uint32_t j = kFrontR; j < bpw; j++) {
+      const uint64_t i = (bin0 + j) * 1024 + t;
+      T x = 0, y = 0, z = 0;
+      if (i < n8) front_point(p, i, x, y, z);
+      visit(j, i, x, y, z);
+    }
+    __syncthreads();
+    if (s.iter == 1) FRONT_MARK(28);
+    if (small) {  // byte map -> 32-voxel words, OR'd into the pass's global bitmap
+      for (uint32_t w = t; w < words; w += kFrontThreads) {
+        uint32_t bits = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          const uint32_t v = table[8 * w + q];
+          bits |= ((v & 1u) | ((v >> 7) & 2u) | ((v >> 14) & 4u) | ((v >> 21) & 8u)) << (4 * q);
+        }
+        if (bits) fresh += __popc(bits & ~atomicOr(&gb[w], bits));
+      }
+    }
+    {  // the other parity's bitmap is the next pass's: zero my slice
+      uint32_t* gn = A.gbits + ((uint64_t)b * 2 + (parity ^ 1u)) * kBitsWords;
+      for (uint32_t w = g * kFrontThreads + t; w < (uint32_t)kBitsWords; w += G * kFrontThreads) st_sc1(gn + w, 0u);
+    }
+    if (s.iter == 1) FRONT_MARK(29);
+    fresh = block_sum_u32(fresh, scratch);
+    if (s.iter == 1) FRONT_MARK(30);
+    uint32_t* rec = A.rec + (((uint64_t)b * kFrontPhases + 1 + 2 * s.iter) * G) * kRecWords;
+    if (t == 0) {
+      uint32_t anyb = 0;
+      for (int w = 0; w < kWorkers; w++) anyb |= s_bad[w] != kInvalid;
+      st_sc1(rec + g * kRecWords + 0, fresh);
+      st_sc1(rec + g * kRecWords + 1, anyb);
+      if (anyb)
+        for (int w = 0; w < kWorkers; w++) st_sc1(rec + g * kRecWords + 2 + w, s_bad[w]);
+      s.count = 0;
+      s.anybad = 0;
+    }
+    FRONT_MARK(3 + 2 * (s.iter < 7 ? s.iter : 7));
+    if (!cloud_sync(s, bar, G)) goto fail;
+    FRONT_MARK(4 + 2 * (s.iter < 7 ? s.iter : 7));
+    if (t < G) {
+      atomicAdd(&s.count, ld_sc1(rec + t * kRecWords + 0));
+      if (ld_sc1(rec + t * kRecWords + 1)) atomicOr(&s.anybad, 1u);
+    }
+    if (t < (uint32_t)kWorkers) s.cut[t] = kInvalid;
+    __syncthreads();
+    if (s.iter == 1) FRONT_MARK(31);
+    uint32_t mode = small ? parity : 2u;
+    if (s.anybad) {
+      // a point out of the grid abandoned the rest of its worker chunk
+      // (normal_distributions.c:47-52): recount the survivors through stamps
+      for (uint32_t e = t; e < G * kWorkers; e += kFrontThreads) {
+        const uint32_t gg = e / kWorkers, w = e % kWorkers;
+        if (ld_sc1(rec + gg * kRecWords + 1)) atomicMin(&s.cut[w], ld_sc1(rec + gg * kRecWords + 2 + w));
+      }
+      for (uint32_t w = t; w < (uint32_t)kFrontTable; w += kFrontThreads) table[w] = kInvalid;
+      __syncthreads();
+      const uint32_t stamp2 = epoch * 32u + 16u + s.iter;
+      uint32_t f2 = 0;
+      for (uint32_t j = 0; j < bpw; j++) {
+        const uint64_t i = (bin0 + j) * 1024 + t;
+        const uint32_t key = binfo[j * 1024 + t];
+        if (key != kInvalid && i < s.cut[i / chunk]) f2 += stamp_key_front(key, table, stamps, stamp2);
+      }
+      f2 = block_sum_u32(f2, scratch);
+      uint32_t* rec2 = A.rec + (((uint64_t)b * kFrontPhases + 2 + 2 * s.iter) * G) * kRecWords;
+      if (t == 0) {
+        st_sc1(rec2 + g * kRecWords, f2);
+        s.count = 0;
+        s.stamp = stamp2;
+      }
+      if (!cloud_sync(s, bar, G)) goto fail;
+      if (t < G) atomicAdd(&s.count, ld_sc1(rec2 + t * kRecWords));
+      mode = 2u;
+      __syncthreads();
+    }
+    // ndt.c:168-187, every workgroup alike
+    if (t == 0) {
+      const uint32_t count = s.count;
+      if (g == 0 && s.iter < 16) {
+        c.guesses[s.iter] = s.guess;
+        c.counts[s.iter] = count;
+      }
+      s.mode = mode;
+      if ((double)count > (double)A.k * (1 + kUpper)) {
+        s.lo = s.guess;
+      } else if (count < A.k) {
+        s.hi = s.guess;
+      } else {
+        s.state = kAccepted;
+        s.vs = s.guess;
+        s.num_nds = count;
+      }
+      s.iter++;
+      if (s.state == kSearching) {
+        const double gn = s.lo + (s.hi - s.lo) / 2.0;
+        s.guess = gn;
+        if (s.iter == (uint32_t)kMaxIters) {
+          s.state = kFailed;
+          s.rc = -3;  // "Reached maximum number of iterations!" (ndt.c:191-194)
+          s.vs = gn;
+        } else {
+          for (int w = 0; w < kWorkers; w++) s.cut[w] = kInvalid;
+        }
+      }
+    }
+    __syncthreads();
+    if (s.state != kSearching) break;
+  }
+
+  // ---- publish the search outcome for the later kernels ----
+  if (g == 0 && t == 0) {
+    for (int a = 0; a < 6; a++) c.lim[a] = s.lim[a];
+    c.guess = s.guess;
+    c.lo = s.lo;
+    c.hi = s.hi;
+    c.vs = s.vs;
+    for (int a = 0; a < 3; a++) {
+      c.len[a] = s.len[a];
+      c.off[a] = s.off[a];
+    }
+    c.V = s.V;
+    c.state = s.state;
+    c.rc = s.rc;
+    c.iter = s.iter;
+    c.stamp = s.stamp;
+    c.accepted_stamp = s.stamp;
+    c.acc_mode = s.mode;
+    c.num_nds = s.state == kAccepted ? s.num_nds : 0u;
+    for (int w = 0; w < kWorkers; w++) c.first_bad[w] = s.cut[w];
+  }
+  if (s.state != kAccepted) return;
+  FRONT_MARK(20);
+
+  {
+    // ---- dense ids of the accepted grid ----
+    const uint64_t V = s.V;
+    const uint32_t ndcap = A.ndcap, nd = s.num_nds;
+    uint32_t* dense = A.dense_of + (uint64_t)b * A.vcap;
+    uint32_t* vox = A.vox + (uint64_t)b * ndcap;
+    const bool bitmap = s.mode < 2;
+    uint32_t* bits_l = table;              // [1024] accepted bitmap
+    uint32_t* pref_l = table + kBitsWords; // [1024] exclusive popcount prefix
+    if (bitmap) {
+      const uint32_t words = (uint32_t)((V + 31) / 32);
+      const uint32_t* gbw = A.gbits + ((uint64_t)b * 2 + s.mode) * kBitsWords;
+      const uint32_t bits = t < words ? ld_sc1(gbw + t) : 0u;  // words <= 1024 = blockDim
+      uint32_t tot;
+      const uint32_t ex = block_excl_scan((uint32_t)__popc(bits), 0u, AddU32(), scratch, tot);
+      bits_l[t] = bits;
+      pref_l[t] = ex;
+      __syncthreads();
+      // my slice of dense_of / vox, one voxel per thread
+      const uint64_t v0 = V * g / G, v1 = V * (g + 1) / G;
+      for (uint64_t v = v0 + t; v < v1; v += kFrontThreads) {
+        const uint32_t w = (uint32_t)(v >> 5), bit = (uint32_t)(v & 31);
+        const uint32_t bw = bits_l[w];
+        if ((bw >> bit) & 1u) {
+          const uint32_t d = pref_l[w] + __popc(bw & ((1u << bit) - 1u));
+          dense[v] = d;
+          if (d < ndcap) vox[d] = (uint32_t)v;
+        } else {
+          dense[v] = kInvalid;
+        }
+      }
+    } else {
+      // stamps: my slice of the voxels, counted, then numbered after the
+      // counts of the earlier workgroups' slices
+      const uint32_t astamp = s.stamp;
+      const uint64_t v0 = V * g / G, v1 = V * (g + 1) / G;
+      uint32_t cnt = 0;
+      for (uint64_t v = v0 + t; v < v1; v += kFrontThreads) cnt += ld_sc1(stamps + v) == astamp;
+      cnt = block_sum_u32(cnt, scratch);
+      uint32_t* rec = A.rec + (((uint64_t)b * kFrontPhases + kPhDenseLarge) * G) * kRecWords;
+      if (t == 0) {
+        st_sc1(rec + g * kRecWords, cnt);
+        s.count = 0;
+      }
+      if (!cloud_sync(s, bar, G)) goto fail;
+      if (t < g) atomicAdd(&s.count, ld_sc1(rec + t * kRecWords));
+      __syncthreads();
+      uint32_t carry = s.count;
+      for (uint64_t base = v0; base < v1; base += kFrontThreads) {
+        const uint64_t v = base + t;
+        const uint32_t occ = v < v1 && ld_sc1(stamps + v) == astamp;
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan(occ, 0u, AddU32(), scratch, tot);
+        if (v < v1) {
+          const uint32_t d = carry + ex;
+          st_sc1(dense + v, occ ? d : kInvalid);
+          if (occ && d < ndcap) vox[d] = (uint32_t)v;
+        }
+        carry += tot;
+      }
+      if (!cloud_sync(s, bar, G)) goto fail;
+    }
+    FRONT_MARK(21);
+
+    // ---- per point: its ND (did), in place of its key ----
+    for (uint32_t e = t; e < nrb * ndcap; e += kFrontThreads) hist[e] = 0;
+    for (uint32_t j = 0; j < bpw; j++) {
+      const uint64_t i = (bin0 + j) * 1024 + t;
+      const uint32_t key = binfo[j * 1024 + t];
+      uint32_t d = kInvalid;
+      if (key != kInvalid && i < s.cut[i / chunk]) {
+        if (bitmap) {
+          const uint32_t bw = bits_l[key >> 5];
+          d = pref_l[key >> 5] + __popc(bw & ((1u << (key & 31)) - 1u));
+        } else {
+          d = ld_sc1(dense + key);
+        }
+      }
+      binfo[j * 1024 + t] = d;
+    }
+    __syncthreads();
+    FRONT_MARK(22);
+
+    // ---- per rank bin (one wave): stable rank of each point among its ND's
+    //      points in the bin, in index order; the bin's ND counts ----
+    for (uint32_t r = wave; r < nrb; r += kFrontWaves) {
+      uint32_t* hr = hist + (uint64_t)r * ndcap;
+      uint32_t* br = binfo + (uint64_t)r * rbs;
+      for (uint32_t st = 0; st < rbs / 64; st++) {
+        const uint32_t d = br[st * 64 + lane];
+        const uint32_t sk = wave_sort64(d == kInvalid ? kInvalid : (d << 6) | lane);
+        const uint32_t sd = sk == kInvalid ? kInvalid : sk >> 6;
+        const uint32_t prev = (uint32_t)__builtin_amdgcn_mov_dpp((int)sd, 0x138, 0xF, 0xF, false);  // wave_shr:1
+        const bool head = lane == 0 || prev != sd;
+        const unsigned long long H = __ballot(head);
+        const unsigned long long upto = (2ull << lane) - 1ull;  // lanes 0..lane (all for lane 63)
+        const uint32_t start = 63u - (uint32_t)__clzll(H & upto);
+        const unsigned long long after = H & ~upto;
+        const uint32_t next = after ? (uint32_t)__ffsll((long long)after) - 1u : 64u;
+        if (sd != kInvalid) {
+          const uint32_t cur = hr[sd];  // same address for the whole run: a broadcast read
+          br[st * 64 + (sk & 63)] = (sd << 10) | (cur + lane - start);
+          if (lane + 1 == next) hr[sd] = cur + next - start;
+        }
+      }
+    }
+    __syncthreads();
+    // per ND: my workgroup's count -> wgcnt; hist[r][d] -> exclusive prefix over my rank bins
+    uint32_t* wg = A.wgcnt + (uint64_t)b * G * ndcap;
+    for (uint32_t d = t; d < nd; d += kFrontThreads) {
+      uint32_t run = 0;
+      for (uint32_t r = 0; r < nrb; r++) {
+        const uint32_t x = hist[(uint64_t)r * ndcap + d];
+        hist[(uint64_t)r * ndcap + d] = run;
+        run += x;
+      }
+      st_sc1(wg + (uint64_t)g * ndcap + d, run);
+    }
+    FRONT_MARK(23);
+    if (!cloud_sync(s, bar, G)) goto fail;
+    FRONT_MARK(24);
+    // ND bases (scan of the per-ND totals over NDs) + earlier workgroups' counts
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < nd; base += kFrontThreads) {
+      const uint32_t d = base + t;
+      uint32_t tot_d = 0, pre = 0;
+      if (d < nd) {
+        uint32_t gg = 0;
+        for (; gg + 4 <= G; gg += 4) {
+          uint32_t x[4];
+#pragma unroll
+          for (int q = 0; q < 4; q++) x[q] = ld_sc1(wg + (uint64_t)(gg + q) * ndcap + d);
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            if (gg + q < g) pre += x[q];
+            tot_d += x[q];
+          }
+        }
+        for (; gg < G; gg++) {
+          const uint32_t x = ld_sc1(wg + (uint64_t)gg * ndcap + d);
+          if (gg < g) pre += x;
+          tot_d += x;
+        }
+      }
+      uint32_t tot;
+      const uint32_t start = carry + block_excl_scan(tot_d, 0u, AddU32(), scratch, tot);
+      if (d < nd) {
+        if (g == 0) {
+          A.nd_n[(uint64_t)b * ndcap + d] = tot_d;
+          A.nd_base[(uint64_t)b * ndcap + d] = start;
+        }
+        for (uint32_t r = 0; r < nrb; r++) hist[(uint64_t)r * ndcap + d] += start + pre;
+      }
+      carry += tot;
+    }
+    __syncthreads();
+    FRONT_MARK(25);
+    // ---- scatter: every point to its ND's run, in index order ----
+    T* out = (T*)A.nd_pts + (uint64_t)b * n * 3;
+    const uint32_t rsub = t / rbs;  // my rank bin within a 1024-point bin
+    auto put = [&](uint32_t j, uint64_t i, T x, T y, T z) {
+      const uint32_t bi = binfo[j * 1024 + t];
+      if (bi == kInvalid) return;
+      const uint32_t d = bi >> 10;
+      const uint32_t r = j * (1024 / rbs) + rsub;
+      const uint32_t dst = hist[(uint64_t)r * ndcap + d] + (bi & 1023u);
+      T* o = out + (uint64_t)dst * 3;
+      o[0] = x;
+      o[1] = y;
+      o[2] = z;
+      if (A.nd_lbl) A.nd_lbl[(uint64_t)b * n + dst] = (uint16_t)A.lbl[(uint64_t)b * n + i];
+    };
+#pragma unroll
+    for (int j = 0; j < kFrontR; j++)
+      if ((uint32_t)j < bpw) put(j, (bin0 + j) * 1024 + t, px[j], py[j], pz[j]);
+    for (uint32_t j = kFrontR; j < bpw; j++) {
+      const uint64_t i = (bin0 + j) * 1024 + t;
+      if (i < n8) {
+        T x, y, z;
+        front_point(p, i, x, y, z);
+        put(j, i, x, y, z);
+      }
+    }
+    FRONT_MARK(26);
+  }
+  return;
+fail:
+  if (t == 0) {
+    c.state = kFailed;
+    c.rc = kNdtErrSync;
+  }
+}

@@ -145,6 +145,16 @@ struct Plan {
   uint32_t* chunk_cnt; // [B][nchunk] (non-NaN count << 16) | NaN count
   double* chunk_min;   // [B][nchunk] min non-NaN value of the chunk (+inf if none)
   ndnet_ndt_stats* d_stats;  // [B] device copy of the stats
+  // k_front (ndt_front.h): the fused front of the pipeline
+  int front;                 // 1: k_front path, 0: the multi-kernel path
+  int front_ok;              // the plan's shape admits k_front
+  uint32_t fG, fbpw, frbs;   // workgroups per cloud, 1024-point bins per workgroup, points per rank bin
+  size_t flds;               // dynamic LDS bytes of k_front
+  unsigned long long* flims; // [B][fG][6]
+  uint32_t* frec;            // [B][kFrontPhases][fG][kRecWords]
+  uint32_t* fwgcnt;          // [B][fG][ndcap]
+  uint32_t* fbar;            // [B][kBarStride]
+  unsigned long long* fmarks; // [B][32] k_front phase stamps (timing level 2)
 };
 
 // ------------------------------------------------------------------ helpers
@@ -237,9 +247,10 @@ __device__ inline void grid_from(const CloudCtl& c, double vs, uint32_t* len, do
 
 // ------------------------------------------------------------------ kernels
 
-__global__ void k_reset(CloudCtl* ctl, int B) {
+__global__ void k_reset(CloudCtl* ctl, int B, uint32_t* bar) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
+  if (bar) bar[(uint64_t)b * 16] = 0;  // k_front's cloud barrier counter (kBarStride)
   CloudCtl& c = ctl[b];
   c.epoch = c.epoch + 1;
   // stamps are epoch*32 + pass; on a wrap the stale stamps are cleared on the
@@ -765,6 +776,8 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_scatter(const T* __restrict
     if (nd_lbl) nd_lbl[(uint64_t)b * n + dst] = (uint16_t)lbl[(uint64_t)b * n + i];
   }
 }
+
+#include "ndt_front.h"
 
 // One lane per ND: sequential Welford over its contiguous, index-ordered points
 // (normal_distributions.c:75-121), bit-exact; loads run 8 points ahead.
@@ -1574,7 +1587,8 @@ static void plan_free(Plan* P) {
   if (P->ev_created)
     for (int i = 0; i < 7; i++) (void)hipEventDestroy(P->ev[i]);
   if (P->kl_marks) (void)hipFree(P->kl_marks);
-  void* bufs[] = {P->ctl, P->stamps, P->dense_of, P->vox, P->gbits, P->pkeys, P->did, P->bin_cnt, P->nd_base,
+  if (P->fmarks) (void)hipFree(P->fmarks);
+  void* bufs[] = {P->flims, P->frec, P->fwgcnt, P->fbar, P->ctl, P->stamps, P->dense_of, P->vox, P->gbits, P->pkeys, P->did, P->bin_cnt, P->nd_base,
                   P->nd_pts, P->nd_lbl, P->nd_n,
                   P->nd_mean, P->nd_cov, P->nd_cov_post, P->nd_cls, P->hist, P->nb, P->keys, P->nkeys,
                   P->chain, P->chain_ps, P->slot_val, P->slot_flag, P->ev_val, P->ev_p, P->ev_q, P->ev_min,
@@ -1646,9 +1660,37 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
   const uint64_t n = P->n;
   if (lbl && P->ncls < 0) return NDNET_ERR_ARG;
   if (P->timing) HIPCHK(hipEventRecord(P->ev[0], st));
-  k_reset<<<(B + 63) / 64, 64, 0, st>>>(P->ctl, B);
-  const uint32_t Gl = (uint32_t)((3 * n + 256 * kLimPPT - 1) / (256 * kLimPPT));
+  k_reset<<<(B + 63) / 64, 64, 0, st>>>(P->ctl, B, P->front ? P->fbar : nullptr);
   P->calls++;
+  if (P->front) {
+    FrontArgs F;
+    F.ctl = P->ctl;
+    F.lbl = lbl;
+    F.stamps = P->stamps;
+    F.gbits = P->gbits;
+    F.dense_of = P->dense_of;
+    F.vox = P->vox;
+    F.nd_n = P->nd_n;
+    F.nd_base = P->nd_base;
+    F.nd_pts = P->nd_pts;
+    F.nd_lbl = lbl ? P->nd_lbl : nullptr;
+    F.lims = P->flims;
+    F.rec = P->frec;
+    F.wgcnt = P->fwgcnt;
+    F.bar = P->fbar;
+    F.marks = P->timing >= 2 ? P->fmarks : nullptr;
+    F.n = n;
+    F.k = P->k;
+    F.vcap = P->vcap;
+    F.ndcap = P->ndcap;
+    F.G = P->fG;
+    F.bpw = P->fbpw;
+    F.rbs = P->frbs;
+    k_front<T><<<dim3(P->fG, B), kFrontThreads, P->flds, st>>>(pts, F);
+    if (P->timing)
+      for (int e = 1; e <= 4; e++) HIPCHK(hipEventRecord(P->ev[e], st));
+  } else {
+  const uint32_t Gl = (uint32_t)((3 * n + 256 * kLimPPT - 1) / (256 * kLimPPT));
   k_limits<T><<<dim3(Gl, B), 256, 0, st>>>(pts, P->ctl, P->gbits, P->stamps, n, Gl, P->vcap);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[1], st));
   for (int it = 0; it < kMaxIters; it++)
@@ -1664,6 +1706,7 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
                                                                (T*)P->nd_pts, lbl ? P->nd_lbl : nullptr, n,
                                                                P->ndcap, P->nbins);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[4], st));
+  }
   k_welford<T><<<dim3((P->ndcap + 255) / 256, B), 256, 0, st>>>(P->ctl, (const T*)P->nd_pts,
                                                                   lbl ? P->nd_lbl : nullptr, P->nd_n, P->nd_base,
                                                                   P->nd_mean, P->nd_cov, P->nd_cls, P->hist, P->ncls,
@@ -1771,8 +1814,44 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   A_(chunk_cnt, B * P->nchunk);
   A_(chunk_min, B * P->nchunk);
   A_(d_stats, B);
+  // k_front: G workgroups per cloud, all resident together (G * B <= CUs);
+  // each owns bpw bins, whose per-ND counts and ranks live in its LDS
+  {
+    int dev = 0, cus = 0;
+    if (e == hipSuccess) e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint32_t gt = (uint32_t)(cus / batch > 0 ? cus / batch : 1);
+    uint32_t bpw = (P->nbins + gt - 1) / gt;
+    uint32_t G = (P->nbins + bpw - 1) / bpw;
+    // rank bins of 512 points when that keeps every wave busy and fits
+    auto lds_of = [&](uint32_t rbs) {
+      return sizeof(uint32_t) * ((size_t)kFrontTable + (size_t)bpw * 1024 + (size_t)bpw * (1024 / rbs) * P->ndcap);
+    };
+    const uint32_t rbs = (2 * bpw <= (uint32_t)kFrontWaves && lds_of(512) <= 150 * 1024) ? 512u : 1024u;
+    const size_t lds = lds_of(rbs);
+    P->fG = G;
+    P->fbpw = bpw;
+    P->frbs = rbs;
+    P->flds = lds;
+    P->front_ok = e == hipSuccess && lds <= 150 * 1024 && (G == 1 || (uint64_t)G * batch <= (uint64_t)cus);
+    if (P->front_ok && e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)k_front<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (P->front_ok && e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)k_front<double>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (P->front_ok && e == hipSuccess) {
+      int nb = 0;
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_front<double>, kFrontThreads, lds);
+      if (e == hipSuccess && nb < 1) P->front_ok = 0;
+    }
+    P->front = P->front_ok;
+    A_(flims, B * G * 6);
+    A_(frec, B * kFrontPhases * G * kRecWords);
+    A_(fwgcnt, B * G * nd);
+    A_(fbar, B * kBarStride);
+  }
 #undef A_
   if (e == hipSuccess) e = hipMemset(P->ctl, 0, B * sizeof(CloudCtl));
+  if (e == hipSuccess) e = hipMemset(P->fbar, 0, B * kBarStride * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(P->stamps, 0, B * P->vcap * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(P->d_stats, 0, B * sizeof(ndnet_ndt_stats));
   if (e == hipSuccess)
@@ -1792,6 +1871,20 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
 
 void ndnet_ndt_plan_destroy(void* plan) { plan_free((Plan*)plan); }
 
+int ndnet_ndt_set_path(void* plan, int path) {
+  Plan* P = (Plan*)plan;
+  if (!P || path < 0 || path > 2) return NDNET_ERR_ARG;
+  if (path == 2 && !P->front_ok) return NDNET_ERR_ARG;
+  P->front = path == 1 ? 0 : P->front_ok;
+  return NDNET_OK;
+}
+
+int ndnet_ndt_get_path(void* plan) {
+  Plan* P = (Plan*)plan;
+  if (!P) return NDNET_ERR_ARG;
+  return P->front ? 2 : 1;
+}
+
 int ndnet_ndt_set_timing(void* plan, int enable) {
   Plan* P = (Plan*)plan;
   if (!P) return NDNET_ERR_ARG;
@@ -1799,6 +1892,10 @@ int ndnet_ndt_set_timing(void* plan, int enable) {
   if (enable && !P->ev_created) {
     for (int i = 0; i < 7; i++) HIPCHK(hipEventCreate(&P->ev[i]));
     P->ev_created = 1;
+  }
+  if (enable >= 2 && !P->fmarks) {
+    HIPCHK(hipMalloc(&P->fmarks, (size_t)P->B * 32 * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(P->fmarks, 0, (size_t)P->B * 32 * sizeof(unsigned long long)));
   }
   if (enable >= 2 && !P->kl_marks) {
     HIPCHK(hipMalloc(&P->kl_marks, (size_t)P->B * 16 * sizeof(unsigned long long)));
@@ -1856,6 +1953,14 @@ int ndnet_ndt_debug_kl_marks(void* plan, unsigned long long* marks) {
   if (!P || !marks || !P->kl_marks) return NDNET_ERR_ARG;
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(marks, P->kl_marks, (size_t)P->B * 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return NDNET_OK;
+}
+
+int ndnet_ndt_debug_front_marks(void* plan, unsigned long long* marks) {
+  Plan* P = (Plan*)plan;
+  if (!P || !marks || !P->fmarks) return NDNET_ERR_ARG;
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(marks, P->fmarks, (size_t)P->B * 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return NDNET_OK;
 }
 

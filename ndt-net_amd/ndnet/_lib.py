@@ -18,6 +18,7 @@ LIB_PATH = os.path.join(ROOT, "lib", "libndnet_amd.so")
 NDNET_OK = 0
 NDNET_ERR_ARG = -20
 NDNET_ERR_HIP = -21
+NDNET_ERR_SYNC = -22
 
 
 class NdtStats(ctypes.Structure):
@@ -63,12 +64,15 @@ EXPORTS = {
     # batched device API
     "ndnet_ndt_plan_create": (_I, [_I, _U64, _U64, _I, _U64, ctypes.POINTER(_P)]),
     "ndnet_ndt_plan_destroy": (None, [_P]),
+    "ndnet_ndt_set_path": (_I, [_P, _I]),
+    "ndnet_ndt_get_path": (_I, [_P]),
     "ndnet_ndt_run": (_I, [_P, _P, _P, _P, _P, _P, _P]),
     "ndnet_ndt_run_f64": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "ndnet_ndt_prune": (_I, [_P, _P, _U64, _P, _P, _P, _P, _P, _P]),
     "ndnet_ndt_debug_dump": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "ndnet_ndt_debug_set_epoch": (_I, [_P, ctypes.c_uint32]),
     "ndnet_ndt_debug_kl_marks": (_I, [_P, _P]),
+    "ndnet_ndt_debug_front_marks": (_I, [_P, _P]),
     "ndnet_ndt_set_timing": (_I, [_P, _I]),
     "ndnet_ndt_stage_ms": (_I, [_P, _P]),
     "ndnet_amd_version": (ctypes.c_char_p, []),

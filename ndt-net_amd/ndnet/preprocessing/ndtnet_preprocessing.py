@@ -58,6 +58,14 @@ class NdtPlan:
             self.stats.data_ptr())
         _lib.check(rc, "ndnet_ndt_run")
 
+    def set_path(self, path: int) -> None:
+        """1: one launch per stage; 2: the fused front kernel (k_front); 0: 2 where allowed."""
+        _lib.check(_lib.lib().ndnet_ndt_set_path(self.handle, int(path)), "ndnet_ndt_set_path")
+
+    @property
+    def path(self) -> int:
+        return int(_lib.lib().ndnet_ndt_get_path(self.handle))
+
     def prune(self, num_nds: int, out: torch.Tensor, out_classes: Optional[torch.Tensor] = None) -> None:
         st = _lib.stream_ptr(self.device)
         rc = _lib.lib().ndnet_ndt_prune(self.handle, st, num_nds, out.data_ptr(),

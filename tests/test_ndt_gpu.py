@@ -195,3 +195,57 @@ def test_legacy_sampler_multilevel():
             assert np.array_equal(c1, c2, equal_nan=True)
         s.cleanup()
         ref.cleanup()
+
+
+def _wide_sparse(n, seed):
+    """Most points in a small box, a few far outliers: the early bisection
+    grids exceed the 32768-voxel bitmap and run through the per-voxel stamps."""
+    rng = np.random.default_rng(seed)
+    a = rng.uniform(-3, 3, (n, 3))
+    a[::997] = rng.uniform(-40, 40, (len(a[::997]), 3))
+    return a.astype(np.float32)
+
+
+@pytest.mark.parametrize("case", ["U", "L", "wide", "mixed"])
+def test_front_kernel_equals_multikernel_path(case):
+    """k_front (one launch: limits, bisection, dense ids, binning) against the
+    one-launch-per-stage path on the same batch: every output row, every
+    stats field and every intermediate the dump exposes, bit for bit; both
+    are also checked against the oracle."""
+    import torch
+    import oracle as O
+    from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
+    from ndnet.synthetic import make_batch
+    if case == "wide":
+        pts = np.stack([_wide_sparse(30_000, s) for s in range(3)])
+        k = 300
+    elif case == "mixed":
+        pts = np.stack([make_batch("U", 1, 30_000, seed0=5)[0], make_batch("L", 1, 30_000, seed0=6)[0],
+                        _wide_sparse(30_000, 9)])
+        k = 300
+    else:
+        pts = make_batch(case, 5, 50_000, seed0=21)
+        k = 700
+    B, n, _ = pts.shape
+    res = {}
+    for path in (1, 2):
+        plan = NdtPlan(B, n, k, -1)
+        plan.set_path(path)
+        assert plan.path == path
+        out = torch.empty((B, k, 12), dtype=torch.float32, device="cuda")
+        plan.run(torch.from_numpy(pts).cuda(), None, out, None)
+        torch.cuda.synchronize()
+        stats = plan.host_stats()
+        dumps = [_dump(plan, b, int(stats[b].num_nds), int(stats[b].num_events)) for b in range(B)]
+        res[path] = (out.cpu().numpy(), stats, dumps)
+    o1, s1, d1 = res[1]
+    o2, s2, d2 = res[2]
+    assert np.array_equal(o1, o2)
+    for b in range(B):
+        assert bytes(s1[b]) == bytes(s2[b]), f"cloud {b} stats"
+        for key in d1[b]:
+            assert np.array_equal(d1[b][key], d2[b][key], equal_nan=True), (b, key)
+        pc, cov, r = O.downsample_f32(pts[b], k)
+        assert s2[b].rc == r.rc
+        if r.rc == 0:
+            assert np.array_equal(o2[b, :, :3], pc) and np.array_equal(o2[b, :, 3:], cov)
