@@ -174,6 +174,12 @@ int ndnet_ndt_debug_kl_marks(void *plan, unsigned long long *marks);
  * 25 offsets, 26 scattered; synchronises. */
 int ndnet_ndt_debug_front_marks(void *plan, unsigned long long *marks);
 
+/* k_welford stamps of the last run at timing level 2: per cloud and
+ * workgroup (16 NDs) 4 marks -- start, points staged, samples folded, end --
+ * as marks[(cloud * wgs + wg) * 4 + i], wgs = ceil((floor(1.2 k) + 1) / 16);
+ * synchronises. */
+int ndnet_ndt_debug_welford_marks(void *plan, unsigned long long *marks);
+
 /* Library identification (no GPU needed). */
 const char *ndnet_amd_version(void);
 

@@ -87,6 +87,44 @@ NDNET_FN uint32_t voxel_key(double x, double y, double z, const double* off, con
   return vz * len[0] * len[1] + vy * len[0] + vx;
 }
 
+// x / n with the reciprocal of n shared between divisions.  The compiler's
+// correctly rounded f64 division is the sequence
+//   d = div_scale(n), r = rcp(d), two Newton steps r += r (1 - d r),
+//   q0 = x' r, rem = x' - d q0, q1 = div_fmas(rem, r, q0), div_fixup(q1, n, x)
+// where div_scale / div_fmas scale only for extreme exponents and div_fixup
+// only changes special operands.  For n >= 1 integer-valued and
+// 2^-900 < |x| < 2^900 none of that applies, so the result is exactly
+// fma(x - n q0, r, q0) with r = recip_refined(n): bit-identical to x / n, and
+// r (depending on n only) is computed once per sample instead of once per
+// division.  Zero is returned as is (0 / n keeps the sign of the zero).
+// Callers take x / n when *ok is false.
+NDNET_FN double recip_refined(double n) {
+  double r = __builtin_amdgcn_rcp(n);
+  double e = fma(-n, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-n, r, 1.0);
+  r = fma(r, e, r);
+  return r;
+}
+NDNET_FN double div_by_recip(double x, double n, double r, bool& ok) {
+  const double ax = fabs(x);
+  ok = (ax > 0x1p-900 && ax < 0x1p900) || x == 0.0;
+  const double q0 = x * r;
+  const double rem = fma(-n, q0, x);
+  // x / n has the sign of x (n > 0); for x = -0 the fma sequence gives +0
+  return copysign(fma(rem, r, q0), x);
+}
+
+// div_by_recip without the operand checks, for callers that have bounded the
+// operands (2^-969 < |x| < 2^900 or x == 0) beforehand.  A zero x gives +0:
+// only its sign could differ from x / n, and the Welford sums it feeds start
+// at +0 and can never become -0, so no sum changes.
+NDNET_FN double div_fast(double x, double n, double r) {
+  const double q0 = x * r;
+  const double rem = fma(-n, q0, x);
+  return fma(rem, r, q0);
+}
+
 // Welford state of one voxel (normal_distributions.h:41-51, class handled apart).
 struct Welford {
   double mean[3];

@@ -75,6 +75,7 @@ struct FrontArgs {
   uint64_t n, k, vcap;
   uint32_t ndcap, G, bpw;
   uint32_t rbs;                 // points per rank bin (512 or 1024)
+  int dbg_store;
 };
 
 // The shared bisection state of one workgroup (every workgroup of a cloud
@@ -269,11 +270,18 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
       mn[a] = v[a] < mn[a] ? v[a] : mn[a];
     }
   };
+  // all loads issued unconditionally (clamped index) so they are in flight
+  // together; a predicated load would compile to a branch + vmcnt(0) each
+#pragma unroll
+  for (int j = 0; j < kFrontR; j++) {
+    const uint64_t i = (bin0 + j) * 1024 + t;
+    const uint64_t ic = i < n ? i : n - 1;
+    front_point(p, ic, px[j], py[j], pz[j]);
+  }
 #pragma unroll
   for (int j = 0; j < kFrontR; j++) {
     const uint64_t i = (bin0 + j) * 1024 + t;
     if ((uint32_t)j < bpw && i < n) {
-      front_point(p, i, px[j], py[j], pz[j]);
       lim_acc(px[j], py[j], pz[j]);
     } else {
       px[j] = py[j] = pz[j] = T(0);
@@ -691,9 +699,19 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
       const uint32_t r = j * (1024 / rbs) + rsub;
       const uint32_t dst = hist[(uint64_t)r * ndcap + d] + (bi & 1023u);
       T* o = out + (uint64_t)dst * 3;
-      o[0] = x;
-      o[1] = y;
-      o[2] = z;
+      if (A.dbg_store == 1) {
+        __builtin_nontemporal_store(x, o);
+        __builtin_nontemporal_store(y, o + 1);
+        __builtin_nontemporal_store(z, o + 2);
+      } else if (A.dbg_store == 2) {
+        __hip_atomic_store(o, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(o + 1, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(o + 2, z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        o[0] = x;
+        o[1] = y;
+        o[2] = z;
+      }
       if (A.nd_lbl) A.nd_lbl[(uint64_t)b * n + dst] = (uint16_t)A.lbl[(uint64_t)b * n + i];
     };
 #pragma unroll

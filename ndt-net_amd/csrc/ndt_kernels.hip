@@ -15,7 +15,7 @@
 //   k_dense        occupied voxels of the accepted grid -> dense ids in
 //                  ascending linear order (the output order, ndt.c:88-90)
 //   k_chunk_sort   stable per-chunk sort of points by dense id
-//   k_welford      one lane per ND, sequential Welford in point order
+//   k_welford      a lane quad per ND, sequential Welford in point order
 //                  (normal_distributions.c:75-121), bit-exact
 //   k_kl           one workgroup per cloud: LU chains, KL events, the
 //                  reference's insertion order, prune, compaction
@@ -27,6 +27,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
+#include <type_traits>
 
 #include "ndt_device.h"
 #include "../../include/ndnet_amd.h"
@@ -155,6 +156,8 @@ struct Plan {
   uint32_t* fwgcnt;          // [B][fG][ndcap]
   uint32_t* fbar;            // [B][kBarStride]
   unsigned long long* fmarks; // [B][32] k_front phase stamps (timing level 2)
+  unsigned long long* wmarks; // [B][wg][4] k_welford stamps (timing level 2)
+  uint32_t wgrid;             // k_welford workgroups: min(CUs, group capacity of the batch)
 };
 
 // ------------------------------------------------------------------ helpers
@@ -779,58 +782,288 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_scatter(const T* __restrict
 
 #include "ndt_front.h"
 
-// One lane per ND: sequential Welford over its contiguous, index-ordered points
-// (normal_distributions.c:75-121), bit-exact; loads run 8 points ahead.
+// Welford per ND (normal_distributions.c:75-121) over its contiguous,
+// index-ordered points, bit-exact.  The update of one sample is three
+// independent axis chains plus three off-diagonal terms, so an ND runs on a
+// lane quad: lane j (0..2) carries mean_j, m2_j and the variance of axis j,
+// plus one off-diagonal term -- lane 0 (0,1), lane 1 (1,2), lane 2 (0,2) --
+// whose other operand comes from the neighbouring lane through one DPP quad
+// permute per sample (the new mean of axis 0 for lane 2, the not yet updated
+// mean of axis j+1 for lanes 0 and 1: the reference updates the axes in
+// order, normal_distributions.c:86-101).  Every lane performs exactly the
+// reference's double operations on the same operands.  The two divisions by
+// the sample count per lane and sample share one refined reciprocal
+// (div_by_recip, bit-identical to the division), which takes them off the
+// loop-carried chain; only the variance's final m2 / n is a plain division.
+// One wave per workgroup (16 NDs): its points (a contiguous range of nd_pts)
+// are staged through LDS with one batch of coalesced 16-byte loads.
+constexpr int kWelfordNDs = 64;          // NDs per workgroup: 4 waves x 16 quads (one wave per SIMD of a CU)
+constexpr int kWelfordThreads = 4 * kWelfordNDs;
+constexpr int kWelfordBytes = 96 * 1024; // LDS window (one workgroup per CU)
+constexpr int kWelfordVecs = 20;         // 16-byte loads per thread per window, all in flight at once
+constexpr int kRtab = 2048;              // refined reciprocals of the counts 1..kRtab, in LDS after the window
+
+__device__ inline double quad_perm_120(double v) {  // lane i of a quad <- lane [1,2,0,3][i]
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, 0xC9, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), 0xC9, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32));
+}
+
+#define W_MARK(i)                                                                                             \
+  do {                                                                                                        \
+    if (marks && threadIdx.x == 0) marks[((uint64_t)b * gpc + gi) * 4 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
+// One group of kWelfordNDs consecutive NDs of cloud b.
+template <int CTRL>
+__device__ inline double dpp_f64(double v) {  // DPP move of a double (both halves, same control)
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32));
+}
+
 template <typename T>
-__global__ void __launch_bounds__(256) k_welford(const CloudCtl* ctl, const T* __restrict__ nd_pts,
+__device__ void welford_group(const CloudCtl& c, const int b, const uint32_t gi, const uint32_t gpc,
+                              const T* __restrict__ nd_pts, const uint16_t* __restrict__ nd_lbl, const uint32_t* nd_n,
+                              const uint32_t* nd_base, double* nd_mean, double* nd_cov, uint16_t* nd_cls,
+                              uint32_t* hist_all, int ncls, uint64_t n, uint32_t ndcap, unsigned long long* marks,
+                              const double* rtab) {
+  constexpr uint32_t kVec = 16 / sizeof(T);                            // elements per 16-byte load
+  constexpr uint32_t kWin = (kWelfordBytes - 32) / (3 * sizeof(T));     // points per window (+ alignment lead)
+  extern __shared__ __attribute__((aligned(16))) unsigned char w_smem[];
+  T* sp = (T*)w_smem;
+  const uint32_t nd = c.num_nds;
+  const uint32_t d0 = gi * kWelfordNDs;
+  W_MARK(0);
+  const uint32_t dl = (d0 + kWelfordNDs < nd ? d0 + kWelfordNDs : nd) - 1;  // last ND of the workgroup
+  const uint64_t ob = (uint64_t)b * ndcap;
+  const uint32_t lane = threadIdx.x & 63, j = lane & 3;
+  const uint32_t d = d0 + (threadIdx.x >> 2);
+  const bool live = d <= dl;
+  const uint32_t dd = live ? d : dl;
+  const uint32_t beg = nd_base[ob + dd], cnt = live ? nd_n[ob + dd] : 0u;
+  const uint32_t r0 = nd_base[ob + d0], r1 = nd_base[ob + dl] + nd_n[ob + dl];  // the workgroup's point range
+  const uint32_t jj = j < 3 ? j : 0u;           // my axis
+  const uint32_t pj = jj == 2 ? 0u : jj + 1u;   // my partner's axis
+  double mean = 0.0, m2 = 0.0, off = 0.0, cntd = 0.0;
+  // fold<false>: divisions through the shared reciprocal; a lane that meets an
+  // operand outside its exact range flags `bad` and the whole workgroup then
+  // folds again with plain divisions (fold<true>; never on ordinary data)
+  auto fold = [&](auto exact_tag) -> bool {
+    constexpr bool kExact = decltype(exact_tag)::value;
+    mean = 0.0;
+    m2 = 0.0;
+    off = 0.0;
+    cntd = 0.0;
+    bool bad = false;
+    for (uint32_t w0 = r0; w0 < r1; w0 += kWin) {
+      const uint32_t wn = r1 - w0 < kWin ? r1 - w0 : kWin;
+      // coalesced 16-byte copy of points [w0, w0 + wn) from the aligned-down
+      // element ge0 (nd_pts is 256-byte aligned and carries kNdSlack points of
+      // padding, so the rounded-up tail stays in bounds)
+      const uint64_t ge0 = ((uint64_t)b * n + w0) * 3;
+      const uint64_t a0 = ge0 & ~(uint64_t)(kVec - 1);
+      const uint32_t lead = (uint32_t)(ge0 - a0);
+      __syncthreads();
+      {
+        typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+        const u32x4* gsrc = (const u32x4*)(nd_pts + a0);
+        u32x4* ldst = (u32x4*)sp;
+        const uint32_t nvec = (lead + 3 * wn + kVec - 1) / kVec;
+        for (uint32_t base = threadIdx.x; base < nvec; base += kWelfordThreads * kWelfordVecs) {
+          // unconditional loads (a clamped index past the end): a predicated
+          // load compiles to a branch with its own vmcnt(0) wait, serialising
+          // the batch
+          u32x4 r[kWelfordVecs];
+#pragma unroll
+          for (int u = 0; u < kWelfordVecs; u++) {
+            const uint32_t i = base + kWelfordThreads * u;
+            r[u] = gsrc[i < nvec ? i : nvec - 1];
+          }
+#pragma unroll
+          for (int u = 0; u < kWelfordVecs; u++) {
+            const uint32_t i = base + kWelfordThreads * u;
+            if (i < nvec) ldst[i] = r[u];
+          }
+          if constexpr (!kExact) {
+            // the fast fold's operand range: every coordinate 0 or 2^-300 <=
+            // |c| <= 2^300 (every finite float is), so no quotient operand
+            // leaves div_fast's exact range and no NaN can arise
+#pragma unroll
+            for (int u = 0; u < kWelfordVecs; u++) {
+              const uint32_t i = base + kWelfordThreads * u;
+              const T* e = (const T*)&r[u];
+#pragma unroll
+              for (uint32_t k = 0; k < kVec; k++) {
+                const uint32_t el = i * kVec + k;
+                bool in;
+                if constexpr (sizeof(T) == 4) {
+                  in = (r[u][k] & 0x7f800000u) != 0x7f800000u;  // finite
+                } else {
+                  const double v = fabs((double)e[k]);
+                  in = v == 0.0 || (v >= 0x1p-300 && v <= 0x1p300);
+                }
+                bad |= i < nvec && el >= lead && el < lead + 3 * wn && !in;
+              }
+            }
+          }
+        }
+      }
+      __syncthreads();
+      W_MARK(1);
+      const uint32_t a = beg > w0 ? beg : w0;
+      const uint32_t e_end = beg + cnt < w0 + wn ? beg + cnt : w0 + wn;
+      // every lane of a quad runs the same trip count (quad-uniform), so the
+      // DPP permutes always read a live neighbour
+      const T* pt = sp + lead + 3 * (a - w0);
+      if constexpr (kExact) {
+        for (uint32_t q = a; q < e_end; q++, pt += 3) {
+          const double x = (double)pt[jj], xp = (double)pt[pj];
+          cntd = cntd + 1.0;
+          const double old = mean;
+          mean = mean + (x - mean) / cntd;
+          m2 = m2 + (x - old) * (x - mean);
+          const double mp_old = quad_perm_120(old);
+          const double mp_new = quad_perm_120(mean);
+          const double A = jj == 2 ? (xp - mp_new) : (x - mean);
+          const double Bv = jj == 2 ? (x - old) : (xp - mp_old);
+          const double cv = off + A * Bv / cntd;
+          off = (cv != cv) ? 0.0 : cv;
+        }
+      } else {
+        // Software-pipelined over the samples: the mean chain of sample q
+        // (stage 1) is issued next to the m2 / off-diagonal updates of sample
+        // q - 1 (stage 2), which only need that sample's old and new means, so
+        // the in-order issue of one wave does not stall on either chain.
+        // The off-diagonal operands come straight from their lanes: lane j
+        // multiplies (x_a - mean_a') by (x_b - mean_b) for its pair (a, b) =
+        // (0,1), (1,2), (0,2): x_a / x_b are read from LDS by axis, mean_a'
+        // is quad_perm [0,1,0,3] of the new means and mean_b quad_perm
+        // [1,2,2,3] of the old ones.
+        const uint32_t ia = jj == 2 ? 0u : jj, ib = jj == 2 ? 2u : jj + 1u;
+        double pxo = 0.0, pxa = 0.0, pxb = 0.0, pold = 0.0, pmean = 0.0, prc = 0.0, pcnt = 0.0;
+        bool pending = false;
+        for (uint32_t q = a; q < e_end; q++, pt += 3) {
+          const double xa = (double)pt[ia], xb = (double)pt[ib];
+          const double xo = jj == 2 ? xb : xa;  // my own axis
+          // stage 1, sample q
+          const double cn = cntd + 1.0;
+          const double rc = rtab[(uint32_t)cntd];  // refined reciprocal of cn
+          const double old = mean;
+          const double nm = mean + div_fast(xo - mean, cn, rc);
+          // stage 2, sample q - 1 (off can not become NaN in the checked range)
+          if (pending) {
+            m2 = m2 + (pxo - pold) * (pxo - pmean);
+            const double ma = dpp_f64<0xC4>(pmean);  // quad_perm [0,1,0,3]
+            const double mb = dpp_f64<0xE9>(pold);   // quad_perm [1,2,2,3]
+            off = off + div_fast((pxa - ma) * (pxb - mb), pcnt, prc);
+          }
+          pending = true;
+          cntd = cn;
+          mean = nm;
+          pxo = xo;
+          pxa = xa;
+          pxb = xb;
+          pold = old;
+          pmean = nm;
+          prc = rc;
+          pcnt = cn;
+        }
+        if (pending) {
+          m2 = m2 + (pxo - pold) * (pxo - pmean);
+          const double ma = dpp_f64<0xC4>(pmean);
+          const double mb = dpp_f64<0xE9>(pold);
+          off = off + div_fast((pxa - ma) * (pxb - mb), pcnt, prc);
+        }
+      }
+    }
+    return bad;
+  };
+  // the fast fold reads the reciprocal table; a count past it takes the exact fold
+  if (__syncthreads_or(cnt > (uint32_t)kRtab)) {
+    fold(std::true_type{});
+  } else {
+    const bool bad = fold(std::false_type{});
+    if (__syncthreads_or(bad && j < 3 && live)) fold(std::true_type{});
+  }
+  if (marks) __syncthreads();
+  W_MARK(2);
+  if (live && j < 3) {
+    const uint64_t o = ob + d;
+    const double v = m2 / cntd;
+    nd_mean[3 * o + j] = mean;
+    nd_cov[9 * o + 4 * j] = (v != v) ? 0.0 : v;
+    const uint32_t ia = j == 2 ? 0u : j, ib = j == 2 ? 2u : j + 1u;
+    nd_cov[9 * o + 3 * ia + ib] = off;
+    nd_cov[9 * o + 3 * ib + ia] = off;
+  }
+  if (live && j == 0) {
+    const uint64_t o = ob + d;
+    uint16_t cls = 0;
+    if (nd_lbl) {  // class histogram, first index of the max (normal_distributions.c:107-121)
+      uint32_t* hist = hist_all + o * (uint32_t)(ncls + 1);
+      for (int k = 0; k <= ncls; k++) hist[k] = 0;
+      const uint16_t* l = nd_lbl + (uint64_t)b * n + beg;
+      for (uint32_t s2 = 0; s2 < cnt; s2++)
+        if (l[s2] <= (uint32_t)ncls) hist[l[s2]]++;
+      uint32_t best = 0;
+      for (int k = 0; k <= ncls; k++)
+        if (hist[k] > best) { best = hist[k]; cls = (uint16_t)k; }
+    }
+    nd_cls[o] = cls;
+  }
+  if (marks) __syncthreads();
+  W_MARK(3);
+}
+#undef W_MARK
+
+// Persistent: one workgroup per CU walks the (cloud, ND group) items that
+// exist in this run (the ND counts are only known on the device), so no CU
+// holds two groups while another idles.
+template <typename T>
+__global__ void __launch_bounds__(kWelfordThreads) k_welford(const CloudCtl* ctl, int B, const T* __restrict__ nd_pts,
                                                  const uint16_t* __restrict__ nd_lbl, const uint32_t* nd_n,
                                                  const uint32_t* nd_base, double* nd_mean, double* nd_cov,
                                                  uint16_t* nd_cls, uint32_t* hist_all, int ncls, uint64_t n,
-                                                 uint32_t ndcap) {
-  const int b = blockIdx.y;
-  const CloudCtl& c = ctl[b];
-  if (c.state != kAccepted) return;
-  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= c.num_nds) return;
-  const uint64_t o = (uint64_t)b * ndcap + d;
-  const uint32_t cnt = nd_n[o];
-  const T* q = nd_pts + ((uint64_t)b * n + nd_base[o]) * 3;
-  Welford w;
-  welford_init(w);
-  constexpr int U = 8;
-  T cur[3 * U], nxt[3 * U];
-  // nd_pts carries kNdSlack points of padding, so these loads run unconditionally
-  // past a run's end (a predicated load would branch and wait on every element)
-#pragma unroll
-  for (int j = 0; j < 3 * U; j++) cur[j] = q[j];
-  for (uint32_t s = 0; s < cnt; s += U) {
-    const T* qn = q + 3 * (s + U < cnt ? s + U : s);
-#pragma unroll
-    for (int j = 0; j < 3 * U; j++) nxt[j] = qn[j];
-#pragma unroll
-    for (int j = 0; j < U; j++) {
-      if (s + j < cnt) {
-        const double x[3] = {(double)cur[3 * j], (double)cur[3 * j + 1], (double)cur[3 * j + 2]};
-        welford_update(w, x);
-      }
+                                                 uint32_t ndcap, unsigned long long* marks) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char w_smem[];
+  double* rtab = (double*)(w_smem + kWelfordBytes);
+  __shared__ uint32_t s_first[257];  // first item of each cloud (chunks of 256 clouds)
+  const uint32_t gpc = (ndcap + kWelfordNDs - 1) / kWelfordNDs;  // group capacity per cloud
+  for (uint32_t k = threadIdx.x; k < (uint32_t)kRtab; k += blockDim.x) rtab[k] = recip_refined((double)(k + 1));
+  // items of this run: clouds' group counts (loaded in parallel), scanned, in
+  // chunks of 256 clouds
+  uint32_t item = blockIdx.x, base_all = 0;
+  for (int b0 = 0; b0 < B; b0 += 256) {
+    __syncthreads();
+    if (threadIdx.x < 256) {
+      const int bb = b0 + (int)threadIdx.x;
+      uint32_t g = 0;
+      if (bb < B && ctl[bb].state == kAccepted) g = (ctl[bb].num_nds + kWelfordNDs - 1) / kWelfordNDs;
+      s_first[threadIdx.x + 1] = g;
     }
-#pragma unroll
-    for (int j = 0; j < 3 * U; j++) cur[j] = nxt[j];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      s_first[0] = base_all;
+      for (int i = 1; i <= 256; i++) s_first[i] += s_first[i - 1];
+    }
+    __syncthreads();
+    const int nb = B - b0 < 256 ? B - b0 : 256;
+    const uint32_t end = s_first[nb];
+    for (; item < end; item += gridDim.x) {
+      int lo = 0, hi = nb - 1;  // last cloud whose first item <= item
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_first[mid] <= item) lo = mid;
+        else hi = mid - 1;
+      }
+      welford_group<T>(ctl[b0 + lo], b0 + lo, item - s_first[lo], gpc, nd_pts, nd_lbl, nd_n, nd_base, nd_mean,
+                       nd_cov, nd_cls, hist_all, ncls, n, ndcap, marks, rtab);
+    }
+    base_all = end;
   }
-  for (int j = 0; j < 3; j++) nd_mean[3 * o + j] = w.mean[j];
-  for (int j = 0; j < 9; j++) nd_cov[9 * o + j] = w.cov[j];
-  uint16_t cls = 0;
-  if (nd_lbl) {  // class histogram, first index of the max (normal_distributions.c:107-121)
-    uint32_t* hist = hist_all + o * (uint32_t)(ncls + 1);
-    for (int j = 0; j <= ncls; j++) hist[j] = 0;
-    const uint16_t* l = nd_lbl + (uint64_t)b * n + nd_base[o];
-    for (uint32_t s = 0; s < cnt; s++)
-      if (l[s] <= (uint32_t)ncls) hist[l[s]]++;
-    uint32_t best = 0;
-    for (int j = 0; j <= ncls; j++)
-      if (hist[j] > best) { best = hist[j]; cls = (uint16_t)j; }
-  }
-  nd_cls[o] = cls;
 }
 
 // Bitonic sort of (key, idx) pairs ascending, n a power of two, within one workgroup.
@@ -1588,6 +1821,7 @@ static void plan_free(Plan* P) {
     for (int i = 0; i < 7; i++) (void)hipEventDestroy(P->ev[i]);
   if (P->kl_marks) (void)hipFree(P->kl_marks);
   if (P->fmarks) (void)hipFree(P->fmarks);
+  if (P->wmarks) (void)hipFree(P->wmarks);
   void* bufs[] = {P->flims, P->frec, P->fwgcnt, P->fbar, P->ctl, P->stamps, P->dense_of, P->vox, P->gbits, P->pkeys, P->did, P->bin_cnt, P->nd_base,
                   P->nd_pts, P->nd_lbl, P->nd_n,
                   P->nd_mean, P->nd_cov, P->nd_cov_post, P->nd_cls, P->hist, P->nb, P->keys, P->nkeys,
@@ -1707,10 +1941,10 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
                                                                P->ndcap, P->nbins);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[4], st));
   }
-  k_welford<T><<<dim3((P->ndcap + 255) / 256, B), 256, 0, st>>>(P->ctl, (const T*)P->nd_pts,
+  k_welford<T><<<P->wgrid, kWelfordThreads, kWelfordBytes + kRtab * sizeof(double), st>>>(P->ctl, B, (const T*)P->nd_pts,
                                                                   lbl ? P->nd_lbl : nullptr, P->nd_n, P->nd_base,
                                                                   P->nd_mean, P->nd_cov, P->nd_cls, P->hist, P->ncls,
-                                                                  n, P->ndcap);
+                                                                  n, P->ndcap, P->timing >= 2 ? P->wmarks : nullptr);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[5], st));
   KLArgs A = kl_args(P, P->k, out, out_cls, pc64, cov64, cls16);
   k_kl_chains<<<dim3((P->ndcap + 255) / 256, B), 256, 0, st>>>(A);
@@ -1844,6 +2078,8 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
       if (e == hipSuccess && nb < 1) P->front_ok = 0;
     }
     P->front = P->front_ok;
+    const uint32_t groups = (uint32_t)batch * ((P->ndcap + kWelfordNDs - 1) / kWelfordNDs);
+    P->wgrid = groups < (uint32_t)(cus > 0 ? cus : 1) ? groups : (uint32_t)(cus > 0 ? cus : 1);
     A_(flims, B * G * 6);
     A_(frec, B * kFrontPhases * G * kRecWords);
     A_(fwgcnt, B * G * nd);
@@ -1857,6 +2093,12 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_kl_merge<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(2 * kMergeLdsChunks * kChunk * sizeof(unsigned long long)));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_welford<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kWelfordBytes + kRtab * (int)sizeof(double));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_welford<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kWelfordBytes + kRtab * (int)sizeof(double));
   if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_bin_count, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                (int)(16384 * sizeof(uint32_t)));
   if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -1892,6 +2134,11 @@ int ndnet_ndt_set_timing(void* plan, int enable) {
   if (enable && !P->ev_created) {
     for (int i = 0; i < 7; i++) HIPCHK(hipEventCreate(&P->ev[i]));
     P->ev_created = 1;
+  }
+  if (enable >= 2 && !P->wmarks) {
+    const size_t nw = (size_t)P->B * ((P->ndcap + kWelfordNDs - 1) / kWelfordNDs) * 4;
+    HIPCHK(hipMalloc(&P->wmarks, nw * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(P->wmarks, 0, nw * sizeof(unsigned long long)));
   }
   if (enable >= 2 && !P->fmarks) {
     HIPCHK(hipMalloc(&P->fmarks, (size_t)P->B * 32 * sizeof(unsigned long long)));
@@ -1961,6 +2208,15 @@ int ndnet_ndt_debug_front_marks(void* plan, unsigned long long* marks) {
   if (!P || !marks || !P->fmarks) return NDNET_ERR_ARG;
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(marks, P->fmarks, (size_t)P->B * 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return NDNET_OK;
+}
+
+int ndnet_ndt_debug_welford_marks(void* plan, unsigned long long* marks) {
+  Plan* P = (Plan*)plan;
+  if (!P || !marks || !P->wmarks) return NDNET_ERR_ARG;
+  HIPCHK(hipDeviceSynchronize());
+  const size_t nw = (size_t)P->B * ((P->ndcap + kWelfordNDs - 1) / kWelfordNDs) * 4;
+  HIPCHK(hipMemcpy(marks, P->wmarks, nw * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return NDNET_OK;
 }
 
