@@ -54,6 +54,8 @@ typedef struct ndnet_pn_chain {
   int32_t max_width2;     // widest activation of LDS region 1 (layers 0, 2, ... outputs); a fused
                           // layer's output is not stored in either region
   float* out;             // mode 1
+  float* clear;           // optional: set clear[0 .. clear_count) to -inf once the chain no longer
+  int64_t clear_count;    // reads it (re-arms a max-pool buffer for the next forward), or NULL
 } ndnet_pn_chain;
 
 /* Runs one chain over `batch` clouds on `stream` (a hipStream_t; NULL = default
@@ -61,6 +63,22 @@ typedef struct ndnet_pn_chain {
  * (layer sizes, LDS region widths) or NDNET_ERR_HIP (-21) on a launch failure.
  * No allocation, no synchronisation: graph-capturable. */
 int ndnet_pn_chain_run(const ndnet_pn_chain *args, int batch, void *stream);
+
+/* The per-cloud steps between the chains (TNet FC heads ndtnet.py:53-60 and
+ * the weight folds of pointnet_hip.py), for batch <= 16 clouds:
+ *   ndnet_pn_fc_run:     out[b][n] = act(bias[n] + sum_k in[b][k] W[n][k]),
+ *                        W row-major [N][K], K % 4 == 0, act = ReLU if relu
+ *                        (Linear + folded BatchNorm1d + ReLU, ndtnet.py:55-56)
+ *   ndnet_pn_head3_run:  t1[b] = h2[b] @ W3^T + b3 (9 outputs; the TNet
+ *                        identity folded into b3, ndtnet.py:57-60) and
+ *                        w1T[b] = t1[b] @ basis ([9][M]) -- conv1 with t1 folded
+ *   ndnet_pn_fold64_run: out[b] (64 x N) = t2[b] (64 x 64) @ rhs (64 x N)
+ * Same return codes as ndnet_pn_chain_run; graph-capturable. */
+int ndnet_pn_fc_run(const float *in, int ld_in, const float *W, const float *bias, float *out, int ld_out,
+                    int batch, int K, int N, int relu, void *stream);
+int ndnet_pn_head3_run(const float *h2, int ld_h, const float *W3, const float *b3, const float *basis,
+                       float *t1, float *w1T, int batch, int K, int M, void *stream);
+int ndnet_pn_fold64_run(const float *t2, const float *rhs, float *out, int batch, int N, void *stream);
 
 #ifdef __cplusplus
 }

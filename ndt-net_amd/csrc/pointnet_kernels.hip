@@ -375,6 +375,8 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int has
     }
     __syncthreads();
   }
+  if (A.clear && blockIdx.x == 0 && blockIdx.y == 0)
+    for (int64_t i = threadIdx.x; i < A.clear_count; i += kThreads) A.clear[i] = -INFINITY;
   if (A.mode == 1) {  // log_softmax over channels (ndtnet.py:239), [B][N][C+1] layout
     const int lg = reg[A.num_layers & 1];
     const int pl = (A.num_layers & 1) ? pitch1 : pitch0;
@@ -394,9 +396,136 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int has
   (void)kSlabFloats;
 }
 
+// ---------------------------------------------------------------------------
+// Per-cloud steps between the chains (the TNet FC heads, ndtnet.py:53-60, and
+// the weight folds), on the same stream.  The batch is small (B clouds, a
+// 16-row GEMM at B = 16), so these are weight-streaming GEMVs, not MFMA tiles.
+
+// out[b][n] = act(bias[n] + sum_k in[b][k] * W[n][k]), b < B <= 16.
+// One wave per output channel (4 per workgroup): its 64 lanes split K in
+// 16-byte pieces and keep one partial sum per cloud, so the weight row is read
+// once for all clouds; the partials meet in a wave reduction.
+__global__ void __launch_bounds__(256) k_pn_fc(const float* __restrict__ in, int ld_in, const float* __restrict__ W,
+                                               const float* __restrict__ bias, float* __restrict__ out, int ld_out,
+                                               int B, int K, int N, int relu) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= N) return;
+  const int kv = K / 4;
+  const f32x4* w = reinterpret_cast<const f32x4*>(W + (int64_t)n * K);
+  float acc[16];
+#pragma unroll
+  for (int b = 0; b < 16; b++) acc[b] = 0.0f;
+  for (int f = lane; f < kv; f += 64) {
+    const f32x4 wv = w[f];
+    f32x4 xv[16];
+#pragma unroll
+    for (int b = 0; b < 16; b++) xv[b] = reinterpret_cast<const f32x4*>(in + (int64_t)(b < B ? b : 0) * ld_in)[f];
+#pragma unroll
+    for (int b = 0; b < 16; b++) {
+      const f32x4 pr = xv[b] * wv;
+      acc[b] += (pr[0] + pr[1]) + (pr[2] + pr[3]);
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < 16; b++)
+    for (int o = 32; o > 0; o >>= 1) acc[b] += __shfl_xor(acc[b], o, 64);
+  if (lane < B) {
+    float v = 0.0f;
+#pragma unroll
+    for (int b = 0; b < 16; b++) v = lane == b ? acc[b] : v;
+    v += bias[n];
+    if (relu) v = fmaxf(v, 0.0f);
+    out[(int64_t)lane * ld_out + n] = v;
+  }
+}
+
+// TNet(3) tail: t1[b] = fc3(h2[b]) (+ I, folded into the bias) and the t1
+// fold of conv1, w1T[b] = t1[b] (1 x 9) @ basis (9 x 768).  One workgroup per cloud.
+__global__ void __launch_bounds__(256) k_pn_head3(const float* __restrict__ h2, int ld_h, const float* __restrict__ W3,
+                                                  const float* __restrict__ b3, const float* __restrict__ basis,
+                                                  float* __restrict__ t1_out, float* __restrict__ w1T, int K, int M) {
+  __shared__ float s_t[9];
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float* h = h2 + (int64_t)b * ld_h;
+  for (int o = wave; o < 9; o += 4) {  // one wave per output, lanes split K
+    float acc = 0.0f;
+    for (int k = lane; k < K; k += 64) acc += h[k] * W3[(int64_t)o * K + k];
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) {
+      s_t[o] = acc + b3[o];
+      t1_out[b * 9 + o] = acc + b3[o];
+    }
+  }
+  __syncthreads();
+  for (int m = threadIdx.x; m < M; m += blockDim.x) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int a = 0; a < 9; a++) acc += s_t[a] * basis[a * M + m];
+    w1T[(int64_t)b * M + m] = acc;
+  }
+}
+
+// TNet(64) fold: out[b] (64 x N) = t2[b] (64 x 64) @ rhs (64 x N), N % 64 == 0.
+// Workgroup (column tile of 64, cloud): both operand tiles in LDS, 4 x 4
+// outputs per thread.
+__global__ void __launch_bounds__(256) k_pn_fold64(const float* __restrict__ t2, const float* __restrict__ rhs,
+                                                   float* __restrict__ out, int N) {
+  __shared__ float s_a[64][65];
+  __shared__ float s_b[64][68];
+  const int b = blockIdx.y, j0 = blockIdx.x * 64;
+  const float* A = t2 + (int64_t)b * 4096;
+  for (int e = threadIdx.x; e < 4096; e += 256) {
+    s_a[e >> 6][e & 63] = A[e];
+    s_b[e >> 6][e & 63] = rhs[(int64_t)(e >> 6) * N + j0 + (e & 63)];
+  }
+  __syncthreads();
+  const int ti = (threadIdx.x >> 4) * 4, tj = (threadIdx.x & 15) * 4;
+  float acc[4][4] = {};
+  for (int k = 0; k < 64; k++) {
+    float av[4], bv[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) av[r] = s_a[ti + r][k];
+#pragma unroll
+    for (int c = 0; c < 4; c++) bv[c] = s_b[k][tj + c];
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+      for (int c = 0; c < 4; c++) acc[r][c] += av[r] * bv[c];
+  }
+  float* o = out + (int64_t)b * 64 * N;
+#pragma unroll
+  for (int r = 0; r < 4; r++)
+    *reinterpret_cast<f32x4*>(o + (int64_t)(ti + r) * N + j0 + tj) = f32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
+}
+
 }  // namespace
 
 extern "C" {
+
+int ndnet_pn_fc_run(const float* in, int ld_in, const float* W, const float* bias, float* out, int ld_out, int batch,
+                    int K, int N, int relu, void* stream) {
+  if (!in || !W || !bias || !out || batch <= 0 || batch > 16 || K <= 0 || K % 4 || N <= 0 || ld_in % 4 ||
+      ((uintptr_t)in | (uintptr_t)W) % 16)
+    return -20;
+  k_pn_fc<<<(N + 3) / 4, 256, 0, (hipStream_t)stream>>>(in, ld_in, W, bias, out, ld_out, batch, K, N, relu);
+  return hipGetLastError() == hipSuccess ? 0 : -21;
+}
+
+int ndnet_pn_head3_run(const float* h2, int ld_h, const float* W3, const float* b3, const float* basis, float* t1,
+                       float* w1T, int batch, int K, int M, void* stream) {
+  if (!h2 || !W3 || !b3 || !basis || !t1 || !w1T || batch <= 0 || K <= 0 || M <= 0) return -20;
+  k_pn_head3<<<batch, 256, 0, (hipStream_t)stream>>>(h2, ld_h, W3, b3, basis, t1, w1T, K, M);
+  return hipGetLastError() == hipSuccess ? 0 : -21;
+}
+
+int ndnet_pn_fold64_run(const float* t2, const float* rhs, float* out, int batch, int N, void* stream) {
+  if (!t2 || !rhs || !out || batch <= 0 || N <= 0 || N % 64 || ((uintptr_t)out % 16)) return -20;
+  k_pn_fold64<<<dim3(N / 64, batch), 256, 0, (hipStream_t)stream>>>(t2, rhs, out, N);
+  return hipGetLastError() == hipSuccess ? 0 : -21;
+}
+
 
 // One fused point-MLP chain over `batch` clouds on `stream` (see pointnet.h).
 int ndnet_pn_chain_run(const ndnet_pn_chain* args, int batch, void* stream) {

@@ -45,7 +45,7 @@ class _Chain(ctypes.Structure):
                 ("num_points", ctypes.c_int32), ("num_layers", ctypes.c_int32), ("L", _Layer * MAX_LAYERS),
                 ("mode", ctypes.c_int32), ("out_cols", ctypes.c_int32), ("gmax", ctypes.c_void_p),
                 ("gmax_ld", ctypes.c_int32), ("max_width", ctypes.c_int32), ("max_width2", ctypes.c_int32),
-                ("out", ctypes.c_void_p)]
+                ("out", ctypes.c_void_p), ("clear", ctypes.c_void_p), ("clear_count", ctypes.c_int64)]
 
 
 
@@ -119,6 +119,7 @@ class _Folded:
             self.C_tail = (_wT(self.c3w, 128, _pad(F, 32)), _bpad(self.c3b, _pad(F, 32)))
             self.s1a = self.s1w[:, :64].contiguous()      # acts on x_t2
             self.s1bT = self.s1w[:, 64:].t().contiguous()  # [F, 512], acts on g3
+            self.s1g = self.s1w[:, 64:].contiguous()       # [512, F] row-major for ndnet_pn_fc_run
             self.D_tail = [(_wT(self.s2w, 512, 256), self.s2b), (_wT(self.s3w, 256, 128), self.s3b),
                            (_wT(self.s4w, 128, _pad(self.C1, 32)), _bpad(self.s4b, _pad(self.C1, 32)))]
             self.c1wT = self.c1w.t().contiguous()         # [12, 64]
@@ -232,7 +233,8 @@ class _Workspace:
         f32 = dict(dtype=torch.float32, device=dev)
         Fp = W.C_tail[0].shape[1]
         # the three max-pooled vectors, -inf before the atomic maxima (ReLU'd maxima are >= 0)
-        self.gbuf = torch.empty((B, 2048 + Fp), **f32)
+        # -inf before the first forward; chain D re-arms it for the next one
+        self.gbuf = torch.full((B, 2048 + Fp), float("-inf"), **f32)
         self.g1, self.g2, self.g3 = self.gbuf[:, :1024], self.gbuf[:, 1024:2048], self.gbuf[:, 2048:]
         self.h1, self.h2 = torch.empty((B, 512), **f32), torch.empty((B, 256), **f32)
         self.t1, self.t2 = torch.empty((B, 9), **f32), torch.empty((B, 4096), **f32)
@@ -262,6 +264,9 @@ class _Workspace:
             return
         if self.structs is None:
             self.structs = [_build_chain(self.N, s[0], s[1], s[2], s[3], **s[4]) for s in self.specs]
+            # the last chain re-arms the max-pool buffer (-inf) for the next forward
+            self.structs[3].clear = self.gbuf.data_ptr()
+            self.structs[3].clear_count = self.gbuf.numel()
         if chain_timing is not None:  # torch events on the launch stream (bench.py)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -284,8 +289,69 @@ def _folded(model):
     return cache
 
 
+def _fc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: torch.Tensor, relu: bool) -> None:
+    """out = act(x @ w^T + b) on the HIP GEMV kernel (chunks of 16 clouds)."""
+    B = x.shape[0]
+    st = _lib.stream_ptr(x.device)
+    for c0 in range(0, B, 16):
+        n = min(16, B - c0)
+        rc = _lib.lib().ndnet_pn_fc_run(x[c0].data_ptr(), x.stride(0), w.data_ptr(), b.data_ptr(), out[c0].data_ptr(),
+                                        out.stride(0), n, w.shape[1], w.shape[0], 1 if relu else 0, st)
+        _lib.check(rc, "ndnet_pn_fc_run")
+
+
+def _glue_hip(W, ws, B: int):
+    """The per-cloud steps as HIP kernels: TNet heads (fc1, fc2, fc3 + I) and the
+    weight folds (t1 into conv1, t2 into conv2 / seg conv1)."""
+    st = lambda: _lib.stream_ptr(ws.gbuf.device)  # noqa: E731
+
+    def head_a():
+        t = W.t1
+        _fc(ws.g1, t["f1"], t["c1"], ws.h1, True)
+        _fc(ws.h1, t["f2"], t["c2"], ws.h2, True)
+        for c0 in range(0, B, 16):
+            n = min(16, B - c0)
+            rc = _lib.lib().ndnet_pn_head3_run(ws.h2[c0].data_ptr(), ws.h2.stride(0), t["f3"].data_ptr(),
+                                               t["c3"].data_ptr(), W.t1_basis.data_ptr(), ws.t1[c0].data_ptr(),
+                                               ws.w1T[c0].data_ptr(), n, 256, 12 * 64, st())
+            _lib.check(rc, "ndnet_pn_head3_run")
+
+    def head_b():
+        t = W.t2
+        _fc(ws.g2, t["f1"], t["c1"], ws.h1, True)
+        _fc(ws.h1, t["f2"], t["c2"], ws.h2, True)
+        _fc(ws.h2, t["f3"], t["c3"], ws.t2, False)
+        rc = _lib.lib().ndnet_pn_fold64_run(ws.t2.data_ptr(), W.t2_rhs.data_ptr(), ws.t2w.data_ptr(), B,
+                                            W.t2_rhs.shape[1], st())
+        _lib.check(rc, "ndnet_pn_fold64_run")
+
+    def seg_bias():
+        _fc(ws.g3[:, : W.F], W.s1g, W.s1b, ws.cvec, False)
+
+    return head_a, head_b, seg_bias
+
+
+def _glue_torch(W, ws, B: int):
+    """The same steps as torch ops (the emulation path of the tests)."""
+    def head_a():
+        t1 = _fc_head(ws.g1, W.t1, 3, ws.h1, ws.h2, ws.t1)
+        torch.matmul(t1.reshape(B, 9), W.t1_basis, out=ws.w1T.view(B, 12 * 64))
+
+    def head_b():
+        t2 = _fc_head(ws.g2, W.t2, 64, ws.h1, ws.h2, ws.t2)
+        torch.matmul(t2, W.t2_rhs, out=ws.t2w)
+
+    def seg_bias():
+        torch.addmm(W.s1b, ws.g3[:, : W.F], W.s1bT, out=ws.cvec)
+
+    return head_a, head_b, seg_bias
+
+
 def segmentation_forward(model, points: torch.Tensor, covariances: torch.Tensor, chain=None) -> torch.Tensor:
-    """model(points [B,N,3], covariances [B,N,9]) -> log-probs [B,N,C+1], eval mode."""
+    """model(points [B,N,3], covariances [B,N,9]) -> log-probs [B,N,C+1], eval mode.
+
+    ``chain``: None runs every step on the HIP kernels; a chain emulator
+    (``_chain_torch``) runs the chains and the per-cloud steps as torch ops."""
     cache = _folded(model)
     W = cache["W"]
     B, N, _ = points.shape
@@ -300,19 +366,17 @@ def segmentation_forward(model, points: torch.Tensor, covariances: torch.Tensor,
         x = points.as_strided((B, N, 12), (N * 12, 12, 1))
     else:
         x = torch.cat((points, covariances), dim=2).float().contiguous()
-    ws.gbuf.fill_(float("-inf"))
-    # A: TNet(3)
-    ws.chain(0, x, chain)
-    t1 = _fc_head(ws.g1, W.t1, 3, ws.h1, ws.h2, ws.t1)                        # [B,3,3]
-    torch.matmul(t1.reshape(B, 9), W.t1_basis, out=ws.w1T.view(B, 12 * 64))  # (W1 M(t1))^T
-    # B: conv1 (+t1) then TNet(64)
-    ws.chain(1, x, chain)
-    t2 = _fc_head(ws.g2, W.t2, 64, ws.h1, ws.h2, ws.t2)                       # [B,64,64]
-    torch.matmul(t2, W.t2_rhs, out=ws.t2w)        # conv2 and seg conv1[:, :64] with t2 folded in
-    # C: conv2, conv3, max over points
-    ws.chain(2, x, chain)
-    # D: seg head; the broadcast global feature enters as a per-cloud bias
-    torch.addmm(W.s1b, ws.g3[:, : W.F], W.s1bT, out=ws.cvec)
+    head_a, head_b, seg_bias = (_glue_hip if chain is None else _glue_torch)(W, ws, B)
+    if chain is not None:
+        ws.gbuf.fill_(float("-inf"))
+    ws.chain(0, x, chain)   # A: TNet(3) -> g1
+    head_a()                # t1, (W1 M(t1))^T
+    ws.chain(1, x, chain)   # B: conv1 (+t1) then TNet(64) -> g2
+    head_b()                # t2, t2 @ [W2^T | Ws1a^T]
+    ws.chain(2, x, chain)   # C: conv2, conv3, max over points -> g3
+    seg_bias()              # the broadcast global feature as a per-cloud bias of the seg head
     out = torch.empty((B, N, W.C1), dtype=torch.float32, device=dev)
     ws.chain(3, x, chain, out=out)
+    if chain is not None:
+        ws.gbuf.fill_(float("-inf"))  # the HIP path expects it armed (chain D re-arms it there)
     return out
