@@ -1118,22 +1118,46 @@ struct KLArgs {
   double* chunk_min;
   uint64_t k;
   int ncls;
+  int kl_lds;            // prune_and_emit keeps its per-cloud arrays in LDS (kl_lds_bytes)
 };
 
 // Prune (ndt.c:28-73) of cloud b's retained list to k NDs, then the output
 // rows (ndt.c:75-117).  Shared by k_kl (level 1) and k_prune (later levels).
-__device__ void prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t* s_u32, uint32_t* scratch) {
+// One workgroup per cloud, so the walk is latency-bound: with kLds the list's
+// ND column, the per-ND first occurrences / alive flags and the walk's
+// scratch live in LDS (lds: 5 ndcap + 8 ecap bytes, dynamic), else in global
+// scratch.
+template <bool kLds>
+__device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t* s_u32, uint32_t* scratch) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t kl_smem[];
   CloudCtl& c = A.ctl[b];
   const uint32_t nd = c.num_nds;
   const uint64_t ob = (uint64_t)b * A.ndcap, eb = (uint64_t)b * A.ecap;
-  uint8_t* alive = A.alive_all + ob;
-  uint32_t* first = A.first_occ_all + ob;
-  const uint32_t* op = A.ord_p_all + eb;
-  uint32_t* tmp = A.tmp_all + eb;
+  uint8_t* const g_alive = A.alive_all + ob;
+  const uint32_t* const g_op = A.ord_p_all + eb;
+  uint32_t* first;
+  uint32_t* tmp;
+  const uint32_t* op;
+  uint8_t* alive;
+  const uint32_t nv0 = c.num_valid, nkl0 = c.num_kl;
+  if constexpr (kLds) {
+    first = kl_smem;                                       // [ndcap]
+    tmp = kl_smem + A.ndcap;                               // [ecap]
+    uint32_t* s_op = kl_smem + A.ndcap + A.ecap;           // [ecap]
+    alive = (uint8_t*)(kl_smem + A.ndcap + 2 * A.ecap);    // [ndcap]
+    for (uint32_t i = threadIdx.x; i < nkl0; i += blockDim.x) s_op[i] = g_op[i];
+    for (uint32_t u = threadIdx.x; u < nd; u += blockDim.x) alive[u] = g_alive[u];
+    op = s_op;
+    __syncthreads();
+  } else {
+    first = A.first_occ_all + ob;
+    tmp = A.tmp_all + eb;
+    op = g_op;
+    alive = g_alive;
+  }
   __shared__ uint32_t s_failc, s_kpos, s_poison, s_kills;
   int32_t rc = 0;
   uint32_t kills = 0;
-  const uint32_t nv0 = c.num_valid, nkl0 = c.num_kl;
   if (k > nv0) {
     rc = -1;  // "Number of desired normal distributions is greater ..." (ndt.c:36-39)
   } else {
@@ -1227,9 +1251,12 @@ __device__ void prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t* s_u
       for (uint32_t i = threadIdx.x; i < nkl1; i += blockDim.x) {
         const uint32_t src = i + shift;
         const bool ok = src < c.num_phys;  // past it: entries the reference never wrote
-        tv[i] = ok ? ov[src] : 0.0;
-        tp[i] = ok ? opw[src] : kInvalid;
-        tq[i] = ok ? oq[src] : kInvalid;
+        const uint32_t sc = ok ? src : 0u;
+        const double v = ov[sc];
+        const uint32_t pv = opw[sc], qv = oq[sc];
+        tv[i] = ok ? v : 0.0;
+        tp[i] = ok ? pv : kInvalid;
+        tq[i] = ok ? qv : kInvalid;
       }
       __syncthreads();
       for (uint32_t i = threadIdx.x; i < nkl1; i += blockDim.x) {
@@ -1246,51 +1273,60 @@ __device__ void prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t* s_u
   }
   __syncthreads();
   KL_MARK(9);
-  // output rows: survivors in ascending voxel order
+  // output rows: survivors in ascending voxel order.  Row numbers by a scan
+  // of the alive flags (rowmap[r] = ND of row r), then one row per thread
+  // with every load issued unconditionally.
   const uint64_t kout = k;
-  const uint32_t* vn = A.nd_n + ob;
+  uint32_t* rowmap = tmp;  // the walk's scratch is free again
   uint32_t carry = 0;
   constexpr int IT = 8;
   for (uint32_t base = 0; base < nd; base += blockDim.x * IT) {
     const uint32_t u0 = base + threadIdx.x * IT;
-    uint32_t row[IT];
+    uint32_t row[IT], live[IT];
 #pragma unroll
-    for (int j = 0; j < IT; j++) row[j] = (u0 + j < nd) && alive[u0 + j];
+    for (int j = 0; j < IT; j++) live[j] = row[j] = (u0 + j < nd) && alive[u0 + j];
     uint32_t tot;
     block_scan_items(row, 0u, AddU32(), scratch, tot);
 #pragma unroll
     for (int j = 0; j < IT; j++) {
-      const uint32_t u = u0 + j;
-      if (u >= nd || !alive[u]) continue;
       const uint32_t rw = carry + row[j];
-      if (rw >= kout) continue;
-      const uint64_t o = (uint64_t)b * kout + rw;
-      const double* m = A.nd_mean + 3 * (ob + u);
-      const double* cv = A.nd_cov_post + 9 * (ob + u);
-      if (A.out) {
-        float* r = A.out + 12 * o;
-        for (int q = 0; q < 3; q++) {
-          const float f = (float)m[q];
-          r[q] = isfinite(f) ? f : 0.0f;  // nan_to_num(nan=0, posinf=0, neginf=0)
-        }
-        for (int q = 0; q < 9; q++) {
-          const float f = (float)cv[q];
-          r[3 + q] = isfinite(f) ? f : 0.0f;
-        }
-      }
-      if (A.out_cls) {
-        float* r = A.out_cls + (uint64_t)(A.ncls + 1) * o;
-        r[A.nd_cls[ob + u]] = 1.0f;
-      }
-      if (A.out_pc64) {
-        for (int q = 0; q < 3; q++) A.out_pc64[3 * o + q] = m[q];
-        for (int q = 0; q < 9; q++) A.out_cov64[9 * o + q] = cv[q];
-      }
-      if (A.out_cls16) A.out_cls16[o] = A.nd_cls[ob + u];
+      if (live[j] && rw < kout) rowmap[rw] = u0 + j;
     }
     carry += tot;
   }
-  (void)vn;
+  __syncthreads();
+  if constexpr (kLds) {  // the alive flags back to global (further prune levels, dumps)
+    for (uint32_t u = threadIdx.x; u < nd; u += blockDim.x) g_alive[u] = alive[u];
+  }
+  const uint32_t nrows = carry < kout ? carry : (uint32_t)kout;
+  for (uint32_t rw = threadIdx.x; rw < nrows; rw += blockDim.x) {
+    const uint32_t u = rowmap[rw];
+    const uint64_t o = (uint64_t)b * kout + rw;
+    const double* m = A.nd_mean + 3 * (ob + u);
+    const double* cv = A.nd_cov_post + 9 * (ob + u);
+    double v[12];
+#pragma unroll
+    for (int q = 0; q < 3; q++) v[q] = m[q];
+#pragma unroll
+    for (int q = 0; q < 9; q++) v[3 + q] = cv[q];
+    if (A.out) {
+      float* r = A.out + 12 * o;
+#pragma unroll
+      for (int q = 0; q < 12; q++) {
+        const float f = (float)v[q];
+        r[q] = isfinite(f) ? f : 0.0f;  // nan_to_num(nan=0, posinf=0, neginf=0)
+      }
+    }
+    if (A.out_cls) {
+      float* r = A.out_cls + (uint64_t)(A.ncls + 1) * o;
+      r[A.nd_cls[ob + u]] = 1.0f;
+    }
+    if (A.out_pc64) {
+      for (int q = 0; q < 3; q++) A.out_pc64[3 * o + q] = v[q];
+      for (int q = 0; q < 9; q++) A.out_cov64[9 * o + q] = v[3 + q];
+    }
+    if (A.out_cls16) A.out_cls16[o] = A.nd_cls[ob + u];
+  }
   __syncthreads();
   KL_MARK(10);
   if (threadIdx.x == 0) {
@@ -1299,6 +1335,7 @@ __device__ void prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t* s_u
     c.last_k = (uint32_t)k;
   }
   (void)s_u32;
+  return carry;  // survivors (block-uniform)
 }
 
 __device__ void write_stats(const KLArgs& A, int b) {
@@ -1338,11 +1375,10 @@ __device__ void zero_outputs(const KLArgs& A, int b, uint64_t k) {
 }
 
 // The class one-hot of rows past the survivors is class 0 (ndtnet_preprocessing.py:55-57).
-__device__ void pad_class_rows(const KLArgs& A, int b, uint64_t k) {
+__device__ void pad_class_rows(const KLArgs& A, int b, uint64_t k, uint32_t num_out) {
   if (!A.out_cls) return;
-  const CloudCtl& c = A.ctl[b];
   const uint64_t w = (uint64_t)(A.ncls + 1);
-  for (uint64_t r = c.num_out + threadIdx.x; r < k; r += blockDim.x) A.out_cls[w * ((uint64_t)b * k + r)] = 1.0f;
+  for (uint64_t r = num_out + threadIdx.x; r < k; r += blockDim.x) A.out_cls[w * ((uint64_t)b * k + r)] = 1.0f;
 }
 
 // Event order of one ND's in-place LU chain: the mutating events
@@ -1744,7 +1780,7 @@ __global__ void __launch_bounds__(kKLThreads) k_kl(KLArgs A) {
       c.num_out = 0;
       write_stats(A, b);
     }
-    pad_class_rows(A, b, A.k);
+    pad_class_rows(A, b, A.k, 0);
     return;
   }
   const uint32_t nd = c.num_nds;
@@ -1778,8 +1814,10 @@ __global__ void __launch_bounds__(kKLThreads) k_kl(KLArgs A) {
   }
   __syncthreads();
   KL_MARK(5);
-  prune_and_emit(A, b, A.k, s_u32, s_u32);
-  pad_class_rows(A, b, A.k);
+  const uint32_t nout = A.kl_lds ? prune_and_emit<true>(A, b, A.k, s_u32, s_u32)
+                                 : prune_and_emit<false>(A, b, A.k, s_u32, s_u32);
+  pad_class_rows(A, b, A.k, nout);
+  __syncthreads();
   if (threadIdx.x == 0) write_stats(A, b);
   KL_MARK(11);
 }
@@ -1790,12 +1828,14 @@ __global__ void __launch_bounds__(kKLThreads) k_prune(KLArgs A) {
   __shared__ uint32_t s_u32[16];
   zero_outputs(A, b, A.k);
   if (c.state != kAccepted) {
-    pad_class_rows(A, b, A.k);
+    pad_class_rows(A, b, A.k, 0);
     if (threadIdx.x == 0) write_stats(A, b);
     return;
   }
-  prune_and_emit(A, b, A.k, s_u32, s_u32);
-  pad_class_rows(A, b, A.k);
+  const uint32_t nout = A.kl_lds ? prune_and_emit<true>(A, b, A.k, s_u32, s_u32)
+                                 : prune_and_emit<false>(A, b, A.k, s_u32, s_u32);
+  pad_class_rows(A, b, A.k, nout);
+  __syncthreads();
   if (threadIdx.x == 0) write_stats(A, b);
 }
 
@@ -1831,6 +1871,12 @@ static void plan_free(Plan* P) {
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete P;
+}
+
+constexpr int kKLLdsMax = 150 * 1024;
+// dynamic LDS of k_kl / k_prune's LDS-resident prune (prune_and_emit<true>)
+static size_t kl_lds_bytes(const Plan* P) {
+  return 4 * ((size_t)P->ndcap + 2 * (size_t)P->ecap) + ((P->ndcap + 3) & ~3u);
 }
 
 static KLArgs kl_args(Plan* P, uint64_t k, float* out, float* out_cls, double* pc64, double* cov64, uint16_t* cls16) {
@@ -1882,6 +1928,7 @@ static KLArgs kl_args(Plan* P, uint64_t k, float* out, float* out_cls, double* p
   A.chunk_min = P->chunk_min;
   A.k = k;
   A.ncls = P->ncls;
+  A.kl_lds = kl_lds_bytes(P) <= (size_t)kKLLdsMax ? 1 : 0;
   return A;
 }
 
@@ -1956,7 +2003,7 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
     k_kl_merge<true><<<dim3(mg, B), kChunk * kMergeRuns, merge_lds_bytes(P), st>>>(A);
   else
     k_kl_merge<false><<<dim3(mg, B), kChunk * kMergeRuns, 0, st>>>(A);
-  k_kl<<<B, kKLThreads, 0, st>>>(A);
+  k_kl<<<B, kKLThreads, A.kl_lds ? kl_lds_bytes(P) : 0, st>>>(A);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[6], st));
   if (stats_dst)
     HIPCHK(hipMemcpyAsync(stats_dst, P->d_stats, sizeof(ndnet_ndt_stats) * B, hipMemcpyDeviceToDevice, st));
@@ -2093,6 +2140,8 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_kl_merge<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(2 * kMergeLdsChunks * kChunk * sizeof(unsigned long long)));
+  if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_kl, hipFuncAttributeMaxDynamicSharedMemorySize, kKLLdsMax);
+  if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_prune, hipFuncAttributeMaxDynamicSharedMemorySize, kKLLdsMax);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_welford<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             kWelfordBytes + kRtab * (int)sizeof(double));
@@ -2187,7 +2236,7 @@ int ndnet_ndt_prune(void* plan, void* stream, uint64_t num_desired, float* d_out
   if (!P || num_desired == 0) return NDNET_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   KLArgs A = kl_args(P, num_desired, d_out, d_out_classes, d_out_points, d_out_covariances, d_out_classes16);
-  k_prune<<<P->B, kKLThreads, 0, st>>>(A);
+  k_prune<<<P->B, kKLThreads, A.kl_lds ? kl_lds_bytes(P) : 0, st>>>(A);
   if (d_stats)
     HIPCHK(hipMemcpyAsync(d_stats, P->d_stats, sizeof(ndnet_ndt_stats) * P->B, hipMemcpyDeviceToDevice, st));
   HIPCHK(hipGetLastError());
