@@ -165,24 +165,29 @@ NDNET_FN void welford_update(Welford& w, const double* x) {
 // sub-column by 1/a_jj (divide when |a_jj| < DBL_MIN), rank-1 update
 // a_ic += a_jc * (-a_ij).  perm/signum from the pivot sequence.
 NDNET_FN void lu3(double* A, uint32_t& perm_packed, int& signum) {
-  int ipiv[3];
+  // Every array index below is a compile-time constant (pivot rows are
+  // applied with selects), so A stays in registers: a dynamically indexed
+  // private array would live in scratch or LDS.
+  int ipiv0 = 0, ipiv1 = 1;
 #pragma unroll
   for (int j = 0; j < 3; j++) {
     double mx = 0.0;
-    int r = 0;
+    int jp = j;
 #pragma unroll
     for (int i = j; i < 3; i++) {
       const double a = fabs(A[i * 3 + j]);
-      if (a > mx) { mx = a; r = i - j; }
+      if (a > mx) { mx = a; jp = i; }
     }
-    const int jp = j + r;
-    ipiv[j] = jp;
-    if (jp != j) {
+    if (j == 0) ipiv0 = jp;
+    if (j == 1) ipiv1 = jp;
+#pragma unroll
+    for (int i = j + 1; i < 3; i++) {
+      const bool sw = jp == i;
 #pragma unroll
       for (int c = 0; c < 3; c++) {
         const double t = A[j * 3 + c];
-        A[j * 3 + c] = A[jp * 3 + c];
-        A[jp * 3 + c] = t;
+        A[j * 3 + c] = sw ? A[i * 3 + c] : t;
+        A[i * 3 + c] = sw ? t : A[i * 3 + c];
       }
     }
     if (j < 2) {
@@ -203,19 +208,23 @@ NDNET_FN void lu3(double* A, uint32_t& perm_packed, int& signum) {
       }
     }
   }
-  int p[3] = {0, 1, 2};
-  int s = 1;
-#pragma unroll
-  for (int i = 0; i < 3; i++) {
-    const int pi = ipiv[i];
-    if (p[i] != p[pi]) {
-      const int t = p[i];
-      p[i] = p[pi];
-      p[pi] = t;
-      s = -s;
-    }
+  // permutation from the pivots (gsl_permutation_swap per step; a swap of
+  // two distinct positions flips the sign, ipiv[2] == 2 always)
+  int p0 = 0, p1 = 1, p2 = 2, s = 1;
+  if (ipiv0 != 0) {
+    const int t = p0;
+    p0 = ipiv0 == 1 ? p1 : p2;
+    if (ipiv0 == 1) p1 = t;
+    else p2 = t;
+    s = -s;
   }
-  perm_packed = (uint32_t)p[0] | ((uint32_t)p[1] << 2) | ((uint32_t)p[2] << 4);
+  if (ipiv1 != 1) {  // ipiv1 == 2
+    const int t = p1;
+    p1 = p2;
+    p2 = t;
+    s = -s;
+  }
+  perm_packed = (uint32_t)p0 | ((uint32_t)p1 << 2) | ((uint32_t)p2 << 4);
   signum = s;
 }
 

@@ -1410,42 +1410,54 @@ __global__ void __launch_bounds__(256) k_kl_chains(KLArgs A) {
   const uint32_t lin = A.vox_all[ob + u];
   const uint32_t z = lin / (lx * ly), y = (lin % (lx * ly)) / lx, x = lin % lx;
   const uint32_t nu = vn[u];
-  uint32_t elig = 0;
+  // neighbours (voxel.c:116-175, directions X+, X-, Y+, Y-, Z+, Z-): every
+  // dense-id load, then every count load, issued unconditionally from
+  // clamped indices (a predicated load would serialise on its own wait)
+  uint32_t dn[6];
+  bool in[6];
 #pragma unroll
   for (int d = 0; d < 6; d++) {
-    // voxel.c:116-175, directions X+, X-, Y+, Y-, Z+, Z-
     const uint32_t xx = x + (d == 0 ? 1u : d == 1 ? ~0u : 0u);
     const uint32_t yy = y + (d == 2 ? 1u : d == 3 ? ~0u : 0u);
     const uint32_t zz = z + (d == 4 ? 1u : d == 5 ? ~0u : 0u);
-    int32_t w = -1;
-    if (xx < lx && yy < ly && zz < lz) {
-      const uint32_t dn = dense[zz * lx * ly + yy * lx + xx];
-      if (dn != kInvalid) w = (int32_t)dn;
-    }
+    in[d] = xx < lx && yy < ly && zz < lz;
+    dn[d] = dense[in[d] ? zz * lx * ly + yy * lx + xx : lin];
+  }
+  uint32_t cn[6];
+#pragma unroll
+  for (int d = 0; d < 6; d++) cn[d] = vn[(in[d] && dn[d] != kInvalid) ? dn[d] : u];
+  uint32_t elig = 0;
+#pragma unroll
+  for (int d = 0; d < 6; d++) {
+    const int32_t w = (in[d] && dn[d] != kInvalid) ? (int32_t)dn[d] : -1;
     A.nb_all[6 * ob + 6 * u + d] = w;
-    if (w >= 0 && nu > 1 && vn[w] > 1) elig |= 1u << d;
+    if (w >= 0 && nu > 1 && cn[d] > 1) elig |= 1u << d;
   }
   const uint32_t mask = chain_mask(elig);
   const int T = __popc(mask);
+  A.nkeys_all[ob + u] = mask;
+  // every in-place LU state of the chain, stored step-major ([t][j][ND]) so a
+  // wave's stores are coalesced
   double S[9];
 #pragma unroll
   for (int j = 0; j < 9; j++) S[j] = A.nd_cov[9 * (ob + u) + j];
-  double* chain = A.chain_all + 108 * (ob + u);
-  uint32_t* ps = A.chain_ps_all + 12 * (ob + u);
+  double* chain = A.chain_all + (uint64_t)b * 108 * A.ndcap + u;
+  uint32_t* ps = A.chain_ps_all + (uint64_t)b * 12 * A.ndcap + u;
   for (int t = 0; t < T; t++) {
     uint32_t perm;
     int sg;
     lu3(S, perm, sg);
 #pragma unroll
-    for (int j = 0; j < 9; j++) chain[9 * t + j] = S[j];
-    ps[t] = perm | (sg < 0 ? 0x100u : 0u);
+    for (int j = 0; j < 9; j++) chain[(uint64_t)(9 * t + j) * A.ndcap] = S[j];
+    ps[(uint64_t)t * A.ndcap] = perm | (sg < 0 ? 0x100u : 0u);
   }
-  A.nkeys_all[ob + u] = mask;
 #pragma unroll
   for (int j = 0; j < 9; j++) A.nd_cov_post[9 * (ob + u) + j] = S[j];
 }
 
 // KL score of every (voxel, direction) slot (kullback_leibler.c:28-127, 141-180).
+// KL score per (ND, direction) slot (kullback_leibler.c:129-202 calling
+// kl_divergence, :28-127) from the two chain states at the event's rank.
 __global__ void __launch_bounds__(256) k_kl_events(KLArgs A) {
   const int b = blockIdx.y;
   const CloudCtl& c = A.ctl[b];
@@ -1457,25 +1469,30 @@ __global__ void __launch_bounds__(256) k_kl_events(KLArgs A) {
   const uint32_t u = s / 6, d = s % 6;
   const uint32_t* vn = A.nd_n + ob;
   const int32_t w = A.nb_all[6 * ob + s];
+  // every load issued unconditionally from clamped indices, in three rounds
+  // (neighbour -> counts and chain masks -> LU states)
+  const uint32_t wu = w >= 0 ? (uint32_t)w : u;
+  const uint32_t nu = vn[u], nw = vn[wu];
+  const uint32_t mu = A.nkeys_all[ob + u], mw = A.nkeys_all[ob + wu];
+  const int rp = __popc(mu & ((1u << (3 + d)) - 1u));
+  const int rq = __popc(mw & ((1u << qslot_of_dir(d ^ 1u)) - 1u));
+  const uint32_t rpc = rp < 12 ? (uint32_t)rp : 0u, rqc = rq < 12 ? (uint32_t)rq : 0u;
+  const double* chain = A.chain_all + (uint64_t)b * 108 * A.ndcap;
+  const uint32_t* cps = A.chain_ps_all + (uint64_t)b * 12 * A.ndcap;
+  double Lp[9], Lq[9];
+#pragma unroll
+  for (int j = 0; j < 9; j++) {
+    Lp[j] = chain[(uint64_t)(9 * rpc + j) * A.ndcap + u];
+    Lq[j] = chain[(uint64_t)(9 * rqc + j) * A.ndcap + wu];
+  }
+  const uint32_t psp = cps[(uint64_t)rpc * A.ndcap + u], psq = cps[(uint64_t)rqc * A.ndcap + wu];
   uint32_t flag = 0;
   double val = 0.0;
   if (w >= 0) {
-    if (vn[u] <= 1 || vn[w] <= 1) {
+    if (nu <= 1 || nw <= 1) {
       flag = 1;  // kl_divergence returns -1 with div 0 and the entry is kept
     } else {
-      const uint32_t mu = A.nkeys_all[ob + u], mw = A.nkeys_all[ob + (uint32_t)w];
-      const int rp = __popc(mu & ((1u << (3 + d)) - 1u));
-      const int rq = __popc(mw & ((1u << qslot_of_dir(d ^ 1u)) - 1u));
-      const double* LUp = A.chain_all + 108 * (ob + u) + 9 * rp;
-      const double* LUq = A.chain_all + 108 * (ob + (uint32_t)w) + 9 * rq;
-      const uint32_t psp = A.chain_ps_all[12 * (ob + u) + rp], psq = A.chain_ps_all[12 * (ob + (uint32_t)w) + rq];
       const int sp = (psp & 0x100) ? -1 : 1, sq = (psq & 0x100) ? -1 : 1;
-      double Lp[9], Lq[9];
-#pragma unroll
-      for (int j = 0; j < 9; j++) {
-        Lp[j] = LUp[j];
-        Lq[j] = LUq[j];
-      }
       const double pd = lu3_det(Lp, sp), qd = lu3_det(Lq, sq);
       if (!(pd == 0 || qd == 0) && lu3_sgndet(Lp, sp) != 0 && lu3_sgndet(Lq, sq) != 0) {
         flag = 1;
@@ -1520,8 +1537,11 @@ __global__ void __launch_bounds__(kChunk) k_kl_rank_chunks(KLArgs A) {
   const uint64_t eb = (uint64_t)b * A.ecap, kb = (uint64_t)b * A.sortcap + (uint64_t)ch * kChunk;
   const uint32_t t = threadIdx.x;
   const uint32_t sl = ch * kChunk + t;
-  const bool f = sl < nslots && A.slot_flag_all[eb + sl];
-  const double v = f ? A.slot_val_all[eb + sl] : 0.0;
+  const uint32_t slc = sl < nslots ? sl : 0u;  // unconditional loads
+  const uint32_t fl = A.slot_flag_all[eb + slc];
+  const double vl = A.slot_val_all[eb + slc];
+  const bool f = sl < nslots && fl;
+  const double v = f ? vl : 0.0;
   const bool isn = f && v != v;
   const bool num = f && !isn;
   const unsigned long long key = num ? score_key(v) : ~0ull;
@@ -1651,7 +1671,7 @@ __device__ inline uint32_t count_composite(KP K, SP S, uint32_t n, unsigned long
   return lo;
 }
 
-constexpr int kMergeRuns = 4;  // chunks merged per k_kl_merge workgroup (1024 threads)
+constexpr int kMergeRuns = 2;  // chunks merged per k_kl_merge workgroup (512 threads; ~one workgroup per CU at B = 16)
 
 template <bool kLds>
 __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
