@@ -165,10 +165,19 @@ def main() -> None:
     chains_info = {"ms": [round(float(v), 4) for v in chain_ms],
                    "tflops": [round(float(f / (t * 1e-3) / 1e12), 2) if t > 0 else None
                               for f, t in zip(cflops, chain_ms)]}
+    # the NDT front (k_reset + k_front: limits, every bisection pass, dense ids
+    # and binning in ONE launch) reads the f32 points once into registers and
+    # writes them grouped by ND: 12 N in + 12 N out per cloud
+    front = bool(stage_ms[1:4].sum() < 0.25 * stage_ms[0])  # events with no kernel between them
+    if front:
+        stage_names = ["k_reset+k_front (limits, bisection, dense ids, binning)", "welford",
+                       "kl (chains+events+order+prune)"]
+        stage_ms = np.array([stage_ms[0:4].sum(), stage_ms[4], stage_ms[5]])
     ndt_single = {  # stage index -> (kernel, algorithmic bytes per launch, what)
-        0: ("k_limits", 12.0 * n * B, "f32 xyz read once (12 N per cloud)"),
-        4: ("k_welford", 12.0 * n * B + (4 + 24 + 72) * k * B,
-            "grouped f32 xyz read once + count/mean/covariance write per ND"),
+        0: ("k_front", 24.0 * n * B, "f32 xyz read once + written once grouped by ND (12 N + 12 N per cloud)")
+           if front else ("k_limits", 12.0 * n * B, "f32 xyz read once (12 N per cloud)"),
+        (1 if front else 4): ("k_welford", 12.0 * n * B + (4 + 24 + 72) * k * B,
+                              "grouped f32 xyz read once + count/mean/covariance write per ND"),
     }
     cand = [("chain", i, float(chain_ms[i])) for i in range(4) if hip_fwd] + \
            [("ndt", i, float(stage_ms[i])) for i in ndt_single]

@@ -10,9 +10,13 @@
  * ndt-net_amd/ndnet/models/pointnet_hip.py (BatchNorm folding, per-cloud
  * steps, the four chains A-D).
  *
- * Layer weights are stored transposed, W^T[K][N] row-major (K input channels x
- * N output channels), with BatchNorm folded in, K padded to a multiple of 4
- * and N to 32.
+ * Layer weights are W^T (K input channels x N output channels) with BatchNorm
+ * folded in, K padded to a multiple of 16 and N to 32 (N <= 32) or 64, stored FRAGMENT-MAJOR
+ * for the 16x16x4 fp32 MFMA: element (k, n) at
+ *   ((n / 16) * (K / 16) + k / 16) * 256 + (((k / 4) % 4) * 16 + n % 16) * 4 + k % 4
+ * i.e. [column block][k-group][lane = 16 ((k/4)%4) + n%16][k%4] -- one 1 KB
+ * (k-group, column block) piece is what one wave loads per k-group, lane l
+ * holding the B operands of four consecutive MFMAs.  Padding is zero.
  */
 #ifndef NDNET_POINTNET_H_
 #define NDNET_POINTNET_H_
@@ -25,15 +29,15 @@ extern "C" {
 #define NDNET_PN_MAX_LAYERS 5
 
 typedef struct ndnet_pn_layer {
-  const float* wT;        // [K][ldw] (+ cloud * w_cloud_stride), 16-byte aligned
-  int64_t w_cloud_stride; // 0 for shared weights, else the per-cloud stride of folded weights
+  const float* w;         // fragment-major W^T, K * N floats (+ cloud * w_cloud_stride), 16-byte aligned
+  int64_t w_cloud_stride; // 0 for shared weights, else the per-cloud stride (floats) of folded weights
   const float* bias;      // [N] (+ cloud * bias_cloud_stride)
   int64_t bias_cloud_stride;
-  int32_t K, N;           // padded sizes: K % 4 == 0, N % 32 == 0
+  int32_t K, N;           // padded sizes: K % 16 == 0; N == 32 or N % 64 == 0
   int32_t relu;
-  int32_t ldw;            // row stride of wT in floats (>= N, % 4 == 0)
-  int32_t fuse_next;      // 1: this layer's output is produced in 64-column chunks, each consumed at once
-                          // by the next layer (whose N <= 256) -- the activation never occupies LDS whole
+  int32_t fuse_next;      // 1: this layer's output (N % 64 == 0) is produced in 64-column chunks, each
+                          // consumed at once by the next layer (whose N % 64 == 0, N <= 256) -- the
+                          // activation never occupies LDS whole
 } ndnet_pn_layer;
 
 // mode: 0 = max-pool the last layer over points into gmax[cloud][N]
@@ -50,8 +54,8 @@ typedef struct ndnet_pn_chain {
   int32_t out_cols;
   float* gmax;            // mode 0: [B][gmax_ld], pre-set to -inf
   int32_t gmax_ld;
-  int32_t max_width;      // widest activation of LDS region 0 (the input, layers 1, 3, ... outputs)
-  int32_t max_width2;     // widest activation of LDS region 1 (layers 0, 2, ... outputs); a fused
+  int32_t max_width;      // widest activation of LDS region 0 (the input, layers 1, 3, ... outputs), % 8 == 0
+  int32_t max_width2;     // widest activation of LDS region 1 (layers 0, 2, ... outputs), % 8 == 0; a fused
                           // layer's output is not stored in either region
   float* out;             // mode 1
   float* clear;           // optional: set clear[0 .. clear_count) to -inf once the chain no longer
@@ -71,13 +75,15 @@ int ndnet_pn_chain_run(const ndnet_pn_chain *args, int batch, void *stream);
  *                        (Linear + folded BatchNorm1d + ReLU, ndtnet.py:55-56)
  *   ndnet_pn_head3_run:  t1[b] = h2[b] @ W3^T + b3 (9 outputs; the TNet
  *                        identity folded into b3, ndtnet.py:57-60) and
- *                        w1T[b] = t1[b] @ basis ([9][M]) -- conv1 with t1 folded
- *   ndnet_pn_fold64_run: out[b] (64 x N) = t2[b] (64 x 64) @ rhs (64 x N)
+ *                        w1f[b] = t1[b] @ basis ([9][kin * nout] row-major) --
+ *                        conv1 with t1 folded, written fragment-major with K
+ *                        padded to 16 (16 * nout floats per cloud)
+ *   ndnet_pn_fold64_run: out[b] (64 x N, fragment-major) = t2[b] (64 x 64) @ rhs (64 x N)
  * Same return codes as ndnet_pn_chain_run; graph-capturable. */
 int ndnet_pn_fc_run(const float *in, int ld_in, const float *W, const float *bias, float *out, int ld_out,
                     int batch, int K, int N, int relu, void *stream);
 int ndnet_pn_head3_run(const float *h2, int ld_h, const float *W3, const float *b3, const float *basis,
-                       float *t1, float *w1T, int batch, int K, int M, void *stream);
+                       float *t1, float *w1f, int batch, int K, int kin, int nout, void *stream);
 int ndnet_pn_fold64_run(const float *t2, const float *rhs, float *out, int batch, int N, void *stream);
 
 #ifdef __cplusplus

@@ -12,12 +12,15 @@
 // epilogue: a column max over the tile, then one float atomic max per
 // channel) or in log-softmax.
 //
-// Tile geometry: 64 points = four 16-row MFMA blocks; 8 waves = 4 row blocks
-// x 2 column halves of a 256-column chunk (up to 8 accumulator blocks of
-// 16x16 per wave).  Weights stream through LDS in 16-row K-slabs of the chunk
-// (16 KB, shared by the four row blocks), loaded with 16-byte global loads by
-// all 512 threads and double-buffered: the next slab's loads are issued into
-// registers before the current slab's MFMAs and written to LDS after them.
+// Tile geometry: 64 points = four 16-row MFMA blocks per workgroup, 16 waves
+// (4 per SIMD, so a wave waiting on its weight loads leaves three to keep the
+// MFMA pipe busy).  A layer's waves split the tile as (row groups x column
+// groups): for N a multiple of 256 each wave takes all four row blocks of one
+// 16-column block (16 x 1), so every weight fragment is loaded once per
+// workgroup; 2 x 8 for N = 128, 4 x 4 for N = 64 / 32.  Weights are stored
+// fragment-major (include/ndnet_pointnet.h) and stream from L2 straight into
+// registers, two k-groups ahead; the activations stay in LDS.  Barriers only
+// separate layers (and the chunks of a fused pair).
 // B=16 clouds x 1000 points is 256 tiles: one workgroup per CU, one round.
 //
 // A layer flagged fuse_next (the seg head's 64 -> 512) is produced 64 columns
@@ -34,19 +37,12 @@
 namespace {
 
 constexpr int kP = 64;          // points per workgroup
-constexpr int kWaves = 8;
+constexpr int kWaves = 16;
 constexpr int kThreads = 64 * kWaves;
 constexpr int kRowBlocks = kP / 16;  // 4 (kWaves / 2)
-constexpr int kNC = 256;        // columns per chunk
 constexpr int kFuseNC = 64;     // columns per chunk of a fused layer
-constexpr int kSlabPitch = kNC + 16;  // floats per slab row (breaks the 2-way bank conflict)
-// KS: K rows per weight slab (template parameter: 32 where LDS allows, 16 for the seg head)
-template <int KS>
-struct Slab {
-  static constexpr int kFloats = KS * kSlabPitch;
-  static constexpr int kVecs = KS * kNC / 4 / kThreads;  // float4 loads per thread per slab
-};
-static_assert(kWaves == 2 * kRowBlocks, "waves = row blocks x 2 column halves");
+constexpr int kDepth = 4;       // weight k-groups in flight per wave
+static_assert(kWaves % kRowBlocks == 0, "every row group has whole column groups");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -56,290 +52,245 @@ __device__ inline void atomic_max_f32(float* addr, float v) {
   else atomicMin(reinterpret_cast<unsigned int*>(addr), __float_as_uint(v));
 }
 
-// dynamic LDS of k_pn_chain; regions are addressed by float offsets into it so
-// every activation/slab access compiles to ds_* (a generic pointer would give
-// flat_* ops, which count against vmcnt and stall on the weight prefetch)
+// dynamic LDS of k_pn_chain: the two activation regions and the fused pair's
+// double buffer, addressed by float offsets so every access is a ds_* op
 extern __shared__ __attribute__((aligned(16))) float g_smem[];
 
-// Loads this thread's share of slab rows [ks, ks + kr) x columns [c0, c0 + nc)
-// of W^T (row stride ldw) into registers.  Out-of-range elements load a valid
-// address and are zeroed at store time, so no vmcnt wait is forced into the
-// middle of the MFMA loop.
-template <int KS>
-__device__ inline unsigned slab_load(f32x4 (&r)[Slab<KS>::kVecs], const float* __restrict__ wT, int ldw, int ks,
-                                     int kr, int c0, int nc) {
-  constexpr int kSlabVecs = Slab<KS>::kVecs;
-  const int vpr = nc / 4;  // float4 per slab row
-  unsigned ok_mask = 0;
-#pragma unroll
-  for (int v = 0; v < kSlabVecs; v++) {
-    const int e = threadIdx.x + kThreads * v;
-    const int row = e / (kNC / 4), col4 = e % (kNC / 4);
-    const bool ok = row < kr && col4 < vpr;
-    ok_mask |= (unsigned)ok << v;
-    r[v] = *reinterpret_cast<const f32x4*>(wT + (int64_t)(ks + (ok ? row : 0)) * ldw + c0 + (ok ? 4 * col4 : 0));
-  }
-  return ok_mask;
-}
-
-template <int KS>
-__device__ inline void slab_store(const f32x4 (&r)[Slab<KS>::kVecs], unsigned ok_mask, float* slab) {
-  constexpr int kSlabVecs = Slab<KS>::kVecs;
-#pragma unroll
-  for (int v = 0; v < kSlabVecs; v++) {
-    const int e = threadIdx.x + kThreads * v;
-    const int row = e / (kNC / 4), col4 = e % (kNC / 4);
-    *reinterpret_cast<f32x4*>(slab + row * kSlabPitch + 4 * col4) =
-        ((ok_mask >> v) & 1) ? r[v] : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-}
-
-// acc[j] += A[this wave's 16 rows][ks, ks + KS) . slab[0, KS)[cw + 16 j + ...]
-// One staged slab's MFMAs; rows of the slab past K are zero and activation
-// columns past K are finite (zero-filled input columns), so every k-step runs
-// unconditionally.  Fragments are software-pipelined one k-step ahead.
-template <int NB, int KS>
-__device__ __attribute__((always_inline)) void mma_slab(f32x4 (&acc)[NB], const float* arow, int ks,
-                                                        const float* slab, int cw) {
-  const int lane = threadIdx.x & 63;
-  const int kq = lane >> 4, cl = lane & 15;
-  const float* bbase = slab + kq * kSlabPitch + cw + cl;
-  float a = arow[ks];
-  float bv[NB];
-#pragma unroll
-  for (int j = 0; j < NB; j++) bv[j] = bbase[16 * j];
-#pragma unroll
-  for (int kk = 0; kk < KS; kk += 4) {
-    float an = 0.f, bn[NB];
-    if (kk + 4 < KS) {
-      an = arow[ks + kk + 4];
-#pragma unroll
-      for (int j = 0; j < NB; j++) bn[j] = bbase[(kk + 4) * kSlabPitch + 16 * j];
-    }
-#pragma unroll
-    for (int j = 0; j < NB; j++) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv[j], acc[j], 0, 0, 0);
-    if (kk + 4 < KS) {
-      a = an;
-#pragma unroll
-      for (int j = 0; j < NB; j++) bv[j] = bn[j];
-    }
-    // keep the next step's fragment reads interleaved with this step's MFMAs
-#pragma unroll
-    for (int j = 0; j < NB; j++) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-    }
-  }
-}
-
-// acc[j] += A[rows of this wave][0, K) . W^T[k0 + (0..K)][c0 + cw + 16 j ...]
-// A: activations at float offset `in` (pitch pin) of g_smem; W^T rows k0.. of
-// the layer, columns [c0, c0 + nc).  Weight slabs double-buffered in LDS.
-template <int NB, int KS>
-__device__ __attribute__((always_inline)) void accumulate(f32x4 (&acc)[NB], int in, int pin,
-                                                          const float* __restrict__ wT, int ldw, int K, int k0,
-                                                          int c0, int nc, int slabs_off) {
-  constexpr int kSlabFloats = Slab<KS>::kFloats;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int kq = lane >> 4, cl = lane & 15;
-  const int cw = wc * (nc / 2);
-  const int nslab = (K + KS - 1) / KS;
-  float* const slabs = g_smem + slabs_off;
-  f32x4 stage[Slab<KS>::kVecs];
-  unsigned ok = slab_load<KS>(stage, wT, ldw, k0, K < KS ? K : KS, c0, nc);
-  slab_store<KS>(stage, ok, slabs);
-  __syncthreads();
-  const float* arow = g_smem + in + (16 * wr + cl) * pin + kq;
-  for (int s = 0; s < nslab; s++) {
-    const int ks = s * KS;
-    const bool more = s + 1 < nslab;
-    if (more) ok = slab_load<KS>(stage, wT, ldw, k0 + ks + KS, K - ks - KS < KS ? K - ks - KS : KS, c0, nc);
-    mma_slab<NB, KS>(acc, arow, ks, slabs + (s & 1) * kSlabFloats, cw);
-    if (more) slab_store<KS>(stage, ok, slabs + ((s + 1) & 1) * kSlabFloats);
-    __syncthreads();
-  }
-}
-
-// Bias + ReLU of this wave's accumulators, stored to an activation region
-// (column c of the chunk goes to column out_c0 + c).
-template <int NB>
-__device__ __attribute__((always_inline)) void store_act(const f32x4 (&acc)[NB], const float* __restrict__ bias,
-                                                         int c0, int nc, int relu, int out, int pout, int out_c0) {
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int kq = lane >> 4, cl = lane & 15;
-  const int cw = wc * (nc / 2);
-#pragma unroll
-  for (int j = 0; j < NB; j++) {
-    const int c = cw + 16 * j + cl;
-    const float bv = bias[c0 + c];
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      float v = acc[j][r] + bv;
-      if (relu) v = fmaxf(v, 0.0f);
-      g_smem[out + (16 * wr + 4 * kq + r) * pout + out_c0 + c] = v;
-    }
-  }
-}
-
-// Bias + ReLU + max over the tile's valid rows, one atomic max per channel:
-// each wave reduces its 16 rows with shuffles, the four row blocks meet in LDS.
-template <int NB>
-__device__ __attribute__((always_inline)) void max_pool(const f32x4 (&acc)[NB], const float* __restrict__ bias, int c0,
-                                                        int nc, int relu, int rows_valid, float* gmax, int cmax_off) {
-  float* const s_cmax = g_smem + cmax_off;  // [kRowBlocks][kNC]
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int kq = lane >> 4, cl = lane & 15;
-  const int cw = wc * (nc / 2);
-#pragma unroll
-  for (int j = 0; j < NB; j++) {
-    const int c = cw + 16 * j + cl;
-    const float bv = bias[c0 + c];
-    float m = -INFINITY;
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      float v = acc[j][r] + bv;
-      if (relu) v = fmaxf(v, 0.0f);
-      if (16 * wr + 4 * kq + r < rows_valid) m = fmaxf(m, v);
-    }
-    m = fmaxf(m, __shfl_xor(m, 16, 64));
-    m = fmaxf(m, __shfl_xor(m, 32, 64));
-    if (lane < 16) s_cmax[wr * kNC + c] = m;
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < nc; c += kThreads) {
-    float m = s_cmax[c];
-#pragma unroll
-    for (int q = 1; q < kRowBlocks; q++) m = fmaxf(m, s_cmax[q * kNC + c]);
-    if (m > -INFINITY) atomic_max_f32(gmax + c0 + c, m);
-  }
-  __syncthreads();
-}
-
+// Weights are fragment-major (include/ndnet_pointnet.h): the 16 x 16 block
+// (k-group kg, column block cb) of W^T is 64 lanes x float4, lane kq * 16 + cl
+// holding W^T[16 kg + 4 kq + s][16 cb + cl] for s = 0..3 -- the B operands of
+// four consecutive 16x16x4 MFMAs, one coalesced 1 KB global_load_dwordx4 per
+// wave.  The A operand uses the same K permutation: lane (kq, cl) reads
+// activation row cl, columns 16 kg + 4 kq .. + 3 with one ds_read_b128.  So
+// the weights stream from L2 straight into registers (no LDS staging, no
+// barrier inside a layer) and only the activations live in LDS.
 struct LayerCtx {
-  const float* __restrict__ wT;
+  const f32x4* __restrict__ w;  // this cloud's fragments, offset by the lane
   const float* __restrict__ bias;
-  int ldw, K, relu;
+  int KG, N, relu;
 };
 
 __device__ inline LayerCtx layer_ctx(const ndnet_pn_chain& A, int l, int b) {
   const ndnet_pn_layer& L = A.L[l];
   LayerCtx C;
-  C.wT = L.wT + (int64_t)b * L.w_cloud_stride;
+  C.w = reinterpret_cast<const f32x4*>(L.w + (int64_t)b * L.w_cloud_stride) + (threadIdx.x & 63);
   C.bias = L.bias + (int64_t)b * L.bias_cloud_stride;
-  C.ldw = L.ldw;
-  C.K = L.K;
+  C.KG = L.K / 16;
+  C.N = L.N;
   C.relu = L.relu;
   return C;
 }
 
-// An ordinary layer: one continuous mainloop over every (256-column chunk,
-// K-slab) pair, so the next chunk's first slab is in flight during the last
-// slab (and epilogue) of the current one.  All chunks of a layer share NB
-// (N <= 256, or N a multiple of 256: checked by the launcher).
-template <int NB, int KS>
-__device__ void plain_layer(const LayerCtx& C, int N, int in, int pin, int out, int pout, float* gmax,
-                            int rows_valid, int slabs_off, int cmax_off) {
-  constexpr int kSlabFloats = Slab<KS>::kFloats;
+template <int RB, int NB>
+__device__ __attribute__((always_inline)) inline void zero_acc(f32x4 (&acc)[RB][NB]) {
+#pragma unroll
+  for (int rb = 0; rb < RB; rb++)
+#pragma unroll
+    for (int j = 0; j < NB; j++) acc[rb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// acc[rb][j] += A(row block rb, one k-group) . W(k-group, column block j)
+template <int RB, int NB>
+__device__ __attribute__((always_inline)) inline void mma_kgroup(f32x4 (&acc)[RB][NB], const f32x4 (&a)[RB],
+                                                                 const f32x4 (&bw)[NB]) {
+#pragma unroll
+  for (int s = 0; s < 4; s++)
+#pragma unroll
+    for (int rb = 0; rb < RB; rb++)
+#pragma unroll
+      for (int j = 0; j < NB; j++) acc[rb][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rb][s], bw[j][s], acc[rb][j], 0, 0, 0);
+}
+
+// T = nchunk * nkg k-group steps.  Step t is k-group kg0 + t % nkg of column
+// chunk c = t / nkg, whose column blocks for this wave are cb0 + c * cbs + j;
+// its A fragment sits at abase + 16 (t % nkg) (+ 16 rb rows).  epi(acc, c)
+// runs at each chunk end.  The weight fragments are prefetched kDepth steps
+// ahead in a ring of register sets; past the last step the loads repeat it.
+template <int RB, int NB, class Epi>
+__device__ __attribute__((always_inline)) inline void run_tiles(f32x4 (&acc)[RB][NB], const f32x4* __restrict__ w,
+                                                                int KG, int kg0, int nkg, int cb0, int cbs,
+                                                                int nchunk, const float* abase, int pin, Epi epi) {
+  const int T = nchunk * nkg;
+  const int64_t jstride = (int64_t)KG * 64;
+  const int64_t chunk_jump = ((int64_t)cbs * KG - (nkg - 1)) * 64;
+  const f32x4* lp = w + ((int64_t)cb0 * KG + kg0) * 64;  // the next load's step
+  int lkk = 0, lleft = T;
+  auto load = [&](f32x4 (&bw)[NB]) {
+#pragma unroll
+    for (int j = 0; j < NB; j++) bw[j] = lp[j * jstride];
+    if (lleft > 1) {
+      lleft--;
+      if (++lkk == nkg) {
+        lkk = 0;
+        lp += chunk_jump;
+      } else {
+        lp += 64;
+      }
+    }
+  };
+  // A fragments are software-pipelined one step ahead too (the A region is
+  // read-only during the layer, so the prefetch may run into the next chunk)
+  int kk = 0, c = 0, akk = 0;
+  f32x4 a[RB];
+  auto load_a = [&]() {
+#pragma unroll
+    for (int rb = 0; rb < RB; rb++) a[rb] = *reinterpret_cast<const f32x4*>(abase + rb * 16 * pin + 16 * akk);
+    akk = akk + 1 == nkg ? 0 : akk + 1;
+  };
+  auto step = [&](const f32x4 (&bw)[NB]) {
+    f32x4 cur[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; rb++) cur[rb] = a[rb];
+    load_a();
+    mma_kgroup<RB, NB>(acc, cur, bw);
+    if (++kk == nkg) {
+      epi(acc, c);
+      kk = 0;
+      c++;
+    }
+  };
+  load_a();
+  f32x4 bq[kDepth][NB];
+#pragma unroll
+  for (int i = 0; i < kDepth; i++) load(bq[i]);
+  for (int t = 0; t < T; t += kDepth) {
+#pragma unroll
+    for (int i = 0; i < kDepth; i++) {
+      if (t + i < T) {
+        step(bq[i]);
+        load(bq[i]);
+      }
+    }
+  }
+}
+
+// Bias + ReLU of this wave's tile (rows row0.., bias columns col0 + 16 j + cl)
+// into an LDS activation region at columns oc0 + 16 j + cl.
+template <int RB, int NB>
+__device__ __attribute__((always_inline)) inline void store_cols(const f32x4 (&acc)[RB][NB],
+                                                                 const float* __restrict__ bias, int col0, int relu,
+                                                                 int row0, int out, int pout, int oc0) {
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
   const int kq = lane >> 4, cl = lane & 15;
-  const int nc = N < kNC ? N : kNC;
-  const int cw = wc * (nc / 2);
-  const int nslab = (C.K + KS - 1) / KS;
-  const int total = (N / nc) * nslab;
-  float* const slabs = g_smem + slabs_off;
-  const float* arow = g_smem + in + (16 * wr + cl) * pin + kq;
-  f32x4 acc[NB];
 #pragma unroll
-  for (int j = 0; j < NB; j++) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 stage[Slab<KS>::kVecs];
-  unsigned ok = slab_load<KS>(stage, C.wT, C.ldw, 0, C.K < KS ? C.K : KS, 0, nc);
-  slab_store<KS>(stage, ok, slabs);
+  for (int j = 0; j < NB; j++) {
+    const float bv = bias[col0 + 16 * j + cl];
+#pragma unroll
+    for (int rb = 0; rb < RB; rb++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        float v = acc[rb][j][r] + bv;
+        if (relu) v = fmaxf(v, 0.0f);
+        g_smem[out + (row0 + 16 * rb + 4 * kq + r) * pout + oc0 + 16 * j + cl] = v;
+      }
+  }
+}
+
+// Bias + ReLU + max over this wave's valid rows, one float atomic max per
+// column and wave into gmax (the workgroup's row groups meet in the atomics).
+template <int RB, int NB>
+__device__ __attribute__((always_inline)) inline void pool_cols(const f32x4 (&acc)[RB][NB],
+                                                                const float* __restrict__ bias, int col0, int relu,
+                                                                int row0, int rows_valid, float* gmax) {
+  const int lane = threadIdx.x & 63;
+  const int kq = lane >> 4, cl = lane & 15;
+#pragma unroll
+  for (int j = 0; j < NB; j++) {
+    const float bv = bias[col0 + 16 * j + cl];
+    float m = -INFINITY;
+#pragma unroll
+    for (int rb = 0; rb < RB; rb++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        float v = acc[rb][j][r] + bv;
+        if (relu) v = fmaxf(v, 0.0f);
+        if (row0 + 16 * rb + 4 * kq + r < rows_valid) m = fmaxf(m, v);
+      }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    if (lane < 16 && m > -INFINITY) atomic_max_f32(gmax + col0 + 16 * j + cl, m);
+  }
+}
+
+// One layer: RB row blocks x NB column blocks per wave; 4 / RB row groups x
+// 4 RB column groups of waves; N in chunks of (column groups x NB x 16).
+template <int RB, int NB>
+__device__ void plain_layer(const LayerCtx& C, int in, int pin, int out, int pout, float* gmax, int rows_valid) {
+  constexpr int WR = kRowBlocks / RB, WC = kWaves / WR, CB = WC * NB;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave / WC, wc = wave % WC;
+  const int kq = lane >> 4, cl = lane & 15;
+  const int row0 = wr * RB * 16;
+  const float* abase = g_smem + in + (row0 + cl) * pin + 4 * kq;
+  // N is a multiple of the chunk width, or narrower than one chunk (then the
+  // waves past column N / 16 idle; there is no barrier inside a layer)
+  if (C.N < CB * 16 && wc * NB * 16 >= C.N) return;
+  f32x4 acc[RB][NB];
+  zero_acc(acc);
+  auto epi = [&](f32x4 (&a)[RB][NB], int c) {
+    const int col0 = (c * CB + wc * NB) * 16;
+    if (gmax) pool_cols<RB, NB>(a, C.bias, col0, C.relu, row0, rows_valid, gmax);
+    else store_cols<RB, NB>(a, C.bias, col0, C.relu, row0, out, pout, col0);
+    zero_acc(a);
+  };
+  const int nchunk = C.N < CB * 16 ? 1 : C.N / (CB * 16);
+  run_tiles<RB, NB>(acc, C.w, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase, pin, epi);
+}
+
+// A fused pair: layer P (K -> N1) produced 64 columns at a time into a
+// double-buffered LDS chunk (waves 4 x 4, one 16 x 16 tile each), each chunk
+// consumed at once as 4 k-groups of layer Q (N1 -> N2 = one chunk of Q's
+// (RB, NB) split), whose accumulators persist across the chunks: the N1-wide
+// activation never needs LDS of its own.  One barrier per chunk.
+template <int RB, int NB>
+__device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin, int fbuf, int out, int pout,
+                           float* gmax, int rows_valid) {
+  constexpr int kFP = kFuseNC + 4;
+  constexpr int WR = kRowBlocks / RB, WC = kWaves / WR;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kq = lane >> 4, cl = lane & 15;
+  // P: row block wave / 4, column block 4 f + wave % 4
+  const int prow0 = (wave >> 2) * 16, pwc = wave & 3;
+  const float* ain = g_smem + in + (prow0 + cl) * pin + 4 * kq;
+  // Q: row group wave / WC, column group wave % WC
+  const int qrow0 = (wave / WC) * RB * 16, qwc = wave % WC;
+  const bool qidle = qwc * NB * 16 >= Q.N;
+  const int nf = P.N / kFuseNC;
+  auto p_chunk = [&](int f) {
+    f32x4 acc1[1][1];
+    zero_acc(acc1);
+    const int fb = fbuf + (f & 1) * kP * kFP;
+    auto epi = [&](f32x4 (&a)[1][1], int) {
+      store_cols<1, 1>(a, P.bias, 64 * f + 16 * pwc, P.relu, prow0, fb, kFP, 16 * pwc);
+    };
+    run_tiles<1, 1>(acc1, P.w, P.KG, 0, P.KG, 4 * f + pwc, 0, 1, ain, pin, epi);
+  };
+  f32x4 acc2[RB][NB];
+  zero_acc(acc2);
+  p_chunk(0);
   __syncthreads();
-  int c0 = 0, s = 0;
-  for (int t = 0; t < total; t++) {
-    const bool more = t + 1 < total;
-    const bool chunk_end = s + 1 == nslab;
-    if (more) {
-      const int s1 = chunk_end ? 0 : s + 1, c1 = chunk_end ? c0 + nc : c0;
-      const int ks1 = s1 * KS;
-      ok = slab_load<KS>(stage, C.wT, C.ldw, ks1, C.K - ks1 < KS ? C.K - ks1 : KS, c1, nc);
+  for (int f = 0; f < nf; f++) {
+    if (!qidle) {
+      const float* af = g_smem + fbuf + (f & 1) * kP * kFP + (qrow0 + cl) * kFP + 4 * kq;
+      run_tiles<RB, NB>(acc2, Q.w, Q.KG, 4 * f, 4, qwc * NB, 0, 1, af, kFP, [](f32x4 (&)[RB][NB], int) {});
     }
-    mma_slab<NB, KS>(acc, arow, s * KS, slabs + (t & 1) * kSlabFloats, cw);
-    if (chunk_end) {
-      if (gmax) max_pool<NB>(acc, C.bias, c0, nc, C.relu, rows_valid, gmax, cmax_off);
-      else store_act<NB>(acc, C.bias, c0, nc, C.relu, out, pout, c0);
-#pragma unroll
-      for (int j = 0; j < NB; j++) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    if (more) slab_store<KS>(stage, ok, slabs + ((t + 1) & 1) * kSlabFloats);
+    if (f + 1 < nf) p_chunk(f + 1);
     __syncthreads();
-    if (chunk_end) {
-      s = 0;
-      c0 += nc;
-    } else {
-      s++;
-    }
   }
-  (void)lane;
-  (void)kq;
-  (void)cl;
+  if (qidle) return;
+  if (gmax) pool_cols<RB, NB>(acc2, Q.bias, 16 * qwc * NB, Q.relu, qrow0, rows_valid, gmax);
+  else store_cols<RB, NB>(acc2, Q.bias, 16 * qwc * NB, Q.relu, qrow0, out, pout, 16 * qwc * NB);
 }
 
-// A fused pair: layer P (K -> N1, produced kFuseNC columns at a time into the
-// F buffer) feeding layer Q (N1 -> N2 <= 256, accumulated across the chunks).
-template <int NB2, int KS>
-__device__ void fused_pair(const LayerCtx& P, int N1, const LayerCtx& Q, int N2, int in, int pin, int fbuf, int out,
-                           int pout, float* gmax, int rows_valid, int slabs, int cmax_off) {
-  constexpr int kFP = kFuseNC + 1;
-  f32x4 acc2[NB2];
-#pragma unroll
-  for (int j = 0; j < NB2; j++) acc2[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int f0 = 0; f0 < N1; f0 += kFuseNC) {
-    f32x4 acc1[kFuseNC / 32];
-#pragma unroll
-    for (int j = 0; j < kFuseNC / 32; j++) acc1[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    accumulate<kFuseNC / 32, KS>(acc1, in, pin, P.wT, P.ldw, P.K, 0, f0, kFuseNC, slabs);
-    store_act<kFuseNC / 32>(acc1, P.bias, f0, kFuseNC, P.relu, fbuf, kFP, 0);  // chunk-local columns
-    __syncthreads();
-    accumulate<NB2, KS>(acc2, fbuf, kFP, Q.wT, Q.ldw, kFuseNC, f0, 0, N2, slabs);  // ends in a barrier
-  }
-  if (gmax) max_pool<NB2>(acc2, Q.bias, 0, N2, Q.relu, rows_valid, gmax, cmax_off);
-  else store_act<NB2>(acc2, Q.bias, 0, N2, Q.relu, out, pout, 0);
-}
-
-#define NDNET_PN_NB_SWITCH(nb, CALL) \
-  switch (nb) {                      \
-    case 8: CALL(8); break;          \
-    case 7: CALL(7); break;          \
-    case 6: CALL(6); break;          \
-    case 5: CALL(5); break;          \
-    case 4: CALL(4); break;          \
-    case 3: CALL(3); break;          \
-    case 2: CALL(2); break;          \
-    default: CALL(1); break;         \
-  }
-
-template <int KS>
-__global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int has_fuse) {
-  constexpr int kSlabFloats = Slab<KS>::kFloats;
+__global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A) {
   const int b = blockIdx.y;
   const int p0 = blockIdx.x * kP;
-  // LDS: activation region 0 | region 1 | [fused-chunk buffer] | two weight slabs | [column maxima]
-  const int pitch0 = A.max_width + 1, pitch1 = A.max_width2 + 1;
+  // LDS: activation region 0 | region 1 | [fused-chunk double buffer]
+  const int pitch0 = A.max_width + 4, pitch1 = A.max_width2 + 4;
   const int reg[2] = {0, kP * pitch0};
   const int fbuf = kP * (pitch0 + pitch1);
-  const int slabs = fbuf + (has_fuse ? kP * (kFuseNC + 1) : 0);
-  const int cmax = slabs + 2 * kSlabFloats;
-  // input tile, zero-filled to a whole slab of columns
-  const int K0 = (A.L[0].K + KS - 1) / KS * KS;
+  // input tile, zero-filled to the first layer's K (a multiple of 16)
+  const int K0 = A.L[0].K;
   for (int e = threadIdx.x; e < kP * K0; e += kThreads) {
     const int r = e / K0, c = e % K0;
     const int p = p0 + r;
@@ -357,21 +308,18 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int has
       const bool last = l + 2 == A.num_layers;
       const int out = reg[(l + 2) & 1], pout = ((l + 2) & 1) ? pitch1 : pitch0;
       float* gm = (last && gmax_b) ? gmax_b : nullptr;
-#define NDNET_PN_FUSED(NB) \
-  fused_pair<NB, KS>(P, A.L[l].N, Q, A.L[l + 1].N, in, pin, fbuf, out, pout, gm, rows_valid, slabs, cmax)
-      NDNET_PN_NB_SWITCH(A.L[l + 1].N / 32, NDNET_PN_FUSED)
-#undef NDNET_PN_FUSED
+      if (Q.N == 256) fused_pair<4, 1>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid);
+      else if (Q.N > 64) fused_pair<2, 1>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid);
+      else fused_pair<1, 1>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid);
       l++;
     } else {
       const LayerCtx C = layer_ctx(A, l, b);
       const bool last = l + 1 == A.num_layers;
       const int out = reg[(l + 1) & 1], pout = ((l + 1) & 1) ? pitch1 : pitch0;
       float* gm = (last && gmax_b) ? gmax_b : nullptr;
-      const int N = A.L[l].N;
-      const int nc = N < kNC ? N : kNC;
-#define NDNET_PN_PLAIN(NB) plain_layer<NB, KS>(C, N, in, pin, out, pout, gm, rows_valid, slabs, cmax)
-      NDNET_PN_NB_SWITCH(nc / 32, NDNET_PN_PLAIN)
-#undef NDNET_PN_PLAIN
+      if (C.N % 256 == 0) plain_layer<4, 1>(C, in, pin, out, pout, gm, rows_valid);
+      else if (C.N % 128 == 0) plain_layer<2, 1>(C, in, pin, out, pout, gm, rows_valid);
+      else plain_layer<1, 1>(C, in, pin, out, pout, gm, rows_valid);  // N % 64 == 0, or N = 32 (half idle)
     }
     __syncthreads();
   }
@@ -393,7 +341,6 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int has
       for (int c = 0; c < A.out_cols; c++) o[c] = (row[c] - m) - ls;
     }
   }
-  (void)kSlabFloats;
 }
 
 // ---------------------------------------------------------------------------
@@ -440,11 +387,18 @@ __global__ void __launch_bounds__(256) k_pn_fc(const float* __restrict__ in, int
   }
 }
 
+// Index of W^T element (k, n) in the fragment-major layout (KG k-groups).
+__device__ inline int64_t frag_index(int k, int n, int KG) {
+  return ((int64_t)((n >> 4) * KG + (k >> 4)) * 64 + ((k >> 2) & 3) * 16 + (n & 15)) * 4 + (k & 3);
+}
+
 // TNet(3) tail: t1[b] = fc3(h2[b]) (+ I, folded into the bias) and the t1
-// fold of conv1, w1T[b] = t1[b] (1 x 9) @ basis (9 x 768).  One workgroup per cloud.
+// fold of conv1, W1'^T[b] = t1[b] (1 x 9) @ basis (9 x kin*nout), written
+// fragment-major with K padded to 16 (rows kin..15 zero).  One workgroup per cloud.
 __global__ void __launch_bounds__(256) k_pn_head3(const float* __restrict__ h2, int ld_h, const float* __restrict__ W3,
                                                   const float* __restrict__ b3, const float* __restrict__ basis,
-                                                  float* __restrict__ t1_out, float* __restrict__ w1T, int K, int M) {
+                                                  float* __restrict__ t1_out, float* __restrict__ w1f, int K, int kin,
+                                                  int nout) {
   __shared__ float s_t[9];
   const int b = blockIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -459,17 +413,23 @@ __global__ void __launch_bounds__(256) k_pn_head3(const float* __restrict__ h2, 
     }
   }
   __syncthreads();
-  for (int m = threadIdx.x; m < M; m += blockDim.x) {
+  const int M = kin * nout, total = 16 * nout;  // one k-group
+  for (int e = threadIdx.x; e < total; e += blockDim.x) {
+    // fragment-major position e -> (k, n)
+    const int cb = e >> 8, ln = (e >> 2) & 63, k = 4 * (ln >> 4) + (e & 3), n = 16 * cb + (ln & 15);
     float acc = 0.0f;
+    if (k < kin) {
 #pragma unroll
-    for (int a = 0; a < 9; a++) acc += s_t[a] * basis[a * M + m];
-    w1T[(int64_t)b * M + m] = acc;
+      for (int a = 0; a < 9; a++) acc += s_t[a] * basis[a * M + k * nout + n];
+    }
+    w1f[(int64_t)b * total + e] = acc;
   }
 }
 
-// TNet(64) fold: out[b] (64 x N) = t2[b] (64 x 64) @ rhs (64 x N), N % 64 == 0.
-// Workgroup (column tile of 64, cloud): both operand tiles in LDS, 4 x 4
-// outputs per thread.
+// TNet(64) fold: out[b] (64 x N, fragment-major, 4 k-groups) = t2[b] (64 x 64)
+// @ rhs (64 x N row-major), N % 64 == 0.  Workgroup (column tile of 64,
+// cloud): both operand tiles in LDS, 4 x 4 outputs per thread; the 4 rows of
+// one column are the 4 consecutive floats of one fragment lane.
 __global__ void __launch_bounds__(256) k_pn_fold64(const float* __restrict__ t2, const float* __restrict__ rhs,
                                                    float* __restrict__ out, int N) {
   __shared__ float s_a[64][65];
@@ -496,8 +456,8 @@ __global__ void __launch_bounds__(256) k_pn_fold64(const float* __restrict__ t2,
   }
   float* o = out + (int64_t)b * 64 * N;
 #pragma unroll
-  for (int r = 0; r < 4; r++)
-    *reinterpret_cast<f32x4*>(o + (int64_t)(ti + r) * N + j0 + tj) = f32x4{acc[r][0], acc[r][1], acc[r][2], acc[r][3]};
+  for (int c = 0; c < 4; c++)
+    *reinterpret_cast<f32x4*>(o + frag_index(ti, j0 + tj + c, 4)) = f32x4{acc[0][c], acc[1][c], acc[2][c], acc[3][c]};
 }
 
 }  // namespace
@@ -514,9 +474,11 @@ int ndnet_pn_fc_run(const float* in, int ld_in, const float* W, const float* bia
 }
 
 int ndnet_pn_head3_run(const float* h2, int ld_h, const float* W3, const float* b3, const float* basis, float* t1,
-                       float* w1T, int batch, int K, int M, void* stream) {
-  if (!h2 || !W3 || !b3 || !basis || !t1 || !w1T || batch <= 0 || K <= 0 || M <= 0) return -20;
-  k_pn_head3<<<batch, 256, 0, (hipStream_t)stream>>>(h2, ld_h, W3, b3, basis, t1, w1T, K, M);
+                       float* w1f, int batch, int K, int kin, int nout, void* stream) {
+  if (!h2 || !W3 || !b3 || !basis || !t1 || !w1f || batch <= 0 || K <= 0 || kin <= 0 || kin > 16 || nout <= 0 ||
+      nout % 16)
+    return -20;
+  k_pn_head3<<<batch, 256, 0, (hipStream_t)stream>>>(h2, ld_h, W3, b3, basis, t1, w1f, K, kin, nout);
   return hipGetLastError() == hipSuccess ? 0 : -21;
 }
 
@@ -526,60 +488,51 @@ int ndnet_pn_fold64_run(const float* t2, const float* rhs, float* out, int batch
   return hipGetLastError() == hipSuccess ? 0 : -21;
 }
 
-
 // One fused point-MLP chain over `batch` clouds on `stream` (see pointnet.h).
 int ndnet_pn_chain_run(const ndnet_pn_chain* args, int batch, void* stream) {
-  if (!args || batch <= 0 || args->num_layers < 1 || args->num_layers > NDNET_PN_MAX_LAYERS) return -20;
+  if (!args || batch <= 0 || args->num_layers < 1 || args->num_layers > NDNET_PN_MAX_LAYERS || args->num_points <= 0 ||
+      args->in_cols < 1 || args->in_cols > args->L[0].K || args->in_cols > args->x_ld)
+    return -20;
   // activation regions: layer l reads region l & 1 (or the fused-chunk buffer
   // after a fused layer) and writes region (l + 1) & 1
-  int w[2] = {(args->L[0].K + 15) / 16 * 16, 0};  // the input tile is zero-filled to a whole K-slab (>= 16)
+  int w[2] = {args->L[0].K, 0};
+  bool has_fuse = false;
   for (int l = 0; l < args->num_layers; l++) {
     const ndnet_pn_layer& L = args->L[l];
-    if (L.K % 4 || L.N % 32 || L.ldw % 4 || L.ldw < L.N) return -20;
+    if (!L.w || !L.bias || L.K <= 0 || L.K % 16 || L.N <= 0 || L.N % 32 || (L.N > 32 && L.N % 64) ||
+        ((uintptr_t)L.w % 16) ||
+        L.w_cloud_stride % 4)
+      return -20;
     const bool fed = l > 0 && args->L[l - 1].fuse_next;
     if (fed) {
-      if (L.K != args->L[l - 1].N || L.N > kNC || L.fuse_next) return -20;
+      if (L.K != args->L[l - 1].N || L.N % 64 || L.N > 256 || L.fuse_next) return -20;
     } else if (l > 0 && L.K > w[l & 1]) {
       return -20;
     }
     if (L.fuse_next) {
       if (l + 1 >= args->num_layers || L.N % kFuseNC) return -20;
+      has_fuse = true;
       continue;  // not stored in a region
     }
     const bool stored = l + 1 < args->num_layers || args->mode == 1;
     if (stored && L.N > w[(l + 1) & 1]) w[(l + 1) & 1] = L.N;
   }
-  if (args->max_width < w[0] || args->max_width2 < w[1]) return -20;
-  bool has_fuse = false;
-  for (int l = 0; l < args->num_layers; l++) {
-    const ndnet_pn_layer& L = args->L[l];
-    has_fuse |= L.fuse_next != 0;
-    const bool fed = l > 0 && args->L[l - 1].fuse_next;
-    if (!L.fuse_next && !fed && L.N > kNC && L.N % kNC) return -20;  // chunks of one layer share a width
-  }
-  // 32-row weight slabs when they fit in LDS, else 16
-  auto lds_for = [&](int ks) {
-    return sizeof(float) * ((size_t)kP * (args->max_width + 1 + args->max_width2 + 1 + (has_fuse ? kFuseNC + 1 : 0)) +
-                            2 * (size_t)ks * kSlabPitch + (args->mode == 0 ? kRowBlocks * kNC : 0));
-  };
-  // (the input tile is zero-filled to a whole slab of columns, so region 0 must hold that many)
-  const int ks = (lds_for(32) <= 160 * 1024 && args->max_width >= (args->L[0].K + 31) / 32 * 32) ? 32 : 16;
-  const size_t lds = lds_for(ks);
+  if (args->max_width < w[0] || args->max_width2 < w[1] || args->max_width % 8 || args->max_width2 % 8) return -20;
+  if (args->mode == 1 && (!args->out || args->out_cols <= 0 || args->out_cols > args->L[args->num_layers - 1].N))
+    return -20;
+  if (args->mode == 0 && !args->gmax) return -20;
+  const size_t lds = sizeof(float) * (size_t)kP *
+                     ((args->max_width + 4) + (args->max_width2 + 4) + (has_fuse ? 2 * (kFuseNC + 4) : 0));
   static bool attr_set = false;
   if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)k_pn_chain<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
-            hipSuccess ||
-        hipFuncSetAttribute((const void*)k_pn_chain<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
-            hipSuccess)
+    if (hipFuncSetAttribute((const void*)k_pn_chain, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+        hipSuccess)
       return -21;
     attr_set = true;
   }
   if (lds > 160 * 1024) return -20;
   dim3 grid((args->num_points + kP - 1) / kP, batch);
-  if (ks == 32)
-    k_pn_chain<32><<<grid, kThreads, lds, (hipStream_t)stream>>>(*args, has_fuse ? 1 : 0);
-  else
-    k_pn_chain<16><<<grid, kThreads, lds, (hipStream_t)stream>>>(*args, has_fuse ? 1 : 0);
+  k_pn_chain<<<grid, kThreads, lds, (hipStream_t)stream>>>(*args);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     fprintf(stderr, "ndnet_amd: k_pn_chain launch failed: %s\n", hipGetErrorString(e));

@@ -35,9 +35,9 @@ chain_timing = None
 
 
 class _Layer(ctypes.Structure):
-    _fields_ = [("wT", ctypes.c_void_p), ("w_cloud_stride", ctypes.c_int64), ("bias", ctypes.c_void_p),
+    _fields_ = [("w", ctypes.c_void_p), ("w_cloud_stride", ctypes.c_int64), ("bias", ctypes.c_void_p),
                 ("bias_cloud_stride", ctypes.c_int64), ("K", ctypes.c_int32), ("N", ctypes.c_int32),
-                ("relu", ctypes.c_int32), ("ldw", ctypes.c_int32), ("fuse_next", ctypes.c_int32)]
+                ("relu", ctypes.c_int32), ("fuse_next", ctypes.c_int32)]
 
 
 class _Chain(ctypes.Structure):
@@ -73,6 +73,22 @@ def _wT(w: torch.Tensor, kpad: int, npad: int) -> torch.Tensor:
     out = torch.zeros((kpad, npad), dtype=torch.float32, device=w.device)
     out[:k, :n] = w.t()
     return out
+
+
+def _frag(wT: torch.Tensor) -> torch.Tensor:
+    """Plain W^T [..., K, N] (K % 16 == 0, N % 16 == 0) -> the fragment-major
+    layout of include/ndnet_pointnet.h, flattened: [cb][kg][kq][cl][s] with
+    k = 16 kg + 4 kq + s, n = 16 cb + cl."""
+    *lead, K, N = wT.shape
+    v = wT.reshape(*lead, K // 16, 4, 4, N // 16, 16)
+    nl = len(lead)
+    perm = list(range(nl)) + [nl + 3, nl + 0, nl + 1, nl + 4, nl + 2]
+    return v.permute(*perm).reshape(*lead, K * N).contiguous()
+
+
+def _npad(n: int) -> int:
+    """Output width the chain kernel splits evenly: 32, or a multiple of 64."""
+    return 32 if n <= 32 else _pad(n, 64)
 
 
 def _bpad(b: torch.Tensor, npad: int) -> torch.Tensor:
@@ -112,16 +128,16 @@ class _Folded:
             self.F, self.C1 = F, m.num_classes + 1
             # shared per-point layers, W^T padded
             t1, t2 = self.t1, self.t2
-            self.A = [(_wT(t1["w1"], 4, 64), t1["b1"]), (_wT(t1["w2"], 64, 128), t1["b2"]),
+            self.A = [(_wT(t1["w1"], 16, 64), t1["b1"]), (_wT(t1["w2"], 64, 128), t1["b2"]),
                       (_wT(t1["w3"], 128, 1024), t1["b3"])]
             self.B_tail = [(_wT(t2["w1"], 64, 64), t2["b1"]), (_wT(t2["w2"], 64, 128), t2["b2"]),
                            (_wT(t2["w3"], 128, 1024), t2["b3"])]
-            self.C_tail = (_wT(self.c3w, 128, _pad(F, 32)), _bpad(self.c3b, _pad(F, 32)))
+            self.C_tail = (_wT(self.c3w, 128, _npad(F)), _bpad(self.c3b, _npad(F)))
             self.s1a = self.s1w[:, :64].contiguous()      # acts on x_t2
             self.s1bT = self.s1w[:, 64:].t().contiguous()  # [F, 512], acts on g3
             self.s1g = self.s1w[:, 64:].contiguous()       # [512, F] row-major for ndnet_pn_fc_run
             self.D_tail = [(_wT(self.s2w, 512, 256), self.s2b), (_wT(self.s3w, 256, 128), self.s3b),
-                           (_wT(self.s4w, 128, _pad(self.C1, 32)), _bpad(self.s4b, _pad(self.C1, 32)))]
+                           (_wT(self.s4w, 128, _npad(self.C1)), _bpad(self.s4b, _npad(self.C1)))]
             self.c1wT = self.c1w.t().contiguous()         # [12, 64]
             self.c2wT = self.c2w.t().contiguous()         # [64, 128]
             self.s1aT = self.s1a.t().contiguous()         # [64, 512]
@@ -137,6 +153,8 @@ class _Folded:
                     for j in range(3):
                         E[3 * a + c, 3 + 3 * a + j, 3 + 3 * c + j] = 1.0
             self.t1_basis = torch.matmul(E.transpose(1, 2), self.c1wT).reshape(9, 12 * 64).contiguous()
+            # fragment-major copies of the shared per-point layers (the HIP chains)
+            self.frag = {id(w): _frag(w) for w, _ in self.A + self.B_tail + [self.C_tail] + self.D_tail}
             # the identity the TNet heads add (ndtnet.py:59), folded into fc3's bias
             self.t1["c3"] = self.t1["c3"] + torch.eye(3, device=dev).reshape(-1)
             self.t2["c3"] = self.t2["c3"] + torch.eye(64, device=dev).reshape(-1)
@@ -160,25 +178,24 @@ def _fc_head(g: torch.Tensor, t: dict, dim: int, h1: torch.Tensor, h2: torch.Ten
     return out.view(-1, dim, dim)
 
 
-def _build_chain(n: int, in_cols: int, layers, relus, mode: int, gmax=None, out_cols=0, per_cloud=(),
-                 fuse=()) -> "_Chain":
+def _build_chain(n: int, in_cols: int, layers, relus, mode: int, gmax=None, out_cols=0, fuse=()) -> "_Chain":
     """ctypes argument block of one ``ndnet_pn_chain_run`` (x / out set per call).
-    Layers in ``fuse`` are produced in 64-column chunks straight into the next
-    layer (include/ndnet_pointnet.h)."""
+    ``layers``: (fragment-major weights, per-cloud stride in floats or 0, bias,
+    K, N) per layer.  Layers in ``fuse`` are produced in 64-column chunks
+    straight into the next layer (include/ndnet_pointnet.h)."""
     ch = _Chain()
     ch.x_ld = 12
     ch.in_cols = in_cols
     ch.num_points = n
     ch.num_layers = len(layers)
     # LDS regions: layer l reads l & 1, writes (l + 1) & 1; the input tile is
-    # zero-filled to a 16-column K-slab; a fused layer's output has no region
-    widths = [_pad(layers[0][0].shape[-2], 16), 4]
-    for i, (w, b) in enumerate(layers):
+    # zero-filled to the first layer's K; a fused layer's output has no region
+    widths = [layers[0][3], 8]
+    for i, (w, stride, b, K, N) in enumerate(layers):
         L = ch.L[i]
-        L.wT = w.data_ptr()
-        L.K, L.N = w.shape[-2], w.shape[-1]
-        L.ldw = w.stride(-2)
-        L.w_cloud_stride = w.stride(0) if (i in per_cloud and w.dim() == 3) else 0
+        L.w = w.data_ptr()
+        L.w_cloud_stride = stride
+        L.K, L.N = K, N
         L.bias = b.data_ptr()
         L.bias_cloud_stride = b.stride(0) if b.dim() == 2 else 0
         L.relu = relus[i]
@@ -186,7 +203,7 @@ def _build_chain(n: int, in_cols: int, layers, relus, mode: int, gmax=None, out_
         if i in fuse:
             continue
         if i + 1 < len(layers) or mode == 1:
-            widths[(i + 1) & 1] = max(widths[(i + 1) & 1], L.N)
+            widths[(i + 1) & 1] = max(widths[(i + 1) & 1], N)
     ch.mode = mode
     ch.out_cols = out_cols
     ch.gmax = gmax.data_ptr() if gmax is not None else None
@@ -203,13 +220,8 @@ def _run_chain(ch: "_Chain", x: torch.Tensor, out=None) -> None:
     _lib.check(rc, "ndnet_pn_chain_run")
 
 
-def _chain_gpu(x: torch.Tensor, n: int, in_cols: int, layers, relus, mode: int, gmax=None, out=None, out_cols=0,
-               per_cloud=(), fuse=()) -> None:
-    _run_chain(_build_chain(n, in_cols, layers, relus, mode, gmax, out_cols, per_cloud, fuse), x, out)
-
-
 def _chain_torch(x: torch.Tensor, n: int, in_cols: int, layers, relus, mode: int, gmax=None, out=None,
-                 out_cols=0, per_cloud=(), fuse=()) -> None:
+                 out_cols=0, fuse=()) -> None:
     """What one ``ndnet_pn_chain_run`` computes, in torch ops (tests: checks the
     folding algebra on CPU and the kernel against it on the GPU)."""
     h = x[..., :in_cols].float()
@@ -238,18 +250,36 @@ class _Workspace:
         self.g1, self.g2, self.g3 = self.gbuf[:, :1024], self.gbuf[:, 1024:2048], self.gbuf[:, 2048:]
         self.h1, self.h2 = torch.empty((B, 512), **f32), torch.empty((B, 256), **f32)
         self.t1, self.t2 = torch.empty((B, 9), **f32), torch.empty((B, 4096), **f32)
+        self.cvec = torch.empty((B, 512), **f32)        # per-cloud bias of the seg head
+        # per-cloud folded weights: plain W^T for the torch emulation ...
         self.w1T = torch.empty((B, 12, 64), **f32)      # (W1 M(t1))^T per cloud
         self.t2w = torch.empty((B, 64, 640), **f32)     # t2 @ [W2^T | Ws1a^T]
         self.w2T, self.sT = self.t2w[:, :, :128], self.t2w[:, :, 128:]
-        self.cvec = torch.empty((B, 512), **f32)        # per-cloud bias of the seg head
-        self.specs = [
+        # ... and fragment-major for the HIP chains (K of conv1 padded 12 -> 16);
+        # column blocks are outermost, so conv2's 8 blocks precede seg conv1a's 32
+        self.w1f = torch.empty((B, 16 * 64), **f32)
+        self.t2wf = torch.empty((B, 64 * 640), **f32)
+        self.specs = [  # torch emulation: (in_cols, [(W^T, bias)], relus, mode, kwargs)
             (3, W.A, (1, 1, 1), 0, dict(gmax=self.g1)),
-            (12, [(self.w1T, W.c1b)] + W.B_tail, (0, 1, 1, 1), 0, dict(gmax=self.g2, per_cloud=(0,))),
-            (12, [(self.w1T, W.c1b), (self.w2T, W.c2b), W.C_tail], (0, 0, 0), 0,
-             dict(gmax=self.g3, per_cloud=(0, 1))),
+            (12, [(self.w1T, W.c1b)] + W.B_tail, (0, 1, 1, 1), 0, dict(gmax=self.g2)),
+            (12, [(self.w1T, W.c1b), (self.w2T, W.c2b), W.C_tail], (0, 0, 0), 0, dict(gmax=self.g3)),
             # the 512-wide seg conv1 output feeds conv2 chunk by chunk (never stored whole)
             (12, [(self.w1T, W.c1b), (self.sT, self.cvec)] + W.D_tail, (0, 1, 1, 1, 0), 1,
-             dict(out_cols=W.C1, per_cloud=(0, 1), fuse=(1,))),
+             dict(out_cols=W.C1, fuse=(1,))),
+        ]
+
+        def shared(wb):
+            w, b = wb
+            return (W.frag[id(w)], 0, b, w.shape[0], w.shape[1])
+
+        L1 = (self.w1f, self.w1f.stride(0), W.c1b, 16, 64)
+        L2 = (self.t2wf, self.t2wf.stride(0), W.c2b, 64, 128)
+        Ls = (self.t2wf[:, 64 * 128:], self.t2wf.stride(0), self.cvec, 64, 512)
+        self.hip_layers = [
+            [shared(x) for x in W.A],
+            [L1] + [shared(x) for x in W.B_tail],
+            [L1, L2, shared(W.C_tail)],
+            [L1, Ls] + [shared(x) for x in W.D_tail],
         ]
         self.N = N
         self.structs = None
@@ -263,7 +293,8 @@ class _Workspace:
             chain_fn(x, self.N, in_cols, layers, relus, mode, **kw)
             return
         if self.structs is None:
-            self.structs = [_build_chain(self.N, s[0], s[1], s[2], s[3], **s[4]) for s in self.specs]
+            self.structs = [_build_chain(self.N, s[0], hl, s[2], s[3], **s[4])
+                            for s, hl in zip(self.specs, self.hip_layers)]
             # the last chain re-arms the max-pool buffer (-inf) for the next forward
             self.structs[3].clear = self.gbuf.data_ptr()
             self.structs[3].clear_count = self.gbuf.numel()
@@ -313,7 +344,7 @@ def _glue_hip(W, ws, B: int):
             n = min(16, B - c0)
             rc = _lib.lib().ndnet_pn_head3_run(ws.h2[c0].data_ptr(), ws.h2.stride(0), t["f3"].data_ptr(),
                                                t["c3"].data_ptr(), W.t1_basis.data_ptr(), ws.t1[c0].data_ptr(),
-                                               ws.w1T[c0].data_ptr(), n, 256, 12 * 64, st())
+                                               ws.w1f[c0].data_ptr(), n, 256, 12, 64, st())
             _lib.check(rc, "ndnet_pn_head3_run")
 
     def head_b():
@@ -321,7 +352,7 @@ def _glue_hip(W, ws, B: int):
         _fc(ws.g2, t["f1"], t["c1"], ws.h1, True)
         _fc(ws.h1, t["f2"], t["c2"], ws.h2, True)
         _fc(ws.h2, t["f3"], t["c3"], ws.t2, False)
-        rc = _lib.lib().ndnet_pn_fold64_run(ws.t2.data_ptr(), W.t2_rhs.data_ptr(), ws.t2w.data_ptr(), B,
+        rc = _lib.lib().ndnet_pn_fold64_run(ws.t2.data_ptr(), W.t2_rhs.data_ptr(), ws.t2wf.data_ptr(), B,
                                             W.t2_rhs.shape[1], st())
         _lib.check(rc, "ndnet_pn_fold64_run")
 

@@ -96,3 +96,24 @@ def test_hip_forward_on_ndt_rows():
         out = m(p, c)
         ref = m.forward_torch(p.contiguous(), c.contiguous())
     assert (out - ref).abs().max().item() < TOL
+
+
+def test_fragment_layout_matches_mfma_operands():
+    """_frag puts W^T[k][n] where k-group kg, column block cb, lane 16 kq + cl,
+    element s of the float4 with k = 16 kg + 4 kq + s, n = 16 cb + cl
+    (include/ndnet_pointnet.h; the kernel's B operand of MFMA step s)."""
+    from ndnet.models import pointnet_hip as ph
+    K, N = 48, 96
+    wT = torch.arange(K * N, dtype=torch.float32).reshape(K, N)
+    f = ph._frag(wT).numpy()
+    KG = K // 16
+    for cb in range(N // 16):
+        for kg in range(KG):
+            for lane in range(64):
+                kq, cl = lane >> 4, lane & 15
+                for s in range(4):
+                    idx = ((cb * KG + kg) * 64 + lane) * 4 + s
+                    assert f[idx] == wT[16 * kg + 4 * kq + s, 16 * cb + cl]
+    # per-cloud leading dims are kept
+    f3 = ph._frag(torch.stack([wT, 2 * wT]))
+    assert f3.shape == (2, K * N) and torch.equal(f3[1], 2 * f3[0])

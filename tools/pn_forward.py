@@ -32,3 +32,20 @@ with torch.no_grad():
         out = m(x[..., :3], x[..., 3:])
 torch.cuda.synchronize()
 print("ok", tuple(out.shape), float(out.float().abs().mean()))
+
+# per-chain HIP-event times (bench.py's roofline figures) over a few more reps
+from ndnet.models import pointnet_hip  # noqa: E402
+import numpy as np  # noqa: E402
+sys.path.insert(0, REPO)
+from bench import chain_flops_per_point  # noqa: E402
+pointnet_hip.chain_timing = []
+with torch.no_grad():
+    for _ in range(a.reps):
+        m(x[..., :3], x[..., 3:])
+torch.cuda.synchronize()
+ms = np.zeros(4)
+for i, e0, e1 in pointnet_hip.chain_timing:
+    ms[i] += e0.elapsed_time(e1) / a.reps
+fl = np.array(chain_flops_per_point(a.feature_dim, a.classes)) * a.nds * a.batch
+for i in range(4):
+    print(f"chain {pointnet_hip.CHAIN_NAMES[i][:40]:40s} {ms[i] * 1e3:7.1f} us  {fl[i] / (ms[i] * 1e-3) / 1e12:6.1f} TFLOP/s")
