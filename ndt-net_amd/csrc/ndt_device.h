@@ -87,6 +87,38 @@ NDNET_FN uint32_t voxel_key(double x, double y, double z, const double* off, con
   return vz * len[0] * len[1] + vy * len[0] + vx;
 }
 
+// Single-precision screen of voxel_key for float points (the reference casts
+// them to double, ndtnet_preprocessing.py:30).  off32 = the float-exact grid
+// offset, inv32 = (float)(1 / vs).  The computed q = fl(fl(p - off) * inv32)
+// is within 3 * 2^-24 |Q| (plus 2^-53 terms) of the real quotient
+// Q = (p - off) / vs, and the reference's fl64(fl64(p - off) / vs) within
+// 2^-52 |Q|; so where frac(q) is more than |q| 2^-19 away from 0 and 1, both
+// floor to the same integer.  *ok is false otherwise (including q = 0 and
+// NaN), and the caller takes voxel_key.
+NDNET_FN uint32_t axis_index_f32(float p, float off32, float inv32, bool& ok) {
+  const float q = (p - off32) * inv32;
+  const float f = floorf(q);
+  const float r = q - f;
+  const float tol = q * 0x1p-19f;
+  ok = r > tol && r < 1.0f - tol && q < 8388608.0f;
+  return (uint32_t)(int32_t)(ok ? f : 0.0f);
+}
+
+constexpr uint32_t kKeyRedo = 0xfffffffeu;  // voxel_key_f32: take voxel_key for this point
+
+// voxel_key for a float point, or kKeyRedo where the screen cannot decide.
+// No fallback inside, so callers can keep the (rare) double path out of
+// their unrolled hot loops.
+NDNET_FN uint32_t voxel_key_f32(float x, float y, float z, const float* off32, float inv32, const uint32_t* len) {
+  bool o0, o1, o2;
+  const uint32_t vx = axis_index_f32(x, off32[0], inv32, o0);
+  const uint32_t vy = axis_index_f32(y, off32[1], inv32, o1);
+  const uint32_t vz = axis_index_f32(z, off32[2], inv32, o2);
+  if (!(o0 && o1 && o2)) return kKeyRedo;
+  if (vx >= len[0] || vy >= len[1] || vz >= len[2]) return kInvalid;
+  return vz * len[0] * len[1] + vy * len[0] + vx;
+}
+
 // x / n with the reciprocal of n shared between divisions.  The compiler's
 // correctly rounded f64 division is the sequence
 //   d = div_scale(n), r = rcp(d), two Newton steps r += r (1 - d r),

@@ -47,7 +47,10 @@
 
 constexpr int kFrontThreads = 1024;
 constexpr int kFrontWaves = kFrontThreads / 64;
-constexpr int kFrontR = 8;          // bins per workgroup whose points stay in registers
+#ifndef NDNET_FRONT_R
+#define NDNET_FRONT_R 8
+#endif
+constexpr int kFrontR = NDNET_FRONT_R;  // bins per workgroup whose points stay in registers
 constexpr int kFrontTable = 8192;   // LDS words: byte map of a small grid (32768 voxels) or hash slots
 constexpr int kFrontPhases = 40;    // record slots per cloud and run
 constexpr int kRecWords = 16;       // per-workgroup record: [0] count, [1] any bad, [2..9] first bad per worker
@@ -90,6 +93,8 @@ struct FrontState {
   int32_t rc;
   uint32_t cut[kWorkers];
   uint32_t sync_no;
+  uint32_t puse[2];                 // uses of the two pass-sum slots
+  unsigned long long psum_prev[2];  // their value after the previous use
   uint32_t ok;
   uint32_t count;
   uint32_t anybad;
@@ -161,6 +166,43 @@ __device__ inline bool cloud_sync(FrontState& s, uint32_t* bar, uint32_t G) {
         }
       }
     }
+  }
+  __syncthreads();
+  return s.ok != 0;
+}
+
+// The barrier that ends a bisection pass, carrying the pass's count: each
+// workgroup adds (1 << 48) + (bad << 32) + fresh to the pass-parity slot
+// (u64 at bar + 2 + 2 parity, zeroed by k_reset) and waits until G arrivals
+// of this use are in; the count and the number of workgroups that saw an
+// out-of-grid point are the slot's growth since its previous use.  One atomic
+// and the poll replace a record per workgroup read back after the barrier.  A
+// workgroup can only be one pass ahead (the next pass's barrier needs
+// everyone), so no use of a slot overlaps the next one.
+__device__ inline bool pass_sync(FrontState& s, uint32_t* bar, uint32_t G, uint32_t fresh, uint32_t anyb,
+                                 uint32_t parity) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long* slot = reinterpret_cast<unsigned long long*>(bar + 2) + parity;
+    const unsigned long long add = (1ull << 48) + ((unsigned long long)anyb << 32) + fresh;
+    s.puse[parity]++;
+    const unsigned long long target = (unsigned long long)G * s.puse[parity];
+    unsigned long long v = __hip_atomic_fetch_add(slot, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + add;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while ((v >> 48) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 100 MHz clock: 2 s
+        s.ok = 0;
+        break;
+      }
+    }
+    const unsigned long long low = v & ((1ull << 48) - 1);
+    const unsigned long long d = low - s.psum_prev[parity];
+    s.psum_prev[parity] = low;
+    s.count = (uint32_t)d;
+    s.anybad = (uint32_t)(d >> 32);
   }
   __syncthreads();
   return s.ok != 0;
@@ -246,6 +288,8 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
 
   if (t == 0) {
     s.sync_no = 0;
+    s.puse[0] = s.puse[1] = 0;
+    s.psum_prev[0] = s.psum_prev[1] = 0;
     s.ok = 1;
     s.rc = 0;
     for (int a = 0; a < 3; a++) {
@@ -383,15 +427,29 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
     const double vs = s.guess, inv_vs = 1.0 / vs;
     double off[3] = {s.off[0], s.off[1], s.off[2]};
     uint32_t len[3] = {s.len[0], s.len[1], s.len[2]};
+    // float points: keys screened in single precision (voxel_key_f32), valid
+    // when the grid offset is a float (it is the minimum of float points)
+    const float off32[3] = {(float)off[0], (float)off[1], (float)off[2]};
+    const float inv32 = (float)inv_vs;
+    const bool fast32 = std::is_same<T, float>::value && (double)off32[0] == off[0] &&
+                        (double)off32[1] == off[1] && (double)off32[2] == off[2];
     uint32_t fresh = 0;
-    // key of every estimated point into binfo (the accepted pass's keys feed the binning)
+    // Hot, unrolled over the register-resident points: the key of every
+    // estimated point into binfo (the accepted pass's keys feed the binning),
+    // single precision for float input; small grids mark the byte map.  The
+    // rest -- the double path where the screen cannot decide (the point is
+    // re-read), out-of-grid points, the stamp dedup of large grids -- runs in
+    // rolled loops below, so the unrolled code stays small.
+    bool redo = false, cold = false;
     auto visit = [&](uint32_t j, uint64_t i, T x, T y, T z) {
       uint32_t key = kInvalid;
       if (i < n8) {
-        key = voxel_key((double)x, (double)y, (double)z, off, len, vs, inv_vs);
-        if (key == kInvalid) atomicMin(&s_bad[i / chunk], (uint32_t)i);
-        else if (small) bytemap[key] = 1;
-        else fresh += stamp_key_front(key, table, stamps, stamp);
+        key = fast32 ? voxel_key_f32((float)x, (float)y, (float)z, off32, inv32, len) : kKeyRedo;
+        redo |= key == kKeyRedo;
+        cold |= key == kInvalid;
+        if (small && key < kKeyRedo) {
+          if (!bytemap[key]) bytemap[key] = 1;  // read first: most lanes of a small grid hit set bytes
+        }
       }
       binfo[j * 1024 + t] = key;
     };
@@ -403,6 +461,30 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
       T x = 0, y = 0, z = 0;
       if (i < n8) front_point(p, i, x, y, z);
       visit(j, i, x, y, z);
+    }
+    if (__any(redo)) {
+#pragma unroll 1
+      for (uint32_t j = 0; j < bpw; j++) {
+        const uint32_t e = j * 1024 + t;
+        if (binfo[e] == kKeyRedo) {
+          T x, y, z;
+          front_point(p, (bin0 + j) * 1024 + t, x, y, z);
+          const uint32_t key = voxel_key((double)x, (double)y, (double)z, off, len, vs, inv_vs);
+          binfo[e] = key;
+          cold |= key == kInvalid;
+          if (small && key != kInvalid && !bytemap[key]) bytemap[key] = 1;
+        }
+      }
+    }
+    if (!small || __any(cold)) {
+#pragma unroll 1
+      for (uint32_t j = 0; j < bpw; j++) {
+        const uint64_t i = (bin0 + j) * 1024 + t;
+        const uint32_t key = binfo[j * 1024 + t];
+        if (i >= n8) continue;
+        if (key == kInvalid) atomicMin(&s_bad[i / chunk], (uint32_t)i);
+        else if (!small) fresh += stamp_key_front(key, table, stamps, stamp);
+      }
     }
     __syncthreads();
     if (s.iter == 1) FRONT_MARK(28);
@@ -425,23 +507,16 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
     fresh = block_sum_u32(fresh, scratch);
     if (s.iter == 1) FRONT_MARK(30);
     uint32_t* rec = A.rec + (((uint64_t)b * kFrontPhases + 1 + 2 * s.iter) * G) * kRecWords;
-    if (t == 0) {
-      uint32_t anyb = 0;
-      for (int w = 0; w < kWorkers; w++) anyb |= s_bad[w] != kInvalid;
-      st_sc1(rec + g * kRecWords + 0, fresh);
+    uint32_t anyb = 0;
+    for (int w = 0; w < kWorkers; w++) anyb |= s_bad[w] != kInvalid;
+    if (t == 0) {  // the record is read back only on a pass with an out-of-grid point
       st_sc1(rec + g * kRecWords + 1, anyb);
       if (anyb)
         for (int w = 0; w < kWorkers; w++) st_sc1(rec + g * kRecWords + 2 + w, s_bad[w]);
-      s.count = 0;
-      s.anybad = 0;
     }
     FRONT_MARK(3 + 2 * (s.iter < 7 ? s.iter : 7));
-    if (!cloud_sync(s, bar, G)) goto fail;
+    if (!pass_sync(s, bar, G, fresh, anyb, s.iter & 1u)) goto fail;
     FRONT_MARK(4 + 2 * (s.iter < 7 ? s.iter : 7));
-    if (t < G) {
-      atomicAdd(&s.count, ld_sc1(rec + t * kRecWords + 0));
-      if (ld_sc1(rec + t * kRecWords + 1)) atomicOr(&s.anybad, 1u);
-    }
     if (t < (uint32_t)kWorkers) s.cut[t] = kInvalid;
     __syncthreads();
     if (s.iter == 1) FRONT_MARK(31);

@@ -253,7 +253,8 @@ __device__ inline void grid_from(const CloudCtl& c, double vs, uint32_t* len, do
 __global__ void k_reset(CloudCtl* ctl, int B, uint32_t* bar) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  if (bar) bar[(uint64_t)b * 16] = 0;  // k_front's cloud barrier counter (kBarStride)
+  if (bar)  // k_front's cloud barrier counter and its two pass-sum slots (kBarStride)
+    for (int i = 0; i < 6; i++) bar[(uint64_t)b * 16 + i] = 0;
   CloudCtl& c = ctl[b];
   c.epoch = c.epoch + 1;
   // stamps are epoch*32 + pass; on a wrap the stale stamps are cleared on the

@@ -13,7 +13,7 @@ import torch  # noqa: F401  -- load torch's HIP runtime first so the library bin
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
-LIB_PATH = os.path.join(ROOT, "lib", "libndnet_amd.so")
+LIB_PATH = os.environ.get("NDNET_AMD_LIB") or os.path.join(ROOT, "lib", "libndnet_amd.so")  # override: A/B builds (tools/)
 
 NDNET_OK = 0
 NDNET_ERR_ARG = -20
