@@ -196,6 +196,19 @@ def main() -> None:
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
                     "algorithmic": f"{nbytes / 1e6:.2f} MB per launch: {what}", "ms": round(ms, 4),
                     "all_chains": chains_info}
+    # HBM bytes per launch of that kernel from the committed rocprofv3 PMC
+    # passes (tools/pmc.sh -> tools/pmc_summary.py --json): FETCH_SIZE doubled
+    # per MI355X_MICROARCH.md's gfx950 correction, plus WRITE_SIZE
+    pmc_path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            pmc = json.load(f)
+        for kname, row in pmc.items():
+            if kname != "_source" and roofline["kernel"].startswith(kname.split("<")[0]) and "hbm_bytes" in row:
+                roofline["traffic"] = round(row["hbm_bytes"])
+                roofline["traffic_source"] = f"{pmc.get('_source', pmc_path)}: {kname}, " \
+                    f"2 x FETCH_SIZE {row['FETCH_SIZE']:.0f} KB + WRITE_SIZE {row['WRITE_SIZE']:.0f} KB per launch"
+                break
     roofline["ndt_end_to_end"] = {"bytes": ndt_bytes, "ms": round(ndt_ms, 4),
                                   "gbs": round(ndt_bytes / (ndt_ms * 1e-3) / 1e9, 2),
                                   "unit": "SURVEY 8d: 24N+48k per cloud over the whole NDT stage"}

@@ -23,14 +23,23 @@ def kname(full):
 
 
 def load(d):
+    """kernel -> counter -> per-dispatch values.  k_pn_chain dispatches are
+    named A-D by their order within each forward (4 per forward)."""
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in sorted(glob.glob(os.path.join(d, "pmc*", "*counter_collection.csv"))):
-        for r in csv.DictReader(open(f)):
+        rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Dispatch_Id"]))
+        chain_seen = {}
+        for r in rows:
             nm = r["Kernel_Name"]
             if "at::" in nm or "Cijk" in nm:
                 continue
             key = kname(nm)
-            if key.startswith("k_pn_chain") or key.startswith("k_pn_fc"):
+            if key.startswith("k_pn_chain"):
+                did = r["Dispatch_Id"]
+                if did not in chain_seen:
+                    chain_seen[did] = len(chain_seen)
+                key = "k_pn_chain " + "ABCD"[chain_seen[did] % 4]
+            elif key.startswith("k_pn_fc"):
                 key += f" grid={r['Grid_Size']}"
             agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return agg
@@ -52,6 +61,7 @@ def main():
         print(k)
         print("   " + ", ".join(f"{c}={v:.4g}" for c, v in row.items()))
     if "--json" in sys.argv:
+        out["_source"] = d
         json.dump(out, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
 
 
