@@ -1,0 +1,145 @@
+"""The training step (reference tools/train.py:16-92):
+the fixed loss, the LR schedule, Adam steps on NDs, and DDP gradient
+averaging at world size 2 over gloo on the CPU (the RCCL path on GPUs is the
+same torch DDP with backend "nccl")."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from ndnet.training import Trainer, accuracy, lr_for_epoch, segmentation_loss
+
+
+def _model(F=64, C=5, seed=0):
+    from ndnet.models.ndtnet import NDTNetSegmentation
+    torch.manual_seed(seed)
+    return NDTNetSegmentation(3, C, F)
+
+
+def _nds(B, k, C, seed):
+    g = torch.Generator().manual_seed(seed)
+    pcl = torch.rand((B, k, 3), generator=g) * 20 - 10
+    covs = torch.randn((B, k, 9), generator=g) * 0.1
+    lbl = torch.randint(0, C + 1, (B, k), generator=g)
+    gt = torch.nn.functional.one_hot(lbl, C + 1).float()
+    return pcl, covs, gt
+
+
+def test_loss_is_class_dim_cross_entropy():
+    g = torch.Generator().manual_seed(0)
+    z = torch.randn((3, 50, 7), generator=g)
+    lbl = torch.randint(0, 7, (3, 50), generator=g)
+    gt = torch.nn.functional.one_hot(lbl, 7).float()
+    ours = segmentation_loss(torch.log_softmax(z, dim=-1), gt)
+    ref = torch.nn.functional.cross_entropy(z.reshape(-1, 7), lbl.reshape(-1))
+    assert torch.allclose(ours, ref, atol=1e-6)
+    assert accuracy(z, gt) == (z.argmax(-1) == lbl).float().mean().item()
+
+
+def test_lr_schedule_halves_every_20_epochs():
+    assert lr_for_epoch(0.034, 0) == 0.034
+    assert lr_for_epoch(0.034, 18) == 0.034
+    assert lr_for_epoch(0.034, 19) == 0.017
+    assert lr_for_epoch(0.034, 39) == 0.034 / 4
+
+
+def test_adam_steps_reduce_loss_cpu():
+    m = _model()
+    tr = Trainer(m, 1e-3, 128, 5, torch.device("cpu"), ddp=False)
+    pcl, covs, gt = _nds(4, 128, 5, seed=1)
+    losses = [tr.step_on_nds(pcl, covs, gt)[0] for _ in range(6)]
+    assert all(np.isfinite(losses))
+    assert losses[-1] < losses[0]
+    # val/test mode: no parameter update (train.py:74-81 stepped in every mode)
+    before = [p.detach().clone() for p in m.parameters()]
+    tr.step_on_nds(pcl, covs, gt, train=False)
+    assert all(torch.equal(a, b) for a, b in zip(before, m.parameters()))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _ddp_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "ndt-net_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(2)
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    from ndnet.training import Trainer as T
+    m = _model()
+    tr = T(m, 1e-3, 96, 5, torch.device("cpu"))
+    assert tr.net is not m, "a world-2 group must wrap the model in DDP"
+    pcl, covs, gt = _nds(2, 96, 5, seed=10 + rank)
+    # the DDP backward alone: gradients all-reduced (averaged) over the ranks
+    m.train()
+    segmentation_loss(tr.net(pcl, covs), gt).backward()
+    grads = [p.grad.detach().numpy().copy() for p in m.parameters()]
+    # then a whole Trainer step: every rank must hold the same parameters after it
+    tr.step_on_nds(pcl, covs, gt)
+    params = [p.detach().numpy().copy() for p in m.parameters()]
+    q.put((rank, grads, params))
+    dist.destroy_process_group()
+
+
+def test_ddp_world2_gloo_averages_gradients():
+    """DDP's backward leaves each rank the mean of the two shards' gradients,
+    and a Trainer step leaves the ranks with identical parameters."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {r: (g, w) for r, g, w in (q.get(timeout=300) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    shard_grads = []
+    for r in range(2):
+        m = _model()
+        m.train()
+        pcl, covs, gt = _nds(2, 96, 5, seed=10 + r)
+        segmentation_loss(m(pcl, covs), gt).backward()
+        shard_grads.append([p.grad.numpy() for p in m.parameters()])
+    # tolerance on the model's gradient scale: biases feeding a BatchNorm have
+    # gradients that are pure rounding noise (the batch mean cancels them)
+    scale = max(float(np.abs((g0 + g1) / 2).max()) for g0, g1 in zip(*shard_grads))
+    for i, (g0, g1) in enumerate(zip(*shard_grads)):
+        ref = (g0 + g1) / 2
+        for r in range(2):
+            assert np.abs(got[r][0][i] - ref).max() <= 1e-5 * scale, f"rank {r} grad {i} is not the mean"
+    for a, b in zip(got[0][1], got[1][1]):
+        assert np.array_equal(a, b), "ranks disagree after the step"
+
+
+@pytest.mark.gpu
+def test_training_step_gpu_labelled_path():
+    """Raw labelled clouds -> labelled NDT path (HIP) -> train-mode forward ->
+    backward -> Adam, then an eval step on the HIP forward."""
+    from ndnet.synthetic import make_labelled_batch
+    dev = torch.device("cuda", 0)
+    m = _model(F=768, C=28)
+    tr = Trainer(m, 1e-3, 500, 28, dev, ddp=False)
+    pts, gt = make_labelled_batch(2, 20_000, 28, seed0=3)
+    before = [p.detach().clone() for p in m.parameters()]
+    losses = [tr.step(torch.from_numpy(pts), torch.from_numpy(gt))[0] for _ in range(3)]
+    assert all(np.isfinite(losses)), losses
+    assert any(not torch.equal(a, b) for a, b in zip(before, m.parameters()))
+    vloss, vacc = tr.step(torch.from_numpy(pts), torch.from_numpy(gt), train=False)
+    assert 0.0 <= vacc <= 1.0
+    # the eval forward re-folds the trained weights: HIP path == torch composition
+    from ndnet.preprocessing.ndtnet_preprocessing import ndt_preprocessing
+    p, c, _ = ndt_preprocessing(500, torch.from_numpy(pts).to(dev))
+    m.eval()
+    with torch.no_grad():
+        out, ref = m(p, c), m.forward_torch(p.contiguous(), c.contiguous())
+    err = ((out - ref).abs() / ref.abs().clamp_min(1.0)).max().item()
+    assert err < 1e-4, err
