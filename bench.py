@@ -68,6 +68,9 @@ def main() -> None:
     ap.add_argument("--cpu-baseline-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch kernels from Python each step (no HIP graph)")
+    ap.add_argument("--levels", default=None,
+                    help="config C5: comma-separated NDs per level, e.g. 2000,1000,500 (downsample, then prune; "
+                         "a forward per level)")
     args = ap.parse_args()
 
     from ndnet import distributed as D
@@ -83,6 +86,9 @@ def main() -> None:
     from ndnet import _lib
 
     B, n, k, F, C = args.batch, args.points, args.nds, args.feature_dim, args.classes
+    levels = tuple(int(v) for v in args.levels.split(",")) if args.levels else None
+    if levels:
+        k = levels[0]  # the stage timing / roofline below cover the first level's downsample + forward
     pts = torch.from_numpy(make_batch(args.kind, B, n, seed0=rank * B)).to(dev)
     torch.manual_seed(1234)
     model = NDTNetSegmentation(3, C, F).to(dev).eval()
@@ -93,6 +99,9 @@ def main() -> None:
                 m.running_var.uniform_(0.5, 1.5)
 
     def eager_step():
+        if levels:
+            from ndnet.preprocessing.ndtnet_preprocessing import ndt_multiscale
+            return [model(p, c) for p, c, _ in ndt_multiscale(levels, pts)]
         p, c, _ = ndt_preprocessing(k, pts)
         return model(p, c)
 
@@ -101,7 +110,7 @@ def main() -> None:
     else:
         # the same kernels, launched from one captured HIP graph per step
         from ndnet.pipeline import GraphedSegmentation
-        graphed = GraphedSegmentation(model, k, B, n, device=dev)
+        graphed = GraphedSegmentation(model, k, B, n, device=dev, levels=levels)
         graphed.points.copy_(pts)
         step = graphed.replay
 
@@ -123,7 +132,7 @@ def main() -> None:
     value = total_clouds / elapsed
     stats = get_plan(B, n, k, -1, dev).host_stats()
     assert all(s.rc == 0 for s in stats), [s.rc for s in stats]
-    assert torch.isfinite(out).all()
+    assert all(torch.isfinite(o).all() for o in (out if isinstance(out, list) else [out]))
 
     # ---- stage timing (HIP events on the stream the kernels run on) ----
     plan = get_plan(B, n, k, -1, dev)
@@ -246,7 +255,9 @@ def main() -> None:
 
     if rank == 0:
         line = {
-            "metric": "clouds/sec NDT preprocess+PointNet fwd, 100k pts->1000 NDs, batch=16",
+            "metric": ("clouds/sec NDT preprocess+PointNet fwd, 100k pts->1000 NDs, batch=16" if not levels else
+                       "clouds/sec NDT multiscale {%s} NDs + PointNet fwd per level, 100k pts, batch=16"
+                       % ",".join(map(str, levels))),
             "value": round(value, 2),
             "unit": "clouds/s",
             "n_gpus": world,
@@ -258,7 +269,11 @@ def main() -> None:
             "vs_baseline": None,
             "dtype": "f64 (NDT core) + fp32 (PointNet)",
             "data": f"synthetic {args.kind} clouds (SURVEY 8d), random-init weights",
-            "config": {"workload": f"batch {B} x {n} pts -> {k} NDs, NDTNetSegmentation F={F} C={C} eval",
+            "config": {"workload": (f"batch {B} x {n} pts -> {k} NDs, NDTNetSegmentation F={F} C={C} eval"
+                                    if not levels else
+                                    f"C5: batch {B} x {n} pts -> downsample {levels[0]} -> prune "
+                                    f"{' -> '.join(map(str, levels[1:]))}, NDTNetSegmentation F={F} C={C} eval "
+                                    f"per level"),
                        "launch": "eager" if args.eager else "hip graph (ndnet.pipeline.GraphedSegmentation)",
                        "global_batch": B * world, "points": n, "nds": k, "parallelism": f"dp{world} (clouds sharded)"},
             "stages_ms": {nm: round(float(v), 4) for nm, v in zip(stage_names, stage_ms)} | {"pointnet_fwd": round(fwd_ms, 4)},

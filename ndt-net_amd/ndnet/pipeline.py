@@ -22,7 +22,7 @@ from typing import Optional
 import torch
 
 from . import _lib
-from .preprocessing.ndtnet_preprocessing import ndt_preprocessing, get_plan
+from .preprocessing.ndtnet_preprocessing import ndt_multiscale, ndt_preprocessing, get_plan
 
 
 class GraphedSegmentation:
@@ -36,6 +36,10 @@ class GraphedSegmentation:
         batch, num_points: the static input shape ``[batch, num_points, 3]``.
         warmup: eager runs before capture (plan / workspace creation, kernel
             attribute setup).
+        levels: optional strictly decreasing NDs per level (config C5:
+            (2000, 1000, 500)): the step is then ndt_multiscale (downsample to
+            levels[0], prune to each further level) and a forward per level;
+            the output is the list of per-level log-probs.
 
     ``points`` is the static float32 input buffer; ``__call__(new_points)``
     copies into it, replays, and returns the static ``[B, num_nds, C+1]``
@@ -43,13 +47,16 @@ class GraphedSegmentation:
     """
 
     def __init__(self, model, num_nds: int, batch: int, num_points: int,
-                 device: Optional[torch.device] = None, warmup: int = 2) -> None:
+                 device: Optional[torch.device] = None, warmup: int = 2, levels=None) -> None:
         _lib.require_gpu()
         if model.training:
             raise ValueError("GraphedSegmentation needs an eval-mode model")
         dev = torch.device(device) if device is not None else next(model.parameters()).device
         if dev.type != "cuda":
             raise ValueError("GraphedSegmentation needs the model on a cuda device")
+        self.levels = tuple(int(k) for k in levels) if levels else None
+        if self.levels:
+            num_nds = self.levels[0]
         self.model, self.num_nds, self.device = model, int(num_nds), dev
         self.points = torch.zeros((batch, num_points, 3), dtype=torch.float32, device=dev)
         side = torch.cuda.Stream(device=dev)
@@ -64,7 +71,9 @@ class GraphedSegmentation:
             self.out = self._step()
         self.plan = get_plan(batch, num_points, self.num_nds, -1, dev)
 
-    def _step(self) -> torch.Tensor:
+    def _step(self):
+        if self.levels:
+            return [self.model(p, c) for p, c, _ in ndt_multiscale(self.levels, self.points)]
         p, c, _ = ndt_preprocessing(self.num_nds, self.points)
         return self.model(p, c)
 

@@ -136,6 +136,33 @@ def ndt_preprocessing(num_nds: int, points: torch.Tensor, classes: torch.Tensor 
 ndt_preprocessing.last_plan = None
 
 
+def ndt_multiscale(levels, points: torch.Tensor, classes: torch.Tensor = None, num_classes: int = None) -> list:
+    """Multi-level NDT of a batch (config C5, tools/train_multiscale.py's
+    levels): ``downsample(levels[0])`` then ``prune(levels[i])`` for each
+    further, smaller level on the retained KL list -- NDT_Sampler.downsample /
+    .prune (ndt_legacy.py:111-240) for every cloud at once, all on the GPU.
+
+    Returns one ``(points [B,k,3], covariances [B,k,9], classes or None)`` per
+    level, as ndt_preprocessing does for one level."""
+    levels = [int(k) for k in levels]
+    if not levels or any(b >= a for a, b in zip(levels, levels[1:])):
+        raise ValueError(f"levels must be strictly decreasing, got {levels}")
+    p, c, cls = ndt_preprocessing(levels[0], points, classes, num_classes)
+    out = [(p, c, cls)]
+    plan = ndt_preprocessing.last_plan
+    dev = plan.device
+    B = p.shape[0]
+    for k in levels[1:]:
+        blk = torch.empty((B, k, 12), dtype=torch.float32, device=dev)
+        blk_cls = torch.empty((B, k, cls.shape[2]), dtype=torch.float32, device=dev) if cls is not None else None
+        plan.prune(k, blk, blk_cls)
+        if points.device != dev:
+            blk = blk.to(points.device)
+            blk_cls = blk_cls.to(points.device) if blk_cls is not None else None
+        out.append((blk[..., :3], blk[..., 3:], blk_cls))
+    return out
+
+
 def ndt_preprocessing_packed(num_nds: int, points: torch.Tensor) -> torch.Tensor:
     """The unlabelled path returning the ``[B, num_nds, 12]`` block itself."""
     p, _, _ = ndt_preprocessing(num_nds, points)

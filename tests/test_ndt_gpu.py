@@ -249,3 +249,25 @@ def test_front_kernel_equals_multikernel_path(case):
         assert s2[b].rc == r.rc
         if r.rc == 0:
             assert np.array_equal(o2[b, :, :3], pc) and np.array_equal(o2[b, :, 3:], cov)
+
+
+@pytest.mark.parametrize("kind", ["U", "L"])
+def test_multiscale_batch_matches_oracle_chain(kind):
+    """Config C5's path batched: downsample(600) -> prune(300) -> prune(150)
+    for 4 clouds at once (ndt_multiscale), every level's rows bit-exact
+    against the oracle's downsample/prune_nds/to_point_cloud chain per cloud
+    after the driver's float32 cast and nan_to_num."""
+    import oracle as O
+    import torch
+    from ndnet.preprocessing.ndtnet_preprocessing import ndt_multiscale
+    from ndnet.synthetic import make_batch
+    pts = make_batch(kind, 4, 30_000, seed0=11)
+    levels = ndt_multiscale((600, 300, 150), torch.from_numpy(pts).cuda())
+    f32 = lambda a: np.nan_to_num(a.astype(np.float32), nan=0.0, posinf=0.0, neginf=0.0)  # noqa: E731
+    for b in range(4):
+        ref = O.LegacyChain(pts[b].astype(np.float64))
+        expect = [ref.downsample(600), ref.prune(300), ref.prune(150)]
+        for (p, c, _), (p2, c2) in zip(levels, expect):
+            assert np.array_equal(p[b].cpu().numpy(), f32(p2))
+            assert np.array_equal(c[b].cpu().numpy(), f32(c2))
+        ref.cleanup()
