@@ -41,7 +41,13 @@ constexpr int kWaves = 16;
 constexpr int kThreads = 64 * kWaves;
 constexpr int kRowBlocks = kP / 16;  // 4 (kWaves / 2)
 constexpr int kFuseNC = 64;     // columns per chunk of a fused layer
-constexpr int kDepth = 4;       // weight k-groups in flight per wave
+#ifndef NDNET_PN_DEPTH
+#define NDNET_PN_DEPTH 2
+#endif
+#ifndef NDNET_PN_WIDE
+#define NDNET_PN_WIDE 0
+#endif
+constexpr int kDepth = NDNET_PN_DEPTH;  // weight k-groups in flight per wave
 static_assert(kWaves % kRowBlocks == 0, "every row group has whole column groups");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -317,7 +323,8 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A) {
       const bool last = l + 1 == A.num_layers;
       const int out = reg[(l + 1) & 1], pout = ((l + 1) & 1) ? pitch1 : pitch0;
       float* gm = (last && gmax_b) ? gmax_b : nullptr;
-      if (C.N % 256 == 0) plain_layer<4, 1>(C, in, pin, out, pout, gm, rows_valid);
+      if (NDNET_PN_WIDE && C.N % 512 == 0) plain_layer<4, 2>(C, in, pin, out, pout, gm, rows_valid);
+      else if (C.N % 256 == 0) plain_layer<4, 1>(C, in, pin, out, pout, gm, rows_valid);
       else if (C.N % 128 == 0) plain_layer<2, 1>(C, in, pin, out, pout, gm, rows_valid);
       else plain_layer<1, 1>(C, in, pin, out, pout, gm, rows_valid);  // N % 64 == 0, or N = 32 (half idle)
     }
