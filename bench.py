@@ -68,6 +68,8 @@ def main() -> None:
     ap.add_argument("--cpu-baseline-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch kernels from Python each step (no HIP graph)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="one HIP graph per step, NDT then forward of the same batch (no cross-step overlap)")
     ap.add_argument("--levels", default=None,
                     help="config C5: comma-separated NDs per level, e.g. 2000,1000,500 (downsample, then prune; "
                          "a forward per level)")
@@ -110,7 +112,12 @@ def main() -> None:
     else:
         # the same kernels, launched from one captured HIP graph per step
         from ndnet.pipeline import GraphedSegmentation
-        graphed = GraphedSegmentation(model, k, B, n, device=dev, levels=levels)
+        if levels or args.no_pipeline:
+            graphed = GraphedSegmentation(model, k, B, n, device=dev, levels=levels)
+        else:
+            # step i: NDT of batch i on one stream || forward of batch i - 1 on another
+            from ndnet.pipeline import PipelinedSegmentation
+            graphed = PipelinedSegmentation(model, k, B, n, device=dev)
         graphed.points.copy_(pts)
         step = graphed.replay
 
@@ -274,7 +281,10 @@ def main() -> None:
                                     f"C5: batch {B} x {n} pts -> downsample {levels[0]} -> prune "
                                     f"{' -> '.join(map(str, levels[1:]))}, NDTNetSegmentation F={F} C={C} eval "
                                     f"per level"),
-                       "launch": "eager" if args.eager else "hip graph (ndnet.pipeline.GraphedSegmentation)",
+                       "launch": "eager" if args.eager else (
+                           "hip graph per step (ndnet.pipeline.GraphedSegmentation)" if (levels or args.no_pipeline)
+                           else "2 hip graphs alternating: NDT(batch i) || forward(batch i-1) on two streams "
+                                "(ndnet.pipeline.PipelinedSegmentation)"),
                        "global_batch": B * world, "points": n, "nds": k, "parallelism": f"dp{world} (clouds sharded)"},
             "stages_ms": {nm: round(float(v), 4) for nm, v in zip(stage_names, stage_ms)} | {"pointnet_fwd": round(fwd_ms, 4)},
             "roofline": roofline,

@@ -81,3 +81,26 @@ def test_epoch_wrap_clears_stamps():
         assert torch.equal(torch.cat((p, c), 2), first)
         st = plan.host_stats()
         assert [s.iters for s in st] == [s.iters for s in st0]
+
+
+def test_pipelined_steps_equal_sequential_batches():
+    """PipelinedSegmentation: step i's forward output is the log-probs of the
+    batch fed at step i - 1, equal to the one-graph-per-step path's."""
+    import torch
+    from ndnet.models.ndtnet import NDTNetSegmentation
+    from ndnet.pipeline import GraphedSegmentation, PipelinedSegmentation
+    from ndnet.synthetic import make_batch
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    m = NDTNetSegmentation(3, 28, 768).to(dev).eval()
+    batches = [torch.from_numpy(make_batch("L", 4, 20_000, seed0=10 * i)).to(dev) for i in range(3)]
+    ref = GraphedSegmentation(m, 400, 4, 20_000, device=dev)
+    expect = [ref(b).clone() for b in batches]
+    pipe = PipelinedSegmentation(m, 400, 4, 20_000, device=dev)
+    outs = []
+    for b in batches + [batches[-1]]:
+        pipe.points.copy_(b)
+        outs.append(pipe.replay().clone())
+    torch.cuda.synchronize()
+    for i in range(3):
+        assert torch.equal(outs[i + 1], expect[i]), f"batch {i}"
