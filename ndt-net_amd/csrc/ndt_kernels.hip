@@ -1113,6 +1113,7 @@ struct KLArgs {
   double* out_cov64;     // [B][k][9] or null
   uint16_t* out_cls16;   // [B][k] or null
   ndnet_ndt_stats* stats;
+  ndnet_ndt_stats* stats_out;  // the caller's copy (written alongside; replaces a D2D copy launch), or null
   uint64_t vcap;
   uint32_t ndcap, ecap, sortcap, nchunk;
   uint32_t* chunk_cnt;
@@ -1339,9 +1340,14 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
   return carry;  // survivors (block-uniform)
 }
 
+__device__ void write_stats_to(const KLArgs& A, int b, ndnet_ndt_stats& s);
 __device__ void write_stats(const KLArgs& A, int b) {
+  write_stats_to(A, b, A.stats[b]);
+  if (A.stats_out) write_stats_to(A, b, A.stats_out[b]);
+}
+
+__device__ void write_stats_to(const KLArgs& A, int b, ndnet_ndt_stats& s) {
   const CloudCtl& c = A.ctl[b];
-  ndnet_ndt_stats& s = A.stats[b];
   s.rc = c.rc;
   s.prune_rc = c.prune_rc;
   s.iters = c.iter;
@@ -1940,6 +1946,7 @@ static KLArgs kl_args(Plan* P, uint64_t k, float* out, float* out_cls, double* p
   A.out_cov64 = cov64;
   A.out_cls16 = cls16;
   A.stats = P->d_stats;
+  A.stats_out = nullptr;
   A.vcap = P->vcap;
   A.ndcap = P->ndcap;
   A.ecap = P->ecap;
@@ -2015,6 +2022,7 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
                                                                   n, P->ndcap, P->timing >= 2 ? P->wmarks : nullptr);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[5], st));
   KLArgs A = kl_args(P, P->k, out, out_cls, pc64, cov64, cls16);
+  A.stats_out = stats_dst;
   k_kl_chains<<<dim3((P->ndcap + 255) / 256, B), 256, 0, st>>>(A);
   k_kl_events<<<dim3((6 * P->ndcap + 255) / 256, B), 256, 0, st>>>(A);
   k_kl_rank_chunks<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
@@ -2026,8 +2034,6 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
     k_kl_merge<false><<<dim3(mg, B), kChunk * kMergeRuns, 0, st>>>(A);
   k_kl<<<B, kKLThreads, A.kl_lds ? kl_lds_bytes(P) : 0, st>>>(A);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[6], st));
-  if (stats_dst)
-    HIPCHK(hipMemcpyAsync(stats_dst, P->d_stats, sizeof(ndnet_ndt_stats) * B, hipMemcpyDeviceToDevice, st));
   HIPCHK(hipGetLastError());
   return NDNET_OK;
 }
@@ -2257,9 +2263,8 @@ int ndnet_ndt_prune(void* plan, void* stream, uint64_t num_desired, float* d_out
   if (!P || num_desired == 0) return NDNET_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   KLArgs A = kl_args(P, num_desired, d_out, d_out_classes, d_out_points, d_out_covariances, d_out_classes16);
+  A.stats_out = d_stats;
   k_prune<<<P->B, kKLThreads, A.kl_lds ? kl_lds_bytes(P) : 0, st>>>(A);
-  if (d_stats)
-    HIPCHK(hipMemcpyAsync(d_stats, P->d_stats, sizeof(ndnet_ndt_stats) * P->B, hipMemcpyDeviceToDevice, st));
   HIPCHK(hipGetLastError());
   return NDNET_OK;
 }
