@@ -36,7 +36,7 @@ typedef struct ndnet_pn_layer {
   int32_t K, N;           // padded sizes: K % 16 == 0; N == 32 or N % 64 == 0
   int32_t relu;
   int32_t fuse_next;      // 1: this layer's output (N % 64 == 0) is produced in 64-column chunks, each
-                          // consumed at once by the next layer (whose N % 64 == 0, N <= 256) -- the
+                          // consumed at once by the next layer (whose N is 64, 128 or 256) -- the
                           // activation never occupies LDS whole
 } ndnet_pn_layer;
 

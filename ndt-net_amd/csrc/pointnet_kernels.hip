@@ -37,7 +37,10 @@
 namespace {
 
 constexpr int kP = 64;          // points per workgroup
-constexpr int kWaves = 16;
+#ifndef NDNET_PN_WAVES
+#define NDNET_PN_WAVES 16
+#endif
+constexpr int kWaves = NDNET_PN_WAVES;
 constexpr int kThreads = 64 * kWaves;
 constexpr int kRowBlocks = kP / 16;  // 4 (kWaves / 2)
 constexpr int kFuseNC = 64;     // columns per chunk of a fused layer
@@ -255,21 +258,22 @@ __device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin
   constexpr int WR = kRowBlocks / RB, WC = kWaves / WR;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int kq = lane >> 4, cl = lane & 15;
-  // P: row block wave / 4, column block 4 f + wave % 4
-  const int prow0 = (wave >> 2) * 16, pwc = wave & 3;
+  // P: row block wave / PWC, PNB column blocks from 4 f + PNB (wave % PWC)
+  constexpr int PWC = kWaves / kRowBlocks, PNB = 4 / PWC;
+  const int prow0 = (wave / PWC) * 16, pwc = (wave % PWC) * PNB;
   const float* ain = g_smem + in + (prow0 + cl) * pin + 4 * kq;
   // Q: row group wave / WC, column group wave % WC
   const int qrow0 = (wave / WC) * RB * 16, qwc = wave % WC;
   const bool qidle = qwc * NB * 16 >= Q.N;
   const int nf = P.N / kFuseNC;
   auto p_chunk = [&](int f) {
-    f32x4 acc1[1][1];
+    f32x4 acc1[1][PNB];
     zero_acc(acc1);
     const int fb = fbuf + (f & 1) * kP * kFP;
-    auto epi = [&](f32x4 (&a)[1][1], int) {
-      store_cols<1, 1>(a, P.bias, 64 * f + 16 * pwc, P.relu, prow0, fb, kFP, 16 * pwc);
+    auto epi = [&](f32x4 (&a)[1][PNB], int) {
+      store_cols<1, PNB>(a, P.bias, 64 * f + 16 * pwc, P.relu, prow0, fb, kFP, 16 * pwc);
     };
-    run_tiles<1, 1>(acc1, P.w, P.KG, 0, P.KG, 4 * f + pwc, 0, 1, ain, pin, epi);
+    run_tiles<1, PNB>(acc1, P.w, P.KG, 0, P.KG, 4 * f + pwc, 0, 1, ain, pin, epi);
   };
   f32x4 acc2[RB][NB];
   zero_acc(acc2);
@@ -314,9 +318,11 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A) {
       const bool last = l + 2 == A.num_layers;
       const int out = reg[(l + 2) & 1], pout = ((l + 2) & 1) ? pitch1 : pitch0;
       float* gm = (last && gmax_b) ? gmax_b : nullptr;
-      if (Q.N == 256) fused_pair<4, 1>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid);
-      else if (Q.N > 64) fused_pair<2, 1>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid);
-      else fused_pair<1, 1>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid);
+      // Q is one chunk of its (RB, NB) split: NB = N2 / (16 * column groups)
+      constexpr int kQ = 16 / kWaves > 0 ? 16 / kWaves : 1;
+      if (Q.N == 256) fused_pair<4, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid);
+      else if (Q.N > 64) fused_pair<2, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid);
+      else fused_pair<1, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid);
       l++;
     } else {
       const LayerCtx C = layer_ctx(A, l, b);
@@ -512,7 +518,7 @@ int ndnet_pn_chain_run(const ndnet_pn_chain* args, int batch, void* stream) {
       return -20;
     const bool fed = l > 0 && args->L[l - 1].fuse_next;
     if (fed) {
-      if (L.K != args->L[l - 1].N || L.N % 64 || L.N > 256 || L.fuse_next) return -20;
+      if (L.K != args->L[l - 1].N || (L.N != 64 && L.N != 128 && L.N != 256) || L.fuse_next) return -20;
     } else if (l > 0 && L.K > w[l & 1]) {
       return -20;
     }
