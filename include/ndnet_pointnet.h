@@ -35,6 +35,11 @@ typedef struct ndnet_pn_layer {
   int64_t bias_cloud_stride;
   int32_t K, N;           // padded sizes: K % 16 == 0; N == 32 or N % 64 == 0
   int32_t relu;
+  int32_t prec;           // 0: fp32 MFMA (v_mfma_f32_16x16x4_f32) on fp32 fragment-major weights;
+                          // 1: split-bf16 "x6" (fp32-accurate, v_mfma_f32_16x16x32_bf16): K % 32 == 0,
+                          //    `w` = bf16 [N/16][K/32][3 planes][64 lanes][8] with W^T = h + m + l and
+                          //    lane l's 8 values W^T[32 kg + 8 (l/16) + j][16 cb + l%16]; the layer's
+                          //    producer must be the previous, unfused layer (it stores bf16 planes)
   int32_t fuse_next;      // 1: this layer's output (N % 64 == 0) is produced in 64-column chunks, each
                           // consumed at once by the next layer (whose N is 64, 128 or 256) -- the
                           // activation never occupies LDS whole

@@ -2128,7 +2128,10 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
     int dev = 0, cus = 0;
     if (e == hipSuccess) e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint32_t gt = (uint32_t)(cus / batch > 0 ? cus / batch : 1);
+#ifndef NDNET_FRONT_CU_SHARE
+#define NDNET_FRONT_CU_SHARE 1
+#endif
+    const uint32_t gt = (uint32_t)(cus / (NDNET_FRONT_CU_SHARE * batch) > 0 ? cus / (NDNET_FRONT_CU_SHARE * batch) : 1);
     uint32_t bpw = (P->nbins + gt - 1) / gt;
     uint32_t G = (P->nbins + bpw - 1) / bpw;
     // rank bins of 512 points when that keeps every wave busy and fits

@@ -47,13 +47,11 @@ constexpr int kFuseNC = 64;     // columns per chunk of a fused layer
 #ifndef NDNET_PN_DEPTH
 #define NDNET_PN_DEPTH 2
 #endif
-#ifndef NDNET_PN_WIDE
-#define NDNET_PN_WIDE 0
-#endif
 constexpr int kDepth = NDNET_PN_DEPTH;  // weight k-groups in flight per wave
 static_assert(kWaves % kRowBlocks == 0, "every row group has whole column groups");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 __device__ inline void atomic_max_f32(float* addr, float v) {
   v = v + 0.0f;  // -0 -> +0 so the integer orderings below agree
@@ -74,17 +72,20 @@ extern __shared__ __attribute__((aligned(16))) float g_smem[];
 // the weights stream from L2 straight into registers (no LDS staging, no
 // barrier inside a layer) and only the activations live in LDS.
 struct LayerCtx {
-  const f32x4* __restrict__ w;  // this cloud's fragments, offset by the lane
+  const f32x4* __restrict__ w;     // this cloud's fragments, offset by the lane (prec 0)
+  const bf16x8* __restrict__ w6;   // split-bf16 fragments, offset by the lane (prec 1)
   const float* __restrict__ bias;
-  int KG, N, relu;
+  int KG, N, relu, prec;           // KG: 16-row k-groups (prec 0) or 32-row (prec 1)
 };
 
 __device__ inline LayerCtx layer_ctx(const ndnet_pn_chain& A, int l, int b) {
   const ndnet_pn_layer& L = A.L[l];
   LayerCtx C;
   C.w = reinterpret_cast<const f32x4*>(L.w + (int64_t)b * L.w_cloud_stride) + (threadIdx.x & 63);
+  C.w6 = reinterpret_cast<const bf16x8*>(L.w + (int64_t)b * L.w_cloud_stride) + (threadIdx.x & 63);
   C.bias = L.bias + (int64_t)b * L.bias_cloud_stride;
-  C.KG = L.K / 16;
+  C.prec = L.prec;
+  C.KG = L.prec ? L.K / 32 : L.K / 16;
   C.N = L.N;
   C.relu = L.relu;
   return C;
@@ -221,16 +222,152 @@ __device__ __attribute__((always_inline)) inline void pool_cols(const f32x4 (&ac
   }
 }
 
+// ---------------------------------------------------------------------------
+// Split-bf16 layers (ndnet_pn_layer.prec = 1): fp32-accurate GEMMs on the
+// bf16 matrix cores.  Every operand x is split x = h + m + l into three bf16
+// (8 + 8 + 8 significant bits = fp32's 24; h = bf16(x), m = bf16(x - h),
+// l = bf16(x - h - m), each residual exact in fp32).  A product keeps the six
+// terms of weight >= 2^-16 (mm, mh, lh, hl, hm, hh in that order) -- each
+// an exact bf16 x bf16 product accumulated in fp32 by v_mfma_f32_16x16x32_bf16;
+// the dropped ml, lm, ll are below 3 * 2^-24 |x y|, the size of fp32's own
+// rounding.  Six 16-cycle MFMAs per 16x16x32 block against eight 32-cycle
+// v_mfma_f32_16x16x4_f32 for the same FLOPs: 2.7x less matrix-core time.
+//
+// The layer's input activations are stored by the producing layer's epilogue
+// as three bf16 planes of the LDS region (plane p at p * kP * pitch, element
+// (row, k) at row * pitch + k, pitch = width + 8 bf16); lane l of a 16x16x32
+// A fragment reads row l & 15, k = 32 kg + 8 (l >> 4) .. + 7 with one
+// ds_read_b128 per plane.  The weights are fragment-major per 32-row k-group:
+// [column block][k-group][plane][lane][8 bf16], lane l holding
+// W^T[32 kg + 8 (l >> 4) + j][16 cb + (l & 15)] (include/ndnet_pointnet.h).
+
+__device__ inline void split3(float v, __bf16& h, __bf16& m, __bf16& l) {
+  h = (__bf16)v;
+  const float r = v - (float)h;
+  m = (__bf16)r;
+  l = (__bf16)(r - (float)m);
+}
+
+// Bias + ReLU of this wave's tile into the three bf16 planes of a region
+// (`out` in floats; pitch in bf16).
+template <int RB, int NB>
+__device__ __attribute__((always_inline)) inline void store_cols_planes(const f32x4 (&acc)[RB][NB],
+                                                                        const float* __restrict__ bias, int col0,
+                                                                        int relu, int row0, int out, int pitchb,
+                                                                        int oc0) {
+  const int lane = threadIdx.x & 63;
+  const int kq = lane >> 4, cl = lane & 15;
+  __bf16* const base = reinterpret_cast<__bf16*>(g_smem + out);
+  const int plane = kP * pitchb;
+#pragma unroll
+  for (int j = 0; j < NB; j++) {
+    const float bv = bias[col0 + 16 * j + cl];
+#pragma unroll
+    for (int rb = 0; rb < RB; rb++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        float v = acc[rb][j][r] + bv;
+        if (relu) v = fmaxf(v, 0.0f);
+        __bf16 h, m, l;
+        split3(v, h, m, l);
+        const int e = (row0 + 16 * rb + 4 * kq + r) * pitchb + oc0 + 16 * j + cl;
+        base[e] = h;
+        base[plane + e] = m;
+        base[2 * plane + e] = l;
+      }
+  }
+}
+
+// One 32-row k-group: the A planes are read one at a time (m, l, h) so only
+// one plane's fragments are live; per plane the B planes its terms need.
+template <int RB, int NB>
+__device__ __attribute__((always_inline)) inline void mma_kgroup_x6(f32x4 (&acc)[RB][NB], const __bf16* a0, int plane,
+                                                                    int rstride, const bf16x8 (&bw)[NB][3]) {
+  bf16x8 a[RB];
+  auto ld = [&](int p) {
+#pragma unroll
+    for (int rb = 0; rb < RB; rb++) a[rb] = *reinterpret_cast<const bf16x8*>(a0 + p * plane + rb * rstride);
+  };
+  auto mm = [&](int pb) {
+#pragma unroll
+    for (int rb = 0; rb < RB; rb++)
+#pragma unroll
+      for (int j = 0; j < NB; j++)
+        acc[rb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], bw[j][pb], acc[rb][j], 0, 0, 0);
+  };
+  ld(1);  // m: m*m, m*h
+  mm(1);
+  mm(0);
+  ld(2);  // l: l*h
+  mm(0);
+  ld(0);  // h: h*l, h*m, h*h
+  mm(2);
+  mm(1);
+  mm(0);
+}
+
+// run_tiles for split-bf16 layers: 32-row k-groups; A from the three planes
+// (abase: this lane's row / k offset in plane 0, in bf16), B three 1 KB
+// fragment pieces per column block, prefetched kDepth steps ahead.
+template <int RB, int NB, class Epi>
+__device__ __attribute__((always_inline)) inline void run_tiles_x6(f32x4 (&acc)[RB][NB],
+                                                                   const bf16x8* __restrict__ w, int KG, int nkg,
+                                                                   int cb0, int cbs, int nchunk,
+                                                                   const __bf16* abase, int pitchb, Epi epi) {
+  const int T = nchunk * nkg;
+  const int plane = kP * pitchb;
+  const int64_t jstride = (int64_t)KG * 3 * 64;
+  const int64_t chunk_jump = ((int64_t)cbs * KG - (nkg - 1)) * 3 * 64;
+  const bf16x8* lp = w + (int64_t)cb0 * KG * 3 * 64;
+  int lkk = 0, lleft = T;
+  auto load = [&](bf16x8 (&bw)[NB][3]) {
+#pragma unroll
+    for (int j = 0; j < NB; j++)
+#pragma unroll
+      for (int p = 0; p < 3; p++) bw[j][p] = lp[j * jstride + p * 64];
+    if (lleft > 1) {
+      lleft--;
+      if (++lkk == nkg) {
+        lkk = 0;
+        lp += chunk_jump;
+      } else {
+        lp += 3 * 64;
+      }
+    }
+  };
+  int kk = 0, c = 0;
+  auto step = [&](const bf16x8 (&bw)[NB][3]) {
+    mma_kgroup_x6<RB, NB>(acc, abase + 32 * kk, plane, 16 * pitchb, bw);
+    if (++kk == nkg) {
+      epi(acc, c);
+      kk = 0;
+      c++;
+    }
+  };
+  bf16x8 bq[kDepth][NB][3];
+#pragma unroll
+  for (int i = 0; i < kDepth; i++) load(bq[i]);
+  for (int t = 0; t < T; t += kDepth) {
+#pragma unroll
+    for (int i = 0; i < kDepth; i++) {
+      if (t + i < T) {
+        step(bq[i]);
+        load(bq[i]);
+      }
+    }
+  }
+}
+
 // One layer: RB row blocks x NB column blocks per wave; 4 / RB row groups x
 // 4 RB column groups of waves; N in chunks of (column groups x NB x 16).
 template <int RB, int NB>
-__device__ void plain_layer(const LayerCtx& C, int in, int pin, int out, int pout, float* gmax, int rows_valid) {
+__device__ void plain_layer(const LayerCtx& C, int in, int pin, int out, int pout, float* gmax, int rows_valid,
+                            bool out_planes) {
   constexpr int WR = kRowBlocks / RB, WC = kWaves / WR, CB = WC * NB;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wr = wave / WC, wc = wave % WC;
   const int kq = lane >> 4, cl = lane & 15;
   const int row0 = wr * RB * 16;
-  const float* abase = g_smem + in + (row0 + cl) * pin + 4 * kq;
   // N is a multiple of the chunk width, or narrower than one chunk (then the
   // waves past column N / 16 idle; there is no barrier inside a layer)
   if (C.N < CB * 16 && wc * NB * 16 >= C.N) return;
@@ -239,11 +376,18 @@ __device__ void plain_layer(const LayerCtx& C, int in, int pin, int out, int pou
   auto epi = [&](f32x4 (&a)[RB][NB], int c) {
     const int col0 = (c * CB + wc * NB) * 16;
     if (gmax) pool_cols<RB, NB>(a, C.bias, col0, C.relu, row0, rows_valid, gmax);
+    else if (out_planes) store_cols_planes<RB, NB>(a, C.bias, col0, C.relu, row0, out, pout + 4, col0);
     else store_cols<RB, NB>(a, C.bias, col0, C.relu, row0, out, pout, col0);
     zero_acc(a);
   };
   const int nchunk = C.N < CB * 16 ? 1 : C.N / (CB * 16);
-  run_tiles<RB, NB>(acc, C.w, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase, pin, epi);
+  if (C.prec) {  // input: three bf16 planes, pitch = width + 8 = pin + 4
+    const __bf16* abase6 = reinterpret_cast<const __bf16*>(g_smem + in) + (row0 + cl) * (pin + 4) + 8 * kq;
+    run_tiles_x6<RB, NB>(acc, C.w6, C.KG, C.KG, wc * NB, CB, nchunk, abase6, pin + 4, epi);
+  } else {
+    const float* abase = g_smem + in + (row0 + cl) * pin + 4 * kq;
+    run_tiles<RB, NB>(acc, C.w, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase, pin, epi);
+  }
 }
 
 // A fused pair: layer P (K -> N1) produced 64 columns at a time into a
@@ -292,13 +436,20 @@ __device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin
   else store_cols<RB, NB>(acc2, Q.bias, 16 * qwc * NB, Q.relu, qrow0, out, pout, 16 * qwc * NB);
 }
 
-__global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A) {
+// Floats of LDS region r: fp32 activations (pitch width + 4) or, when it ever
+// holds a split-bf16 layer's input (planes bit r), three bf16 planes.
+__host__ __device__ inline int region_floats(int width, int planes) {
+  const int f32 = kP * (width + 4), b16 = 3 * kP * (width + 8) / 2;
+  return planes && b16 > f32 ? b16 : f32;
+}
+
+__global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int planes) {
   const int b = blockIdx.y;
   const int p0 = blockIdx.x * kP;
   // LDS: activation region 0 | region 1 | [fused-chunk double buffer]
   const int pitch0 = A.max_width + 4, pitch1 = A.max_width2 + 4;
-  const int reg[2] = {0, kP * pitch0};
-  const int fbuf = kP * (pitch0 + pitch1);
+  const int reg[2] = {0, region_floats(A.max_width, planes & 1)};
+  const int fbuf = reg[1] + region_floats(A.max_width2, planes & 2);
   // input tile, zero-filled to the first layer's K (a multiple of 16)
   const int K0 = A.L[0].K;
   for (int e = threadIdx.x; e < kP * K0; e += kThreads) {
@@ -329,10 +480,10 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A) {
       const bool last = l + 1 == A.num_layers;
       const int out = reg[(l + 1) & 1], pout = ((l + 1) & 1) ? pitch1 : pitch0;
       float* gm = (last && gmax_b) ? gmax_b : nullptr;
-      if (NDNET_PN_WIDE && C.N % 512 == 0) plain_layer<4, 2>(C, in, pin, out, pout, gm, rows_valid);
-      else if (C.N % 256 == 0) plain_layer<4, 1>(C, in, pin, out, pout, gm, rows_valid);
-      else if (C.N % 128 == 0) plain_layer<2, 1>(C, in, pin, out, pout, gm, rows_valid);
-      else plain_layer<1, 1>(C, in, pin, out, pout, gm, rows_valid);  // N % 64 == 0, or N = 32 (half idle)
+      const bool op = !last && A.L[l + 1].prec;  // the next layer reads bf16 planes
+      if (C.N % 256 == 0) plain_layer<4, 1>(C, in, pin, out, pout, gm, rows_valid, op);
+      else if (C.N % 128 == 0) plain_layer<2, 1>(C, in, pin, out, pout, gm, rows_valid, op);
+      else plain_layer<1, 1>(C, in, pin, out, pout, gm, rows_valid, op);  // N % 64 == 0, or N = 32 (half idle)
     }
     __syncthreads();
   }
@@ -510,6 +661,7 @@ int ndnet_pn_chain_run(const ndnet_pn_chain* args, int batch, void* stream) {
   // after a fused layer) and writes region (l + 1) & 1
   int w[2] = {args->L[0].K, 0};
   bool has_fuse = false;
+  int planes = 0;
   for (int l = 0; l < args->num_layers; l++) {
     const ndnet_pn_layer& L = args->L[l];
     if (!L.w || !L.bias || L.K <= 0 || L.K % 16 || L.N <= 0 || L.N % 32 || (L.N > 32 && L.N % 64) ||
@@ -517,6 +669,11 @@ int ndnet_pn_chain_run(const ndnet_pn_chain* args, int batch, void* stream) {
         L.w_cloud_stride % 4)
       return -20;
     const bool fed = l > 0 && args->L[l - 1].fuse_next;
+    if (L.prec != 0 && L.prec != 1) return -20;
+    if (L.prec) {  // split-bf16: reads planes its (stored, unfused) producer writes
+      if (l == 0 || fed || L.fuse_next || L.K % 32 || args->L[l - 1].N != L.K) return -20;
+      planes |= 1 << (l & 1);
+    }
     if (fed) {
       if (L.K != args->L[l - 1].N || (L.N != 64 && L.N != 128 && L.N != 256) || L.fuse_next) return -20;
     } else if (l > 0 && L.K > w[l & 1]) {
@@ -534,8 +691,9 @@ int ndnet_pn_chain_run(const ndnet_pn_chain* args, int batch, void* stream) {
   if (args->mode == 1 && (!args->out || args->out_cols <= 0 || args->out_cols > args->L[args->num_layers - 1].N))
     return -20;
   if (args->mode == 0 && !args->gmax) return -20;
-  const size_t lds = sizeof(float) * (size_t)kP *
-                     ((args->max_width + 4) + (args->max_width2 + 4) + (has_fuse ? 2 * (kFuseNC + 4) : 0));
+  const size_t lds = sizeof(float) * ((size_t)region_floats(args->max_width, planes & 1) +
+                                      region_floats(args->max_width2, planes & 2) +
+                                      (has_fuse ? 2 * (size_t)kP * (kFuseNC + 4) : 0));
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)k_pn_chain, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
@@ -545,7 +703,7 @@ int ndnet_pn_chain_run(const ndnet_pn_chain* args, int batch, void* stream) {
   }
   if (lds > 160 * 1024) return -20;
   dim3 grid((args->num_points + kP - 1) / kP, batch);
-  k_pn_chain<<<grid, kThreads, lds, (hipStream_t)stream>>>(*args);
+  k_pn_chain<<<grid, kThreads, lds, (hipStream_t)stream>>>(*args, planes);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     fprintf(stderr, "ndnet_amd: k_pn_chain launch failed: %s\n", hipGetErrorString(e));

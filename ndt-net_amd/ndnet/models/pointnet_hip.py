@@ -21,6 +21,7 @@ linear layer.  Per-point GEMMs run in FP32 on MFMA; the per-cloud steps
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -33,11 +34,18 @@ CHAIN_NAMES = ("A: TNet(3) 3-64-128-1024 + max", "B: conv1(t1) + TNet(64) 64-64-
 # set to a list to collect (chain index, start event, end event) per chain launch
 chain_timing = None
 
+# The three wide max-pooled layers (TNet(3) / TNet(64) conv3, NDTNet conv3:
+# 128 -> 1024 / 768, 90% of chains A-C's FLOPs) run as split-bf16 "x6" GEMMs
+# (include/ndnet_pointnet.h prec = 1): fp32-accurate (operands split into three
+# bf16, six exact partial products accumulated in fp32) on the bf16 matrix
+# cores.  NDNET_PN_PRECISION=fp32 keeps every layer on the fp32 MFMA.
+SPLIT_BF16 = os.environ.get("NDNET_PN_PRECISION", "x6") != "fp32"
+
 
 class _Layer(ctypes.Structure):
     _fields_ = [("w", ctypes.c_void_p), ("w_cloud_stride", ctypes.c_int64), ("bias", ctypes.c_void_p),
                 ("bias_cloud_stride", ctypes.c_int64), ("K", ctypes.c_int32), ("N", ctypes.c_int32),
-                ("relu", ctypes.c_int32), ("fuse_next", ctypes.c_int32)]
+                ("relu", ctypes.c_int32), ("prec", ctypes.c_int32), ("fuse_next", ctypes.c_int32)]
 
 
 class _Chain(ctypes.Structure):
@@ -89,6 +97,22 @@ def _frag(wT: torch.Tensor) -> torch.Tensor:
 def _npad(n: int) -> int:
     """Output width the chain kernel splits evenly: 32, or a multiple of 64."""
     return 32 if n <= 32 else _pad(n, 64)
+
+
+def _frag_x6(wT: torch.Tensor) -> torch.Tensor:
+    """Plain W^T [K, N] (K % 32 == 0, N % 16 == 0) -> the split-bf16 layout of
+    include/ndnet_pointnet.h (prec 1), flattened bf16: W^T = h + m + l
+    (h = bf16(w), m = bf16(w - h), l = bf16(w - h - m), residuals exact in
+    fp32), [cb][kg][plane][kq][cl][j] with k = 32 kg + 8 kq + j, n = 16 cb + cl."""
+    K, N = wT.shape
+    w = wT.float()
+    h = w.to(torch.bfloat16)
+    r = w - h.float()
+    m = r.to(torch.bfloat16)
+    lo = (r - m.float()).to(torch.bfloat16)
+    planes = torch.stack([h, m, lo])                                  # [3, K, N]
+    v = planes.reshape(3, K // 32, 4, 8, N // 16, 16)                 # plane, kg, kq, j, cb, cl
+    return v.permute(4, 1, 0, 2, 5, 3).reshape(-1).contiguous()        # cb, kg, plane, kq, cl, j
 
 
 def _bpad(b: torch.Tensor, npad: int) -> torch.Tensor:
@@ -155,6 +179,9 @@ class _Folded:
             self.t1_basis = torch.matmul(E.transpose(1, 2), self.c1wT).reshape(9, 12 * 64).contiguous()
             # fragment-major copies of the shared per-point layers (the HIP chains)
             self.frag = {id(w): _frag(w) for w, _ in self.A + self.B_tail + [self.C_tail] + self.D_tail}
+            # the wide pooled layers in split-bf16 form
+            self.wide = [self.A[2][0], self.B_tail[2][0], self.C_tail[0]]
+            self.frag6 = {id(w): _frag_x6(w) for w in self.wide}
             # the identity the TNet heads add (ndtnet.py:59), folded into fc3's bias
             self.t1["c3"] = self.t1["c3"] + torch.eye(3, device=dev).reshape(-1)
             self.t2["c3"] = self.t2["c3"] + torch.eye(64, device=dev).reshape(-1)
@@ -181,7 +208,7 @@ def _fc_head(g: torch.Tensor, t: dict, dim: int, h1: torch.Tensor, h2: torch.Ten
 def _build_chain(n: int, in_cols: int, layers, relus, mode: int, gmax=None, out_cols=0, fuse=()) -> "_Chain":
     """ctypes argument block of one ``ndnet_pn_chain_run`` (x / out set per call).
     ``layers``: (fragment-major weights, per-cloud stride in floats or 0, bias,
-    K, N) per layer.  Layers in ``fuse`` are produced in 64-column chunks
+    K, N[, prec]) per layer.  Layers in ``fuse`` are produced in 64-column chunks
     straight into the next layer (include/ndnet_pointnet.h)."""
     ch = _Chain()
     ch.x_ld = 12
@@ -191,8 +218,9 @@ def _build_chain(n: int, in_cols: int, layers, relus, mode: int, gmax=None, out_
     # LDS regions: layer l reads l & 1, writes (l + 1) & 1; the input tile is
     # zero-filled to the first layer's K; a fused layer's output has no region
     widths = [layers[0][3], 8]
-    for i, (w, stride, b, K, N) in enumerate(layers):
+    for i, (w, stride, b, K, N, *prec) in enumerate(layers):
         L = ch.L[i]
+        L.prec = prec[0] if prec else 0
         L.w = w.data_ptr()
         L.w_cloud_stride = stride
         L.K, L.N = K, N
@@ -270,6 +298,8 @@ class _Workspace:
 
         def shared(wb):
             w, b = wb
+            if SPLIT_BF16 and id(w) in W.frag6:
+                return (W.frag6[id(w)], 0, b, w.shape[0], w.shape[1], 1)
             return (W.frag[id(w)], 0, b, w.shape[0], w.shape[1])
 
         L1 = (self.w1f, self.w1f.stride(0), W.c1b, 16, 64)

@@ -117,3 +117,55 @@ def test_fragment_layout_matches_mfma_operands():
     # per-cloud leading dims are kept
     f3 = ph._frag(torch.stack([wT, 2 * wT]))
     assert f3.shape == (2, K * N) and torch.equal(f3[1], 2 * f3[0])
+
+
+def test_split_bf16_fragment_layout():
+    """_frag_x6: three bf16 planes summing to W^T exactly where representable,
+    at [cb][kg][plane][lane][j] with k = 32 kg + 8 (lane >> 4) + j,
+    n = 16 cb + (lane & 15) (the 16x16x32 bf16 MFMA B operand)."""
+    from ndnet.models import pointnet_hip as ph
+    K, N = 64, 32
+    g = torch.Generator().manual_seed(0)
+    wT = torch.randn((K, N), generator=g)
+    f = ph._frag_x6(wT).float().reshape(N // 16, K // 32, 3, 64, 8)
+    rec = torch.zeros((K, N))
+    for cb in range(N // 16):
+        for kg in range(K // 32):
+            for lane in range(64):
+                for j in range(8):
+                    k, n = 32 * kg + 8 * (lane >> 4) + j, 16 * cb + (lane & 15)
+                    rec[k, n] = f[cb, kg, 0, lane, j] + f[cb, kg, 1, lane, j] + f[cb, kg, 2, lane, j]
+    # h + m + l carries 24 significant bits: equal to the fp32 weight
+    assert torch.equal(rec, wT)
+
+
+@pytest.mark.gpu
+def test_split_bf16_layers_are_fp32_accurate():
+    """The split-bf16 ("x6") wide layers against a float64 evaluation of the
+    same model: their error is at the level of the all-fp32 MFMA path and of
+    torch's own fp32 forward (not at bf16's 2^-8)."""
+    import copy
+    from ndnet.models import pointnet_hip as ph
+    m = _model(768, 28, "cuda")
+    g = torch.Generator(device="cuda").manual_seed(5)
+    p = torch.rand((16, 1000, 3), device="cuda", generator=g) * 20 - 10
+    c = torch.randn((16, 1000, 9), device="cuda", generator=g)
+    with torch.no_grad():
+        ref64 = copy.deepcopy(m).double().forward_torch(p.double(), c.double())
+        saved = ph.SPLIT_BF16
+        try:
+            ph.SPLIT_BF16 = True
+            m._hip = None
+            out_x6 = m(p, c).double()
+            ph.SPLIT_BF16 = False
+            m._hip = None
+            out_32 = m(p, c).double()
+        finally:
+            ph.SPLIT_BF16 = saved
+            m._hip = None
+        out_t32 = m.forward_torch(p, c).double()
+    e_x6 = (out_x6 - ref64).abs().max().item()
+    e_32 = (out_32 - ref64).abs().max().item()
+    e_t32 = (out_t32 - ref64).abs().max().item()
+    print(f"max |err| vs fp64: x6 {e_x6:.3e}, fp32 MFMA {e_32:.3e}, torch fp32 {e_t32:.3e}")
+    assert e_x6 <= 2.0 * max(e_32, e_t32) + 1e-6
