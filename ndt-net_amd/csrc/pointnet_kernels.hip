@@ -48,6 +48,10 @@ constexpr int kFuseNC = 64;     // columns per chunk of a fused layer
 #define NDNET_PN_DEPTH 2
 #endif
 constexpr int kDepth = NDNET_PN_DEPTH;  // weight k-groups in flight per wave
+#ifndef NDNET_PN_DEPTH6
+#define NDNET_PN_DEPTH6 1
+#endif
+constexpr int kDepth6 = NDNET_PN_DEPTH6;  // the same for split-bf16 layers (3 fragment planes each)
 static_assert(kWaves % kRowBlocks == 0, "every row group has whole column groups");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -308,17 +312,17 @@ __device__ __attribute__((always_inline)) inline void mma_kgroup_x6(f32x4 (&acc)
 
 // run_tiles for split-bf16 layers: 32-row k-groups; A from the three planes
 // (abase: this lane's row / k offset in plane 0, in bf16), B three 1 KB
-// fragment pieces per column block, prefetched kDepth steps ahead.
+// fragment pieces per column block, prefetched kDepth6 steps ahead.
 template <int RB, int NB, class Epi>
 __device__ __attribute__((always_inline)) inline void run_tiles_x6(f32x4 (&acc)[RB][NB],
-                                                                   const bf16x8* __restrict__ w, int KG, int nkg,
-                                                                   int cb0, int cbs, int nchunk,
+                                                                   const bf16x8* __restrict__ w, int KG, int kg0,
+                                                                   int nkg, int cb0, int cbs, int nchunk,
                                                                    const __bf16* abase, int pitchb, Epi epi) {
   const int T = nchunk * nkg;
   const int plane = kP * pitchb;
   const int64_t jstride = (int64_t)KG * 3 * 64;
   const int64_t chunk_jump = ((int64_t)cbs * KG - (nkg - 1)) * 3 * 64;
-  const bf16x8* lp = w + (int64_t)cb0 * KG * 3 * 64;
+  const bf16x8* lp = w + ((int64_t)cb0 * KG + kg0) * 3 * 64;
   int lkk = 0, lleft = T;
   auto load = [&](bf16x8 (&bw)[NB][3]) {
 #pragma unroll
@@ -344,12 +348,12 @@ __device__ __attribute__((always_inline)) inline void run_tiles_x6(f32x4 (&acc)[
       c++;
     }
   };
-  bf16x8 bq[kDepth][NB][3];
+  bf16x8 bq[kDepth6][NB][3];
 #pragma unroll
-  for (int i = 0; i < kDepth; i++) load(bq[i]);
-  for (int t = 0; t < T; t += kDepth) {
+  for (int i = 0; i < kDepth6; i++) load(bq[i]);
+  for (int t = 0; t < T; t += kDepth6) {
 #pragma unroll
-    for (int i = 0; i < kDepth; i++) {
+    for (int i = 0; i < kDepth6; i++) {
       if (t + i < T) {
         step(bq[i]);
         load(bq[i]);
@@ -383,11 +387,17 @@ __device__ void plain_layer(const LayerCtx& C, int in, int pin, int out, int pou
   const int nchunk = C.N < CB * 16 ? 1 : C.N / (CB * 16);
   if (C.prec) {  // input: three bf16 planes, pitch = width + 8 = pin + 4
     const __bf16* abase6 = reinterpret_cast<const __bf16*>(g_smem + in) + (row0 + cl) * (pin + 4) + 8 * kq;
-    run_tiles_x6<RB, NB>(acc, C.w6, C.KG, C.KG, wc * NB, CB, nchunk, abase6, pin + 4, epi);
+    run_tiles_x6<RB, NB>(acc, C.w6, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase6, pin + 4, epi);
   } else {
     const float* abase = g_smem + in + (row0 + cl) * pin + 4 * kq;
     run_tiles<RB, NB>(acc, C.w, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase, pin, epi);
   }
+}
+
+// Floats of the fused pair's double buffer: two 64-column chunks, fp32 or
+// (split-bf16 consumer) three bf16 planes of pitch 72.
+__host__ __device__ inline int fbuf_floats(int qprec) {
+  return qprec ? 2 * 3 * kP * (kFuseNC + 8) / 2 : 2 * kP * (kFuseNC + 4);
 }
 
 // A fused pair: layer P (K -> N1) produced 64 columns at a time into a
@@ -410,12 +420,15 @@ __device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin
   const int qrow0 = (wave / WC) * RB * 16, qwc = wave % WC;
   const bool qidle = qwc * NB * 16 >= Q.N;
   const int nf = P.N / kFuseNC;
+  // a split-bf16 Q reads its chunks as three bf16 planes (pitch 72)
+  const int fbsz = Q.prec ? fbuf_floats(1) / 2 : kP * kFP;
   auto p_chunk = [&](int f) {
     f32x4 acc1[1][PNB];
     zero_acc(acc1);
-    const int fb = fbuf + (f & 1) * kP * kFP;
+    const int fb = fbuf + (f & 1) * fbsz;
     auto epi = [&](f32x4 (&a)[1][PNB], int) {
-      store_cols<1, PNB>(a, P.bias, 64 * f + 16 * pwc, P.relu, prow0, fb, kFP, 16 * pwc);
+      if (Q.prec) store_cols_planes<1, PNB>(a, P.bias, 64 * f + 16 * pwc, P.relu, prow0, fb, kFuseNC + 8, 16 * pwc);
+      else store_cols<1, PNB>(a, P.bias, 64 * f + 16 * pwc, P.relu, prow0, fb, kFP, 16 * pwc);
     };
     run_tiles<1, PNB>(acc1, P.w, P.KG, 0, P.KG, 4 * f + pwc, 0, 1, ain, pin, epi);
   };
@@ -425,8 +438,15 @@ __device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin
   __syncthreads();
   for (int f = 0; f < nf; f++) {
     if (!qidle) {
-      const float* af = g_smem + fbuf + (f & 1) * kP * kFP + (qrow0 + cl) * kFP + 4 * kq;
-      run_tiles<RB, NB>(acc2, Q.w, Q.KG, 4 * f, 4, qwc * NB, 0, 1, af, kFP, [](f32x4 (&)[RB][NB], int) {});
+      if (Q.prec) {
+        const __bf16* af6 = reinterpret_cast<const __bf16*>(g_smem + fbuf + (f & 1) * fbsz) +
+                            (qrow0 + cl) * (kFuseNC + 8) + 8 * kq;
+        run_tiles_x6<RB, NB>(acc2, Q.w6, Q.KG, 2 * f, 2, qwc * NB, 0, 1, af6, kFuseNC + 8,
+                             [](f32x4 (&)[RB][NB], int) {});
+      } else {
+        const float* af = g_smem + fbuf + (f & 1) * fbsz + (qrow0 + cl) * kFP + 4 * kq;
+        run_tiles<RB, NB>(acc2, Q.w, Q.KG, 4 * f, 4, qwc * NB, 0, 1, af, kFP, [](f32x4 (&)[RB][NB], int) {});
+      }
     }
     if (f + 1 < nf) p_chunk(f + 1);
     __syncthreads();
@@ -661,7 +681,7 @@ int ndnet_pn_chain_run(const ndnet_pn_chain* args, int batch, void* stream) {
   // after a fused layer) and writes region (l + 1) & 1
   int w[2] = {args->L[0].K, 0};
   bool has_fuse = false;
-  int planes = 0;
+  int planes = 0, qprec = 0;
   for (int l = 0; l < args->num_layers; l++) {
     const ndnet_pn_layer& L = args->L[l];
     if (!L.w || !L.bias || L.K <= 0 || L.K % 16 || L.N <= 0 || L.N % 32 || (L.N > 32 && L.N % 64) ||
@@ -670,9 +690,10 @@ int ndnet_pn_chain_run(const ndnet_pn_chain* args, int batch, void* stream) {
       return -20;
     const bool fed = l > 0 && args->L[l - 1].fuse_next;
     if (L.prec != 0 && L.prec != 1) return -20;
-    if (L.prec) {  // split-bf16: reads planes its (stored, unfused) producer writes
-      if (l == 0 || fed || L.fuse_next || L.K % 32 || args->L[l - 1].N != L.K) return -20;
-      planes |= 1 << (l & 1);
+    if (L.prec) {  // split-bf16: reads planes its producer writes (into a region, or the fused chunks)
+      if (l == 0 || L.fuse_next || L.K % 32 || args->L[l - 1].N != L.K) return -20;
+      if (fed) qprec = 1;
+      else planes |= 1 << (l & 1);
     }
     if (fed) {
       if (L.K != args->L[l - 1].N || (L.N != 64 && L.N != 128 && L.N != 256) || L.fuse_next) return -20;
@@ -693,7 +714,7 @@ int ndnet_pn_chain_run(const ndnet_pn_chain* args, int batch, void* stream) {
   if (args->mode == 0 && !args->gmax) return -20;
   const size_t lds = sizeof(float) * ((size_t)region_floats(args->max_width, planes & 1) +
                                       region_floats(args->max_width2, planes & 2) +
-                                      (has_fuse ? 2 * (size_t)kP * (kFuseNC + 4) : 0));
+                                      (has_fuse ? (size_t)fbuf_floats(qprec) : 0));
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)k_pn_chain, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
