@@ -93,8 +93,8 @@ NDNET_FN uint32_t voxel_key(double x, double y, double z, const double* off, con
 // is within 3 * 2^-24 |Q| (plus 2^-53 terms) of the real quotient
 // Q = (p - off) / vs, and the reference's fl64(fl64(p - off) / vs) within
 // 2^-52 |Q|; so where frac(q) is more than |q| 2^-19 away from 0 and 1, both
-// floor to the same integer.  *ok is false otherwise (including q = 0 and
-// NaN), and the caller takes voxel_key.
+// floor to the same integer.  Otherwise (including q = 0 and NaN) the caller
+// takes voxel_key.  (axis_index_f32 is the per-axis form, kept for tests.)
 NDNET_FN uint32_t axis_index_f32(float p, float off32, float inv32, bool& ok) {
   const float q = (p - off32) * inv32;
   const float f = floorf(q);
@@ -108,15 +108,21 @@ constexpr uint32_t kKeyRedo = 0xfffffffeu;  // voxel_key_f32: take voxel_key for
 
 // voxel_key for a float point, or kKeyRedo where the screen cannot decide.
 // No fallback inside, so callers can keep the (rare) double path out of
-// their unrolled hot loops.
-NDNET_FN uint32_t voxel_key_f32(float x, float y, float z, const float* off32, float inv32, const uint32_t* len) {
-  bool o0, o1, o2;
-  const uint32_t vx = axis_index_f32(x, off32[0], inv32, o0);
-  const uint32_t vy = axis_index_f32(y, off32[1], inv32, o1);
-  const uint32_t vz = axis_index_f32(z, off32[2], inv32, o2);
-  if (!(o0 && o1 && o2)) return kKeyRedo;
-  if (vx >= len[0] || vy >= len[1] || vz >= len[2]) return kInvalid;
-  return vz * len[0] * len[1] + vy * len[0] + vx;
+// their unrolled hot loops.  tol32 = max(len) * 2^-19 >= q * 2^-19 for every
+// in-grid q (a point whose q is past the grid either floors past len, and is
+// out of grid in the reference too, or sits within tol32 of len and is
+// redone): the per-axis screen is |frac(q) - 1/2| < 1/2 - tol32, no per-point
+// tolerance product, and the in-grid test is on the float floor.
+NDNET_FN uint32_t voxel_key_f32(float x, float y, float z, const float* off32, float inv32, float half_tol,
+                                const float* lenf, const uint32_t* len) {
+  const float qx = (x - off32[0]) * inv32, qy = (y - off32[1]) * inv32, qz = (z - off32[2]) * inv32;
+  const float fx = floorf(qx), fy = floorf(qy), fz = floorf(qz);
+  // branch-free (selects, no exec-mask regions in the caller's unrolled loop)
+  const bool ok = (fabsf(qx - fx - 0.5f) < half_tol) & (fabsf(qy - fy - 0.5f) < half_tol) &
+                  (fabsf(qz - fz - 0.5f) < half_tol);
+  const bool in = (fx < lenf[0]) & (fy < lenf[1]) & (fz < lenf[2]);
+  const uint32_t k = ((uint32_t)fz * len[1] + (uint32_t)fy) * len[0] + (uint32_t)fx;
+  return ok ? (in ? k : kInvalid) : kKeyRedo;
 }
 
 // x / n with the reciprocal of n shared between divisions.  The compiler's

@@ -431,6 +431,9 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
     // when the grid offset is a float (it is the minimum of float points)
     const float off32[3] = {(float)off[0], (float)off[1], (float)off[2]};
     const float inv32 = (float)inv_vs;
+    const float lenf[3] = {(float)len[0], (float)len[1], (float)len[2]};
+    const float lmax = fmaxf(lenf[0], fmaxf(lenf[1], lenf[2]));
+    const float half_tol = 0.5f - lmax * 0x1p-19f;  // |frac(q) - 1/2| bound of voxel_key_f32
     const bool fast32 = std::is_same<T, float>::value && (double)off32[0] == off[0] &&
                         (double)off32[1] == off[1] && (double)off32[2] == off[2];
     uint32_t fresh = 0;
@@ -444,7 +447,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
     auto visit = [&](uint32_t j, uint64_t i, T x, T y, T z) {
       uint32_t key = kInvalid;
       if (i < n8) {
-        key = fast32 ? voxel_key_f32((float)x, (float)y, (float)z, off32, inv32, len) : kKeyRedo;
+        key = fast32 ? voxel_key_f32((float)x, (float)y, (float)z, off32, inv32, half_tol, lenf, len) : kKeyRedo;
         redo |= key == kKeyRedo;
         cold |= key == kInvalid;
         if (small && key < kKeyRedo) {
