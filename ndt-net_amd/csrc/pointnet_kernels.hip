@@ -407,7 +407,7 @@ __host__ __device__ inline int fbuf_floats(int qprec) {
 // activation never needs LDS of its own.  One barrier per chunk.
 template <int RB, int NB>
 __device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin, int fbuf, int out, int pout,
-                           float* gmax, int rows_valid) {
+                           float* gmax, int rows_valid, bool out_planes) {
   constexpr int kFP = kFuseNC + 4;
   constexpr int WR = kRowBlocks / RB, WC = kWaves / WR;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -453,6 +453,7 @@ __device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin
   }
   if (qidle) return;
   if (gmax) pool_cols<RB, NB>(acc2, Q.bias, 16 * qwc * NB, Q.relu, qrow0, rows_valid, gmax);
+  else if (out_planes) store_cols_planes<RB, NB>(acc2, Q.bias, 16 * qwc * NB, Q.relu, qrow0, out, pout + 4, 16 * qwc * NB);
   else store_cols<RB, NB>(acc2, Q.bias, 16 * qwc * NB, Q.relu, qrow0, out, pout, 16 * qwc * NB);
 }
 
@@ -463,13 +464,13 @@ __host__ __device__ inline int region_floats(int width, int planes) {
   return planes && b16 > f32 ? b16 : f32;
 }
 
-__global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int planes) {
+__global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int planes, int fbuf) {
   const int b = blockIdx.y;
   const int p0 = blockIdx.x * kP;
   // LDS: activation region 0 | region 1 | [fused-chunk double buffer]
   const int pitch0 = A.max_width + 4, pitch1 = A.max_width2 + 4;
   const int reg[2] = {0, region_floats(A.max_width, planes & 1)};
-  const int fbuf = reg[1] + region_floats(A.max_width2, planes & 2);
+  // fbuf (the fused pair's chunks): float offset chosen by the launcher
   // input tile, zero-filled to the first layer's K (a multiple of 16)
   const int K0 = A.L[0].K;
   for (int e = threadIdx.x; e < kP * K0; e += kThreads) {
@@ -491,9 +492,10 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
       float* gm = (last && gmax_b) ? gmax_b : nullptr;
       // Q is one chunk of its (RB, NB) split: NB = N2 / (16 * column groups)
       constexpr int kQ = 16 / kWaves > 0 ? 16 / kWaves : 1;
-      if (Q.N == 256) fused_pair<4, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid);
-      else if (Q.N > 64) fused_pair<2, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid);
-      else fused_pair<1, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid);
+      const bool op = !last && A.L[l + 2].prec;  // the layer after Q reads bf16 planes
+      if (Q.N == 256) fused_pair<4, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op);
+      else if (Q.N > 64) fused_pair<2, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op);
+      else fused_pair<1, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op);
       l++;
     } else {
       const LayerCtx C = layer_ctx(A, l, b);
@@ -712,9 +714,22 @@ int ndnet_pn_chain_run(const ndnet_pn_chain* args, int batch, void* stream) {
   if (args->mode == 1 && (!args->out || args->out_cols <= 0 || args->out_cols > args->L[args->num_layers - 1].N))
     return -20;
   if (args->mode == 0 && !args->gmax) return -20;
-  const size_t lds = sizeof(float) * ((size_t)region_floats(args->max_width, planes & 1) +
-                                      region_floats(args->max_width2, planes & 2) +
-                                      (has_fuse ? (size_t)fbuf_floats(qprec) : 0));
+  // LDS: region 0 | region 1, then the fused pair's chunks.  Q writes the
+  // region P reads, after its last chunk, so the chunks may start right after
+  // P's input inside that region (and run past its end when it is region 1)
+  const int r0f = region_floats(args->max_width, planes & 1), r1f = region_floats(args->max_width2, planes & 2);
+  int fbuf_off = r0f + r1f;
+  size_t total = (size_t)r0f + r1f;
+  if (has_fuse) {
+    int lf = 0;
+    while (!args->L[lf].fuse_next) lf++;
+    const int r = lf & 1, fb = fbuf_floats(qprec);
+    const int p_in = kP * ((r ? args->max_width2 : args->max_width) + 4);  // P's fp32 input (region pitch)
+    const int inside = (r ? r0f : 0) + p_in;
+    if (!args->L[lf].prec && (r == 1 || inside + fb <= r0f)) fbuf_off = inside;
+    total = fbuf_off + (size_t)fb > total ? fbuf_off + (size_t)fb : total;
+  }
+  const size_t lds = sizeof(float) * total;
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)k_pn_chain, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
@@ -724,7 +739,7 @@ int ndnet_pn_chain_run(const ndnet_pn_chain* args, int batch, void* stream) {
   }
   if (lds > 160 * 1024) return -20;
   dim3 grid((args->num_points + kP - 1) / kP, batch);
-  k_pn_chain<<<grid, kThreads, lds, (hipStream_t)stream>>>(*args, planes);
+  k_pn_chain<<<grid, kThreads, lds, (hipStream_t)stream>>>(*args, planes, fbuf_off);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     fprintf(stderr, "ndnet_amd: k_pn_chain launch failed: %s\n", hipGetErrorString(e));

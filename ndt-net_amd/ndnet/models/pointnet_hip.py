@@ -36,7 +36,7 @@ chain_timing = None
 
 # The three wide max-pooled layers (TNet(3) / TNet(64) conv3, NDTNet conv3:
 # 128 -> 1024 / 768, 90% of chains A-C's FLOPs) and the seg head's 512 -> 256
-# (fed chunk by chunk from the fused 64 -> 512) run as split-bf16 "x6" GEMMs
+# (fed chunk by chunk from the fused 64 -> 512) and 256 -> 128 run as split-bf16 "x6" GEMMs
 # (include/ndnet_pointnet.h prec = 1): fp32-accurate (operands split into three
 # bf16, six exact partial products accumulated in fp32) on the bf16 matrix
 # cores.  NDNET_PN_PRECISION=fp32 keeps every layer on the fp32 MFMA.
@@ -181,7 +181,7 @@ class _Folded:
             # fragment-major copies of the shared per-point layers (the HIP chains)
             self.frag = {id(w): _frag(w) for w, _ in self.A + self.B_tail + [self.C_tail] + self.D_tail}
             # the wide pooled layers in split-bf16 form
-            self.wide = [self.A[2][0], self.B_tail[2][0], self.C_tail[0], self.D_tail[0][0]]
+            self.wide = [self.A[2][0], self.B_tail[2][0], self.C_tail[0], self.D_tail[0][0], self.D_tail[1][0]]
             self.frag6 = {id(w): _frag_x6(w) for w in self.wide}
             # the identity the TNet heads add (ndtnet.py:59), folded into fc3's bias
             self.t1["c3"] = self.t1["c3"] + torch.eye(3, device=dev).reshape(-1)
