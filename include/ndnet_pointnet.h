@@ -90,6 +90,9 @@ int ndnet_pn_fc_run(const float *in, int ld_in, const float *W, const float *bia
 int ndnet_pn_head3_run(const float *h2, int ld_h, const float *W3, const float *b3, const float *basis,
                        float *t1, float *w1f, int batch, int K, int kin, int nout, void *stream);
 int ndnet_pn_fold64_run(const float *t2, const float *rhs, float *out, int batch, int N, void *stream);
+/* The same fold in the split-bf16 layout (prec = 1 layers, K = 64): out6[b] =
+ * bf16 [N/16][2][3 planes][64 lanes][8] (3 * 64 * N bf16 per cloud). */
+int ndnet_pn_fold64_x6_run(const float *t2, const float *rhs, void *out6, int batch, int N, void *stream);
 
 #ifdef __cplusplus
 }

@@ -380,14 +380,15 @@ __device__ void plain_layer(const LayerCtx& C, int in, int pin, int out, int pou
   auto epi = [&](f32x4 (&a)[RB][NB], int c) {
     const int col0 = (c * CB + wc * NB) * 16;
     if (gmax) pool_cols<RB, NB>(a, C.bias, col0, C.relu, row0, rows_valid, gmax);
-    else if (out_planes) store_cols_planes<RB, NB>(a, C.bias, col0, C.relu, row0, out, pout + 4, col0);
+    else if (out_planes) store_cols_planes<RB, NB>(a, C.bias, col0, C.relu, row0, out, C.N + 8, col0);
     else store_cols<RB, NB>(a, C.bias, col0, C.relu, row0, out, pout, col0);
     zero_acc(a);
   };
   const int nchunk = C.N < CB * 16 ? 1 : C.N / (CB * 16);
-  if (C.prec) {  // input: three bf16 planes, pitch = width + 8 = pin + 4
-    const __bf16* abase6 = reinterpret_cast<const __bf16*>(g_smem + in) + (row0 + cl) * (pin + 4) + 8 * kq;
-    run_tiles_x6<RB, NB>(acc, C.w6, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase6, pin + 4, epi);
+  if (C.prec) {  // input: three bf16 planes of pitch K + 8 (the producer's N + 8)
+    const int pb = 32 * C.KG + 8;
+    const __bf16* abase6 = reinterpret_cast<const __bf16*>(g_smem + in) + (row0 + cl) * pb + 8 * kq;
+    run_tiles_x6<RB, NB>(acc, C.w6, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase6, pb, epi);
   } else {
     const float* abase = g_smem + in + (row0 + cl) * pin + 4 * kq;
     run_tiles<RB, NB>(acc, C.w, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase, pin, epi);
@@ -416,6 +417,7 @@ __device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin
   constexpr int PWC = kWaves / kRowBlocks, PNB = 4 / PWC;
   const int prow0 = (wave / PWC) * 16, pwc = (wave % PWC) * PNB;
   const float* ain = g_smem + in + (prow0 + cl) * pin + 4 * kq;
+  const __bf16* ain6 = reinterpret_cast<const __bf16*>(g_smem + in) + (prow0 + cl) * (32 * P.KG + 8) + 8 * kq;
   // Q: row group wave / WC, column group wave % WC
   const int qrow0 = (wave / WC) * RB * 16, qwc = wave % WC;
   const bool qidle = qwc * NB * 16 >= Q.N;
@@ -430,7 +432,8 @@ __device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin
       if (Q.prec) store_cols_planes<1, PNB>(a, P.bias, 64 * f + 16 * pwc, P.relu, prow0, fb, kFuseNC + 8, 16 * pwc);
       else store_cols<1, PNB>(a, P.bias, 64 * f + 16 * pwc, P.relu, prow0, fb, kFP, 16 * pwc);
     };
-    run_tiles<1, PNB>(acc1, P.w, P.KG, 0, P.KG, 4 * f + pwc, 0, 1, ain, pin, epi);
+    if (P.prec) run_tiles_x6<1, PNB>(acc1, P.w6, P.KG, 0, P.KG, 4 * f + pwc, 0, 1, ain6, 32 * P.KG + 8, epi);
+    else run_tiles<1, PNB>(acc1, P.w, P.KG, 0, P.KG, 4 * f + pwc, 0, 1, ain, pin, epi);
   };
   f32x4 acc2[RB][NB];
   zero_acc(acc2);
@@ -453,7 +456,7 @@ __device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin
   }
   if (qidle) return;
   if (gmax) pool_cols<RB, NB>(acc2, Q.bias, 16 * qwc * NB, Q.relu, qrow0, rows_valid, gmax);
-  else if (out_planes) store_cols_planes<RB, NB>(acc2, Q.bias, 16 * qwc * NB, Q.relu, qrow0, out, pout + 4, 16 * qwc * NB);
+  else if (out_planes) store_cols_planes<RB, NB>(acc2, Q.bias, 16 * qwc * NB, Q.relu, qrow0, out, Q.N + 8, 16 * qwc * NB);
   else store_cols<RB, NB>(acc2, Q.bias, 16 * qwc * NB, Q.relu, qrow0, out, pout, 16 * qwc * NB);
 }
 
@@ -646,6 +649,47 @@ __global__ void __launch_bounds__(256) k_pn_fold64(const float* __restrict__ t2,
     *reinterpret_cast<f32x4*>(o + frag_index(ti, j0 + tj + c, 4)) = f32x4{acc[0][c], acc[1][c], acc[2][c], acc[3][c]};
 }
 
+// The same fold written in the split-bf16 layout (K = 64: two 32-row
+// k-groups): out6[b] = [N/16][2][3 planes][64 lanes][8] bf16.
+__global__ void __launch_bounds__(256) k_pn_fold64_x6(const float* __restrict__ t2, const float* __restrict__ rhs,
+                                                      __bf16* __restrict__ out6, int N) {
+  __shared__ float s_a[64][65];
+  __shared__ float s_b[64][68];
+  const int b = blockIdx.y, j0 = blockIdx.x * 64;
+  const float* A = t2 + (int64_t)b * 4096;
+  for (int e = threadIdx.x; e < 4096; e += 256) {
+    s_a[e >> 6][e & 63] = A[e];
+    s_b[e >> 6][e & 63] = rhs[(int64_t)(e >> 6) * N + j0 + (e & 63)];
+  }
+  __syncthreads();
+  const int ti = (threadIdx.x >> 4) * 4, tj = (threadIdx.x & 15) * 4;
+  float acc[4][4] = {};
+  for (int k = 0; k < 64; k++) {
+    float av[4], bv[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) av[r] = s_a[ti + r][k];
+#pragma unroll
+    for (int c = 0; c < 4; c++) bv[c] = s_b[k][tj + c];
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+      for (int c = 0; c < 4; c++) acc[r][c] += av[r] * bv[c];
+  }
+  __bf16* o = out6 + (int64_t)b * 64 * N * 3;
+#pragma unroll
+  for (int r = 0; r < 4; r++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int k = ti + r, n = j0 + tj + c;
+      const int64_t e = ((((int64_t)(n >> 4) * 2 + (k >> 5)) * 3) * 64 + ((k >> 3) & 3) * 16 + (n & 15)) * 8 + (k & 7);
+      __bf16 h, m, l;
+      split3(acc[r][c], h, m, l);
+      o[e] = h;
+      o[e + 64 * 8] = m;
+      o[e + 2 * 64 * 8] = l;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -665,6 +709,12 @@ int ndnet_pn_head3_run(const float* h2, int ld_h, const float* W3, const float* 
       nout % 16)
     return -20;
   k_pn_head3<<<batch, 256, 0, (hipStream_t)stream>>>(h2, ld_h, W3, b3, basis, t1, w1f, K, kin, nout);
+  return hipGetLastError() == hipSuccess ? 0 : -21;
+}
+
+int ndnet_pn_fold64_x6_run(const float* t2, const float* rhs, void* out6, int batch, int N, void* stream) {
+  if (!t2 || !rhs || !out6 || batch <= 0 || N <= 0 || N % 64) return -20;
+  k_pn_fold64_x6<<<dim3(N / 64, batch), 256, 0, (hipStream_t)stream>>>(t2, rhs, (__bf16*)out6, N);
   return hipGetLastError() == hipSuccess ? 0 : -21;
 }
 
@@ -693,7 +743,7 @@ int ndnet_pn_chain_run(const ndnet_pn_chain* args, int batch, void* stream) {
     const bool fed = l > 0 && args->L[l - 1].fuse_next;
     if (L.prec != 0 && L.prec != 1) return -20;
     if (L.prec) {  // split-bf16: reads planes its producer writes (into a region, or the fused chunks)
-      if (l == 0 || L.fuse_next || L.K % 32 || args->L[l - 1].N != L.K) return -20;
+      if (l == 0 || L.K % 32 || args->L[l - 1].N != L.K) return -20;
       if (fed) qprec = 1;
       else planes |= 1 << (l & 1);
     }
@@ -724,9 +774,10 @@ int ndnet_pn_chain_run(const ndnet_pn_chain* args, int batch, void* stream) {
     int lf = 0;
     while (!args->L[lf].fuse_next) lf++;
     const int r = lf & 1, fb = fbuf_floats(qprec);
-    const int p_in = kP * ((r ? args->max_width2 : args->max_width) + 4);  // P's fp32 input (region pitch)
+    const int p_in = args->L[lf].prec ? 3 * kP * (args->L[lf].K + 8) / 2    // P's input: bf16 planes, pitch K + 8
+                                      : kP * ((r ? args->max_width2 : args->max_width) + 4);  // or fp32, region pitch
     const int inside = (r ? r0f : 0) + p_in;
-    if (!args->L[lf].prec && (r == 1 || inside + fb <= r0f)) fbuf_off = inside;
+    if (r == 1 || inside + fb <= r0f) fbuf_off = inside;
     total = fbuf_off + (size_t)fb > total ? fbuf_off + (size_t)fb : total;
   }
   const size_t lds = sizeof(float) * total;

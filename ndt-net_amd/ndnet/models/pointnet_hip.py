@@ -36,7 +36,8 @@ chain_timing = None
 
 # The three wide max-pooled layers (TNet(3) / TNet(64) conv3, NDTNet conv3:
 # 128 -> 1024 / 768, 90% of chains A-C's FLOPs) and the seg head's 512 -> 256
-# (fed chunk by chunk from the fused 64 -> 512) and 256 -> 128 run as split-bf16 "x6" GEMMs
+# (fed chunk by chunk from the fused 64 -> 512), the 64 -> 512 itself, 256 -> 128
+# and NDTNet's t2-folded conv2 run as split-bf16 "x6" GEMMs
 # (include/ndnet_pointnet.h prec = 1): fp32-accurate (operands split into three
 # bf16, six exact partial products accumulated in fp32) on the bf16 matrix
 # cores.  NDNET_PN_PRECISION=fp32 keeps every layer on the fp32 MFMA.
@@ -288,6 +289,8 @@ class _Workspace:
         # column blocks are outermost, so conv2's 8 blocks precede seg conv1a's 32
         self.w1f = torch.empty((B, 16 * 64), **f32)
         self.t2wf = torch.empty((B, 64 * 640), **f32)
+        # t2-folded conv2 / seg conv1a also in the split-bf16 layout ([cb][kg][plane][lane][8])
+        self.t2wf6 = torch.empty((B, 3 * 64 * 640), dtype=torch.bfloat16, device=dev) if SPLIT_BF16 else None
         self.specs = [  # torch emulation: (in_cols, [(W^T, bias)], relus, mode, kwargs)
             (3, W.A, (1, 1, 1), 0, dict(gmax=self.g1)),
             (12, [(self.w1T, W.c1b)] + W.B_tail, (0, 1, 1, 1), 0, dict(gmax=self.g2)),
@@ -304,8 +307,13 @@ class _Workspace:
             return (W.frag[id(w)], 0, b, w.shape[0], w.shape[1])
 
         L1 = (self.w1f, self.w1f.stride(0), W.c1b, 16, 64)
-        L2 = (self.t2wf, self.t2wf.stride(0), W.c2b, 64, 128)
-        Ls = (self.t2wf[:, 64 * 128:], self.t2wf.stride(0), self.cvec, 64, 512)
+        if SPLIT_BF16:  # per-cloud stride in floats (bf16 pairs); conv2's 8 column blocks come first
+            s6 = self.t2wf6.stride(0) // 2
+            L2 = (self.t2wf6, s6, W.c2b, 64, 128, 1)
+            Ls = (self.t2wf6[:, 8 * 2 * 3 * 64 * 8:], s6, self.cvec, 64, 512, 1)
+        else:
+            L2 = (self.t2wf, self.t2wf.stride(0), W.c2b, 64, 128)
+            Ls = (self.t2wf[:, 64 * 128:], self.t2wf.stride(0), self.cvec, 64, 512)
         self.hip_layers = [
             [shared(x) for x in W.A],
             [L1] + [shared(x) for x in W.B_tail],
@@ -383,9 +391,14 @@ def _glue_hip(W, ws, B: int):
         _fc(ws.g2, t["f1"], t["c1"], ws.h1, True)
         _fc(ws.h1, t["f2"], t["c2"], ws.h2, True)
         _fc(ws.h2, t["f3"], t["c3"], ws.t2, False)
-        rc = _lib.lib().ndnet_pn_fold64_run(ws.t2.data_ptr(), W.t2_rhs.data_ptr(), ws.t2wf.data_ptr(), B,
-                                            W.t2_rhs.shape[1], st())
-        _lib.check(rc, "ndnet_pn_fold64_run")
+        if ws.t2wf6 is not None:
+            rc = _lib.lib().ndnet_pn_fold64_x6_run(ws.t2.data_ptr(), W.t2_rhs.data_ptr(), ws.t2wf6.data_ptr(), B,
+                                                   W.t2_rhs.shape[1], st())
+            _lib.check(rc, "ndnet_pn_fold64_x6_run")
+        else:
+            rc = _lib.lib().ndnet_pn_fold64_run(ws.t2.data_ptr(), W.t2_rhs.data_ptr(), ws.t2wf.data_ptr(), B,
+                                                W.t2_rhs.shape[1], st())
+            _lib.check(rc, "ndnet_pn_fold64_run")
 
     def seg_bias():
         _fc(ws.g3[:, : W.F], W.s1g, W.s1b, ws.cvec, False)
