@@ -581,6 +581,64 @@ __device__ inline int64_t frag_index(int k, int n, int KG) {
   return ((int64_t)((n >> 4) * KG + (k >> 4)) * 64 + ((k >> 2) & 3) * 16 + (n & 15)) * 4 + (k & 3);
 }
 
+// The same GEMV with K split across the lanes of WPO waves (K = 256 WPO,
+// WPO = 2 or 4; at K = 256 the one-wave kernel above measured faster): every thread loads ONE float4 of the weight row and the
+// matching float4 of all B inputs up front -- a single memory round trip
+// per launch instead of one per K-chunk of 64 lanes -- then the partial sums
+// of the 16 clouds are reduced across the wave (shuffles) and the WPO waves
+// (LDS).  4 / WPO output channels per 256-thread workgroup.
+template <int WPO>
+__global__ void __launch_bounds__(256) k_pn_fc_split(const float* __restrict__ in, int ld_in,
+                                                     const float* __restrict__ W, const float* __restrict__ bias,
+                                                     float* __restrict__ out, int ld_out, int B, int N, int relu) {
+  constexpr int K = 256 * WPO, OPW = 4 / WPO;
+  __shared__ float s_part[4][16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int o = wave / WPO, wq = wave % WPO;  // output within the workgroup, K quarter of that output
+  const int n = blockIdx.x * OPW + o;
+  const int nn = n < N ? n : N - 1;
+  const int c4 = wq * 64 + lane;  // this thread's float4 of the row
+  const f32x4 wv = reinterpret_cast<const f32x4*>(W + (int64_t)nn * K)[c4];
+  f32x4 xv[16];
+#pragma unroll
+  for (int b = 0; b < 16; b++) xv[b] = reinterpret_cast<const f32x4*>(in + (int64_t)(b < B ? b : 0) * ld_in)[c4];
+  float acc[16];
+#pragma unroll
+  for (int b = 0; b < 16; b++) {
+    const f32x4 pr = xv[b] * wv;
+    acc[b] = (pr[0] + pr[1]) + (pr[2] + pr[3]);
+  }
+#pragma unroll
+  for (int b = 0; b < 16; b++)
+    for (int off = 32; off > 0; off >>= 1) acc[b] += __shfl_xor(acc[b], off, 64);
+  if (WPO > 1) {
+    if (lane < 16) {
+      float v = 0.0f;
+#pragma unroll
+      for (int b = 0; b < 16; b++) v = lane == b ? acc[b] : v;
+      s_part[wave][lane] = v;
+    }
+    __syncthreads();
+    if (wq != 0) return;
+    if (lane < 16) {
+      float v = 0.0f;
+#pragma unroll
+      for (int q = 0; q < WPO; q++) v += s_part[wave + q][lane];
+      acc[0] = v;
+    }
+  } else if (lane < 16) {
+    float v = 0.0f;
+#pragma unroll
+    for (int b = 0; b < 16; b++) v = lane == b ? acc[b] : v;
+    acc[0] = v;
+  }
+  if (lane < B && n < N) {
+    float v = acc[0] + bias[n];
+    if (relu) v = fmaxf(v, 0.0f);
+    out[(int64_t)lane * ld_out + n] = v;
+  }
+}
+
 // TNet(3) tail: t1[b] = fc3(h2[b]) (+ I, folded into the bias) and the t1
 // fold of conv1, W1'^T[b] = t1[b] (1 x 9) @ basis (9 x kin*nout), written
 // fragment-major with K padded to 16 (rows kin..15 zero).  One workgroup per cloud.
@@ -699,7 +757,12 @@ int ndnet_pn_fc_run(const float* in, int ld_in, const float* W, const float* bia
   if (!in || !W || !bias || !out || batch <= 0 || batch > 16 || K <= 0 || K % 4 || N <= 0 || ld_in % 4 ||
       ((uintptr_t)in | (uintptr_t)W) % 16)
     return -20;
-  k_pn_fc<<<(N + 3) / 4, 256, 0, (hipStream_t)stream>>>(in, ld_in, W, bias, out, ld_out, batch, K, N, relu);
+  hipStream_t st = (hipStream_t)stream;
+  switch (K % 256 == 0 && K <= 1024 ? K / 256 : 0) {
+    case 2: k_pn_fc_split<2><<<(N + 1) / 2, 256, 0, st>>>(in, ld_in, W, bias, out, ld_out, batch, N, relu); break;
+    case 4: k_pn_fc_split<4><<<N, 256, 0, st>>>(in, ld_in, W, bias, out, ld_out, batch, N, relu); break;
+    default: k_pn_fc<<<(N + 3) / 4, 256, 0, st>>>(in, ld_in, W, bias, out, ld_out, batch, K, N, relu);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -21;
 }
 
