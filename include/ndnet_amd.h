@@ -173,6 +173,9 @@ int ndnet_ndt_debug_kl_marks(void *plan, unsigned long long *marks);
  * 20 accepted, 21 dense ids, 22 point NDs, 23/24 offsets barrier in/out,
  * 25 offsets, 26 scattered; synchronises. */
 int ndnet_ndt_debug_front_marks(void *plan, unsigned long long *marks);
+/* Start / end stamps (s_memrealtime) of every k_front workgroup of the last
+ * run at timing level 2: marks[B][G][2]; *G = workgroups per cloud. */
+int ndnet_ndt_debug_front_wg_marks(void *plan, unsigned long long *marks, int *G);
 
 /* k_welford stamps of the last run at timing level 2: per cloud and
  * workgroup (16 NDs) 4 marks -- start, points staged, samples folded, end --

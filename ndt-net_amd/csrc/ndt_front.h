@@ -55,6 +55,7 @@ constexpr int kFrontTable = 8192;   // LDS words: byte map of a small grid (3276
 constexpr int kFrontPhases = 40;    // record slots per cloud and run
 constexpr int kRecWords = 16;       // per-workgroup record: [0] count, [1] any bad, [2..9] first bad per worker
 constexpr int kPhDenseLarge = 36;
+constexpr int kFrontMarkStride = 32 + 2 * 256;  // per cloud: 32 phase stamps of WG 0, then start/end of WG g < 256
 constexpr int kBarStride = 16;      // u32 between the barrier counters of two clouds (64 B)
 constexpr int kNdtErrSync = -22;    // NDNET_ERR_SYNC
 static_assert(kFrontTable * 4 >= kBitsCap, "the byte map holds a whole small grid");
@@ -258,9 +259,15 @@ __device__ inline void front_point(const T* p, uint64_t i, T& x, T& y, T& z) {
 }
 
 // phase stamp (s_memrealtime, 100 MHz) of workgroup 0 of the cloud
-#define FRONT_MARK(i)                                                                                     \
-  do {                                                                                                    \
-    if (A.marks && g == 0 && t == 0) A.marks[(uint64_t)b * 32 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+#define FRONT_MARK(i)                                                                                  \
+  do {                                                                                                 \
+    if (A.marks && g == 0 && t == 0)                                                                   \
+      A.marks[(uint64_t)b * kFrontMarkStride + (i)] = __builtin_amdgcn_s_memrealtime();               \
+  } while (0)
+#define FRONT_WG_MARK(e)                                                                               \
+  do {                                                                                                 \
+    if (A.marks && t == 0 && g < 256)                                                                  \
+      A.marks[(uint64_t)b * kFrontMarkStride + 32 + 2 * g + (e)] = __builtin_amdgcn_s_memrealtime();  \
   } while (0)
 
 template <typename T>
@@ -285,6 +292,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
   const uint64_t bin0 = (uint64_t)g * bpw;
   const uint32_t epoch = c.epoch;
   FRONT_MARK(0);
+  FRONT_WG_MARK(0);
 
   if (t == 0) {
     s.sync_no = 0;
@@ -805,6 +813,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
     }
     FRONT_MARK(26);
   }
+  FRONT_WG_MARK(1);
   return;
 fail:
   if (t == 0) {

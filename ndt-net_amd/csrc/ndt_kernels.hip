@@ -155,7 +155,7 @@ struct Plan {
   uint32_t* frec;            // [B][kFrontPhases][fG][kRecWords]
   uint32_t* fwgcnt;          // [B][fG][ndcap]
   uint32_t* fbar;            // [B][kBarStride]
-  unsigned long long* fmarks; // [B][32] k_front phase stamps (timing level 2)
+  unsigned long long* fmarks; // [B][kFrontMarkStride]: k_front phase stamps of WG 0 + start/end of every WG (timing level 2)
   unsigned long long* wmarks; // [B][wg][4] k_welford stamps (timing level 2)
   uint32_t wgrid;             // k_welford workgroups: min(CUs, group capacity of the batch)
 };
@@ -2220,8 +2220,8 @@ int ndnet_ndt_set_timing(void* plan, int enable) {
     HIPCHK(hipMemset(P->wmarks, 0, nw * sizeof(unsigned long long)));
   }
   if (enable >= 2 && !P->fmarks) {
-    HIPCHK(hipMalloc(&P->fmarks, (size_t)P->B * 32 * sizeof(unsigned long long)));
-    HIPCHK(hipMemset(P->fmarks, 0, (size_t)P->B * 32 * sizeof(unsigned long long)));
+    HIPCHK(hipMalloc(&P->fmarks, (size_t)P->B * kFrontMarkStride * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(P->fmarks, 0, (size_t)P->B * kFrontMarkStride * sizeof(unsigned long long)));
   }
   if (enable >= 2 && !P->kl_marks) {
     HIPCHK(hipMalloc(&P->kl_marks, (size_t)P->B * 16 * sizeof(unsigned long long)));
@@ -2285,7 +2285,19 @@ int ndnet_ndt_debug_front_marks(void* plan, unsigned long long* marks) {
   Plan* P = (Plan*)plan;
   if (!P || !marks || !P->fmarks) return NDNET_ERR_ARG;
   HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpy(marks, P->fmarks, (size_t)P->B * 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy2D(marks, 32 * sizeof(unsigned long long), P->fmarks, kFrontMarkStride * sizeof(unsigned long long),
+                     32 * sizeof(unsigned long long), P->B, hipMemcpyDeviceToHost));
+  return NDNET_OK;
+}
+
+int ndnet_ndt_debug_front_wg_marks(void* plan, unsigned long long* marks, int* G) {
+  Plan* P = (Plan*)plan;
+  if (!P || !marks || !G || !P->fmarks) return NDNET_ERR_ARG;
+  HIPCHK(hipDeviceSynchronize());
+  *G = (int)P->fG;
+  HIPCHK(hipMemcpy2D(marks, 2 * P->fG * sizeof(unsigned long long),
+                     P->fmarks + 32, kFrontMarkStride * sizeof(unsigned long long),
+                     2 * P->fG * sizeof(unsigned long long), P->B, hipMemcpyDeviceToHost));
   return NDNET_OK;
 }
 

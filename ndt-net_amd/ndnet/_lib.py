@@ -73,6 +73,7 @@ EXPORTS = {
     "ndnet_ndt_debug_set_epoch": (_I, [_P, ctypes.c_uint32]),
     "ndnet_ndt_debug_kl_marks": (_I, [_P, _P]),
     "ndnet_ndt_debug_front_marks": (_I, [_P, _P]),
+    "ndnet_ndt_debug_front_wg_marks": (_I, [_P, _P, ctypes.POINTER(_I)]),
     "ndnet_ndt_debug_welford_marks": (_I, [_P, _P]),
     "ndnet_ndt_set_timing": (_I, [_P, _I]),
     "ndnet_ndt_stage_ms": (_I, [_P, _P]),

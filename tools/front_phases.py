@@ -5,6 +5,7 @@ binning) from workgroup 0's s_memrealtime stamps (timing level 2).
     python tools/front_phases.py [--batch 16 --points 100000 --nds 1000 --kind U]
 """
 import argparse
+import ctypes
 import os
 import sys
 
@@ -45,8 +46,16 @@ for _ in range(a.reps):
     valid = m > 0
     rel = (m - m[:, :1]) * 0.01  # 100 MHz ticks -> us
     acc += np.where(valid, rel, np.nan).mean(axis=0)
+G = ctypes.c_int(0)
+wgm = np.zeros(a.batch * 256 * 2, np.uint64)
+_lib.check(_lib.lib().ndnet_ndt_debug_front_wg_marks(plan.handle, wgm.ctypes.data, ctypes.byref(G)), "wg_marks")
 _lib.lib().ndnet_ndt_set_timing(plan.handle, 0)
 acc /= a.reps
+wg = wgm[: a.batch * G.value * 2].reshape(a.batch * G.value, 2).astype(np.float64)
+t0 = wg[:, 0].min()
+print(f"k_front workgroups ({a.batch} x {G.value}, last run): start skew {(wg[:, 0].max() - t0) * 0.01:.2f} us, "
+      f"first end {(wg[:, 1].min() - t0) * 0.01:.2f} us, last end {(wg[:, 1].max() - t0) * 0.01:.2f} us "
+      f"(from the first workgroup's start)")
 prev = 0.0
 for i in sorted(names, key=lambda i: acc[i] if np.isfinite(acc[i]) else 1e9):
     if np.isfinite(acc[i]):
