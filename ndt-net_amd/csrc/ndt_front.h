@@ -703,24 +703,28 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
 
     // ---- per rank bin (one wave): stable rank of each point among its ND's
     //      points in the bin, in index order; the bin's ND counts ----
+    // Lanes holding the same ND are found by matching the ND id bit by bit
+    // with ballots (no sort): a lane's rank is the number of lower lanes in
+    // its match set, and the set's last lane advances the ND's bin counter.
+    const uint32_t nbits = 32u - (uint32_t)__clz((int)(ndcap > 1 ? ndcap - 1 : 1));
+    const unsigned long long below = (1ull << lane) - 1ull;
     for (uint32_t r = wave; r < nrb; r += kFrontWaves) {
       uint32_t* hr = hist + (uint64_t)r * ndcap;
       uint32_t* br = binfo + (uint64_t)r * rbs;
       for (uint32_t st = 0; st < rbs / 64; st++) {
         const uint32_t d = br[st * 64 + lane];
-        const uint32_t sk = wave_sort64(d == kInvalid ? kInvalid : (d << 6) | lane);
-        const uint32_t sd = sk == kInvalid ? kInvalid : sk >> 6;
-        const uint32_t prev = (uint32_t)__builtin_amdgcn_mov_dpp((int)sd, 0x138, 0xF, 0xF, false);  // wave_shr:1
-        const bool head = lane == 0 || prev != sd;
-        const unsigned long long H = __ballot(head);
-        const unsigned long long upto = (2ull << lane) - 1ull;  // lanes 0..lane (all for lane 63)
-        const uint32_t start = 63u - (uint32_t)__clzll(H & upto);
-        const unsigned long long after = H & ~upto;
-        const uint32_t next = after ? (uint32_t)__ffsll((long long)after) - 1u : 64u;
-        if (sd != kInvalid) {
-          const uint32_t cur = hr[sd];  // same address for the whole run: a broadcast read
-          br[st * 64 + (sk & 63)] = (sd << 10) | (cur + lane - start);
-          if (lane + 1 == next) hr[sd] = cur + next - start;
+        const bool valid = d != kInvalid;
+        unsigned long long m = __ballot(valid);
+        for (uint32_t bit = 0; bit < nbits; bit++) {
+          const bool on = (d >> bit) & 1u;
+          const unsigned long long bb = __ballot(on);
+          m &= on ? bb : ~bb;
+        }
+        if (valid) {
+          const uint32_t rank = (uint32_t)__popcll(m & below), cnt = (uint32_t)__popcll(m);
+          const uint32_t cur = hr[d];  // read by every lane of the set before its last lane writes
+          br[st * 64 + lane] = (d << 10) | (cur + rank);
+          if (rank + 1 == cnt) hr[d] = cur + cnt;
         }
       }
     }
