@@ -229,28 +229,6 @@ __device__ inline uint32_t stamp_key_front(uint32_t key, uint32_t* table, uint32
   return atomicExch(sp, stamp) != stamp;
 }
 
-// 64 keys sorted ascending across the wave (bitonic network in registers).
-__device__ inline uint32_t wave_sort64(uint32_t key) {
-  const uint32_t lane = threadIdx.x & 63;
-#define NDNET_BITONIC(SIZE, STRIDE)                                             \
-  {                                                                             \
-    const uint32_t o = xor_lane<STRIDE>(key);                                   \
-    const bool up = (SIZE) == 64 || (lane & (SIZE)) == 0;                       \
-    const bool lower = (lane & (STRIDE)) == 0;                                  \
-    const uint32_t mn = key < o ? key : o, mx = key < o ? o : key;              \
-    key = (lower == up) ? mn : mx;                                              \
-  }
-  NDNET_BITONIC(2, 1)
-  NDNET_BITONIC(4, 2) NDNET_BITONIC(4, 1)
-  NDNET_BITONIC(8, 4) NDNET_BITONIC(8, 2) NDNET_BITONIC(8, 1)
-  NDNET_BITONIC(16, 8) NDNET_BITONIC(16, 4) NDNET_BITONIC(16, 2) NDNET_BITONIC(16, 1)
-  NDNET_BITONIC(32, 16) NDNET_BITONIC(32, 8) NDNET_BITONIC(32, 4) NDNET_BITONIC(32, 2) NDNET_BITONIC(32, 1)
-  NDNET_BITONIC(64, 32) NDNET_BITONIC(64, 16) NDNET_BITONIC(64, 8) NDNET_BITONIC(64, 4) NDNET_BITONIC(64, 2)
-  NDNET_BITONIC(64, 1)
-#undef NDNET_BITONIC
-  return key;
-}
-
 template <typename T>
 __device__ inline void front_point(const T* p, uint64_t i, T& x, T& y, T& z) {
   x = p[3 * i + 0];
