@@ -37,8 +37,8 @@
 //         (normal_distributions.c NDs are allocated per linear index); each
 //         workgroup writes its slice of dense_of / vox.
 //   bins  per point its ND; per bin a stable rank of the point among the
-//         bin's points of the same ND (one wave per bin: 64-key bitonic sort
-//         in registers, runs, an LDS cursor per ND); per-workgroup ND counts
+//         bin's points of the same ND (one wave per bin: ballot matching of
+//         the ND ids bit by bit, an LDS cursor per ND); per-workgroup ND counts
 //         -> [B][G][ndcap], barrier, ND bases (scan over NDs) + the counts of
 //         earlier workgroups and bins, and every point written to its ND's
 //         contiguous run in index order -- the order the reference's
