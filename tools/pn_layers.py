@@ -62,3 +62,19 @@ out = torch.empty(B, n, 29, device=dev)
 flops = 2.0 * B * n * (64 * 512 + 512 * 256)
 us = time_chain([layer(16, 64), layer(64, 512), layer(512, 256)], (1, 1, 1), 0, gmax=gmax, fuse=(1,)) - base[64]
 print(f"  64 -> 512 -> 256 fused (minus producer) {us:7.1f} us  {flops / (us * 1e-6) / 1e12:6.1f} TFLOP/s")
+
+
+# split-bf16 (prec 1) layers: bf16-MFMA utilisation (6 bf16 products per fp32 FLOP)
+def layer_x6(K, N):
+    w = torch.randn(K, N, device=dev) * 0.05
+    return (ph._frag_x6(w), 0, torch.zeros(N, device=dev), K, N, 1)
+
+
+BF16_PEAK = 2.5e15
+for K, N in [(128, 1024), (128, 768), (128, 512), (128, 256), (64, 1024), (256, 1024)]:
+    flops = 2.0 * B * n * K * N
+    if K not in base:
+        base[K] = time_chain([layer(16, K)], (1,), 0, gmax=gmax)
+    us = time_chain([layer(16, K), layer_x6(K, N)], (1, 1), 0, gmax=gmax) - base[K]
+    print(f"x6 {K:4d} -> {N:4d} (max-pool, minus producer) {us:7.1f} us  {flops / (us * 1e-6) / 1e12:6.1f} TFLOP/s fp32-eq,"
+          f" bf16 MFMA {6 * flops / (us * 1e-6) / BF16_PEAK * 100:5.1f}% of peak   (producer {base[K]:.1f} us)")
