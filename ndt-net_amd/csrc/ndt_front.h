@@ -409,7 +409,9 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
     }
     if (t < (uint32_t)kWorkers) s_bad[t] = kInvalid;
     __syncthreads();
+#ifndef NDNET_FRONT_BINMARKS
     if (s.iter == 1) FRONT_MARK(27);
+#endif
     const double vs = s.guess, inv_vs = 1.0 / vs;
     double off[3] = {s.off[0], s.off[1], s.off[2]};
     uint32_t len[3] = {s.len[0], s.len[1], s.len[2]};
@@ -476,7 +478,9 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
       }
     }
     __syncthreads();
+#ifndef NDNET_FRONT_BINMARKS
     if (s.iter == 1) FRONT_MARK(28);
+#endif
     if (small) {  // byte map -> 32-voxel words, OR'd into the pass's global bitmap
       for (uint32_t w = t; w < words; w += kFrontThreads) {
         uint32_t bits = 0;
@@ -492,9 +496,13 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
       uint32_t* gn = A.gbits + ((uint64_t)b * 2 + (parity ^ 1u)) * kBitsWords;
       for (uint32_t w = g * kFrontThreads + t; w < (uint32_t)kBitsWords; w += G * kFrontThreads) st_sc1(gn + w, 0u);
     }
+#ifndef NDNET_FRONT_BINMARKS
     if (s.iter == 1) FRONT_MARK(29);
+#endif
     fresh = block_sum_u32(fresh, scratch);
+#ifndef NDNET_FRONT_BINMARKS
     if (s.iter == 1) FRONT_MARK(30);
+#endif
     uint32_t* rec = A.rec + (((uint64_t)b * kFrontPhases + 1 + 2 * s.iter) * G) * kRecWords;
     uint32_t anyb = 0;
     for (int w = 0; w < kWorkers; w++) anyb |= s_bad[w] != kInvalid;
@@ -508,7 +516,9 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
     FRONT_MARK(4 + 2 * (s.iter < 7 ? s.iter : 7));
     if (t < (uint32_t)kWorkers) s.cut[t] = kInvalid;
     __syncthreads();
+#ifndef NDNET_FRONT_BINMARKS
     if (s.iter == 1) FRONT_MARK(31);
+#endif
     uint32_t mode = small ? parity : 2u;
     if (s.anybad) {
       // a point out of the grid abandoned the rest of its worker chunk
@@ -706,7 +716,13 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
         }
       }
     }
+#ifdef NDNET_FRONT_BINMARKS
+    FRONT_MARK(27);
+#endif
     __syncthreads();
+#ifdef NDNET_FRONT_BINMARKS
+    FRONT_MARK(28);
+#endif
     // per ND: my workgroup's count -> wgcnt; hist[r][d] -> exclusive prefix over my rank bins
     uint32_t* wg = A.wgcnt + (uint64_t)b * G * ndcap;
     for (uint32_t d = t; d < nd; d += kFrontThreads) {
