@@ -694,7 +694,10 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
     // Lanes holding the same ND are found by matching the ND id bit by bit
     // with ballots (no sort): a lane's rank is the number of lower lanes in
     // its match set, and the set's last lane advances the ND's bin counter.
-    const uint32_t nbits = 32u - (uint32_t)__clz((int)(ndcap > 1 ? ndcap - 1 : 1));
+    // nbits is uniform (readfirstlane) so the unrolled bit loop branches on
+    // SGPRs; per bit: a 1-bit signed extract (0 / -1), its ballot, and
+    // m &= ~(ballot ^ mask) on both halves -- the lanes that agree on the bit.
+    const uint32_t nbits = __builtin_amdgcn_readfirstlane(32u - (uint32_t)__clz((int)(ndcap > 1 ? ndcap - 1 : 1)));
     const unsigned long long below = (1ull << lane) - 1ull;
     for (uint32_t r = wave; r < nrb; r += kFrontWaves) {
       uint32_t* hr = hist + (uint64_t)r * ndcap;
@@ -702,12 +705,18 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
       for (uint32_t st = 0; st < rbs / 64; st++) {
         const uint32_t d = br[st * 64 + lane];
         const bool valid = d != kInvalid;
-        unsigned long long m = __ballot(valid);
-        for (uint32_t bit = 0; bit < nbits; bit++) {
-          const bool on = (d >> bit) & 1u;
-          const unsigned long long bb = __ballot(on);
-          m &= on ? bb : ~bb;
+        const unsigned long long mv = __ballot(valid);
+        uint32_t mlo = (uint32_t)mv, mhi = (uint32_t)(mv >> 32);
+#pragma unroll
+        for (uint32_t bit = 0; bit < 15; bit++) {  // ndcap <= 16384 (k_front host check)
+          if (bit < nbits) {
+            const uint32_t mask = (uint32_t)__builtin_amdgcn_sbfe((int)d, bit, 1);
+            const unsigned long long bb = __ballot(mask != 0u);
+            mlo &= ~((uint32_t)bb ^ mask);
+            mhi &= ~((uint32_t)(bb >> 32) ^ mask);
+          }
         }
+        const unsigned long long m = ((unsigned long long)mhi << 32) | mlo;
         if (valid) {
           const uint32_t rank = (uint32_t)__popcll(m & below), cnt = (uint32_t)__popcll(m);
           const uint32_t cur = hr[d];  // read by every lane of the set before its last lane writes
@@ -726,8 +735,18 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
     // per ND: my workgroup's count -> wgcnt; hist[r][d] -> exclusive prefix over my rank bins
     uint32_t* wg = A.wgcnt + (uint64_t)b * G * ndcap;
     for (uint32_t d = t; d < nd; d += kFrontThreads) {
-      uint32_t run = 0;
-      for (uint32_t r = 0; r < nrb; r++) {
+      uint32_t run = 0, r = 0;
+      for (; r + 4 <= nrb; r += 4) {  // four rank bins per LDS round trip
+        uint32_t x[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) x[q] = hist[(uint64_t)(r + q) * ndcap + d];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          hist[(uint64_t)(r + q) * ndcap + d] = run;
+          run += x[q];
+        }
+      }
+      for (; r < nrb; r++) {
         const uint32_t x = hist[(uint64_t)r * ndcap + d];
         hist[(uint64_t)r * ndcap + d] = run;
         run += x;
@@ -744,20 +763,27 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
       uint32_t tot_d = 0, pre = 0;
       if (d < nd) {
         uint32_t gg = 0;
-        for (; gg + 4 <= G; gg += 4) {
-          uint32_t x[4];
+        for (; gg + 16 <= G; gg += 16) {  // 16 loads in flight: one memory round trip for G <= 16
+          uint32_t x[16];
 #pragma unroll
-          for (int q = 0; q < 4; q++) x[q] = ld_sc1(wg + (uint64_t)(gg + q) * ndcap + d);
+          for (int q = 0; q < 16; q++) x[q] = ld_sc1(wg + (uint64_t)(gg + q) * ndcap + d);
 #pragma unroll
-          for (int q = 0; q < 4; q++) {
+          for (int q = 0; q < 16; q++) {
             if (gg + q < g) pre += x[q];
             tot_d += x[q];
           }
         }
-        for (; gg < G; gg++) {
-          const uint32_t x = ld_sc1(wg + (uint64_t)gg * ndcap + d);
-          if (gg < g) pre += x;
-          tot_d += x;
+        if (gg < G) {  // the rest, loads clamped to workgroup G - 1 and masked
+          uint32_t x[16];
+#pragma unroll
+          for (int q = 0; q < 16; q++) x[q] = ld_sc1(wg + (uint64_t)(gg + q < G ? gg + q : G - 1) * ndcap + d);
+#pragma unroll
+          for (int q = 0; q < 16; q++) {
+            if (gg + q < G) {
+              if (gg + q < g) pre += x[q];
+              tot_d += x[q];
+            }
+          }
         }
       }
       uint32_t tot;
@@ -767,7 +793,17 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
           A.nd_n[(uint64_t)b * ndcap + d] = tot_d;
           A.nd_base[(uint64_t)b * ndcap + d] = start;
         }
-        for (uint32_t r = 0; r < nrb; r++) hist[(uint64_t)r * ndcap + d] += start + pre;
+        // four rank bins per LDS round trip (loads, then stores)
+        const uint32_t add = start + pre;
+        uint32_t r = 0;
+        for (; r + 4 <= nrb; r += 4) {
+          uint32_t x[4];
+#pragma unroll
+          for (int q = 0; q < 4; q++) x[q] = hist[(uint64_t)(r + q) * ndcap + d];
+#pragma unroll
+          for (int q = 0; q < 4; q++) hist[(uint64_t)(r + q) * ndcap + d] = x[q] + add;
+        }
+        for (; r < nrb; r++) hist[(uint64_t)r * ndcap + d] += add;
       }
       carry += tot;
     }
