@@ -1631,38 +1631,68 @@ __global__ void __launch_bounds__(kChunk) k_kl_nan_keys(KLArgs A) {
 }
 
 // #entries of a sorted, ~0-padded kChunk-key run ahead of x: keys <= x (le)
-// or keys < x; four runs searched together (eight halving probes each).
-template <typename KP>
-__device__ inline void count_before4(KP K, const uint32_t (&run)[4], unsigned long long x, const bool (&le)[4],
-                                     uint32_t (&base)[4]) {
+// or keys < x; Q runs searched together (eight halving probes each), so a
+// lane has Q independent LDS reads in flight per probe round.  "k <= x" is
+// "k < x + 1" (x + 1 saturating: ~0 is padding, never a score key), so a probe
+// is one read at a constant offset from the run cursor, one 64-bit compare
+// and a conditional cursor step.
+template <int Q, typename KP>
+__device__ inline void count_before_q(KP K, const uint32_t (&run)[Q], unsigned long long x, const bool (&le)[Q],
+                                      uint32_t (&base)[Q]) {
+  KP cur[Q];
+  unsigned long long xq[Q];
 #pragma unroll
-  for (int q = 0; q < 4; q++) base[q] = 0;
+  for (int q = 0; q < Q; q++) {
+    cur[q] = K + run[q] * kChunk;
+    xq[q] = le[q] && x != ~0ull ? x + 1 : x;
+  }
 #pragma unroll
   for (uint32_t half = kChunk / 2; half >= 1; half >>= 1) {
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const unsigned long long k = K[run[q] * kChunk + base[q] + half - 1];
-      base[q] += (le[q] ? k <= x : k < x) ? half : 0u;
-    }
+    for (int q = 0; q < Q; q++) cur[q] += cur[q][half - 1] < xq[q] ? half : 0u;
   }
 #pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const unsigned long long k = K[run[q] * kChunk + base[q]];
-    base[q] += (le[q] ? k <= x : k < x) ? 1u : 0u;
-  }
+  for (int q = 0; q < Q; q++) base[q] = (uint32_t)(cur[q] - (K + run[q] * kChunk)) + (cur[q][0] < xq[q] ? 1u : 0u);
 }
 
-// #entries of the sorted K[lo, hi) with key <= x (le) or < x.
-template <typename KP>
-__device__ inline uint32_t count_sorted(KP K, uint32_t lo, uint32_t hi, unsigned long long x, bool le) {
-  const uint32_t lo0 = lo;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    const unsigned long long k = K[mid];
-    if (le ? k <= x : k < x) lo = mid + 1;
-    else hi = mid;
+// The three NaN-run counts of a score event x (slot s) interleaved, one probe
+// of each per round: NaN keys of the earlier chunks <= x, of its own chunk
+// before (x, s), of the later chunks < x.  N: the cloud's NaN keys in slot
+// order [0, total); own chunk's at [nb0, nb0 + nn), slots S[0, nn).
+// Branch-free halving (the range lengths, hence the rounds, are the same for
+// every lane of the wave): b moves to b + h where the probe is still ahead of
+// x; the count is b - lo + [N[b] ahead of x].
+template <typename KP, typename SP>
+__device__ inline uint32_t count_nan3(KP N, SP S, uint32_t nb0, uint32_t nn, uint32_t total, unsigned long long x,
+                                      uint32_t s) {
+  const unsigned long long x1 = x != ~0ull ? x + 1 : x;  // k <= x as k < x1
+  auto ahead1 = [&](uint32_t i) {
+    const unsigned long long k = N[i];
+    return k < x || (k == x && S[i - nb0] < s);
+  };
+  uint32_t n0 = nb0, n1 = nn, n2 = total - nb0 - nn;
+  uint32_t b0 = 0, b1 = nb0, b2 = nb0 + nn;
+  while (n0 > 1 || n1 > 1 || n2 > 1) {
+    if (n0 > 1) {
+      const uint32_t h = n0 >> 1;
+      b0 += N[b0 + h] < x1 ? h : 0u;
+      n0 -= h;
+    }
+    if (n1 > 1) {
+      const uint32_t h = n1 >> 1;
+      b1 += ahead1(b1 + h) ? h : 0u;
+      n1 -= h;
+    }
+    if (n2 > 1) {
+      const uint32_t h = n2 >> 1;
+      b2 += N[b2 + h] < x ? h : 0u;
+      n2 -= h;
+    }
   }
-  return lo - lo0;
+  const uint32_t c0 = n0 ? b0 + (N[b0] < x1 ? 1u : 0u) : 0u;
+  const uint32_t c1 = n1 ? b1 - nb0 + (ahead1(b1) ? 1u : 0u) : 0u;
+  const uint32_t c2 = n2 ? b2 - nb0 - nn + (N[b2] < x ? 1u : 0u) : 0u;
+  return c0 + c1 + c2;
 }
 
 // #entries (K[i], S[i]), i < n, preceding (x, s) (keys and slots both sorted).
@@ -1678,6 +1708,10 @@ __device__ inline uint32_t count_composite(KP K, SP S, uint32_t n, unsigned long
   return lo;
 }
 
+#ifndef NDNET_MERGE_Q
+#define NDNET_MERGE_Q 8
+#endif
+constexpr int kMergeQ = NDNET_MERGE_Q;  // other runs searched together per probe round
 constexpr int kMergeRuns = 2;  // chunks merged per k_kl_merge workgroup (512 threads; ~one workgroup per CU at B = 16)
 
 template <bool kLds>
@@ -1691,6 +1725,11 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
   const uint32_t tid = threadIdx.x;
   const uint32_t lc = tid / kChunk, t = tid % kChunk;
   const uint32_t ch = blockIdx.x * kMergeRuns + lc;
+#define MERGE_MARK(i)                                                                              \
+  do {                                                                                             \
+    if (A.marks && blockIdx.x == 0 && tid == 0) A.marks[(uint64_t)b * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+  MERGE_MARK(12);
   extern __shared__ __attribute__((aligned(16))) unsigned long long dynk[];
   __shared__ uint32_t s_cnt[kMaxChunks];
   __shared__ uint32_t s_nb[kMaxChunks + 1];
@@ -1745,6 +1784,7 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
     }
   }
   __syncthreads();
+  MERGE_MARK(13);
   if (ch >= nch) return;
   const bool is_num = t < nnum;
   if (!is_num && t >= nnum + nnan) return;
@@ -1760,9 +1800,7 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
       pos = t;
       // NaN events ahead: earlier chunks (key <= x), this chunk (composite), later chunks (key < x)
       if (nnan_tot) {
-        pos += count_sorted(N, 0, nb0, x, true);
-        pos += count_composite(N + nb0, own_nan_slot, nnan, x, sl);
-        pos += count_sorted(N, nb0 + nnan, nnan_tot, x, false);
+        pos += count_nan3(N, own_nan_slot, nb0, nnan, nnan_tot, x, sl);
       }
     } else {
       const uint32_t j = t - nnum;
@@ -1771,19 +1809,19 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
       // scores of its own chunk ahead of it, then every earlier NaN
       pos = count_composite(K + ch * kChunk, own_num_slot, nnum, x, sl) + nb0 + j;
     }
-    // scores of the other chunks ahead of it, four runs per pass
-    for (uint32_t c0 = 0; c0 < nch; c0 += 4) {
-      uint32_t run[4], add[4];
-      bool le[4];
+    // scores of the other chunks ahead of it, kMergeQ runs per pass
+    for (uint32_t c0 = 0; c0 < nch; c0 += kMergeQ) {
+      uint32_t run[kMergeQ], add[kMergeQ];
+      bool le[kMergeQ];
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
+      for (int q = 0; q < kMergeQ; q++) {
         const uint32_t c2 = c0 + q;
         run[q] = (c2 < nch && c2 != ch) ? c2 : ch;  // own run: masked below
         le[q] = c2 < ch;
       }
-      count_before4(K, run, x, le, add);
+      count_before_q<kMergeQ>(K, run, x, le, add);
 #pragma unroll
-      for (int q = 0; q < 4; q++)
+      for (int q = 0; q < kMergeQ; q++)
         if (c0 + q < nch && c0 + q != ch) pos += add[q];
     }
     A.ord_val_all[eb + pos] = A.slot_val_all[eb + sl];
@@ -1792,6 +1830,8 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
   };
   if (kLds) body(static_cast<const unsigned long long*>(lK), static_cast<const unsigned long long*>(lN));
   else body(gK, gN);
+  MERGE_MARK(14);
+#undef MERGE_MARK
 }
 
 // Prune and output rows: one workgroup per cloud.

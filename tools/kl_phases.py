@@ -36,15 +36,21 @@ pts = torch.from_numpy(make_batch(a.kind, a.batch, a.points, seed0=0)).to(dev)
 ndt_preprocessing(a.nds, pts)
 plan = get_plan(a.batch, a.points, a.nds, -1, dev)
 _lib.check(_lib.lib().ndnet_ndt_set_timing(plan.handle, 2), "set_timing")
+# k_kl_merge, workgroup 0 of each cloud (marks 12-14): staging, searches; then the gap to k_kl
+MPHASES = [(12, 13, "merge: stage runs"), (13, 14, "merge: searches+writes"), (14, 0, "merge end -> k_kl start")]
 acc = np.zeros(len(PHASES))
+macc = np.zeros(len(MPHASES))
 for _ in range(a.reps):
     ndt_preprocessing(a.nds, pts)
     m = np.zeros(a.batch * 16, np.uint64)
     _lib.check(_lib.lib().ndnet_ndt_debug_kl_marks(plan.handle, m.ctypes.data), "kl_marks")
     m = m.reshape(a.batch, 16).astype(np.float64)
     acc += np.array([((m[:, j] - m[:, i]) * 0.01).mean() for i, j, _ in PHASES])  # 100 MHz ticks -> us
+    macc += np.array([((m[:, j] - m[:, i]) * 0.01).mean() for i, j, _ in MPHASES])
 _lib.lib().ndnet_ndt_set_timing(plan.handle, 0)
 acc /= a.reps
 for (_, _, nm), v in zip(PHASES, acc):
     print(f"  {nm:20s} {v:8.2f} us")
 print(f"  {'total':20s} {acc.sum():8.2f} us (mean over clouds)")
+for (_, _, nm), v in zip(MPHASES, macc / a.reps):
+    print(f"  {nm:24s} {v:8.2f} us")
