@@ -1552,7 +1552,7 @@ __global__ void __launch_bounds__(kChunk) k_kl_rank_chunks(KLArgs A) {
   const bool isn = f && v != v;
   const bool num = f && !isn;
   const unsigned long long key = num ? score_key(v) : ~0ull;
-  __shared__ unsigned long long s_key[kChunk];
+  __shared__ __attribute__((aligned(16))) unsigned long long s_key[kChunk];
   __shared__ double s_f64[16];
   __shared__ uint32_t s_u32[16];
   s_key[t] = key;
@@ -1563,12 +1563,26 @@ __global__ void __launch_bounds__(kChunk) k_kl_rank_chunks(KLArgs A) {
   block_scan_items(pm, __builtin_inf(), MinF64(), s_f64, mtot);
   block_scan_items(cnt, 0u, AddU32(), s_u32, ctot);
   __syncthreads();
-  // rank in the chunk: keys below, then equal keys at lower slots
-  uint32_t r = 0;
-#pragma unroll 8
-  for (uint32_t j = 0; j < (uint32_t)kChunk; j++) {
-    const unsigned long long kj = s_key[j];
-    r += (kj < key) | ((kj == key) & (j < t));
+  // rank in the chunk: keys below, then equal keys at lower slots.  One pass
+  // counts keys below and keys equal (two keys per LDS read); the slot order
+  // among equal scores is recounted only where a score tie exists (rare).
+  // Non-score slots (key ~0) go after the chunk's scores in slot order: only
+  // the scores' positions are read (k_kl_merge), the rest must only be ~0.
+  uint32_t lt = 0, eq = 0;
+#pragma unroll 16
+  for (uint32_t j = 0; j < (uint32_t)kChunk; j += 2) {
+    const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(&s_key[j]);
+    lt += (kk.x < key ? 1u : 0u) + (kk.y < key ? 1u : 0u);
+    eq += (kk.x == key ? 1u : 0u) + (kk.y == key ? 1u : 0u);
+  }
+  uint32_t r;
+  if (num) {
+    r = lt;
+    if (eq > 1) {  // a tie: equal scores at lower slots of the chunk come first
+      for (uint32_t j = 0; j < t; j++) r += s_key[j] == key ? 1u : 0u;
+    }
+  } else {
+    r = (ctot >> 16) + (t - (cnt[0] >> 16));
   }
   A.sort_key_all[kb + r] = key;  // positions past the chunk's scores hold ~0
   A.sort_idx_all[kb + r] = sl;
