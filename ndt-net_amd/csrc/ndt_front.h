@@ -174,7 +174,7 @@ __device__ inline bool cloud_sync(FrontState& s, uint32_t* bar, uint32_t G) {
 
 // The barrier that ends a bisection pass, carrying the pass's count: each
 // workgroup adds (1 << 48) + (bad << 32) + fresh to the pass-parity slot
-// (u64 at bar + 2 + 2 parity, zeroed by k_reset) and waits until G arrivals
+// (u64 at bar + 2 + 2 parity, zeroed at plan creation and by the last workgroup out) and waits until G arrivals
 // of this use are in; the count and the number of workgroups that saw an
 // out-of-grid point are the slot's growth since its previous use.  One atomic
 // and the poll replace a record per workgroup read back after the barrier.  A
@@ -268,7 +268,12 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
   uint32_t* hist = binfo + (uint64_t)bpw * 1024;              // [nrb][ndcap]
   uint32_t* stamps = A.stamps + (uint64_t)b * A.vcap;
   const uint64_t bin0 = (uint64_t)g * bpw;
-  const uint32_t epoch = c.epoch;
+  // this run's stamp epoch: every workgroup derives it from the previous
+  // run's (stamps are epoch * 32 + pass; on the 2^26 wrap the stale stamps are
+  // cleared here), and the last workgroup out stores it (no k_reset launch)
+  uint32_t epoch = c.epoch + 1;
+  const bool clear_stamps = epoch >= (1u << 26);
+  if (clear_stamps) epoch = 1;
   FRONT_MARK(0);
   FRONT_WG_MARK(0);
 
@@ -283,7 +288,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
       s.limkey[3 + a] = ord_key(kDblMax);  // min starts at DBL_MAX
     }
   }
-  if (c.clear_stamps) {  // epoch wrap (k_reset): rare, cost irrelevant
+  if (clear_stamps) {  // epoch wrap: rare, cost irrelevant
     for (uint64_t v = (uint64_t)g * kFrontThreads + t; v < A.vcap; v += (uint64_t)G * kFrontThreads)
       st_sc1(stamps + v, 0u);
   }
@@ -603,7 +608,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
     c.num_nds = s.state == kAccepted ? s.num_nds : 0u;
     for (int w = 0; w < kWorkers; w++) c.first_bad[w] = s.cut[w];
   }
-  if (s.state != kAccepted) return;
+  if (s.state != kAccepted) goto out;
   FRONT_MARK(20);
 
   {
@@ -848,10 +853,23 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
     FRONT_MARK(26);
   }
   FRONT_WG_MARK(1);
-  return;
+  goto out;
 fail:
   if (t == 0) {
     c.state = kFailed;
     c.rc = kNdtErrSync;
+  }
+out:
+  // The last workgroup of the cloud out (every one has passed its last
+  // barrier poll) re-arms the cloud for the next run: barrier counter and
+  // pass-sum slots zeroed, the epoch stored, the prune-list counters (set by
+  // the KL kernels, read by further prune levels) cleared.
+  if (t == 0 && __hip_atomic_fetch_add(bar + 6, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1) {
+    for (int i = 0; i < 7; i++) st_sc1(bar + i, 0u);
+    c.epoch = epoch;
+    c.clear_stamps = clear_stamps ? 1u : 0u;
+    c.num_valid = c.num_kl = c.num_phys = c.num_events = 0;
+    c.prune_rc = 0;
+    c.num_out = c.last_k = 0;
   }
 }

@@ -2023,7 +2023,8 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
   const uint64_t n = P->n;
   if (lbl && P->ncls < 0) return NDNET_ERR_ARG;
   if (P->timing) HIPCHK(hipEventRecord(P->ev[0], st));
-  k_reset<<<(B + 63) / 64, 64, 0, st>>>(P->ctl, B, P->front ? P->fbar : nullptr);
+  // k_front re-arms its clouds itself (epoch, barrier words, list counters)
+  if (!P->front) k_reset<<<(B + 63) / 64, 64, 0, st>>>(P->ctl, B, nullptr);
   P->calls++;
   if (P->front) {
     FrontArgs F;
