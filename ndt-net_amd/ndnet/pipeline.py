@@ -103,8 +103,13 @@ class PipelinedSegmentation:
     forward of step i returns the log-probs of the batch of step i - 1 (the
     first step's forward runs on the warm-up batch).
 
-    ``points`` is the static input buffer; ``replay()`` returns the static
-    ``[B, num_nds, C+1]`` output of that step's forward.
+    The two graphs read alternating input buffers: ``points`` is the buffer
+    the NEXT ``replay()`` reads (fill it, then replay); ``load_resident(pts)``
+    fills both.  ``replay_streamed(host_next)`` replays the next step and, on
+    a copy stream overlapped with it, copies ``host_next`` (pinned host
+    memory) into the buffer of the step after it -- the PCIe-inclusive
+    serving loop.  ``replay()`` returns the static ``[B, num_nds, C+1]``
+    output of that step's forward.
     """
 
     def __init__(self, model, num_nds: int, batch: int, num_points: int,
@@ -114,7 +119,10 @@ class PipelinedSegmentation:
             raise ValueError("PipelinedSegmentation needs an eval-mode model")
         dev = torch.device(device) if device is not None else next(model.parameters()).device
         self.model, self.num_nds, self.device = model, int(num_nds), dev
-        self.points = torch.zeros((batch, num_points, 3), dtype=torch.float32, device=dev)
+        self.inputs = [torch.zeros((batch, num_points, 3), dtype=torch.float32, device=dev) for _ in range(2)]
+        self.s_copy = torch.cuda.Stream(device=dev)
+        self.done = [torch.cuda.Event(), torch.cuda.Event()]    # graph j finished (its input is free)
+        self.copied = [torch.cuda.Event(), torch.cuda.Event()]  # input j holds the streamed batch
         self.rows = [torch.zeros((batch, self.num_nds, 12), dtype=torch.float32, device=dev) for _ in range(2)]
         self.plan = get_plan(batch, num_points, self.num_nds, -1, dev)
         # the forward's launches go first; stream priorities (either way) measured
@@ -142,16 +150,40 @@ class PipelinedSegmentation:
             prev = self.rows[1 - j]
             out = self.model(prev[..., :3], prev[..., 3:])
         with torch.cuda.stream(self.s_ndt):
-            self.plan.run(self.points, None, self.rows[j], None)
+            self.plan.run(self.inputs[j], None, self.rows[j], None)
         cur.wait_stream(self.s_ndt)
         cur.wait_stream(self.s_fwd)
         return out
 
+    @property
+    def points(self) -> torch.Tensor:
+        """The input buffer the next ``replay()`` reads."""
+        return self.inputs[self.i & 1]
+
+    def load_resident(self, points: torch.Tensor) -> None:
+        """Fill both input buffers (every later step re-reads this batch)."""
+        for buf in self.inputs:
+            buf.copy_(points)
+
     def replay(self) -> torch.Tensor:
         j = self.i & 1
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_event(self.copied[j])  # no-op unless a streamed copy targets input j
         self.graphs[j].replay()
+        self.done[j].record(cur)
         self.i += 1
         return self.out[j]
+
+    def replay_streamed(self, host_next: torch.Tensor) -> torch.Tensor:
+        """``replay()`` with the H2D copy of the batch after it overlapped."""
+        j = self.i & 1
+        out = self.replay()
+        # input 1-j was last read by the previous step's graph
+        self.s_copy.wait_event(self.done[1 - j])
+        with torch.cuda.stream(self.s_copy):
+            self.inputs[1 - j].copy_(host_next, non_blocking=True)
+            self.copied[1 - j].record(self.s_copy)
+        return out
 
     def stats(self) -> list:
         return self.plan.host_stats()

@@ -104,3 +104,28 @@ def test_pipelined_steps_equal_sequential_batches():
     torch.cuda.synchronize()
     for i in range(3):
         assert torch.equal(outs[i + 1], expect[i]), f"batch {i}"
+
+
+def test_pipelined_streamed_host_batches():
+    """replay_streamed: host batches copied on a copy stream one step ahead
+    (double-buffered inputs) give the same outputs as the one-graph path."""
+    import torch
+    from ndnet.models.ndtnet import NDTNetSegmentation
+    from ndnet.pipeline import GraphedSegmentation, PipelinedSegmentation
+    from ndnet.synthetic import make_batch
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    m = NDTNetSegmentation(3, 28, 768).to(dev).eval()
+    host = [torch.from_numpy(make_batch("L", 4, 20_000, seed0=10 * i)).pin_memory() for i in range(4)]
+    ref = GraphedSegmentation(m, 400, 4, 20_000, device=dev)
+    expect = [ref(b.to(dev)).clone() for b in host]
+    pipe = PipelinedSegmentation(m, 400, 4, 20_000, device=dev)
+    pipe.points.copy_(host[0])
+    outs = []
+    # replay i runs batch i and streams batch i + 1; its forward is batch i - 1's
+    for i in range(len(host)):
+        outs.append(pipe.replay_streamed(host[min(i + 1, len(host) - 1)]).clone())
+    outs.append(pipe.replay().clone())
+    torch.cuda.synchronize()
+    for i in range(len(host)):
+        assert torch.equal(outs[i + 1], expect[i]), f"batch {i}"
