@@ -8,9 +8,15 @@ Metric (BASELINE.json): "clouds/sec NDT preprocess+PointNet fwd, 100k pts ->
 eval-mode ``NDTNetSegmentation(point_dim=3, num_classes=28, feature_dim=768)``
 forward -- the path tools/train.py:67-69 runs each iteration.
 
-Multi-GPU (torchrun, one process per GPU): every rank processes its own batch
-of 16 clouds (weak scaling, no collective on the data path -- SURVEY §8e);
-value = all clouds / max-over-ranks time.
+Multi-GPU (one process per GPU): every rank processes its own contiguous
+shard of 16 clouds (weak scaling, no collective on the data path -- SURVEY
+§8e; config C4 at --gpus 8: 128 clouds, 16 per rank); value = all clouds /
+max-over-ranks time.  ``--gpus N`` with N > 1 and no WORLD_SIZE in the
+environment launches the N ranks itself (torch.distributed.run as a child
+process, before this process touches the GPU); under torch.distributed.run
+WORLD_SIZE must equal --gpus.  ``--dry-run`` runs the launcher, rendezvous,
+shard split and the timing/max-over-ranks logic on CPU (gloo) with no GPU
+work (tests/test_bench_launcher.py).
 
 The JSON line carries
   roofline     -- the dominant kernel stage, achieved vs MI355X peak
@@ -54,6 +60,49 @@ def chain_flops_per_point(F: int, C: int) -> tuple:
     return tuple(2.0 * v for v in (a, b, c, d))
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _self_launch(nproc: int) -> int:
+    """One rank per GPU as fresh child processes (no GPU call has happened in
+    this process: importing torch does not initialise HIP)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
+def _dry_run(args, rank: int, world: int) -> None:
+    """The multi-rank skeleton on CPU: gloo rendezvous, the shard split, the
+    barrier / max-over-ranks timing of --steps no-op steps, the JSON line."""
+    import torch.distributed as tdist
+    from ndnet import distributed as D
+    D.init("gloo")
+    start, count = D.shard(args.batch * world, world, rank)
+    shards = [None] * world
+    if tdist.is_initialized():
+        tdist.all_gather_object(shards, (start, count))
+    else:
+        shards = [(start, count)]
+    D.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    D.barrier()
+    elapsed = D.max_over_ranks(max(time.perf_counter() - t0, 1e-9))
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run (no GPU work)", "n_gpus": world, "steps": args.steps,
+                          "global_batch": args.batch * world, "shards": shards,
+                          "max_elapsed_s": elapsed}))
+    if tdist.is_initialized():
+        tdist.destroy_process_group()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -73,10 +122,20 @@ def main() -> None:
     ap.add_argument("--levels", default=None,
                     help="config C5: comma-separated NDs per level, e.g. 2000,1000,500 (downsample, then prune; "
                          "a forward per level)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / shard split / timing skeleton on CPU (gloo), no GPU work")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_self_launch(args.gpus))
     from ndnet import distributed as D
     rank, local, world = D.world_from_env()
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE {world} != --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
+    if args.dry_run:
+        _dry_run(args, rank, world)
+        return
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = D.init("nccl", dev)  # RCCL; used only for the barrier and the max-over-ranks time
@@ -91,7 +150,11 @@ def main() -> None:
     levels = tuple(int(v) for v in args.levels.split(",")) if args.levels else None
     if levels:
         k = levels[0]  # the stage timing / roofline below cover the first level's downsample + forward
-    pts = torch.from_numpy(make_batch(args.kind, B, n, seed0=rank * B)).to(dev)
+    # this rank's contiguous shard of the job's B * world clouds (cloud i of the
+    # job is the SURVEY §8d generator's seed i)
+    shard0, shard_n = D.shard(B * world, world, rank)
+    assert shard_n == B
+    pts = torch.from_numpy(make_batch(args.kind, B, n, seed0=shard0)).to(dev)
     torch.manual_seed(1234)
     model = NDTNetSegmentation(3, C, F).to(dev).eval()
     with torch.no_grad():
@@ -317,6 +380,9 @@ def main() -> None:
             "dtype": "f64 (NDT core) + fp32 (PointNet)",
             "data": f"synthetic {args.kind} clouds (SURVEY 8d), random-init weights",
             "config": {"workload": (f"batch {B} x {n} pts -> {k} NDs, NDTNetSegmentation F={F} C={C} eval"
+                                    if not levels and world == 1 else
+                                    f"C4: {B * world} clouds end to end ({n} pts -> {k} NDs -> NDTNetSegmentation "
+                                    f"F={F} C={C} eval), {B} per rank over {world} GPUs, contiguous shards"
                                     if not levels else
                                     f"C5: batch {B} x {n} pts -> downsample {levels[0]} -> prune "
                                     f"{' -> '.join(map(str, levels[1:]))}, NDTNetSegmentation F={F} C={C} eval "

@@ -116,7 +116,13 @@ void ndnet_ndt_plan_destroy(void *plan);
  * k_front (limits through binning in one launch; needs every workgroup of a
  * cloud resident, so only where the plan's shape allows it), 0 = 2 where
  * allowed, else 1 (the default).  Both paths give identical results.
- * ndnet_ndt_get_path returns the path in use. */
+ * ndnet_ndt_get_path returns the path in use.
+ * Concurrency: path 2's grid barrier assumes no other k_front grid competes
+ * for the CUs at the same time (two partly resident grids wait for each
+ * other until the ~2 s barrier timeout fails their clouds with
+ * NDNET_ERR_SYNC).  Run at most one path-2 plan per device at a time, or
+ * select path 1 for plans that run concurrently; the legacy entry points
+ * above always use path 1. */
 int ndnet_ndt_set_path(void *plan, int path);
 int ndnet_ndt_get_path(void *plan);
 

@@ -82,6 +82,14 @@ int ndt_downsample(double* point_cloud, unsigned short point_dim, unsigned long 
   h->k = num_desired_points;
   h->refs = 1;
   int rc = ndnet_ndt_plan_create(1, num_points, num_desired_points, (int)num_classes, 0, &h->plan);
+  // One launch per stage, not the fused k_front: k_front's grid barrier needs
+  // every workgroup of the cloud resident at once (at B = 1 that is one per
+  // CU), and this entry point is called concurrently -- the reference's
+  // DataLoader workers (tools/train.py:135-137) each run NDT_Sampler in their
+  // own process -- so two partly resident k_front grids could each wait for
+  // the other until the barrier timeout.  The multi-launch path has no
+  // residency requirement and computes the same bits (test_front_kernel_equals_multikernel_path).
+  if (rc == NDNET_OK) rc = ndnet_ndt_set_path(h->plan, 1);
   if (rc != NDNET_OK) {
     release(h);
     return rc;

@@ -10,12 +10,14 @@ Module tree and parameter names follow the reference
       conv1..conv4, bn1..bn3
 
 Two forward paths:
-  * eval mode on a gfx950 GPU -> the fused HIP kernels of
+  * eval mode on a gfx950 GPU with no autograd wanted (``torch.no_grad()``,
+    or nothing requires grad) -> the fused HIP kernels of
     lib/libndnet_amd.so (``ndnet.models.pointnet_hip``): BatchNorm folded into
-    the 1x1 convolutions, FP32 MFMA GEMMs over (points x channels), global
+    the 1x1 convolutions, MFMA GEMMs over (points x channels), global
     max-pool fused into the producing GEMM.
-  * anything else (training, autograd, CPU) -> the PyTorch composition below,
-    which is also the fp32 reference the kernels are tested against.
+  * anything else (training, eval-mode autograd, CPU) -> the PyTorch
+    composition below, which is also the fp32 reference the kernels are
+    tested against.
 """
 from __future__ import annotations
 
@@ -136,13 +138,26 @@ class NDTNetSegmentation(nn.Module):
         x = torch.nn.functional.log_softmax(self.conv4(x), dim=1)
         return x.transpose(2, 1)
 
+    def _needs_autograd(self, points: torch.Tensor, covariances: torch.Tensor) -> bool:
+        """The reference forward is differentiable in eval mode too (frozen-BN
+        fine-tuning, saliency): with grad enabled and anything requiring grad,
+        the autograd composition runs, not the inference kernels."""
+        if not torch.is_grad_enabled():
+            return False
+        return points.requires_grad or covariances.requires_grad or any(p.requires_grad for p in self.parameters())
+
     def forward(self, points: torch.Tensor, covariances: torch.Tensor) -> torch.Tensor:
-        if not self.training and points.is_cuda and self.point_dim == 3:
+        if (not self.training and points.is_cuda and self.point_dim == 3
+                and not self._needs_autograd(points, covariances)):
             from . import pointnet_hip
             if pointnet_hip.available():
                 return pointnet_hip.segmentation_forward(self, points, covariances)
         return self.forward_torch(points, covariances)
 
     def train(self, mode: bool = True):
-        self._hip = None  # weights may change; re-fold on the next eval forward
+        # entering training: weights will change, drop the folded copy (a
+        # captured graph keeps its own reference, ndnet.pipeline); a redundant
+        # eval() keeps it
+        if bool(mode) != self.training:
+            self._hip = None
         return super().train(mode)

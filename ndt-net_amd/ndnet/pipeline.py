@@ -25,6 +25,29 @@ from . import _lib
 from .preprocessing.ndtnet_preprocessing import ndt_multiscale, ndt_preprocessing, get_plan
 
 
+class _Pinned:
+    """What a captured graph reads through raw pointers, kept alive for the
+    graph's lifetime: the model's folded-weight cache (weights, workspace,
+    prebuilt argument blocks) and the NDT plans.  ``check()`` raises when the
+    model's weights changed since capture (the graph would replay the old
+    fold): ``model.train()``, a re-fold by an eager forward or an in-place
+    update no longer free or silently bypass the captured buffers."""
+
+    def __init__(self, model, plans) -> None:
+        from .models import pointnet_hip
+        self.model, self.plans = model, list(plans)
+        self.cache = model._hip
+        if self.cache is None or "W" not in self.cache:
+            raise RuntimeError("the capture ran no HIP forward (is the HIP path built?)")
+        self.W, self.ws, self.sig = self.cache["W"], dict(self.cache["ws"]), self.cache["sig"]
+        self._signature = lambda: pointnet_hip._signature(self.cache["tensors"])
+
+    def check(self) -> None:
+        if self._signature() != self.sig:
+            raise RuntimeError("the model's weights changed after the graph was captured: "
+                               "build a new graph (the captured one replays the old fold)")
+
+
 class GraphedSegmentation:
     """Replays ``model(*ndt_preprocessing(num_nds, points)[:2])`` from a graph.
 
@@ -70,6 +93,7 @@ class GraphedSegmentation:
         with torch.no_grad(), torch.cuda.graph(self.graph):
             self.out = self._step()
         self.plan = get_plan(batch, num_points, self.num_nds, -1, dev)
+        self._pinned = _Pinned(model, [self.plan])
 
     def _step(self):
         if self.levels:
@@ -78,6 +102,7 @@ class GraphedSegmentation:
         return self.model(p, c)
 
     def replay(self) -> torch.Tensor:
+        self._pinned.check()
         self.graph.replay()
         return self.out
 
@@ -140,6 +165,7 @@ class PipelinedSegmentation:
         for j in range(2):
             with torch.no_grad(), torch.cuda.graph(self.graphs[j]):
                 self.out[j] = self._step(j)
+        self._pinned = _Pinned(model, [self.plan])
         self.i = 0
 
     def _step(self, j: int) -> torch.Tensor:
@@ -166,6 +192,7 @@ class PipelinedSegmentation:
             buf.copy_(points)
 
     def replay(self) -> torch.Tensor:
+        self._pinned.check()
         j = self.i & 1
         cur = torch.cuda.current_stream(self.device)
         cur.wait_event(self.copied[j])  # no-op unless a streamed copy targets input j

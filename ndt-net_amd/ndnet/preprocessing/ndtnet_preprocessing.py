@@ -12,6 +12,7 @@ reference does (ndtnet_preprocessing.py:66-69).
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -90,8 +91,31 @@ def get_plan(batch: int, num_points: int, num_nds: int, num_classes: int, device
     return p
 
 
+# opt-in failure check of every eager ndt_preprocessing call (see its docstring)
+CHECK_RC = os.environ.get("NDNET_CHECK_RC", "0") == "1"
+
+
+class NdtCloudError(RuntimeError):
+    """A cloud of the batch failed (``rcs``: per-cloud return codes)."""
+
+    def __init__(self, rcs):
+        self.rcs = list(rcs)
+        bad = {b: rc for b, rc in enumerate(self.rcs) if rc != 0}
+        super().__init__(f"ndt_downsample failed for clouds {bad} (rc -3: search hit 15 iterations, "
+                         f"-1: grid above the voxel capacity, -22: front barrier timeout)")
+
+
+def check_stats(plan: "NdtPlan") -> None:
+    """Raises ``NdtCloudError`` if any cloud of the plan's last run failed
+    (synchronises with the plan's stream)."""
+    rcs = [s.rc for s in plan.host_stats()]
+    if any(rc != 0 for rc in rcs):
+        raise NdtCloudError(rcs)
+
+
 def ndt_preprocessing(num_nds: int, points: torch.Tensor, classes: torch.Tensor = None,
-                      num_classes: int = None) -> Tuple[torch.Tensor, torch.Tensor, Optional[torch.Tensor]]:
+                      num_classes: int = None, *, check: Optional[bool] = None
+                      ) -> Tuple[torch.Tensor, torch.Tensor, Optional[torch.Tensor]]:
     """Downsample a batch of clouds to ``num_nds`` normal distributions.
 
     Args:
@@ -105,6 +129,16 @@ def ndt_preprocessing(num_nds: int, points: torch.Tensor, classes: torch.Tensor 
         [B, num_nds, num_classes + 1] or None)`` float32 on ``points.device``.
         The first two are views of one ``[B, num_nds, 12]`` block, the layout
         the NDTNet kernels read.
+
+    Failures: like the reference (ndt_legacy.py:153 ignores the return code;
+    the zero-filled outputs of ndt_legacy.py:126-143 pass through), a failed
+    cloud yields all-zero rows and a class-0 one-hot.  Failure modes are the
+    reference's (-3: the bisection reached 15 iterations, ndt.c:191-194) plus
+    this build's capacities: a bisection grid above the plan's voxel capacity
+    (default 2^22 voxels per cloud) fails the cloud with -1 where the
+    reference would malloc it.  ``check=True`` (or ``NDNET_CHECK_RC=1``)
+    synchronises and raises ``NdtCloudError`` instead; it is skipped while a
+    HIP graph is being captured.  Per-cloud codes: ``last_stats()``.
     """
     _lib.require_gpu()
     src_device = points.device
@@ -127,6 +161,8 @@ def ndt_preprocessing(num_nds: int, points: torch.Tensor, classes: torch.Tensor 
         out_cls = torch.empty((B, num_nds, ncls + 1), dtype=torch.float32, device=dev)
     plan.run(pts, labels, out, out_cls)
     ndt_preprocessing.last_plan = plan
+    if (CHECK_RC if check is None else check) and not torch.cuda.is_current_stream_capturing():
+        check_stats(plan)
     if src_device != dev:
         out = out.to(src_device)
         out_cls = out_cls.to(src_device) if out_cls is not None else None

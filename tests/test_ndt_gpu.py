@@ -271,3 +271,44 @@ def test_multiscale_batch_matches_oracle_chain(kind):
             assert np.array_equal(p[b].cpu().numpy(), f32(p2))
             assert np.array_equal(c[b].cpu().numpy(), f32(c2))
         ref.cleanup()
+
+
+@pytest.mark.parametrize("kind", ["U", "L"])
+def test_c5_full_size_levels(kind):
+    """Config C5 as configured (BASELINE.json config 5): 16 x 100k points ->
+    downsample(2000) -> prune(1000) -> prune(500), batched on the GPU
+    (ndt_multiscale), every level of every cloud bit-exact against the
+    oracle's NDT_Sampler chain (ndt_legacy.py:111-240: ndt_downsample, then
+    prune_nds + to_point_cloud on the retained KL list)."""
+    import oracle as O
+    import torch
+    from ndnet.preprocessing.ndtnet_preprocessing import ndt_multiscale
+    from ndnet.synthetic import make_batch
+    B, n, levels = 16, 100_000, (2000, 1000, 500)
+    pts = make_batch(kind, B, n)
+    out = ndt_multiscale(levels, torch.from_numpy(pts).cuda())
+    got = [(p.cpu().numpy(), c.cpu().numpy()) for p, c, _ in out]
+    f32 = lambda a: np.nan_to_num(a.astype(np.float32), nan=0.0, posinf=0.0, neginf=0.0)  # noqa: E731
+    for b in range(B):
+        ref = O.LegacyChain(pts[b].astype(np.float64))
+        expect = [ref.downsample(levels[0])] + [ref.prune(k) for k in levels[1:]]
+        assert ref.rc == 0
+        for lv, ((p, c), (p2, c2)) in enumerate(zip(got, expect)):
+            assert np.array_equal(p[b], f32(p2)), f"cloud {b} level {lv} means"
+            assert np.array_equal(c[b], f32(c2)), f"cloud {b} level {lv} covariances"
+        ref.cleanup()
+
+
+def test_check_flag_raises_on_failed_cloud():
+    """opt-in failure check (the reference ignores return codes)."""
+    import torch
+    from ndnet.preprocessing.ndtnet_preprocessing import NdtCloudError, ndt_preprocessing
+    rng = np.random.default_rng(2)
+    pts = rng.uniform(-5, 5, (2, 4096, 3)).astype(np.float32)
+    pts[1, :, 2] = 1.5  # a zero-length axis: the search reaches 15 iterations (-3)
+    t = torch.from_numpy(pts).cuda()
+    p, c, _ = ndt_preprocessing(200, t)  # default: zero rows, like the reference
+    assert not p[1].any().item() and p[0].any().item()
+    with pytest.raises(NdtCloudError) as ei:
+        ndt_preprocessing(200, t, check=True)
+    assert ei.value.rcs == [0, -3]

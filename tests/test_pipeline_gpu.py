@@ -129,3 +129,80 @@ def test_pipelined_streamed_host_batches():
     torch.cuda.synchronize()
     for i in range(len(host)):
         assert torch.equal(outs[i + 1], expect[i]), f"batch {i}"
+
+
+def test_graph_keeps_captured_fold_alive():
+    """a captured graph reads the model's folded weights and
+    workspace through raw pointers.  A redundant eval() or an eager forward
+    after capture must not free them; a weight change must be refused."""
+    import torch
+    from ndnet.synthetic import make_batch
+    from ndnet.pipeline import GraphedSegmentation
+    B, n, k = 2, 8000, 200
+    m = _model()
+    pts = torch.from_numpy(make_batch("U", B, n, seed0=3)).cuda()
+    g = GraphedSegmentation(m, k, B, n)
+    first = g(pts).clone()
+    m.eval()                       # redundant: keeps the fold
+    m.train()                      # drops the model's cache (the graph keeps its own)
+    m.eval()
+    with torch.no_grad():
+        from ndnet.preprocessing.ndtnet_preprocessing import ndt_preprocessing
+        p, c, _ = ndt_preprocessing(k, pts)
+        eager = m(p, c).clone()   # re-folds into fresh buffers
+        junk = [torch.randn(1 << 20, device="cuda") for _ in range(8)]  # reuse freed blocks, if any
+    again = g(pts).clone()
+    torch.cuda.synchronize()
+    del junk
+    assert torch.equal(again, first) and torch.equal(eager, first)
+    with torch.no_grad():
+        m.conv4.bias.add_(1.0)
+    with pytest.raises(RuntimeError, match="weights changed"):
+        g(pts)
+
+
+def test_eval_mode_autograd_uses_differentiable_path():
+    """the reference forward is differentiable in eval mode; with
+    grad enabled the model must not return a grad-less kernel output."""
+    import torch
+    m = _model()
+    p = torch.rand((2, 64, 3), device="cuda")
+    c = torch.randn((2, 64, 9), device="cuda", requires_grad=True)
+    out = m(p, c)
+    assert out.grad_fn is not None
+    out.sum().backward()
+    assert c.grad is not None and torch.isfinite(c.grad).all()
+    assert m.conv4.weight.grad is not None
+    with torch.no_grad():
+        hip = m(p, c)
+    assert hip.grad_fn is None and (hip - out.detach()).abs().max().item() < 1e-4
+
+
+def test_legacy_entry_points_run_concurrently():
+    """the reference ABI is called from several DataLoader workers
+    at once; its plans use the multi-launch path (no grid barrier), so
+    concurrent callers all succeed."""
+    import threading
+    import oracle as O
+    from ndnet.preprocessing.ndt_legacy import NDT_Sampler
+    from ndnet.synthetic import lidar_cloud, uniform_cloud
+    clouds = [uniform_cloud(40_000, s).astype(np.float64) for s in range(2)] + \
+             [lidar_cloud(40_000, s).astype(np.float64) for s in range(2)]
+    res = [None] * len(clouds)
+
+    def work(i):
+        s = NDT_Sampler(clouds[i])
+        res[i] = s.downsample(500)
+        s.cleanup()
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(len(clouds))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=60)
+    for i, cl in enumerate(clouds):
+        assert res[i] is not None, f"worker {i} did not finish"
+        ref = O.LegacyChain(cl)
+        pc, cov = ref.downsample(500)
+        assert np.array_equal(res[i][0], pc) and np.array_equal(res[i][1], cov, equal_nan=True)
+        ref.cleanup()
