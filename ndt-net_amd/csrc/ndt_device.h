@@ -118,9 +118,9 @@ NDNET_FN uint32_t voxel_key_f32(float x, float y, float z, const float* off32, f
   const float qx = (x - off32[0]) * inv32, qy = (y - off32[1]) * inv32, qz = (z - off32[2]) * inv32;
   const float fx = floorf(qx), fy = floorf(qy), fz = floorf(qz);
   // branch-free (selects, no exec-mask regions in the caller's unrolled loop)
-  const bool ok = (fabsf(qx - fx - 0.5f) < half_tol) & (fabsf(qy - fy - 0.5f) < half_tol) &
-                  (fabsf(qz - fz - 0.5f) < half_tol);
-  const bool in = (fx < lenf[0]) & (fy < lenf[1]) & (fz < lenf[2]);
+  const bool ok = ((int)(fabsf(qx - fx - 0.5f) < half_tol) & (int)(fabsf(qy - fy - 0.5f) < half_tol) &
+                   (int)(fabsf(qz - fz - 0.5f) < half_tol)) != 0;
+  const bool in = ((int)(fx < lenf[0]) & (int)(fy < lenf[1]) & (int)(fz < lenf[2])) != 0;
   const uint32_t k = ((uint32_t)fz * len[1] + (uint32_t)fy) * len[0] + (uint32_t)fx;
   return ok ? (in ? k : kInvalid) : kKeyRedo;
 }
@@ -284,8 +284,11 @@ NDNET_FN int lu3_sgndet(const double* LU, int signum) {
   return s;
 }
 
-// Inverse from LU, column by column (P e_j, unit-lower forward, upper back
-// substitution in gslcblas dtrsv order).
+#ifdef NDNET_LU_INVERT_COLUMNS
+// Variant (round 1): inverse from LU column by column (P e_j, unit-lower
+// forward, upper back substitution in gslcblas dtrsv order).  Rounds
+// differently from GSL 2.7.1's LU_invert below (<= 3.7e-13 relative on a KL
+// score); kept for A/B runs only.
 NDNET_FN void lu3_invert(const double* LU, uint32_t perm_packed, double* inv) {
   int perm[3] = {(int)(perm_packed & 3), (int)((perm_packed >> 2) & 3), (int)((perm_packed >> 4) & 3)};
 #pragma unroll
@@ -307,6 +310,95 @@ NDNET_FN void lu3_invert(const double* LU, uint32_t perm_packed, double* inv) {
     inv[2 * 3 + j] = x2;
   }
 }
+#else
+// gsl_linalg_LU_invert as GSL 2.7.1 publishes it (linalg/lu.c): the inverse
+// is the LU copy run through gsl_linalg_LU_invx --
+//   1. gsl_linalg_tri_invert(CblasUpper, CblasNonUnit): U^-1 in place
+//      (linalg/tri.c triangular_inverse_L2, N = 3 below the Level-3
+//      crossover): per column i, T_ii = 1 / T_ii, then the column above the
+//      diagonal = -T_ii * dtrmv(Upper, NoTrans, NonUnit, T[0:i,0:i]) of itself;
+//   2. gsl_linalg_tri_invert(CblasLower, CblasUnit): L^-1 in place, columns
+//      j = N-1 .. 0, the column below the diagonal = -dtrmv(Lower, NoTrans,
+//      Unit, T[j+1:,j+1:]) of itself;
+//   3. gsl_linalg_tri_UL: U^-1 L^-1 in place (triangular_mult_L2, Upper):
+//      per row i, A_ii += ddot(L col below, U row right); for 0 < i < N-1 the
+//      row's L part = dgemv(Trans, 1, L_BL, U row, beta = a_ii) and the
+//      column's U part += dgemv(NoTrans, 1, U_TR, L col); the last row's L
+//      part scaled by a_NN;
+//   4. every row through gsl_permute_vector_inverse (out[p[k]] = row[k]).
+// Each BLAS call in gslcblas's loop order (cblas/source_trmv_r.h,
+// source_dot_r.h, source_gemv_r.h, source_scal_r.h), every operation rounded
+// separately (no contraction): the same IEEE sequence as oracle/ndt_oracle.c
+// orc_lu_invert_gsl.
+NDNET_FN void lu3_invert(const double* LU, uint32_t perm_packed, double* inv) {
+  double a00 = LU[0], a01 = LU[1], a02 = LU[2];
+  double a10 = LU[3], a11 = LU[4], a12 = LU[5];
+  double a20 = LU[6], a21 = LU[7], a22 = LU[8];
+  // 1. U^-1.  i = 0: the diagonal only
+  a00 = 1.0 / a00;
+  {  // i = 1: v = (a01), trmv over [a00]: v0 = 0 + v0 * a00; scal(-a11)
+    a11 = 1.0 / a11;
+    const double s = -a11;
+    a01 = 0.0 + a01 * a00;
+    a01 = a01 * s;
+  }
+  {  // i = 2: v = (a02, a12), trmv over [[a00, a01], [., a11]]; scal(-a22)
+    a22 = 1.0 / a22;
+    const double s = -a22;
+    const double t0 = 0.0 + a12 * a01;
+    a02 = t0 + a02 * a00;
+    a12 = 0.0 + a12 * a11;
+    a02 = a02 * s;
+    a12 = a12 * s;
+  }
+  // 2. L^-1 (unit).  j = 2: nothing below the diagonal
+  {  // j = 1: v = (a21), trmv over [1]: v0 += 0; scal(-1)
+    a21 = a21 + 0.0;
+    a21 = a21 * -1.0;
+  }
+  {  // j = 0: v = (a10, a20), trmv over [[1, .], [a21, 1]] bottom-up; scal(-1)
+    const double t1 = 0.0 + a10 * a21;
+    a20 = a20 + t1;
+    a10 = a10 + 0.0;
+    a10 = a10 * -1.0;
+    a20 = a20 * -1.0;
+  }
+  // 3. U^-1 L^-1
+  {  // i = 0: a00 += ddot((a10, a20), (a01, a02))
+    double t = 0.0 + a10 * a01;
+    t = t + a20 * a02;
+    a00 = a00 + t;
+  }
+  {  // i = 1
+    const double aii = a11;
+    const double t = 0.0 + a21 * a12;
+    a11 = a11 + t;
+    // lr = (a10): beta = aii first, then += (1 * a12) * a20 when non-zero
+    a10 = aii == 0.0 ? 0.0 : (aii != 1.0 ? a10 * aii : a10);
+    const double x = 1.0 * a12;
+    if (x != 0.0) a10 = a10 + x * a20;
+    // ut = (a01): beta = 1; += 1 * (0 + a21 * a02)
+    const double u = 0.0 + a21 * a02;
+    a01 = a01 + 1.0 * u;
+  }
+  {  // i = 2: the last row's L part times a22
+    const double aii = a22;
+    a20 = a20 * aii;
+    a21 = a21 * aii;
+  }
+  // 4. column permutation of every row: out[p[k]] = row[k]
+  const int p0 = (int)(perm_packed & 3), p1 = (int)((perm_packed >> 2) & 3), p2 = (int)((perm_packed >> 4) & 3);
+  const double r[9] = {a00, a01, a02, a10, a11, a12, a20, a21, a22};
+#pragma unroll
+  for (int row = 0; row < 3; row++) {
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      // column c of the output row is the input element k with p[k] == c
+      inv[row * 3 + c] = p0 == c ? r[row * 3 + 0] : (p1 == c ? r[row * 3 + 1] : r[row * 3 + 2]);
+    }
+  }
+}
+#endif
 
 // kullback_leibler.c:98-115 given both operands already decomposed:
 // 0.5 * (0 + tr(inv_q * LU_p) - log(det_q / det_p) - 3), the trace summed as

@@ -43,6 +43,16 @@
 #include "../ndt-net_amd/csrc/ndt_log.h"
 
 #define ORC_WORKERS 8            /* NUM_PCL_WORKERS, normal_distributions.h:39 */
+
+/* Stage hooks: oracle/cpu_ref.c includes this file and swaps in the
+ * reference-structured (threaded, mutex-per-voxel, heap-allocating) estimate
+ * and KL call for its CPU baseline; the arithmetic stays this file's. */
+#ifndef ORC_ESTIMATE
+#define ORC_ESTIMATE orc_estimate
+#endif
+#ifndef ORC_KL_DIVERGENCE
+#define ORC_KL_DIVERGENCE orc_kl_divergence
+#endif
 #define ORC_MIN_GUESS 0.01       /* ndt.h:41 */
 #define ORC_MAX_GUESS 30.0       /* ndt.h:42 */
 #define ORC_MAX_ITERS 15         /* ndt.h:43 */
@@ -203,7 +213,7 @@ static int orc_search_impl(const double* pc, int dim, uint64_t n, const uint16_t
     orc_nd* nds = (orc_nd*)malloc((V ? V : 1) * sizeof(orc_nd));
     if (!nds) { s->rc = -1; return -1; }
     uint64_t c = 0;
-    if (orc_estimate(pc, n, cls, ncls, guess, s->len, s->off, nds, &c) < 0) {
+    if (ORC_ESTIMATE(pc, n, cls, ncls, guess, s->len, s->off, nds, &c) < 0) {
       orc_free_class_counts(nds, V);
       free(nds);
       s->rc = -2;
@@ -309,11 +319,12 @@ static int orc_lu_sgndet(const double* LU, int signum) {
   return s;
 }
 
-/* Inverse from the LU factors, column by column: b = P e_j, then gslcblas dtrsv
- * lower-unit forward and upper-nonunit back substitution.  (GSL 2.7's
- * tri_invert-based LU_invert rounds differently; the effect on the KL score was
- * measured at <= 3.7e-13 relative with no change to the pruned set) */
-static void orc_lu_invert(const double* LU, const int* perm, double* inv) {
+/* Variant: inverse from the LU factors column by column (b = P e_j, then
+ * gslcblas dtrsv lower-unit forward and upper-nonunit back substitution).
+ * This is what round 1 used; it rounds differently from GSL 2.7.1's
+ * LU_invert (below) by <= 3.7e-13 relative on a KL score.
+ * Selected by orc_use_gsl_invert = 0, for A/B comparisons only. */
+static void orc_lu_invert_columns(const double* LU, const int* perm, double* inv) {
   for (int j = 0; j < 3; j++) {
     double x[3];
     for (int i = 0; i < 3; i++) x[i] = (perm[i] == j) ? 1.0 : 0.0;
@@ -330,6 +341,147 @@ static void orc_lu_invert(const double* LU, const int* perm, double* inv) {
     }
     for (int i = 0; i < 3; i++) inv[i * 3 + j] = x[i];
   }
+}
+
+/* ---- GSL 2.7.1 gsl_linalg_LU_invert, as published (the reference's call at
+ * kullback_leibler.c:92; GSL version inferred).  linalg/lu.c:
+ * LU_invert = memcpy(inverse, LU) + gsl_linalg_LU_invx(inverse, p), which is
+ *   tri_invert(Upper, NonUnit); tri_invert(Lower, Unit); tri_UL; then
+ *   gsl_permute_vector_inverse(p, row i) for every row.
+ * linalg/tri.c runs the Level-2 forms for N = 3 (below the Level-3
+ * crossover); the BLAS calls are gslcblas's (cblas/source_*_r.h) and are
+ * restated with their loop orders below.  Row-major T, leading dim 3. */
+
+/* gslcblas dtrmv, RowMajor, NoTrans, on the n x n block at T (ld 3), x stride sx */
+static void orc_trmv(int upper, int nonunit, int n, const double* T, double* x, int sx) {
+  if (upper) {
+    for (int i = 0; i < n; i++) {
+      double temp = 0.0;
+      for (int j = i + 1; j < n; j++) temp += x[j * sx] * T[3 * i + j];
+      if (nonunit) x[i * sx] = temp + x[i * sx] * T[3 * i + i];
+      else x[i * sx] += temp;
+    }
+  } else {
+    for (int i = n - 1; i >= 0; i--) {
+      double temp = 0.0;
+      for (int j = 0; j < i; j++) temp += x[j * sx] * T[3 * i + j];
+      if (nonunit) x[i * sx] = temp + x[i * sx] * T[3 * i + i];
+      else x[i * sx] += temp;
+    }
+  }
+}
+
+static void orc_scal(int n, double alpha, double* x, int sx) {
+  for (int i = 0; i < n; i++) x[i * sx] *= alpha;
+}
+
+/* linalg/tri.c triangular_inverse_L2 */
+static void orc_tri_invert_L2(int upper, int nonunit, double* T) {
+  const int N = 3;
+  if (upper) {
+    for (int i = 0; i < N; i++) {
+      double aii;
+      if (nonunit) {
+        T[3 * i + i] = 1.0 / T[3 * i + i];
+        aii = -T[3 * i + i];
+      } else {
+        aii = -1.0;
+      }
+      if (i > 0) {
+        orc_trmv(1, nonunit, i, T, &T[i], 3);          /* m = T[0:i,0:i], v = T[0:i, i] */
+        orc_scal(i, aii, &T[i], 3);
+      }
+    }
+  } else {
+    for (int i = 0; i < N; i++) {
+      const int j = N - i - 1;
+      double ajj;
+      if (nonunit) {
+        T[3 * j + j] = 1.0 / T[3 * j + j];
+        ajj = -T[3 * j + j];
+      } else {
+        ajj = -1.0;
+      }
+      if (j < N - 1) {
+        const int m = N - j - 1;
+        orc_trmv(0, nonunit, m, &T[3 * (j + 1) + (j + 1)], &T[3 * (j + 1) + j], 3);
+        orc_scal(m, ajj, &T[3 * (j + 1) + j], 3);
+      }
+    }
+  }
+}
+
+/* linalg/tri.c triangular_mult_L2, Upper: A <- U L (U upper, L unit lower).
+ * (gcc -O2 warns about indices of loop trips that i < N - 1 excludes.) */
+#pragma GCC diagnostic push
+#pragma GCC diagnostic ignored "-Warray-bounds"
+static void orc_tri_UL_L2(double* A) {
+  const int N = 3;
+  for (int i = 0; i < N; i++) {
+    double* Aii = &A[3 * i + i];
+    const double aii = *Aii;
+    if (i < N - 1) {
+      const int m = N - i - 1;
+      /* ddot(lb = A[i+1:, i], ur = A[i, i+1:]) */
+      double tmp = 0.0;
+      for (int k = 0; k < m; k++) tmp += A[3 * (i + 1 + k) + i] * A[3 * i + (i + 1 + k)];
+      *Aii += tmp;
+      if (i > 0) {
+        /* dgemv(Trans, 1.0, L_BL = A[i+1:, 0:i], ur, aii, lr = A[i, 0:i]) */
+        for (int c = 0; c < i; c++) {
+          double* y = &A[3 * i + c];
+          if (aii == 0.0) *y = 0.0;
+          else if (aii != 1.0) *y *= aii;
+        }
+        for (int r = 0; r < m; r++) {
+          const double temp = 1.0 * A[3 * i + (i + 1 + r)];
+          if (temp != 0.0)
+            for (int c = 0; c < i; c++) A[3 * i + c] += temp * A[3 * (i + 1 + r) + c];
+        }
+        /* dgemv(NoTrans, 1.0, U_TR = A[0:i, i+1:], lb, 1.0, ut = A[0:i, i]) */
+        for (int r = 0; r < i; r++) {
+          double temp = 0.0;
+          for (int c = 0; c < m; c++) temp += A[3 * (i + 1 + c) + i] * A[3 * r + (i + 1 + c)];
+          A[3 * r + i] += 1.0 * temp;
+        }
+      }
+    } else {
+      /* the last row's L part (A[N-1, 0:N-1]) times a_NN */
+      orc_scal(N - 1, aii, &A[3 * (N - 1)], 1);
+    }
+  }
+}
+
+#pragma GCC diagnostic pop
+
+static void orc_lu_invert_gsl(const double* LU, const int* perm, double* inv) {
+  double A[9];
+  memcpy(A, LU, sizeof(A));
+  orc_tri_invert_L2(1, 1, A);  /* U^-1 */
+  orc_tri_invert_L2(0, 0, A);  /* L^-1, unit diagonal */
+  orc_tri_UL_L2(A);            /* U^-1 L^-1 */
+  /* gsl_permute_vector_inverse(p, row): row[p[k]] <- row[k] */
+  for (int r = 0; r < 3; r++)
+    for (int k = 0; k < 3; k++) inv[3 * r + perm[k]] = A[3 * r + k];
+}
+
+int orc_use_gsl_invert = 1;
+
+static void orc_lu_invert(const double* LU, const int* perm, double* inv) {
+  if (orc_use_gsl_invert) orc_lu_invert_gsl(LU, perm, inv);
+  else orc_lu_invert_columns(LU, perm, inv);
+}
+
+/* test hook: one inverse through the selected variant */
+void orc_lu_invert_test(const double* A, double* LU_out, int* perm_out, double* inv, int variant) {
+  double LU[9];
+  int perm[3], sg;
+  memcpy(LU, A, sizeof(LU));
+  orc_lu_decomp(LU, perm, &sg);
+  if (variant) orc_lu_invert_gsl(LU, perm, inv);
+  else orc_lu_invert_columns(LU, perm, inv);
+  memcpy(LU_out, LU, sizeof(LU));
+  for (int i = 0; i < 3; i++) perm_out[i] = perm[i];
 }
 
 /* kullback_leibler.c:28-127.  Returns -1 (n<=1, div 0, no mutation), -2 (singular,
@@ -393,7 +545,7 @@ static int orc_kl_all(orc_nd* nds, const int* len, uint64_t* num_valid, orc_kl* 
       if (orc_neighbor(v, len, d, &w) < 0) continue;
       if (nds[w].n == 0) continue;
       double div = 0;
-      const int rc = orc_kl_divergence(&nds[v], &nds[w], &div);
+      const int rc = ORC_KL_DIVERGENCE(&nds[v], &nds[w], &div);
       if (ev_div) {
         ev_div[e] = div;
         ev_p[e] = (int64_t)v;

@@ -79,6 +79,12 @@ def set_portable_log(on: bool) -> None:
     ctypes.c_int.in_dll(lib(), "orc_use_portable_log").value = 1 if on else 0
 
 
+def set_gsl_invert(on: bool) -> None:
+    """1: gsl_linalg_LU_invert as GSL 2.7.1 publishes it (default);
+    0: the column-solve variant (A/B comparisons only)."""
+    ctypes.c_int.in_dll(lib(), "orc_use_gsl_invert").value = 1 if on else 0
+
+
 @dataclass
 class SearchResult:
     rc: int
@@ -303,3 +309,58 @@ class LegacyChain:
         self.L.free_kl_divergences(self.kl)
         self.nd = ctypes.c_void_p()
         self.kl = ctypes.c_void_p()
+
+
+# ---------------- the reference-structured CPU baseline (oracle/cpu_ref.c) ----------------
+
+CPUREF_LIB = os.path.join(HERE, "libcpu_ref.so")
+_cref = None
+
+
+def cref_lib():
+    global _cref
+    if _cref is None:
+        if not os.path.exists(CPUREF_LIB):
+            build()
+        _cref = ctypes.CDLL(CPUREF_LIB)
+        _cref.cref_downsample.restype = ctypes.c_int
+        _cref.cref_estimate_only.restype = ctypes.c_int
+    return _cref
+
+
+def cref_downsample(points: np.ndarray, k: int):
+    """One ndt_downsample through the reference-structured baseline (8
+    pthreads, mutex per voxel, GSL-style heap traffic, -O0): rows and rc."""
+    pts = np.ascontiguousarray(points, dtype=np.float64)
+    pc, cov = np.zeros((k, 3)), np.zeros((k, 9))
+    nout = _U64(0)
+    rc = cref_lib().cref_downsample(_ptr(pts), _U64(len(pts)), _U64(k), _ptr(pc), _ptr(cov), ctypes.byref(nout))
+    return pc, cov, rc
+
+
+def cref_estimate_only(points: np.ndarray, voxel_size: float, length, offset) -> int:
+    pts = np.ascontiguousarray(points, dtype=np.float64)
+    ln = np.array(length, dtype=np.int32)
+    off = np.array(offset, dtype=np.float64)
+    nn = _U64(0)
+    rc = cref_lib().cref_estimate_only(_ptr(pts), _U64(len(pts)), ctypes.c_double(voxel_size), _ptr(ln), _ptr(off),
+                                       ctypes.byref(nn))
+    assert rc == 0
+    return nn.value
+
+
+def legacy_downsample_rows(points: np.ndarray, k: int) -> int:
+    """One oracle ndt_downsample through its legacy ABI (the lightest call:
+    k output rows, handles freed at once); returns the reference's code.
+    The ctypes call releases the GIL, so threads run clouds in parallel."""
+    pts = np.ascontiguousarray(points, dtype=np.float64)
+    ch = LegacyChain.__new__(LegacyChain)
+    ch.pts, ch.L = pts, lib()
+    ch.lx, ch.ly, ch.lz = ctypes.c_uint(0), ctypes.c_uint(0), ctypes.c_uint(0)
+    ch.ox, ch.oy, ch.oz, ch.vs = (ctypes.c_double(0) for _ in range(4))
+    ch.nd, ch.kl = ctypes.c_void_p(), ctypes.c_void_p()
+    ch.nvalid, ch.nkl, ch.rc = ctypes.c_ulong(0), ctypes.c_ulong(0), 0
+    ch.downsample(k)
+    rc = ch.rc
+    ch.cleanup()
+    return rc

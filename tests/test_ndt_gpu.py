@@ -312,3 +312,31 @@ def test_check_flag_raises_on_failed_cloud():
     with pytest.raises(NdtCloudError) as ei:
         ndt_preprocessing(200, t, check=True)
     assert ei.value.rcs == [0, -3]
+
+
+def _sha_rows(a) -> bytes:
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a, dtype=np.float32).tobytes()).digest()
+
+
+@pytest.mark.parametrize("cfg,kind", [("C2", "U"), ("C2", "L"), ("C5", "U"), ("C5", "L")])
+def test_fullsize_fixture(cfg, kind):
+    """Configs C2 and C5 at full size against the committed full-size fixture
+    (tests/golden/make_fullsize.py): every cloud's float32 rows at every level
+    hash-equal to the oracle's canonical variant (portable log + GSL 2.7.1
+    LU_invert).  The fixture also records, per cloud and level, how many kept
+    NDs the glibc-log and column-inverse variants change: zero everywhere at
+    these sizes, so the HIP rows equal those variants' too."""
+    import torch
+    from ndnet.preprocessing.ndtnet_preprocessing import ndt_multiscale
+    from ndnet.synthetic import make_batch
+    z = golden("fullsize_rows.npz")
+    B, n = int(z["batch"]), int(z["points"])
+    levels = tuple(int(v) for v in z[f"levels_{cfg}"])
+    out = ndt_multiscale(levels, torch.from_numpy(make_batch(kind, B, n)).cuda())
+    sha = z[f"{cfg}_{kind}_sha"]
+    for lv, (p, c, _) in enumerate(out):
+        rows = torch.cat((p, c), dim=2).cpu().numpy()
+        for b in range(B):
+            assert _sha_rows(rows[b]) == sha[b, lv].tobytes(), f"{cfg} {kind} cloud {b} level {levels[lv]}"
+    assert not z[f"{cfg}_{kind}_glibc_extra"].any() and not z[f"{cfg}_{kind}_columns_extra"].any()

@@ -144,3 +144,59 @@ def test_prune_walk_quirks():
     ch.prune(128)
     assert ch.rc == 0 and ch.nvalid.value == 128 and ch.nkl.value == nkl0 - 128
     ch.cleanup()
+
+
+def _lu_invert(A, variant):
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    LU, perm, inv = np.zeros(9), np.zeros(3, np.int32), np.zeros(9)
+    O.lib().orc_lu_invert_test(O._ptr(A), O._ptr(LU), O._ptr(perm), O._ptr(inv), ctypes.c_int(variant))
+    return inv.reshape(3, 3), LU.reshape(3, 3), perm
+
+
+def test_gsl_lu_invert_restatement():
+    """gsl_linalg_LU_invert as GSL 2.7.1 publishes it (tri_invert U, tri_invert
+    L unit, tri_UL, inverse column permutation; kullback_leibler.c:92): an
+    inverse to rounding, its permutation handling exact, and a rounding
+    sequence of its own (it differs in the last bits from the column-solve
+    variant round 1 used)."""
+    rng = np.random.default_rng(0)
+    differs = 0
+    for _ in range(2000):
+        A = rng.normal(size=(3, 3))
+        g, _, _ = _lu_invert(A, 1)
+        c, _, _ = _lu_invert(A, 0)
+        ref = np.linalg.inv(A)
+        assert np.abs(g - ref).max() <= 1e-11 * np.abs(ref).max()
+        differs += not np.array_equal(g, c)
+    assert differs > 1000
+    # a pure permutation with exact entries: exact inverse, and U^-1 L^-1 by hand
+    P = 2.0 * np.array([[0, 1, 0], [0, 0, 1], [1, 0, 0]], dtype=np.float64)
+    g, _, perm = _lu_invert(P, 1)
+    assert np.array_equal(g, P.T / 4.0)
+    A = np.array([[4.0, 3.0, 2.0], [2.0, 1.0, 3.0], [3.0, 2.0, 1.0]])
+    g, LU, perm = _lu_invert(A, 1)
+    U, L = np.triu(LU), np.tril(LU, -1) + np.eye(3)
+    Pm = np.zeros((3, 3))
+    Pm[np.arange(3), perm] = 1.0
+    assert np.allclose(Pm @ A, L @ U, rtol=0, atol=1e-15)
+    assert np.allclose(g, np.linalg.inv(U) @ np.linalg.inv(L) @ Pm, rtol=1e-15, atol=1e-15)
+
+
+def test_fullsize_fixture_pins_oracle():
+    """The oracle still produces the committed full-size digests (one cloud of
+    each C2 / C5 case; tests/golden/make_fullsize.py)."""
+    import hashlib
+    from ndnet.synthetic import make_batch
+    z = golden("fullsize_rows.npz")
+    for cfg in ("C2", "C5"):
+        levels = [int(v) for v in z[f"levels_{cfg}"]]
+        for kind, b in (("U", 3), ("L", 5)):
+            pts = make_batch(kind, b + 1, int(z["points"]))[b].astype(np.float64)
+            ch = O.LegacyChain(pts)
+            res = [ch.downsample(levels[0])] + [ch.prune(k) for k in levels[1:]]
+            ch.cleanup()
+            for lv, (pc, cov) in enumerate(res):
+                rows = np.zeros((len(pc), 12), np.float32)
+                rows[:, :3] = np.nan_to_num(pc.astype(np.float32), nan=0.0, posinf=0.0, neginf=0.0)
+                rows[:, 3:] = np.nan_to_num(cov.astype(np.float32), nan=0.0, posinf=0.0, neginf=0.0)
+                assert hashlib.sha256(rows.tobytes()).digest() == z[f"{cfg}_{kind}_sha"][b, lv].tobytes()

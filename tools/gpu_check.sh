@@ -1,5 +1,6 @@
 #!/bin/bash
-# One GPU-box pass: parity tests, smoke, bench, rocprofv3 kernel stats.
+# One GPU-box pass: parity tests, smoke, bench, rocprofv3 kernel stats of the
+# pipelined bench and of an isolated (one graph per step, no overlap) run.
 # Usage (from the repo root, on the GPU box): bash tools/gpu_check.sh TAG
 set -o pipefail
 TAG=${1:-run}
@@ -14,4 +15,5 @@ timeout -k 10 300 python -u bench.py > $OUT/bench.log 2>&1 || { echo "bench fail
 tail -1 $OUT/bench.log
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $R/bench.py --steps 10 --no-cpu-baseline > $OUT/prof.log 2>&1 || { echo "rocprof failed"; tail -30 $OUT/prof.log; exit 1; }
-find $OUT/prof -name "*stats*" | head
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_iso -o run -- python3 $R/bench.py --steps 10 --no-pipeline --no-cpu-baseline > $OUT/prof_iso.log 2>&1 || { echo "rocprof iso failed"; tail -30 $OUT/prof_iso.log; exit 1; }
+find $OUT/prof $OUT/prof_iso -name "*stats*" | head

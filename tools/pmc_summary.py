@@ -54,8 +54,10 @@ def main():
         row["dispatches"] = max(len(v) for v in cs.values())
         if "FETCH_SIZE" in row and "WRITE_SIZE" in row:
             row["hbm_bytes"] = 2 * row["FETCH_SIZE"] * 1024 + row["WRITE_SIZE"] * 1024
-        if "SQ_VALU_MFMA_BUSY_CYCLES" in row and "SQ_BUSY_CYCLES" in row and row["SQ_BUSY_CYCLES"]:
-            row["mfma_busy_per_sq_busy"] = row["SQ_VALU_MFMA_BUSY_CYCLES"] / row["SQ_BUSY_CYCLES"]
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in row and row.get("GRBM_GUI_ACTIVE"):
+            # MFMA cycles summed over all SIMDs / (GUI-active cycles summed over
+            # the 8 XCDs x 128 SIMDs per XCD): the matrix pipes' busy fraction
+            row["mfma_busy_frac"] = row["SQ_VALU_MFMA_BUSY_CYCLES"] / (row["GRBM_GUI_ACTIVE"] * 128.0)
         out[k] = row
     for k, row in sorted(out.items(), key=lambda kv: -kv[1].get("GRBM_GUI_ACTIVE", 0)):
         print(k)
