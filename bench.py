@@ -122,6 +122,7 @@ def main() -> None:
     ap.add_argument("--levels", default=None,
                     help="config C5: comma-separated NDs per level, e.g. 2000,1000,500 (downsample, then prune; "
                          "a forward per level)")
+    ap.add_argument("--no-other", action="store_true", help="skip the other-distribution (U <-> L) timing")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / shard split / timing skeleton on CPU (gloo), no GPU work")
     args = ap.parse_args()
@@ -207,7 +208,7 @@ def main() -> None:
     # ---- the other synthetic distribution on the same graph (SURVEY §8d "also
     # report L"): the L clouds exercise the prune (~128 of ~1128 NDs removed) ----
     other = None
-    if not args.eager and not levels:
+    if not args.eager and not levels and not args.no_other:
         okind = "L" if args.kind == "U" else "U"
         opts = torch.from_numpy(make_batch(okind, B, n, seed0=shard0)).to(dev)
         if hasattr(graphed, "load_resident"):

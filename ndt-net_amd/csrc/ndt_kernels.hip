@@ -158,6 +158,8 @@ struct Plan {
   unsigned long long* fmarks; // [B][kFrontMarkStride]: k_front phase stamps of WG 0 + start/end of every WG (timing level 2)
   unsigned long long* wmarks; // [B][wg][4] k_welford stamps (timing level 2)
   uint32_t wgrid;             // k_welford workgroups: min(CUs, group capacity of the batch)
+  double* rtab;               // [n + 1] refined reciprocals of the counts 1..n+1 (k_welford_q)
+  size_t wq_lds;              // k_welford_q dynamic LDS (labelled runs: class histograms)
 };
 
 // ------------------------------------------------------------------ helpers
@@ -1067,6 +1069,215 @@ __global__ void __launch_bounds__(kWelfordThreads) k_welford(const CloudCtl* ctl
   }
 }
 
+// k_welford_q: the same per-ND Welford (same lane quad, same double
+// operations on the same operands, so the same bits), without LDS windows:
+// every quad streams its own ND's points from nd_pts, so a wave runs as long as
+// its longest ND and no ND waits for another's window.  Per sample, lane j
+// (< 3) loads its own coordinate x_j, updates
+//   t = x - mean; mean += t / n; u = x - mean; m2 += t * u
+// and for its off-diagonal pair (a, b) = (0,1), (1,2), (0,2) takes u_a (axis
+// a already updated) and t_b (axis b not yet: x_b - old mean_b) from the quad
+// by DPP: cov_ab += u_a * t_b / n (normal_distributions.c:82-103, axes in
+// order).  The two divisions by n use the refined reciprocal of n
+// (div_fast: bit-identical to the division over the operand range that
+// finite float coordinates guarantee); n = step + 1 is the same for every
+// quad of a wave at a given step, so the reciprocal comes from a
+// plan-lifetime table by a scalar load.  Coordinates are prefetched into two
+// register blocks of kWqU samples (one block in flight while the other is
+// folded).  A quad that meets a coordinate outside that range (non-finite
+// float, or a double outside [2^-300, 2^300]) refolds its ND with IEEE
+// divisions and the reference's NaN -> 0 step.  Labelled runs: lane 0 of the
+// quad builds the class histogram in LDS (first index of the max,
+// normal_distributions.c:107-121).
+constexpr int kWqThreads = 256;              // 4 waves x 16 quads
+constexpr int kWqNDs = kWqThreads / 4;
+constexpr int kWqU = 16;                     // samples per prefetch block
+constexpr int kWqHistMax = 64 * 1024;        // LDS class histograms up to this size, else global
+
+template <int CTRL>
+__device__ inline double dpp_d(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32));
+}
+
+template <typename T>
+__device__ inline bool wq_in_range(T v) {
+  if constexpr (sizeof(T) == 4) {
+    return (__builtin_bit_cast(uint32_t, v) & 0x7f800000u) != 0x7f800000u;  // finite
+  } else {
+    const double a = fabs((double)v);
+    return a == 0.0 || (a >= 0x1p-300 && a <= 0x1p300);
+  }
+}
+
+// v_cndmask on both halves of a double, as inline asm: a plain `c ? a : b`
+// lets the compiler turn the update it selects into an exec-masked branch,
+// which ends the basic block and with it the overlap of consecutive samples.
+__device__ inline double sel_d(unsigned long long lanes, double a, double b) {  // lanes set: a
+  const unsigned long long ua = __builtin_bit_cast(unsigned long long, a);
+  const unsigned long long ub = __builtin_bit_cast(unsigned long long, b);
+  uint32_t lo, hi;
+  asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(lo) : "v"((uint32_t)ub), "v"((uint32_t)ua), "s"(lanes));
+  asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(hi) : "v"((uint32_t)(ub >> 32)), "v"((uint32_t)(ua >> 32)), "s"(lanes));
+  return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32));
+}
+
+__device__ inline uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t w = (uint32_t)__shfl_xor((int)v, o, 64);
+    v = w > v ? w : v;
+  }
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
+__global__ void k_rtab_init(double* rtab, uint64_t count) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) rtab[i] = recip_refined((double)(i + 1));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, const T* __restrict__ nd_pts,
+                                                          const uint16_t* __restrict__ nd_lbl,
+                                                          const uint32_t* __restrict__ nd_n,
+                                                          const uint32_t* __restrict__ nd_base,
+                                                          const double* __restrict__ rtab, double* nd_mean,
+                                                          double* nd_cov, uint16_t* nd_cls, uint32_t* hist_all,
+                                                          int ncls, uint64_t n, uint32_t ndcap) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t wq_hist[];
+  const int b = blockIdx.y;
+  const CloudCtl& c = ctl[b];
+  if (c.state != kAccepted) return;
+  const uint32_t nd = c.num_nds;
+  const uint32_t lane = threadIdx.x & 63, j = lane & 3;
+  const uint32_t wd0 = blockIdx.x * kWqNDs + (threadIdx.x >> 6) * 16;  // first ND of my wave
+  if (wd0 >= nd) return;                                                  // wave-uniform
+  const uint32_t d = wd0 + (lane >> 2);
+  const bool live = d < nd;
+  const uint64_t o = (uint64_t)b * ndcap + (live ? d : wd0);
+  const uint32_t beg = nd_base[o];
+  const uint32_t cnt = live ? nd_n[o] : 0u;
+  const uint32_t last = cnt ? cnt - 1u : 0u;
+  const uint32_t jj = j < 3 ? j : 0u;
+  const T* src = nd_pts + ((uint64_t)b * n + beg) * 3 + jj;
+  const uint32_t mx = wave_max_u32(cnt);
+
+  double mean = 0.0, m2 = 0.0, off = 0.0;
+  bool bad = false;
+  // the reciprocals ride in the same in-order vector-load stream as the points
+  // (a uniform address would become a scalar load, waited for at its use with
+  // lgkmcnt(0) behind every younger scalar load): an opaque zero makes the
+  // address per-lane
+  uint32_t zero;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
+  const double* rt = rtab + zero;
+  const uint32_t rlast = mx ? mx - 1u : 0u;
+  T ra[kWqU], rb[kWqU];
+  double ca[kWqU], cb[kWqU];
+  auto load = [&](T (&r)[kWqU], double (&cr)[kWqU], uint32_t q0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < kWqU; u++) {
+      const uint32_t q = q0 + (uint32_t)u;
+      r[u] = src[3u * (q < last ? q : last)];
+      cr[u] = rt[q < rlast ? q : rlast];
+    }
+  };
+  // one block of samples; kExact: IEEE divisions and the NaN -> 0 step
+  // Branch-free over the block (a lane past its count keeps its state by
+  // selects), so the scheduler overlaps the off-diagonal tail of sample q
+  // with the mean chain of sample q + 1.
+  auto fold = [&](const T (&r)[kWqU], const double (&cr)[kWqU], uint32_t q0, bool act,
+                  auto exact_tag) __attribute__((always_inline)) {
+    constexpr bool kExact = decltype(exact_tag)::value;
+#pragma unroll
+    for (int u = 0; u < kWqU; u++) {
+      const uint32_t q = q0 + (uint32_t)u;
+      const bool on = act && q < cnt;          // quad-uniform
+      const double cn = (double)(q + 1u);
+      const double rc = cr[u];
+      const double x = (double)r[u];
+      if constexpr (!kExact) bad |= on && !wq_in_range(r[u]);
+      const double t = x - mean;
+      const double nm = mean + (kExact ? t / cn : div_fast(t, cn, rc));
+      const double uu = x - nm;
+      const double nm2 = m2 + t * uu;
+      const double ua = dpp_d<0xC4>(uu);   // quad_perm [0,1,0,3]: u of axis a
+      const double tb = dpp_d<0xE9>(t);    // quad_perm [1,2,2,3]: t of axis b
+      const double pr = ua * tb;
+      double noff;
+      if constexpr (kExact) {
+        const double cv = off + pr / cn;
+        noff = (cv != cv) ? 0.0 : cv;
+      } else {
+        noff = off + div_fast(pr, cn, rc);
+      }
+      const unsigned long long lanes = __ballot(on);
+      mean = sel_d(lanes, nm, mean);
+      m2 = sel_d(lanes, nm2, m2);
+      off = sel_d(lanes, noff, off);
+    }
+  };
+  auto run = [&](uint32_t lim, bool act, auto exact_tag) __attribute__((always_inline)) {
+    load(ra, ca, 0);
+    load(rb, cb, kWqU);
+    for (uint32_t q0 = 0; q0 < lim; q0 += 2 * kWqU) {
+      fold(ra, ca, q0, act, exact_tag);
+      load(ra, ca, q0 + 2 * kWqU);
+      if (q0 + kWqU < lim) fold(rb, cb, q0 + kWqU, act, exact_tag);  // wave-uniform
+      load(rb, cb, q0 + 3 * kWqU);
+    }
+  };
+  run(mx, true, std::false_type{});
+  // a quad whose coordinates left the fast range refolds exactly
+  const bool qbad = __builtin_amdgcn_mov_dpp((int)bad, 0x00, 0xF, 0xF, false) |
+                    __builtin_amdgcn_mov_dpp((int)bad, 0x55, 0xF, 0xF, false) |
+                    __builtin_amdgcn_mov_dpp((int)bad, 0xAA, 0xF, 0xF, false);  // lanes 0..2 of the quad
+  if (__any(qbad)) {
+    const uint32_t mx2 = wave_max_u32(qbad ? cnt : 0u);
+    if (qbad) {
+      mean = 0.0;
+      m2 = 0.0;
+      off = 0.0;
+    }
+    run(mx2, qbad, std::true_type{});
+  }
+  if (live && j < 3) {
+    const double v = m2 / (double)cnt;
+    nd_mean[3 * o + j] = mean;
+    nd_cov[9 * o + 4 * j] = (v != v) ? 0.0 : v;
+    const uint32_t ia = j == 2 ? 0u : j, ib = j == 2 ? 2u : j + 1u;
+    nd_cov[9 * o + 3 * ia + ib] = off;
+    nd_cov[9 * o + 3 * ib + ia] = off;
+  }
+  if (live && j == 0) {
+    uint16_t cls = 0;
+    if (nd_lbl) {
+      const uint32_t nb = (uint32_t)ncls + 1u;
+      const bool lds = (size_t)kWqNDs * nb * sizeof(uint32_t) <= (size_t)kWqHistMax;
+      uint32_t* hist = lds ? wq_hist + (threadIdx.x >> 2) * nb : hist_all + o * nb;
+      for (uint32_t k = 0; k < nb; k++) hist[k] = 0;
+      const uint16_t* l = nd_lbl + (uint64_t)b * n + beg;
+      uint32_t s2 = 0;
+      for (; s2 + 8 <= cnt; s2 += 8) {
+        uint16_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = l[s2 + k];
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+          if (v[k] < nb) hist[v[k]]++;
+      }
+      for (; s2 < cnt; s2++)
+        if (l[s2] < nb) hist[l[s2]]++;
+      uint32_t best = 0;
+      for (uint32_t k = 0; k < nb; k++)
+        if (hist[k] > best) { best = hist[k]; cls = (uint16_t)k; }
+    }
+    nd_cls[o] = cls;
+  }
+}
+
 // Bitonic sort of (key, idx) pairs ascending, n a power of two, within one workgroup.
 // phase stamp of k_kl (timing level 2): 100 MHz constant clock
 #define KL_MARK(i)                                                                   \
@@ -1948,7 +2159,7 @@ static void plan_free(Plan* P) {
                   P->nd_mean, P->nd_cov, P->nd_cov_post, P->nd_cls, P->hist, P->nb, P->keys, P->nkeys,
                   P->chain, P->chain_ps, P->slot_val, P->slot_flag, P->ev_val, P->ev_p, P->ev_q, P->ev_min,
                   P->sort_key, P->sort_idx, P->nan_list, P->nan_key, P->nan_slot, P->chunk_nanbase, P->ord_val, P->ord_p, P->ord_q,
-                  P->first_occ, P->tmp_u32, P->alive, P->d_stats, P->chunk_cnt, P->chunk_min};
+                  P->first_occ, P->tmp_u32, P->alive, P->d_stats, P->chunk_cnt, P->chunk_min, P->rtab};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete P;
@@ -2071,10 +2282,9 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
                                                                P->ndcap, P->nbins);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[4], st));
   }
-  k_welford<T><<<P->wgrid, kWelfordThreads, kWelfordBytes + kRtab * sizeof(double), st>>>(P->ctl, B, (const T*)P->nd_pts,
-                                                                  lbl ? P->nd_lbl : nullptr, P->nd_n, P->nd_base,
-                                                                  P->nd_mean, P->nd_cov, P->nd_cls, P->hist, P->ncls,
-                                                                  n, P->ndcap, P->timing >= 2 ? P->wmarks : nullptr);
+  k_welford_q<T><<<dim3((P->ndcap + kWqNDs - 1) / kWqNDs, B), kWqThreads, lbl ? P->wq_lds : 0, st>>>(
+      P->ctl, (const T*)P->nd_pts, lbl ? P->nd_lbl : nullptr, P->nd_n, P->nd_base, P->rtab, P->nd_mean, P->nd_cov,
+      P->nd_cls, P->hist, P->ncls, n, P->ndcap);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[5], st));
   KLArgs A = kl_args(P, P->k, out, out_cls, pc64, cov64, cls16);
   A.stats_out = stats_dst;
@@ -2177,6 +2387,7 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   A_(chunk_cnt, B * P->nchunk);
   A_(chunk_min, B * P->nchunk);
   A_(d_stats, B);
+  A_(rtab, n + 1);
   // k_front: G workgroups per cloud, all resident together (G * B <= CUs);
   // each owns bpw bins, whose per-ND counts and ranks live in its LDS
   {
@@ -2222,6 +2433,14 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   if (e == hipSuccess) e = hipMemset(P->fbar, 0, B * kBarStride * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(P->stamps, 0, B * P->vcap * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(P->d_stats, 0, B * sizeof(ndnet_ndt_stats));
+  if (e == hipSuccess) {
+    k_rtab_init<<<(unsigned)((n + 1 + 255) / 256), 256>>>(P->rtab, n + 1);
+    e = hipGetLastError();
+  }
+  {
+    const size_t hb = (size_t)kWqNDs * (size_t)nb * sizeof(uint32_t);
+    P->wq_lds = num_classes >= 0 && hb <= (size_t)kWqHistMax ? hb : 0;
+  }
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_kl_merge<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(2 * kMergeLdsChunks * kChunk * sizeof(unsigned long long)));

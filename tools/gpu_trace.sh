@@ -1,0 +1,13 @@
+#!/bin/bash
+# Kernel trace of one bench configuration (isolated: one graph per step).
+# Usage (repo root, GPU box): bash tools/gpu_trace.sh TAG [bench args...]
+set -o pipefail
+TAG=${1:-trace}
+shift
+R=$(pwd)
+OUT=$R/gpurun_out/$TAG
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $R/bench.py --no-pipeline --no-cpu-baseline --no-other "$@" > $OUT/prof.log 2>&1 || { echo "rocprof failed"; tail -30 $OUT/prof.log; exit 1; }
+tail -1 $OUT/prof.log | cut -c1-300
+python3 $R/tools/trace_summary.py $OUT/prof --skip 3 | head -30

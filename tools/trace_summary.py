@@ -1,0 +1,35 @@
+#!/usr/bin/env python3
+"""Per-kernel duration distribution from a rocprofv3 --kernel-trace CSV dir.
+
+    python tools/trace_summary.py gpurun_out/TAG/prof [--skip N]
+
+--skip drops the first N dispatches of every kernel (warm-up)."""
+import collections
+import csv
+import glob
+import os
+import re
+import sys
+
+import numpy as np
+
+
+def main():
+    d = sys.argv[1]
+    skip = int(sys.argv[sys.argv.index("--skip") + 1]) if "--skip" in sys.argv else 0
+    f = glob.glob(os.path.join(d, "*kernel_trace.csv"))[0]
+    rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
+    dur = collections.defaultdict(list)
+    for r in rows:
+        m = re.search(r"(k_\w+(?:<[^>]*>)?)", r["Kernel_Name"])
+        k = m.group(1) if m else r["Kernel_Name"][:40]
+        dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0)
+    tot = 0.0
+    print(f"{'kernel':34s} {'n':>5s} {'median us':>10s} {'p10':>8s} {'p90':>8s}")
+    for k, v in sorted(dur.items(), key=lambda kv: -np.median(kv[1][skip:] or kv[1]) * len(kv[1])):
+        v = np.array(v[skip:] or v)
+        print(f"{k:34s} {len(v):5d} {np.median(v):10.1f} {np.percentile(v, 10):8.1f} {np.percentile(v, 90):8.1f}")
+
+
+if __name__ == "__main__":
+    main()
