@@ -126,6 +126,14 @@ void ndnet_ndt_plan_destroy(void *plan);
 int ndnet_ndt_set_path(void *plan, int path);
 int ndnet_ndt_get_path(void *plan);
 
+/* The bisection (ndt.c:144-187) takes hi = guess whenever a grid has fewer
+ * voxels (or the cloud fewer estimated points) than num_desired: such a grid
+ * cannot reach k occupied voxels, so path 2 does not count it and the debug
+ * dump reports its count as 0xFFFFFFFF.  Guesses, decisions and outputs are
+ * unchanged.  on = 1 counts every grid anyway (the parity tests compare every
+ * count with the reference's); default 0.  Path 1 always counts. */
+int ndnet_ndt_set_exact_counts(void *plan, int on);
+
 /* d_points: [batch][num_points][3] float32 on the device (the tensor
  * ndt_preprocessing receives).  d_labels: [batch][num_points] int32 class ids
  * or NULL.  d_out: [batch][num_desired][12] float32 = mean(3) | covariance(9)
@@ -182,12 +190,6 @@ int ndnet_ndt_debug_front_marks(void *plan, unsigned long long *marks);
 /* Start / end stamps (s_memrealtime) of every k_front workgroup of the last
  * run at timing level 2: marks[B][G][2]; *G = workgroups per cloud. */
 int ndnet_ndt_debug_front_wg_marks(void *plan, unsigned long long *marks, int *G);
-
-/* k_welford stamps of the last run at timing level 2: per cloud and
- * workgroup (16 NDs) 4 marks -- start, points staged, samples folded, end --
- * as marks[(cloud * wgs + wg) * 4 + i], wgs = ceil((floor(1.2 k) + 1) / 16);
- * synchronises. */
-int ndnet_ndt_debug_welford_marks(void *plan, unsigned long long *marks);
 
 /* Library identification (no GPU needed). */
 const char *ndnet_amd_version(void);

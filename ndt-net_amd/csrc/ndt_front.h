@@ -80,6 +80,7 @@ struct FrontArgs {
   uint32_t ndcap, G, bpw;
   uint32_t rbs;                 // points per rank bin (512 or 1024)
   int dbg_store;
+  int eval_all;                 // 1: count every bisection grid (debug / parity); 0: skip grids too small to matter
 };
 
 // The shared bisection state of one workgroup (every workgroup of a cloud
@@ -91,6 +92,8 @@ struct FrontState {
   uint32_t len[3];
   uint64_t V;
   uint32_t state, iter, stamp, mode, num_nds;
+  uint32_t npass;                   // passes actually counted (their parity alternates the pass slots)
+  uint32_t skip;                    // this iteration's grid has fewer voxels than k: no pass
   int32_t rc;
   uint32_t cut[kWorkers];
   uint32_t sync_no;
@@ -279,6 +282,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
 
   if (t == 0) {
     s.sync_no = 0;
+    s.npass = 0;
     s.puse[0] = s.puse[1] = 0;
     s.psum_prev[0] = s.psum_prev[1] = 0;
     s.ok = 1;
@@ -393,18 +397,44 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
       }
       s.V = V;
       s.stamp = epoch * 32u + s.iter;
+      // A grid of fewer voxels than k (or than the n8 estimated points)
+      // cannot hold k occupied voxels: ndt.c:176-179 takes hi = guess
+      // whatever the count, so the pass is not run (eval_all: it is, for the
+      // parity tests that compare every count with the reference's).
+      const uint64_t bound = V < n8 ? V : n8;
+      s.skip = !A.eval_all && bound < A.k;
       if (V > A.vcap) {  // the reference's malloc of V NDs would be the failure point
         s.state = kFailed;
         s.rc = -1;
         s.vs = s.guess;
+        s.skip = 0;
       }
     }
     __syncthreads();
     if (s.state != kSearching) break;
+    if (s.skip) {
+      if (t == 0) {
+        if (g == 0 && s.iter < 16) {
+          c.guesses[s.iter] = s.guess;
+          c.counts[s.iter] = kInvalid;  // not counted (< k)
+        }
+        s.hi = s.guess;
+        s.iter++;
+        const double gn = s.lo + (s.hi - s.lo) / 2.0;
+        s.guess = gn;
+        if (s.iter == (uint32_t)kMaxIters) {
+          s.state = kFailed;
+          s.rc = -3;  // "Reached maximum number of iterations!" (ndt.c:191-194)
+          s.vs = gn;
+        }
+      }
+      __syncthreads();
+      continue;
+    }
     const uint64_t V = s.V;
     const bool small = V <= (uint64_t)kBitsCap;
     const uint32_t words = small ? (uint32_t)((V + 31) / 32) : 0u;
-    const uint32_t parity = s.iter & 1u;
+    const uint32_t parity = s.npass & 1u;
     const uint32_t stamp = s.stamp;
     uint32_t* gb = A.gbits + ((uint64_t)b * 2 + parity) * kBitsWords;
     if (small) {
@@ -517,7 +547,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
         for (int w = 0; w < kWorkers; w++) st_sc1(rec + g * kRecWords + 2 + w, s_bad[w]);
     }
     FRONT_MARK(3 + 2 * (s.iter < 7 ? s.iter : 7));
-    if (!pass_sync(s, bar, G, fresh, anyb, s.iter & 1u)) goto fail;
+    if (!pass_sync(s, bar, G, fresh, anyb, parity)) goto fail;
     FRONT_MARK(4 + 2 * (s.iter < 7 ? s.iter : 7));
     if (t < (uint32_t)kWorkers) s.cut[t] = kInvalid;
     __syncthreads();
@@ -561,6 +591,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
         c.counts[s.iter] = count;
       }
       s.mode = mode;
+      s.npass++;
       if ((double)count > (double)A.k * (1 + kUpper)) {
         s.lo = s.guess;
       } else if (count < A.k) {

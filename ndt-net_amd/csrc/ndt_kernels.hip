@@ -156,10 +156,10 @@ struct Plan {
   uint32_t* fwgcnt;          // [B][fG][ndcap]
   uint32_t* fbar;            // [B][kBarStride]
   unsigned long long* fmarks; // [B][kFrontMarkStride]: k_front phase stamps of WG 0 + start/end of every WG (timing level 2)
-  unsigned long long* wmarks; // [B][wg][4] k_welford stamps (timing level 2)
-  uint32_t wgrid;             // k_welford workgroups: min(CUs, group capacity of the batch)
-  double* rtab;               // [n + 1] refined reciprocals of the counts 1..n+1 (k_welford_q)
+  int exact_counts;           // k_front counts every bisection grid (ndnet_ndt_set_exact_counts)
   size_t wq_lds;              // k_welford_q dynamic LDS (labelled runs: class histograms)
+  uint32_t wq_grid;           // k_welford_q workgroups: one per CU
+  uint32_t* wq_ctr;           // [2] k_welford_q dynamic item counter (re-armed by k_kl_chains)
 };
 
 // ------------------------------------------------------------------ helpers
@@ -785,290 +785,6 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_scatter(const T* __restrict
 
 #include "ndt_front.h"
 
-// Welford per ND (normal_distributions.c:75-121) over its contiguous,
-// index-ordered points, bit-exact.  The update of one sample is three
-// independent axis chains plus three off-diagonal terms, so an ND runs on a
-// lane quad: lane j (0..2) carries mean_j, m2_j and the variance of axis j,
-// plus one off-diagonal term -- lane 0 (0,1), lane 1 (1,2), lane 2 (0,2) --
-// whose other operand comes from the neighbouring lane through one DPP quad
-// permute per sample (the new mean of axis 0 for lane 2, the not yet updated
-// mean of axis j+1 for lanes 0 and 1: the reference updates the axes in
-// order, normal_distributions.c:86-101).  Every lane performs exactly the
-// reference's double operations on the same operands.  The two divisions by
-// the sample count per lane and sample share one refined reciprocal
-// (div_by_recip, bit-identical to the division), which takes them off the
-// loop-carried chain; only the variance's final m2 / n is a plain division.
-// One wave per workgroup (16 NDs): its points (a contiguous range of nd_pts)
-// are staged through LDS with one batch of coalesced 16-byte loads.
-constexpr int kWelfordNDs = 64;          // NDs per workgroup: 4 waves x 16 quads (one wave per SIMD of a CU)
-constexpr int kWelfordThreads = 4 * kWelfordNDs;
-constexpr int kWelfordBytes = 96 * 1024; // LDS window (one workgroup per CU)
-constexpr int kWelfordVecs = 20;         // 16-byte loads per thread per window, all in flight at once
-constexpr int kRtab = 2048;              // refined reciprocals of the counts 1..kRtab, in LDS after the window
-
-__device__ inline double quad_perm_120(double v) {  // lane i of a quad <- lane [1,2,0,3][i]
-  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, 0xC9, 0xF, 0xF, false);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), 0xC9, 0xF, 0xF, false);
-  return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32));
-}
-
-#define W_MARK(i)                                                                                             \
-  do {                                                                                                        \
-    if (marks && threadIdx.x == 0) marks[((uint64_t)b * gpc + gi) * 4 + (i)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-
-// One group of kWelfordNDs consecutive NDs of cloud b.
-template <int CTRL>
-__device__ inline double dpp_f64(double v) {  // DPP move of a double (both halves, same control)
-  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, false);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
-  return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32));
-}
-
-template <typename T>
-__device__ void welford_group(const CloudCtl& c, const int b, const uint32_t gi, const uint32_t gpc,
-                              const T* __restrict__ nd_pts, const uint16_t* __restrict__ nd_lbl, const uint32_t* nd_n,
-                              const uint32_t* nd_base, double* nd_mean, double* nd_cov, uint16_t* nd_cls,
-                              uint32_t* hist_all, int ncls, uint64_t n, uint32_t ndcap, unsigned long long* marks,
-                              const double* rtab) {
-  constexpr uint32_t kVec = 16 / sizeof(T);                            // elements per 16-byte load
-  constexpr uint32_t kWin = (kWelfordBytes - 32) / (3 * sizeof(T));     // points per window (+ alignment lead)
-  extern __shared__ __attribute__((aligned(16))) unsigned char w_smem[];
-  T* sp = (T*)w_smem;
-  const uint32_t nd = c.num_nds;
-  const uint32_t d0 = gi * kWelfordNDs;
-  W_MARK(0);
-  const uint32_t dl = (d0 + kWelfordNDs < nd ? d0 + kWelfordNDs : nd) - 1;  // last ND of the workgroup
-  const uint64_t ob = (uint64_t)b * ndcap;
-  const uint32_t lane = threadIdx.x & 63, j = lane & 3;
-  const uint32_t d = d0 + (threadIdx.x >> 2);
-  const bool live = d <= dl;
-  const uint32_t dd = live ? d : dl;
-  const uint32_t beg = nd_base[ob + dd], cnt = live ? nd_n[ob + dd] : 0u;
-  const uint32_t r0 = nd_base[ob + d0], r1 = nd_base[ob + dl] + nd_n[ob + dl];  // the workgroup's point range
-  const uint32_t jj = j < 3 ? j : 0u;           // my axis
-  const uint32_t pj = jj == 2 ? 0u : jj + 1u;   // my partner's axis
-  double mean = 0.0, m2 = 0.0, off = 0.0, cntd = 0.0;
-  // fold<false>: divisions through the shared reciprocal; a lane that meets an
-  // operand outside its exact range flags `bad` and the whole workgroup then
-  // folds again with plain divisions (fold<true>; never on ordinary data)
-  auto fold = [&](auto exact_tag) -> bool {
-    constexpr bool kExact = decltype(exact_tag)::value;
-    mean = 0.0;
-    m2 = 0.0;
-    off = 0.0;
-    cntd = 0.0;
-    bool bad = false;
-    for (uint32_t w0 = r0; w0 < r1; w0 += kWin) {
-      const uint32_t wn = r1 - w0 < kWin ? r1 - w0 : kWin;
-      // coalesced 16-byte copy of points [w0, w0 + wn) from the aligned-down
-      // element ge0 (nd_pts is 256-byte aligned and carries kNdSlack points of
-      // padding, so the rounded-up tail stays in bounds)
-      const uint64_t ge0 = ((uint64_t)b * n + w0) * 3;
-      const uint64_t a0 = ge0 & ~(uint64_t)(kVec - 1);
-      const uint32_t lead = (uint32_t)(ge0 - a0);
-      __syncthreads();
-      {
-        typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
-        const u32x4* gsrc = (const u32x4*)(nd_pts + a0);
-        u32x4* ldst = (u32x4*)sp;
-        const uint32_t nvec = (lead + 3 * wn + kVec - 1) / kVec;
-        for (uint32_t base = threadIdx.x; base < nvec; base += kWelfordThreads * kWelfordVecs) {
-          // unconditional loads (a clamped index past the end): a predicated
-          // load compiles to a branch with its own vmcnt(0) wait, serialising
-          // the batch
-          u32x4 r[kWelfordVecs];
-#pragma unroll
-          for (int u = 0; u < kWelfordVecs; u++) {
-            const uint32_t i = base + kWelfordThreads * u;
-            r[u] = gsrc[i < nvec ? i : nvec - 1];
-          }
-#pragma unroll
-          for (int u = 0; u < kWelfordVecs; u++) {
-            const uint32_t i = base + kWelfordThreads * u;
-            if (i < nvec) ldst[i] = r[u];
-          }
-          if constexpr (!kExact) {
-            // the fast fold's operand range: every coordinate 0 or 2^-300 <=
-            // |c| <= 2^300 (every finite float is), so no quotient operand
-            // leaves div_fast's exact range and no NaN can arise
-#pragma unroll
-            for (int u = 0; u < kWelfordVecs; u++) {
-              const uint32_t i = base + kWelfordThreads * u;
-              const T* e = (const T*)&r[u];
-#pragma unroll
-              for (uint32_t k = 0; k < kVec; k++) {
-                const uint32_t el = i * kVec + k;
-                bool in;
-                if constexpr (sizeof(T) == 4) {
-                  in = (r[u][k] & 0x7f800000u) != 0x7f800000u;  // finite
-                } else {
-                  const double v = fabs((double)e[k]);
-                  in = v == 0.0 || (v >= 0x1p-300 && v <= 0x1p300);
-                }
-                bad |= i < nvec && el >= lead && el < lead + 3 * wn && !in;
-              }
-            }
-          }
-        }
-      }
-      __syncthreads();
-      W_MARK(1);
-      const uint32_t a = beg > w0 ? beg : w0;
-      const uint32_t e_end = beg + cnt < w0 + wn ? beg + cnt : w0 + wn;
-      // every lane of a quad runs the same trip count (quad-uniform), so the
-      // DPP permutes always read a live neighbour
-      const T* pt = sp + lead + 3 * (a - w0);
-      if constexpr (kExact) {
-        for (uint32_t q = a; q < e_end; q++, pt += 3) {
-          const double x = (double)pt[jj], xp = (double)pt[pj];
-          cntd = cntd + 1.0;
-          const double old = mean;
-          mean = mean + (x - mean) / cntd;
-          m2 = m2 + (x - old) * (x - mean);
-          const double mp_old = quad_perm_120(old);
-          const double mp_new = quad_perm_120(mean);
-          const double A = jj == 2 ? (xp - mp_new) : (x - mean);
-          const double Bv = jj == 2 ? (x - old) : (xp - mp_old);
-          const double cv = off + A * Bv / cntd;
-          off = (cv != cv) ? 0.0 : cv;
-        }
-      } else {
-        // Software-pipelined over the samples: the mean chain of sample q
-        // (stage 1) is issued next to the m2 / off-diagonal updates of sample
-        // q - 1 (stage 2), which only need that sample's old and new means, so
-        // the in-order issue of one wave does not stall on either chain.
-        // The off-diagonal operands come straight from their lanes: lane j
-        // multiplies (x_a - mean_a') by (x_b - mean_b) for its pair (a, b) =
-        // (0,1), (1,2), (0,2): x_a / x_b are read from LDS by axis, mean_a'
-        // is quad_perm [0,1,0,3] of the new means and mean_b quad_perm
-        // [1,2,2,3] of the old ones.
-        const uint32_t ia = jj == 2 ? 0u : jj, ib = jj == 2 ? 2u : jj + 1u;
-        double pxo = 0.0, pxa = 0.0, pxb = 0.0, pold = 0.0, pmean = 0.0, prc = 0.0, pcnt = 0.0;
-        bool pending = false;
-        for (uint32_t q = a; q < e_end; q++, pt += 3) {
-          const double xa = (double)pt[ia], xb = (double)pt[ib];
-          const double xo = jj == 2 ? xb : xa;  // my own axis
-          // stage 1, sample q
-          const double cn = cntd + 1.0;
-          const double rc = rtab[(uint32_t)cntd];  // refined reciprocal of cn
-          const double old = mean;
-          const double nm = mean + div_fast(xo - mean, cn, rc);
-          // stage 2, sample q - 1 (off can not become NaN in the checked range)
-          if (pending) {
-            m2 = m2 + (pxo - pold) * (pxo - pmean);
-            const double ma = dpp_f64<0xC4>(pmean);  // quad_perm [0,1,0,3]
-            const double mb = dpp_f64<0xE9>(pold);   // quad_perm [1,2,2,3]
-            off = off + div_fast((pxa - ma) * (pxb - mb), pcnt, prc);
-          }
-          pending = true;
-          cntd = cn;
-          mean = nm;
-          pxo = xo;
-          pxa = xa;
-          pxb = xb;
-          pold = old;
-          pmean = nm;
-          prc = rc;
-          pcnt = cn;
-        }
-        if (pending) {
-          m2 = m2 + (pxo - pold) * (pxo - pmean);
-          const double ma = dpp_f64<0xC4>(pmean);
-          const double mb = dpp_f64<0xE9>(pold);
-          off = off + div_fast((pxa - ma) * (pxb - mb), pcnt, prc);
-        }
-      }
-    }
-    return bad;
-  };
-  // the fast fold reads the reciprocal table; a count past it takes the exact fold
-  if (__syncthreads_or(cnt > (uint32_t)kRtab)) {
-    fold(std::true_type{});
-  } else {
-    const bool bad = fold(std::false_type{});
-    if (__syncthreads_or(bad && j < 3 && live)) fold(std::true_type{});
-  }
-  if (marks) __syncthreads();
-  W_MARK(2);
-  if (live && j < 3) {
-    const uint64_t o = ob + d;
-    const double v = m2 / cntd;
-    nd_mean[3 * o + j] = mean;
-    nd_cov[9 * o + 4 * j] = (v != v) ? 0.0 : v;
-    const uint32_t ia = j == 2 ? 0u : j, ib = j == 2 ? 2u : j + 1u;
-    nd_cov[9 * o + 3 * ia + ib] = off;
-    nd_cov[9 * o + 3 * ib + ia] = off;
-  }
-  if (live && j == 0) {
-    const uint64_t o = ob + d;
-    uint16_t cls = 0;
-    if (nd_lbl) {  // class histogram, first index of the max (normal_distributions.c:107-121)
-      uint32_t* hist = hist_all + o * (uint32_t)(ncls + 1);
-      for (int k = 0; k <= ncls; k++) hist[k] = 0;
-      const uint16_t* l = nd_lbl + (uint64_t)b * n + beg;
-      for (uint32_t s2 = 0; s2 < cnt; s2++)
-        if (l[s2] <= (uint32_t)ncls) hist[l[s2]]++;
-      uint32_t best = 0;
-      for (int k = 0; k <= ncls; k++)
-        if (hist[k] > best) { best = hist[k]; cls = (uint16_t)k; }
-    }
-    nd_cls[o] = cls;
-  }
-  if (marks) __syncthreads();
-  W_MARK(3);
-}
-#undef W_MARK
-
-// Persistent: one workgroup per CU walks the (cloud, ND group) items that
-// exist in this run (the ND counts are only known on the device), so no CU
-// holds two groups while another idles.
-template <typename T>
-__global__ void __launch_bounds__(kWelfordThreads) k_welford(const CloudCtl* ctl, int B, const T* __restrict__ nd_pts,
-                                                 const uint16_t* __restrict__ nd_lbl, const uint32_t* nd_n,
-                                                 const uint32_t* nd_base, double* nd_mean, double* nd_cov,
-                                                 uint16_t* nd_cls, uint32_t* hist_all, int ncls, uint64_t n,
-                                                 uint32_t ndcap, unsigned long long* marks) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char w_smem[];
-  double* rtab = (double*)(w_smem + kWelfordBytes);
-  __shared__ uint32_t s_first[257];  // first item of each cloud (chunks of 256 clouds)
-  const uint32_t gpc = (ndcap + kWelfordNDs - 1) / kWelfordNDs;  // group capacity per cloud
-  for (uint32_t k = threadIdx.x; k < (uint32_t)kRtab; k += blockDim.x) rtab[k] = recip_refined((double)(k + 1));
-  // items of this run: clouds' group counts (loaded in parallel), scanned, in
-  // chunks of 256 clouds
-  uint32_t item = blockIdx.x, base_all = 0;
-  for (int b0 = 0; b0 < B; b0 += 256) {
-    __syncthreads();
-    if (threadIdx.x < 256) {
-      const int bb = b0 + (int)threadIdx.x;
-      uint32_t g = 0;
-      if (bb < B && ctl[bb].state == kAccepted) g = (ctl[bb].num_nds + kWelfordNDs - 1) / kWelfordNDs;
-      s_first[threadIdx.x + 1] = g;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      s_first[0] = base_all;
-      for (int i = 1; i <= 256; i++) s_first[i] += s_first[i - 1];
-    }
-    __syncthreads();
-    const int nb = B - b0 < 256 ? B - b0 : 256;
-    const uint32_t end = s_first[nb];
-    for (; item < end; item += gridDim.x) {
-      int lo = 0, hi = nb - 1;  // last cloud whose first item <= item
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (s_first[mid] <= item) lo = mid;
-        else hi = mid - 1;
-      }
-      welford_group<T>(ctl[b0 + lo], b0 + lo, item - s_first[lo], gpc, nd_pts, nd_lbl, nd_n, nd_base, nd_mean,
-                       nd_cov, nd_cls, hist_all, ncls, n, ndcap, marks, rtab);
-    }
-    base_all = end;
-  }
-}
-
 // k_welford_q: the same per-ND Welford (same lane quad, same double
 // operations on the same operands, so the same bits), without LDS windows:
 // every quad streams its own ND's points from nd_pts, so a wave runs as long as
@@ -1092,6 +808,8 @@ __global__ void __launch_bounds__(kWelfordThreads) k_welford(const CloudCtl* ctl
 constexpr int kWqThreads = 256;              // 4 waves x 16 quads
 constexpr int kWqNDs = kWqThreads / 4;
 constexpr int kWqU = 16;                     // samples per prefetch block
+constexpr int kWqNB = 4;                     // register blocks in the prefetch ring
+constexpr int kWqRt = 4096;                  // reciprocals tabled in LDS (32 KB)
 constexpr int kWqHistMax = 64 * 1024;        // LDS class histograms up to this size, else global
 
 template <int CTRL>
@@ -1124,6 +842,15 @@ __device__ inline double sel_d(unsigned long long lanes, double a, double b) {  
   return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32));
 }
 
+__device__ inline uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t w = (uint32_t)__shfl_xor((int)v, o, 64);
+    v = w < v ? w : v;
+  }
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
 __device__ inline uint32_t wave_max_u32(uint32_t v) {
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -1133,27 +860,57 @@ __device__ inline uint32_t wave_max_u32(uint32_t v) {
   return __builtin_amdgcn_readfirstlane(v);
 }
 
-__global__ void k_rtab_init(double* rtab, uint64_t count) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < count) rtab[i] = recip_refined((double)(i + 1));
-}
-
 template <typename T>
-__global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, const T* __restrict__ nd_pts,
+__global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, int B, const T* __restrict__ nd_pts,
                                                           const uint16_t* __restrict__ nd_lbl,
                                                           const uint32_t* __restrict__ nd_n,
-                                                          const uint32_t* __restrict__ nd_base,
-                                                          const double* __restrict__ rtab, double* nd_mean,
+                                                          const uint32_t* __restrict__ nd_base, double* nd_mean,
                                                           double* nd_cov, uint16_t* nd_cls, uint32_t* hist_all,
-                                                          int ncls, uint64_t n, uint32_t ndcap) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t wq_hist[];
-  const int b = blockIdx.y;
-  const CloudCtl& c = ctl[b];
-  if (c.state != kAccepted) return;
-  const uint32_t nd = c.num_nds;
+                                                          int ncls, uint64_t n, uint32_t ndcap, uint32_t* wq_ctr) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char wq_smem[];
+  double* lrt = (double*)wq_smem;                                // [kWqRt] refined reciprocals of 1..kWqRt
+  uint32_t* pre = (uint32_t*)(wq_smem + kWqRt * sizeof(double));  // [B + 1] first item of each cloud
+  uint32_t* wq_hist = pre + ((B + 1 + 3) & ~3);                   // labelled runs: [kWqNDs][ncls + 1]
+  for (uint32_t i = threadIdx.x; i < (uint32_t)kWqRt; i += kWqThreads) lrt[i] = recip_refined((double)(i + 1));
+  // items = (cloud, group of 16 NDs) of this run, in cloud order: one per wave
+  // of a persistent grid (one workgroup per CU, one wave per SIMD), so no
+  // SIMD holds two ND groups while another idles
+  for (int i = threadIdx.x; i < B; i += kWqThreads)
+    pre[i + 1] = ctl[i].state == kAccepted ? (ctl[i].num_nds + 15u) / 16u : 0u;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    pre[0] = 0;
+    for (int i = 0; i < B; i++) pre[i + 1] += pre[i];
+  }
+  __syncthreads();
+  const uint32_t total = pre[B];
   const uint32_t lane = threadIdx.x & 63, j = lane & 3;
-  const uint32_t wd0 = blockIdx.x * kWqNDs + (threadIdx.x >> 6) * 16;  // first ND of my wave
-  if (wd0 >= nd) return;                                                  // wave-uniform
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // first round static (one item per wave), then a shared counter: a wave
+  // that finishes a light ND group takes the next one, so a heavy group is
+  // never queued behind another.  A wave first reads the counter and only
+  // increments it while items remain (one contended word takes ~11 ns per
+  // atomic: a thousand waves each adding would cost ~10 us).  k_kl_chains,
+  // the next kernel on the stream, re-arms it.
+  const uint32_t nwaves = gridDim.x * (kWqThreads / 64);
+  auto next_item = [&]() -> uint32_t {
+    uint32_t v = total;
+    if (lane == 0) {
+      const uint32_t seen = __hip_atomic_load(wq_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (nwaves + seen < total) v = nwaves + __hip_atomic_fetch_add(wq_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return __builtin_amdgcn_readfirstlane(v);
+  };
+  for (uint32_t item = blockIdx.x * (kWqThreads / 64) + wave; item < total; item = next_item()) {
+  int lo = 0, hi = B - 1;  // the cloud whose items hold `item`
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (pre[mid] <= item) lo = mid;
+    else hi = mid - 1;
+  }
+  const int b = lo;
+  const uint32_t nd = ctl[b].num_nds;
+  const uint32_t wd0 = (item - pre[b]) * 16u;  // first ND of my wave
   const uint32_t d = wd0 + (lane >> 2);
   const bool live = d < nd;
   const uint64_t o = (uint64_t)b * ndcap + (live ? d : wd0);
@@ -1166,70 +923,160 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, c
 
   double mean = 0.0, m2 = 0.0, off = 0.0;
   bool bad = false;
-  // the reciprocals ride in the same in-order vector-load stream as the points
-  // (a uniform address would become a scalar load, waited for at its use with
-  // lgkmcnt(0) behind every younger scalar load): an opaque zero makes the
-  // address per-lane
-  uint32_t zero;
-  asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
-  const double* rt = rtab + zero;
-  const uint32_t rlast = mx ? mx - 1u : 0u;
-  T ra[kWqU], rb[kWqU];
-  double ca[kWqU], cb[kWqU];
-  auto load = [&](T (&r)[kWqU], double (&cr)[kWqU], uint32_t q0) __attribute__((always_inline)) {
+  // points: a ring of kWqNB register blocks of kWqU samples, kWqNB - 1 blocks
+  // in flight ahead of the one being folded (memory latency ~2 us under load
+  // against ~0.5 us per block of compute)
+  T r0[kWqU], r1[kWqU], r2[kWqU], r3[kWqU];
+  auto load = [&](T (&r)[kWqU], uint32_t q0) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < kWqU; u++) {
       const uint32_t q = q0 + (uint32_t)u;
+#ifdef NDNET_WQ_NOLOAD  // timing experiment only: no point loads (wrong results)
+      r[u] = (T)(1.0f + 0.001f * (float)(q & 7));
+#else
       r[u] = src[3u * (q < last ? q : last)];
-      cr[u] = rt[q < rlast ? q : rlast];
+#endif
     }
   };
-  // one block of samples; kExact: IEEE divisions and the NaN -> 0 step
-  // Branch-free over the block (a lane past its count keeps its state by
-  // selects), so the scheduler overlaps the off-diagonal tail of sample q
-  // with the mean chain of sample q + 1.
-  auto fold = [&](const T (&r)[kWqU], const double (&cr)[kWqU], uint32_t q0, bool act,
-                  auto exact_tag) __attribute__((always_inline)) {
-    constexpr bool kExact = decltype(exact_tag)::value;
+  // the block's reciprocals: broadcast LDS reads, computed past the table
+  auto recips = [&](double (&cr)[kWqU], uint32_t q0) __attribute__((always_inline)) {
+    if (q0 + kWqU <= (uint32_t)kWqRt) {  // wave-uniform
 #pragma unroll
-    for (int u = 0; u < kWqU; u++) {
-      const uint32_t q = q0 + (uint32_t)u;
-      const bool on = act && q < cnt;          // quad-uniform
-      const double cn = (double)(q + 1u);
-      const double rc = cr[u];
-      const double x = (double)r[u];
-      if constexpr (!kExact) bad |= on && !wq_in_range(r[u]);
-      const double t = x - mean;
-      const double nm = mean + (kExact ? t / cn : div_fast(t, cn, rc));
-      const double uu = x - nm;
-      const double nm2 = m2 + t * uu;
-      const double ua = dpp_d<0xC4>(uu);   // quad_perm [0,1,0,3]: u of axis a
-      const double tb = dpp_d<0xE9>(t);    // quad_perm [1,2,2,3]: t of axis b
-      const double pr = ua * tb;
-      double noff;
-      if constexpr (kExact) {
+      for (int u = 0; u < kWqU; u++) cr[u] = lrt[q0 + u];
+    } else {
+#pragma unroll
+      for (int u = 0; u < kWqU; u++) cr[u] = recip_refined((double)(q0 + u + 1));
+    }
+  };
+  // One block of samples; kExact: IEEE divisions and the NaN -> 0 step.
+  // Branch-free over the block (a lane past its count keeps its state by
+  // selects).  Two dependent chains per sample: the head of sample q (the
+  // mean: t = x - mean, mean += t / n, u = x - mean; 6 FP64 ops of ~10 cycles
+  // latency each) and the tail of sample q - 1 (m2 += t u, the off-diagonal
+  // product u_a t_b through two DPP moves and its division, 6 deep).  The
+  // fast fold issues them interleaved in pairs, with a scheduling barrier
+  // after each pair, so every head op finds its operand ready: the in-order
+  // wave issues ~18 instructions per sample back to back instead of waiting
+  // out each chain link.
+  auto fold = [&](const T (&r)[kWqU], uint32_t q0, bool act, auto exact_tag,
+                  auto masked_tag) __attribute__((always_inline)) {
+    constexpr bool kExact = decltype(exact_tag)::value;
+    constexpr bool kMasked = decltype(masked_tag)::value;  // false: every live quad has >= q0 + kWqU samples
+    double cr[kWqU];
+    if constexpr (!kExact) recips(cr, q0);
+    double pt = 0.0, pu = 0.0, pcn = 1.0, prc = 1.0;       // the previous sample's head results
+    unsigned long long plane = 0;
+    if constexpr (kExact) {
+      // the refold (never on ordinary data): plain order
+#pragma unroll
+      for (int u = 0; u < kWqU; u++) {
+        const uint32_t q = q0 + (uint32_t)u;
+        const unsigned long long lanes = __ballot(act && q < cnt);
+        const double cn = (double)(q + 1u);
+        const double x = (double)r[u];
+        const double t = x - mean;
+        const double nm = mean + t / cn;
+        const double uu = x - nm;
+        const double nm2 = m2 + t * uu;
+        const double pr = dpp_d<0xC4>(uu) * dpp_d<0xE9>(t);
         const double cv = off + pr / cn;
-        noff = (cv != cv) ? 0.0 : cv;
-      } else {
-        noff = off + div_fast(pr, cn, rc);
+        mean = sel_d(lanes, nm, mean);
+        m2 = sel_d(lanes, nm2, m2);
+        off = sel_d(lanes, (cv != cv) ? 0.0 : cv, off);
       }
-      const unsigned long long lanes = __ballot(on);
-      mean = sel_d(lanes, nm, mean);
-      m2 = sel_d(lanes, nm2, m2);
-      off = sel_d(lanes, noff, off);
+    } else {
+// pins a pair's results at this point of the instruction stream (an empty
+// volatile asm that "modifies" them: nothing computing them sinks below it,
+// nothing using them hoists above it, and volatile asms keep their order)
+#define WQ_PIN2(a, b) asm volatile("" : "+v"(a), "+v"(b))
+      // A lane past its count folds x = mean: t = 0, the mean gains +0, u = 0,
+      // m2 and the off-diagonal gain +0 -- an exact no-op (the sums start at +0
+      // and never become -0), so one select on x replaces three on the state.
+#pragma unroll
+      for (int u = 0; u <= kWqU; u++) {  // u == kWqU: the last sample's tail alone
+        const bool head = u < kWqU, tail = u > 0;
+        const uint32_t q = q0 + (uint32_t)u;
+        const double cn = (double)(q + 1u);
+        const double rc = head ? cr[u < kWqU ? u : 0] : 0.0;
+        double x = 0.0, t = 0.0, q0v = 0.0, rem = 0.0, qq = 0.0, nm = 0.0, uu = 0.0;
+        double pm = 0.0, ua = 0.0, tb = 0.0, pr = 0.0, q1 = 0.0, rm1 = 0.0, qq1 = 0.0;
+        if constexpr (!std::is_same<T, float>::value) {
+          if (head) bad |= (!kMasked || (act && q < cnt)) && !wq_in_range(r[u < kWqU ? u : 0]);
+        }
+        // pair 1: t | u_a
+        if (head) {
+          x = (double)r[u < kWqU ? u : 0];
+          if constexpr (kMasked) x = sel_d(__ballot(act && q < cnt), x, mean);
+          t = x - mean;
+        }
+        if (tail) { ua = dpp_d<0xC4>(pu); }
+        WQ_PIN2(t, ua);
+        // pair 2: t / n (1) | t_b, t u
+        if (head) q0v = t * rc;
+        if (tail) { tb = dpp_d<0xE9>(pt); pm = pt * pu; }
+        WQ_PIN2(q0v, tb);
+        // pair 3: t / n (2) | u_a t_b
+        if (head) rem = fma(-cn, q0v, t);
+        if (tail) pr = ua * tb;
+        WQ_PIN2(rem, pr);
+        // pair 4: t / n (3) | its division (1)
+        if (head) qq = fma(rem, rc, q0v);
+        if (tail) q1 = pr * prc;
+        WQ_PIN2(qq, q1);
+        // pair 5: the new mean | the division (2), m2
+        if (head) nm = mean + qq;
+        if (tail) {
+          rm1 = fma(-pcn, q1, pr);
+          m2 = m2 + pm;
+        }
+        WQ_PIN2(nm, rm1);
+        // pair 6: u | the division (3)
+        if (head) {
+          uu = x - nm;
+          mean = nm;
+        }
+        if (tail) qq1 = fma(rm1, prc, q1);
+        WQ_PIN2(uu, qq1);
+        if (tail) off = off + qq1;
+        pt = t;
+        pu = uu;
+        pcn = cn;
+        prc = rc;
+      }
+#undef WQ_PIN2
     }
   };
   auto run = [&](uint32_t lim, bool act, auto exact_tag) __attribute__((always_inline)) {
-    load(ra, ca, 0);
-    load(rb, cb, kWqU);
-    for (uint32_t q0 = 0; q0 < lim; q0 += 2 * kWqU) {
-      fold(ra, ca, q0, act, exact_tag);
-      load(ra, ca, q0 + 2 * kWqU);
-      if (q0 + kWqU < lim) fold(rb, cb, q0 + kWqU, act, exact_tag);  // wave-uniform
-      load(rb, cb, q0 + 3 * kWqU);
+    load(r0, 0);
+    load(r1, kWqU);
+    load(r2, 2 * kWqU);
+    load(r3, 3 * kWqU);
+    // blocks every live quad fills run without the per-sample selects
+    // (the exact refold keeps the state of the quads it does not redo: always masked)
+    const uint32_t full = decltype(exact_tag)::value ? 0u : wave_min_u32(live ? cnt : 0xffffffffu);
+    auto step = [&](const T (&r)[kWqU], uint32_t q0) __attribute__((always_inline)) {
+      if (q0 + kWqU <= full) fold(r, q0, act, exact_tag, std::false_type{});
+      else fold(r, q0, act, exact_tag, std::true_type{});
+    };
+    for (uint32_t q0 = 0; q0 < lim; q0 += kWqNB * kWqU) {  // every branch below is wave-uniform
+      step(r0, q0);
+      load(r0, q0 + 4 * kWqU);
+      if (q0 + kWqU >= lim) break;
+      step(r1, q0 + kWqU);
+      load(r1, q0 + 5 * kWqU);
+      if (q0 + 2 * kWqU >= lim) break;
+      step(r2, q0 + 2 * kWqU);
+      load(r2, q0 + 6 * kWqU);
+      if (q0 + 3 * kWqU >= lim) break;
+      step(r3, q0 + 3 * kWqU);
+      load(r3, q0 + 7 * kWqU);
     }
   };
   run(mx, true, std::false_type{});
+  // float input: every finite coordinate is in div_fast's exact range, and a
+  // non-finite one makes the running mean non-finite from then on (x - mean
+  // and mean + ... stay inf / NaN), so the final state flags it
+  if constexpr (std::is_same<T, float>::value) bad = !(fabs(mean) <= 0x1.fffffffffffffp+1023);
   // a quad whose coordinates left the fast range refolds exactly
   const bool qbad = __builtin_amdgcn_mov_dpp((int)bad, 0x00, 0xF, 0xF, false) |
                     __builtin_amdgcn_mov_dpp((int)bad, 0x55, 0xF, 0xF, false) |
@@ -1276,6 +1123,7 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, c
     }
     nd_cls[o] = cls;
   }
+  }  // item
 }
 
 // Bitonic sort of (key, idx) pairs ascending, n a power of two, within one workgroup.
@@ -1288,6 +1136,7 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, c
 struct KLArgs {
   unsigned long long* marks;  // [B][16] phase stamps of k_kl, or null
   CloudCtl* ctl;
+  uint32_t* wq_ctr;           // k_welford_q's item counter, re-armed by k_kl_chains
   const uint32_t* dense_all;
   const uint32_t* vox_all;
   const uint32_t* nd_n;
@@ -1615,6 +1464,7 @@ __device__ inline uint32_t qslot_of_dir(uint32_t d) {  // q-slot of the neighbou
 
 // Neighbours, chain masks and LU chains, one lane per ND.
 __global__ void __launch_bounds__(256) k_kl_chains(KLArgs A) {
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *A.wq_ctr = 0u;  // k_welford_q has finished
   const int b = blockIdx.y;
   const CloudCtl& c = A.ctl[b];
   if (c.state != kAccepted) return;
@@ -2153,13 +2003,12 @@ static void plan_free(Plan* P) {
     for (int i = 0; i < 7; i++) (void)hipEventDestroy(P->ev[i]);
   if (P->kl_marks) (void)hipFree(P->kl_marks);
   if (P->fmarks) (void)hipFree(P->fmarks);
-  if (P->wmarks) (void)hipFree(P->wmarks);
   void* bufs[] = {P->flims, P->frec, P->fwgcnt, P->fbar, P->ctl, P->stamps, P->dense_of, P->vox, P->gbits, P->pkeys, P->did, P->bin_cnt, P->nd_base,
                   P->nd_pts, P->nd_lbl, P->nd_n,
                   P->nd_mean, P->nd_cov, P->nd_cov_post, P->nd_cls, P->hist, P->nb, P->keys, P->nkeys,
                   P->chain, P->chain_ps, P->slot_val, P->slot_flag, P->ev_val, P->ev_p, P->ev_q, P->ev_min,
                   P->sort_key, P->sort_idx, P->nan_list, P->nan_key, P->nan_slot, P->chunk_nanbase, P->ord_val, P->ord_p, P->ord_q,
-                  P->first_occ, P->tmp_u32, P->alive, P->d_stats, P->chunk_cnt, P->chunk_min, P->rtab};
+                  P->first_occ, P->tmp_u32, P->alive, P->d_stats, P->chunk_cnt, P->chunk_min, P->wq_ctr};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete P;
@@ -2175,6 +2024,7 @@ static KLArgs kl_args(Plan* P, uint64_t k, float* out, float* out_cls, double* p
   KLArgs A;
   A.marks = P->timing >= 2 ? P->kl_marks : nullptr;
   A.ctl = P->ctl;
+  A.wq_ctr = P->wq_ctr;
   A.dense_all = P->dense_of;
   A.vox_all = P->vox;
   A.nd_n = P->nd_n;
@@ -2261,6 +2111,8 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
     F.G = P->fG;
     F.bpw = P->fbpw;
     F.rbs = P->frbs;
+    F.dbg_store = 0;
+    F.eval_all = P->exact_counts;
     k_front<T><<<dim3(P->fG, B), kFrontThreads, P->flds, st>>>(pts, F);
     if (P->timing)
       for (int e = 1; e <= 4; e++) HIPCHK(hipEventRecord(P->ev[e], st));
@@ -2282,9 +2134,10 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
                                                                P->ndcap, P->nbins);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[4], st));
   }
-  k_welford_q<T><<<dim3((P->ndcap + kWqNDs - 1) / kWqNDs, B), kWqThreads, lbl ? P->wq_lds : 0, st>>>(
-      P->ctl, (const T*)P->nd_pts, lbl ? P->nd_lbl : nullptr, P->nd_n, P->nd_base, P->rtab, P->nd_mean, P->nd_cov,
-      P->nd_cls, P->hist, P->ncls, n, P->ndcap);
+  k_welford_q<T><<<P->wq_grid, kWqThreads, kWqRt * sizeof(double) + 4 * ((B + 1 + 3) & ~3) + (lbl ? P->wq_lds : 0),
+                    st>>>(
+      P->ctl, B, (const T*)P->nd_pts, lbl ? P->nd_lbl : nullptr, P->nd_n, P->nd_base, P->nd_mean, P->nd_cov,
+      P->nd_cls, P->hist, P->ncls, n, P->ndcap, P->wq_ctr);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[5], st));
   KLArgs A = kl_args(P, P->k, out, out_cls, pc64, cov64, cls16);
   A.stats_out = stats_dst;
@@ -2387,7 +2240,7 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   A_(chunk_cnt, B * P->nchunk);
   A_(chunk_min, B * P->nchunk);
   A_(d_stats, B);
-  A_(rtab, n + 1);
+  A_(wq_ctr, 2);
   // k_front: G workgroups per cloud, all resident together (G * B <= CUs);
   // each owns bpw bins, whose per-ND counts and ranks live in its LDS
   {
@@ -2421,8 +2274,6 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
       if (e == hipSuccess && nb < 1) P->front_ok = 0;
     }
     P->front = P->front_ok;
-    const uint32_t groups = (uint32_t)batch * ((P->ndcap + kWelfordNDs - 1) / kWelfordNDs);
-    P->wgrid = groups < (uint32_t)(cus > 0 ? cus : 1) ? groups : (uint32_t)(cus > 0 ? cus : 1);
     A_(flims, B * G * 6);
     A_(frec, B * kFrontPhases * G * kRecWords);
     A_(fwgcnt, B * G * nd);
@@ -2433,25 +2284,26 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   if (e == hipSuccess) e = hipMemset(P->fbar, 0, B * kBarStride * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(P->stamps, 0, B * P->vcap * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(P->d_stats, 0, B * sizeof(ndnet_ndt_stats));
-  if (e == hipSuccess) {
-    k_rtab_init<<<(unsigned)((n + 1 + 255) / 256), 256>>>(P->rtab, n + 1);
-    e = hipGetLastError();
-  }
+  if (e == hipSuccess) e = hipMemset(P->wq_ctr, 0, 2 * sizeof(uint32_t));
   {
     const size_t hb = (size_t)kWqNDs * (size_t)nb * sizeof(uint32_t);
     P->wq_lds = num_classes >= 0 && hb <= (size_t)kWqHistMax ? hb : 0;
+    int dv = 0, ncu = 0;
+    if (e == hipSuccess) e = hipGetDevice(&dv);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dv);
+    P->wq_grid = ncu > 0 ? (uint32_t)ncu : 1u;
   }
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_welford_q<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(kWqRt * sizeof(double) + 4 * ((batch + 1 + 3) & ~3) + kWqHistMax));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_welford_q<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(kWqRt * sizeof(double) + 4 * ((batch + 1 + 3) & ~3) + kWqHistMax));
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_kl_merge<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(2 * kMergeLdsChunks * kChunk * sizeof(unsigned long long)));
   if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_kl, hipFuncAttributeMaxDynamicSharedMemorySize, kKLLdsMax);
   if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_prune, hipFuncAttributeMaxDynamicSharedMemorySize, kKLLdsMax);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_welford<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            kWelfordBytes + kRtab * (int)sizeof(double));
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_welford<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            kWelfordBytes + kRtab * (int)sizeof(double));
   if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_bin_count, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                (int)(16384 * sizeof(uint32_t)));
   if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -2474,6 +2326,13 @@ int ndnet_ndt_set_path(void* plan, int path) {
   return NDNET_OK;
 }
 
+int ndnet_ndt_set_exact_counts(void* plan, int on) {
+  Plan* P = (Plan*)plan;
+  if (!P || on < 0 || on > 1) return NDNET_ERR_ARG;
+  P->exact_counts = on;
+  return NDNET_OK;
+}
+
 int ndnet_ndt_get_path(void* plan) {
   Plan* P = (Plan*)plan;
   if (!P) return NDNET_ERR_ARG;
@@ -2487,11 +2346,6 @@ int ndnet_ndt_set_timing(void* plan, int enable) {
   if (enable && !P->ev_created) {
     for (int i = 0; i < 7; i++) HIPCHK(hipEventCreate(&P->ev[i]));
     P->ev_created = 1;
-  }
-  if (enable >= 2 && !P->wmarks) {
-    const size_t nw = (size_t)P->B * ((P->ndcap + kWelfordNDs - 1) / kWelfordNDs) * 4;
-    HIPCHK(hipMalloc(&P->wmarks, nw * sizeof(unsigned long long)));
-    HIPCHK(hipMemset(P->wmarks, 0, nw * sizeof(unsigned long long)));
   }
   if (enable >= 2 && !P->fmarks) {
     HIPCHK(hipMalloc(&P->fmarks, (size_t)P->B * kFrontMarkStride * sizeof(unsigned long long)));
@@ -2572,15 +2426,6 @@ int ndnet_ndt_debug_front_wg_marks(void* plan, unsigned long long* marks, int* G
   HIPCHK(hipMemcpy2D(marks, 2 * P->fG * sizeof(unsigned long long),
                      P->fmarks + 32, kFrontMarkStride * sizeof(unsigned long long),
                      2 * P->fG * sizeof(unsigned long long), P->B, hipMemcpyDeviceToHost));
-  return NDNET_OK;
-}
-
-int ndnet_ndt_debug_welford_marks(void* plan, unsigned long long* marks) {
-  Plan* P = (Plan*)plan;
-  if (!P || !marks || !P->wmarks) return NDNET_ERR_ARG;
-  HIPCHK(hipDeviceSynchronize());
-  const size_t nw = (size_t)P->B * ((P->ndcap + kWelfordNDs - 1) / kWelfordNDs) * 4;
-  HIPCHK(hipMemcpy(marks, P->wmarks, nw * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return NDNET_OK;
 }
 

@@ -66,6 +66,7 @@ EXPORTS = {
     "ndnet_ndt_plan_destroy": (None, [_P]),
     "ndnet_ndt_set_path": (_I, [_P, _I]),
     "ndnet_ndt_get_path": (_I, [_P]),
+    "ndnet_ndt_set_exact_counts": (_I, [_P, _I]),
     "ndnet_ndt_run": (_I, [_P, _P, _P, _P, _P, _P, _P]),
     "ndnet_ndt_run_f64": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "ndnet_ndt_prune": (_I, [_P, _P, _U64, _P, _P, _P, _P, _P, _P]),
@@ -74,7 +75,6 @@ EXPORTS = {
     "ndnet_ndt_debug_kl_marks": (_I, [_P, _P]),
     "ndnet_ndt_debug_front_marks": (_I, [_P, _P]),
     "ndnet_ndt_debug_front_wg_marks": (_I, [_P, _P, ctypes.POINTER(_I)]),
-    "ndnet_ndt_debug_welford_marks": (_I, [_P, _P]),
     "ndnet_ndt_set_timing": (_I, [_P, _I]),
     "ndnet_ndt_stage_ms": (_I, [_P, _P]),
     "ndnet_amd_version": (ctypes.c_char_p, []),

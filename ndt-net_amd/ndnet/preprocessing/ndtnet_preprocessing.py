@@ -63,6 +63,11 @@ class NdtPlan:
         """1: one launch per stage; 2: the fused front kernel (k_front); 0: 2 where allowed."""
         _lib.check(_lib.lib().ndnet_ndt_set_path(self.handle, int(path)), "ndnet_ndt_set_path")
 
+    def set_exact_counts(self, on: bool) -> None:
+        """Count every bisection grid, also those with fewer voxels than k
+        (include/ndnet_amd.h ndnet_ndt_set_exact_counts; debug / parity)."""
+        _lib.check(_lib.lib().ndnet_ndt_set_exact_counts(self.handle, 1 if on else 0), "ndnet_ndt_set_exact_counts")
+
     @property
     def path(self) -> int:
         return int(_lib.lib().ndnet_ndt_get_path(self.handle))

@@ -18,11 +18,12 @@ FIXTURES = ["ndt_U4096_k256_s0.npz", "ndt_U4096_k256_s1.npz", "ndt_L4096_k256_s0
             "ndt_U2003_k128_s7.npz"]
 
 
-def _run_plan(points_b: np.ndarray, k: int, labels_b=None, num_classes=-1):
+def _run_plan(points_b: np.ndarray, k: int, labels_b=None, num_classes=-1, exact_counts=True):
     import torch
     from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
     B, n, _ = points_b.shape
     plan = NdtPlan(B, n, k, num_classes)
+    plan.set_exact_counts(exact_counts)
     pts = torch.from_numpy(np.ascontiguousarray(points_b, dtype=np.float32)).cuda()
     lbl = None if labels_b is None else torch.from_numpy(labels_b.astype(np.int32)).cuda()
     out = torch.empty((B, k, 12), dtype=torch.float32, device="cuda")
@@ -97,6 +98,34 @@ def test_stages_match_reference_and_oracle(name):
     onehot = np.zeros((k, ncls + 1), np.float32)
     onehot[np.arange(k), z["orc_out_cls"]] = 1.0
     assert np.array_equal(out_cls[0], onehot)
+
+
+@pytest.mark.parametrize("name", FIXTURES[:3])
+def test_skipped_grids_change_nothing(name):
+    """Default mode: grids with fewer voxels than k are not counted (their
+    bisection decision, hi = guess, needs no count).  Same guesses, same
+    counted counts, same outputs and stats as counting every grid; a count is
+    skipped only where the grid has fewer than k voxels."""
+    z = golden(name)
+    k = int(z["k"])
+    runs = {}
+    for exact in (True, False):
+        plan, out, _ = _run_plan(z["points"][None], k, exact_counts=exact)
+        st = plan.host_stats()[0]
+        d = _dump(plan, 0, int(st.num_nds), int(st.num_events))
+        runs[exact] = (out, bytes(st), d)
+    (o1, s1, d1), (o0, s0, d0) = runs[True], runs[False]
+    assert np.array_equal(o1, o0) and s1 == s0
+    it = d1["iters"]
+    assert d0["iters"] == it and np.array_equal(d0["guesses"][:it], d1["guesses"][:it])
+    skipped = d0["counts"][:it] == 0xFFFFFFFF
+    assert skipped.any()
+    assert np.array_equal(d0["counts"][:it][~skipped], d1["counts"][:it][~skipped])
+    lim = z["points"].astype(np.float64)
+    ext = lim.max(0) - lim.min(0)
+    for g, sk in zip(d1["guesses"][:it], skipped):
+        V = int(np.prod(np.ceil(ext / g)))
+        assert sk == (V < k)
 
 
 def test_reference_driver_fixture():
@@ -231,6 +260,7 @@ def test_front_kernel_equals_multikernel_path(case):
     for path in (1, 2):
         plan = NdtPlan(B, n, k, -1)
         plan.set_path(path)
+        plan.set_exact_counts(True)
         assert plan.path == path
         out = torch.empty((B, k, 12), dtype=torch.float32, device="cuda")
         plan.run(torch.from_numpy(pts).cuda(), None, out, None)

@@ -66,22 +66,3 @@ for i in sorted(names, key=lambda i: acc[i] if np.isfinite(acc[i]) else 1e9):
         print(f"  {i:2d} {names[i]:12s} {acc[i]:8.2f} us  (+{acc[i] - prev:6.2f})")
         prev = acc[i]
 
-# k_welford: per-workgroup stamps (start, staged, folded, end), relative to the
-# earliest start in the cloud
-ndt_preprocessing(a.nds, pts)
-_lib.check(_lib.lib().ndnet_ndt_set_timing(plan.handle, 2), "set_timing")
-ndt_preprocessing(a.nds, pts)
-ndcap = int(a.nds * 1.2) + 1
-wgs = (ndcap + 63) // 64
-wm = np.zeros(a.batch * wgs * 4, np.uint64)
-_lib.check(_lib.lib().ndnet_ndt_debug_welford_marks(plan.handle, wm.ctypes.data), "welford_marks")
-_lib.lib().ndnet_ndt_set_timing(plan.handle, 0)
-wm = wm.reshape(a.batch * wgs, 4).astype(np.float64)
-wm = wm[wm[:, 0] > 0]
-t0 = wm[:, 0].min()
-rel = (wm - t0) * 0.01
-q = lambda v: "%.1f/%.1f/%.1f" % (np.min(v), np.median(v), np.max(v))  # noqa: E731
-print("k_welford per workgroup (min/median/max us): start", q(rel[:, 0]), " staged", q(rel[:, 1] - rel[:, 0]),
-      " folded", q(rel[:, 2] - rel[:, 1]), " stored", q(rel[:, 3] - rel[:, 2]), " end", q(rel[:, 3]))
-print("k_welford (us from the first workgroup start): start min/max %.2f/%.2f, staged +%.2f, folded +%.2f, end max %.2f"
-      % (rel[:, 0].min(), rel[:, 0].max(), (rel[:, 1] - rel[:, 0]).mean(), (rel[:, 2] - rel[:, 1]).mean(), rel[:, 3].max()))
