@@ -78,6 +78,9 @@ struct FrontArgs {
   unsigned long long* marks;    // [B][32] phase stamps of workgroup 0 (timing level 2), or null
   uint64_t n, k, vcap;
   uint32_t ndcap, G, bpw;
+  uint32_t B;                   // clouds in the launch
+  uint32_t nbins;               // 1024-point bins per cloud
+  int xcd_local;                // 1: the G workgroups of a cloud share blockIdx % 8 (one XCD)
   uint32_t rbs;                 // points per rank bin (512 or 1024)
   int dbg_store;
   int eval_all;                 // 1: count every bisection grid (debug / parity); 0: skip grids too small to matter
@@ -257,8 +260,24 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
   __shared__ FrontState s;
   __shared__ uint32_t scratch[32];
   __shared__ uint32_t s_bad[kWorkers];
-  const int b = blockIdx.y;
-  const uint32_t g = blockIdx.x, G = A.G, bpw = A.bpw, rbs = A.rbs, nrb = bpw * (1024 / A.rbs);
+  // Workgroup -> (cloud, g).  Blocks are dealt round-robin over the 8 XCDs
+  // (MI355X_MICROARCH.md, speed only: the barriers below hold whatever the
+  // placement), so with B % 8 == 0 the G workgroups of a cloud are given
+  // linear ids with one residue mod 8: the cloud's points, bitmaps and grouped
+  // output stay in one XCD's L2, whose partial 12-byte writes then merge
+  // into whole lines before write-back instead of leaving partial lines dirty
+  // in several XCDs.
+  const uint32_t L = blockIdx.x, G = A.G, bpw = A.bpw, rbs = A.rbs, nrb = bpw * (1024 / A.rbs);
+  uint32_t g;
+  int b;
+  if (A.xcd_local) {
+    const uint32_t cpx = A.B / 8u, slot = L / 8u;  // clouds per XCD, slot within the XCD
+    b = (int)((slot % cpx) * 8u + L % 8u);
+    g = slot / cpx;
+  } else {
+    b = (int)(L / G);
+    g = L % G;
+  }
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
   CloudCtl& c = A.ctl[b];
   const uint64_t n = A.n;
@@ -270,7 +289,11 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
   uint32_t* binfo = f_smem + kFrontTable;                     // [bpw][1024]: key, then did << 10 | rank
   uint32_t* hist = binfo + (uint64_t)bpw * 1024;              // [nrb][ndcap]
   uint32_t* stamps = A.stamps + (uint64_t)b * A.vcap;
-  const uint64_t bin0 = (uint64_t)g * bpw;
+  // my bins: [bin0, bin0 + nbw), nbw <= bpw (the bins of a cloud split as evenly as G allows)
+  const uint64_t bin0 = (uint64_t)g * A.nbins / G;
+  const uint64_t bin1 = (uint64_t)(g + 1) * A.nbins / G;
+  const uint64_t iend = bin1 * 1024u < n ? bin1 * 1024u : n;    // my points: [bin0 * 1024, iend)
+  const uint64_t iend8 = iend < n8 ? iend : n8;                   // ... that the workers estimate
   // this run's stamp epoch: every workgroup derives it from the previous
   // run's (stamps are epoch * 32 + pass; on the 2^26 wrap the stale stamps are
   // cleared here), and the last workgroup out stores it (no k_reset launch)
@@ -320,7 +343,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
 #pragma unroll
   for (int j = 0; j < kFrontR; j++) {
     const uint64_t i = (bin0 + j) * 1024 + t;
-    if ((uint32_t)j < bpw && i < n) {
+    if ((uint32_t)j < bpw && i < iend) {
       lim_acc(px[j], py[j], pz[j]);
     } else {
       px[j] = py[j] = pz[j] = T(0);
@@ -328,7 +351,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
   }
   for (uint32_t j = kFrontR; j < bpw; j++) {
     const uint64_t i = (bin0 + j) * 1024 + t;
-    if (i < n) {
+    if (i < iend) {
       T x, y, z;
       front_point(p, i, x, y, z);
       lim_acc(x, y, z);
@@ -469,7 +492,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
     bool redo = false, cold = false;
     auto visit = [&](uint32_t j, uint64_t i, T x, T y, T z) {
       uint32_t key = kInvalid;
-      if (i < n8) {
+      if (i < iend8) {
         key = fast32 ? voxel_key_f32((float)x, (float)y, (float)z, off32, inv32, half_tol, lenf, len) : kKeyRedo;
         redo |= key == kKeyRedo;
         cold |= key == kInvalid;
@@ -485,7 +508,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
     for (uint32_t j = kFrontR; j < bpw; j++) {
       const uint64_t i = (bin0 + j) * 1024 + t;
       T x = 0, y = 0, z = 0;
-      if (i < n8) front_point(p, i, x, y, z);
+      if (i < iend8) front_point(p, i, x, y, z);
       visit(j, i, x, y, z);
     }
     if (__any(redo)) {
@@ -507,7 +530,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
       for (uint32_t j = 0; j < bpw; j++) {
         const uint64_t i = (bin0 + j) * 1024 + t;
         const uint32_t key = binfo[j * 1024 + t];
-        if (i >= n8) continue;
+        if (i >= iend8) continue;
         if (key == kInvalid) atomicMin(&s_bad[i / chunk], (uint32_t)i);
         else if (!small) fresh += stamp_key_front(key, table, stamps, stamp);
       }
@@ -875,7 +898,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
       if ((uint32_t)j < bpw) put(j, (bin0 + j) * 1024 + t, px[j], py[j], pz[j]);
     for (uint32_t j = kFrontR; j < bpw; j++) {
       const uint64_t i = (bin0 + j) * 1024 + t;
-      if (i < n8) {
+      if (i < iend8) {
         T x, y, z;
         front_point(p, i, x, y, z);
         put(j, i, x, y, z);

@@ -2113,7 +2113,10 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
     F.rbs = P->frbs;
     F.dbg_store = 0;
     F.eval_all = P->exact_counts;
-    k_front<T><<<dim3(P->fG, B), kFrontThreads, P->flds, st>>>(pts, F);
+    F.B = (uint32_t)B;
+    F.nbins = P->nbins;
+    F.xcd_local = (B % 8) == 0 ? 1 : 0;
+    k_front<T><<<P->fG * B, kFrontThreads, P->flds, st>>>(pts, F);
     if (P->timing)
       for (int e = 1; e <= 4; e++) HIPCHK(hipEventRecord(P->ev[e], st));
   } else {
@@ -2251,8 +2254,10 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
 #define NDNET_FRONT_CU_SHARE 1
 #endif
     const uint32_t gt = (uint32_t)(cus / (NDNET_FRONT_CU_SHARE * batch) > 0 ? cus / (NDNET_FRONT_CU_SHARE * batch) : 1);
-    uint32_t bpw = (P->nbins + gt - 1) / gt;
-    uint32_t G = (P->nbins + bpw - 1) / bpw;
+    // G workgroups per cloud (every CU busy at B = 16), the cloud's bins split
+    // as evenly as G allows: bpw = the most bins a workgroup holds
+    uint32_t G = gt < P->nbins ? gt : P->nbins;
+    uint32_t bpw = (P->nbins + G - 1) / G;
     // rank bins of 512 points when that keeps every wave busy and fits
     auto lds_of = [&](uint32_t rbs) {
       return sizeof(uint32_t) * ((size_t)kFrontTable + (size_t)bpw * 1024 + (size_t)bpw * (1024 / rbs) * P->ndcap);
