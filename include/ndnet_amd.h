@@ -134,6 +134,15 @@ int ndnet_ndt_get_path(void *plan);
  * count with the reference's); default 0.  Path 1 always counts. */
 int ndnet_ndt_set_exact_counts(void *plan, int on);
 
+/* The retained divergence list (kl_divergences, ndt.c:189-205) is read by the
+ * level-1 prune only when it removes NDs.  A cloud with num_nds <= num_desired
+ * keeps every ND (or fails with rc -1 before reading the list), so by default
+ * its run only counts the events (stats num_events / num_kl are unchanged)
+ * and builds the list on demand, before ndnet_ndt_prune or
+ * ndnet_ndt_debug_dump reads it; the built list is the eagerly built one,
+ * entry for entry.  on = 0 builds every list in the run.  Default 1. */
+int ndnet_ndt_set_lazy_list(void *plan, int on);
+
 /* d_points: [batch][num_points][3] float32 on the device (the tensor
  * ndt_preprocessing receives).  d_labels: [batch][num_points] int32 class ids
  * or NULL.  d_out: [batch][num_desired][12] float32 = mean(3) | covariance(9)

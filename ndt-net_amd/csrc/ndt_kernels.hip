@@ -82,6 +82,7 @@ struct CloudCtl {
   uint32_t num_out;
   uint32_t last_k;
   uint32_t clear_stamps; // the epoch wrapped this run: k_limits zeroes the cloud's stamps
+  uint32_t kl_deferred;  // the retained list was not built by the run (lazy list, num_nds <= k)
 };
 
 struct Plan {
@@ -160,6 +161,7 @@ struct Plan {
   size_t wq_lds;              // k_welford_q dynamic LDS (labelled runs: class histograms)
   uint32_t wq_grid;           // k_welford_q workgroups: one per CU
   uint32_t* wq_ctr;           // [2] k_welford_q dynamic item counter (re-armed by k_kl_chains)
+  int eager_list;             // build every cloud's retained list in the run (ndnet_ndt_set_lazy_list(plan, 0))
 };
 
 // ------------------------------------------------------------------ helpers
@@ -1181,7 +1183,27 @@ struct KLArgs {
   uint64_t k;
   int ncls;
   int kl_lds;            // prune_and_emit keeps its per-cloud arrays in LDS (kl_lds_bytes)
+  int mode;              // kKLEager, kKLLazy or kKLBuild (see kl_list_skipped)
 };
+
+// The retained list (the reference's kl_divergences array, in insertion
+// order) only matters to the level-1 prune when it removes something: with
+// num_nds <= k the prune keeps every ND (to_remove = 0) or fails with rc -1
+// before reading it (ndt.c:36-39), and the output rows are the NDs in voxel
+// order either way.  A lazy run (kKLLazy) then scores no events and sorts
+// nothing for that cloud, it only counts the events (num_events / num_kl
+// as the reference reports them); the list is built on demand (kKLBuild)
+// before anything reads it: a further prune level (ndnet_ndt_prune, the
+// legacy prune_nds) or a debug dump.  The built list is the one the eager
+// run builds, entry for entry.
+enum KLMode : int { kKLEager = 0, kKLLazy = 1, kKLBuild = 2 };
+__device__ inline bool kl_list_deferrable(const KLArgs& A, const CloudCtl& c) {
+  return A.mode == kKLLazy && (uint64_t)c.num_nds <= A.k;
+}
+// the sort kernels skip a cloud whose list this launch does not build
+__device__ inline bool kl_list_skipped(const KLArgs& A, const CloudCtl& c) {
+  return A.mode == kKLBuild ? !c.kl_deferred : kl_list_deferrable(A, c);
+}
 
 // Prune (ndt.c:28-73) of cloud b's retained list to k NDs, then the output
 // rows (ndt.c:75-117).  Shared by k_kl (level 1) and k_prune (later levels).
@@ -1202,12 +1224,14 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
   const uint32_t* op;
   uint8_t* alive;
   const uint32_t nv0 = c.num_valid, nkl0 = c.num_kl;
+  const bool walk = k < nv0;  // the prune removes something: the walk reads the list
   if constexpr (kLds) {
     first = kl_smem;                                       // [ndcap]
     tmp = kl_smem + A.ndcap;                               // [ecap]
     uint32_t* s_op = kl_smem + A.ndcap + A.ecap;           // [ecap]
     alive = (uint8_t*)(kl_smem + A.ndcap + 2 * A.ecap);    // [ndcap]
-    for (uint32_t i = threadIdx.x; i < nkl0; i += blockDim.x) s_op[i] = g_op[i];
+    if (walk)
+      for (uint32_t i = threadIdx.x; i < nkl0; i += blockDim.x) s_op[i] = g_op[i];
     for (uint32_t u = threadIdx.x; u < nd; u += blockDim.x) alive[u] = g_alive[u];
     op = s_op;
     __syncthreads();
@@ -1222,6 +1246,10 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
   uint32_t kills = 0;
   if (k > nv0) {
     rc = -1;  // "Number of desired normal distributions is greater ..." (ndt.c:36-39)
+  } else if (!walk) {
+    // to_remove = 0: the loop of ndt.c:44-67 runs no iteration, the shift
+    // moves nothing; list, counts and flags stay as they are
+    if (threadIdx.x == 0) c.num_kl = nkl0;
   } else {
     const uint32_t to_remove = (uint32_t)(nv0 - k);
     for (uint32_t u = threadIdx.x; u < nd; u += blockDim.x) first[u] = kInvalid;
@@ -1526,10 +1554,13 @@ __global__ void __launch_bounds__(256) k_kl_chains(KLArgs A) {
 // KL score of every (voxel, direction) slot (kullback_leibler.c:28-127, 141-180).
 // KL score per (ND, direction) slot (kullback_leibler.c:129-202 calling
 // kl_divergence, :28-127) from the two chain states at the event's rank.
+// A lazy run only flags the events of a deferred cloud (no score).
 __global__ void __launch_bounds__(256) k_kl_events(KLArgs A) {
   const int b = blockIdx.y;
   const CloudCtl& c = A.ctl[b];
   if (c.state != kAccepted) return;
+  if (A.mode == kKLBuild && !c.kl_deferred) return;
+  const bool score = !kl_list_deferrable(A, c);
   const uint32_t nd = c.num_nds;
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= 6 * nd) return;
@@ -1564,11 +1595,11 @@ __global__ void __launch_bounds__(256) k_kl_events(KLArgs A) {
       const double pd = lu3_det(Lp, sp), qd = lu3_det(Lq, sq);
       if (!(pd == 0 || qd == 0) && lu3_sgndet(Lp, sp) != 0 && lu3_sgndet(Lq, sq) != 0) {
         flag = 1;
-        val = kl_score(Lp, Lq, psq & 0x3f, pd, qd);
+        if (score) val = kl_score(Lp, Lq, psq & 0x3f, pd, qd);
       }
     }
   }
-  A.slot_val_all[eb + s] = val;
+  if (score) A.slot_val_all[eb + s] = val;
   A.slot_flag_all[eb + s] = flag;
 }
 
@@ -1598,7 +1629,7 @@ __device__ inline unsigned long long score_key(double v) { return ~ord_key(v + 0
 __global__ void __launch_bounds__(kChunk) k_kl_rank_chunks(KLArgs A) {
   const int b = blockIdx.y;
   const CloudCtl& c = A.ctl[b];
-  if (c.state != kAccepted) return;
+  if (c.state != kAccepted || kl_list_skipped(A, c)) return;
   const uint32_t nslots = 6 * c.num_nds;
   const uint32_t ch = blockIdx.x;
   if (ch * kChunk >= nslots) return;
@@ -1664,7 +1695,7 @@ __global__ void __launch_bounds__(kChunk) k_kl_rank_chunks(KLArgs A) {
 __global__ void __launch_bounds__(kChunk) k_kl_nan_keys(KLArgs A) {
   const int b = blockIdx.y;
   const CloudCtl& c = A.ctl[b];
-  if (c.state != kAccepted) return;
+  if (c.state != kAccepted || kl_list_skipped(A, c)) return;
   const uint32_t nch = (6 * c.num_nds + kChunk - 1) / kChunk;
   const uint32_t ch = blockIdx.x;
   if (ch >= nch) return;
@@ -1793,7 +1824,7 @@ template <bool kLds>
 __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
   const int b = blockIdx.y;
   const CloudCtl& c = A.ctl[b];
-  if (c.state != kAccepted) return;
+  if (c.state != kAccepted || kl_list_skipped(A, c)) return;
   const uint32_t nch = (6 * c.num_nds + kChunk - 1) / kChunk;
   if (blockIdx.x * kMergeRuns >= nch) return;
   const uint64_t eb = (uint64_t)b * A.ecap, kb = (uint64_t)b * A.sortcap, cb = (uint64_t)b * A.nchunk;
@@ -1909,6 +1940,29 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
 #undef MERGE_MARK
 }
 
+// Poison beyond the written list (the reference's uninitialised tail).
+__device__ void kl_poison_tail(const KLArgs& A, uint64_t eb, uint32_t E) {
+  double* ov = A.ord_val_all + eb;
+  uint32_t* opp = A.ord_p_all + eb;
+  uint32_t* oq = A.ord_q_all + eb;
+  for (uint32_t i = E + threadIdx.x; i < A.ecap; i += blockDim.x) {
+    opp[i] = kInvalid;
+    oq[i] = kInvalid;
+    ov[i] = 0.0;
+  }
+}
+
+// The end of an on-demand list build (kKLBuild): the tail poisoned, the
+// cloud's list marked built.  Counts and flags were set by the run.
+__global__ void __launch_bounds__(256) k_kl_list_done(KLArgs A) {
+  const int b = blockIdx.x;
+  CloudCtl& c = A.ctl[b];
+  if (c.state != kAccepted || !c.kl_deferred) return;
+  kl_poison_tail(A, (uint64_t)b * A.ecap, c.num_events);
+  __syncthreads();
+  if (threadIdx.x == 0) c.kl_deferred = 0;
+}
+
 // Prune and output rows: one workgroup per cloud.
 __global__ void __launch_bounds__(kKLThreads) k_kl(KLArgs A) {
   const int b = blockIdx.x;
@@ -1920,6 +1974,7 @@ __global__ void __launch_bounds__(kKLThreads) k_kl(KLArgs A) {
   if (c.state != kAccepted) {
     if (threadIdx.x == 0) {
       c.num_out = 0;
+      c.kl_deferred = 0;
       write_stats(A, b);
     }
     pad_class_rows(A, b, A.k, 0);
@@ -1928,27 +1983,26 @@ __global__ void __launch_bounds__(kKLThreads) k_kl(KLArgs A) {
   const uint32_t nd = c.num_nds;
   const uint64_t ob = (uint64_t)b * A.ndcap, eb = (uint64_t)b * A.ecap;
   const uint32_t nch = (6 * nd + kChunk - 1) / kChunk;
-  // event count from the chunk counters
+  const bool deferred = kl_list_deferrable(A, c);
+  // event count: from the chunk counters, or (deferred list) from the flags
   uint32_t e_part = 0;
-  for (uint32_t c2 = threadIdx.x; c2 < nch; c2 += blockDim.x) {
-    const uint32_t cc = A.chunk_cnt[(uint64_t)b * A.nchunk + c2];
-    e_part += (cc >> 16) + (cc & 0xffffu);
+  if (deferred) {
+    const uint32_t* fl = A.slot_flag_all + eb;
+    for (uint32_t s2 = threadIdx.x; s2 < 6 * nd; s2 += blockDim.x) e_part += fl[s2];
+  } else {
+    for (uint32_t c2 = threadIdx.x; c2 < nch; c2 += blockDim.x) {
+      const uint32_t cc = A.chunk_cnt[(uint64_t)b * A.nchunk + c2];
+      e_part += (cc >> 16) + (cc & 0xffffu);
+    }
   }
   uint32_t ev[1] = {e_part};
   uint32_t E;
   block_scan_items(ev, 0u, AddU32(), s_u32, E);
   KL_MARK(2);
-  double* ov = A.ord_val_all + eb;
-  uint32_t* opp = A.ord_p_all + eb;
-  uint32_t* oq = A.ord_q_all + eb;
-  // poison beyond the written list (the reference's uninitialised tail)
-  for (uint32_t i = E + threadIdx.x; i < A.ecap; i += blockDim.x) {
-    opp[i] = kInvalid;
-    oq[i] = kInvalid;
-    ov[i] = 0.0;
-  }
+  if (!deferred) kl_poison_tail(A, eb, E);
   for (uint32_t u = threadIdx.x; u < nd; u += blockDim.x) A.alive_all[ob + u] = 1;
   if (threadIdx.x == 0) {
+    c.kl_deferred = deferred ? 1u : 0u;
     c.num_events = E;
     c.num_kl = E;
     c.num_phys = E;
@@ -2072,7 +2126,36 @@ static KLArgs kl_args(Plan* P, uint64_t k, float* out, float* out_cls, double* p
   A.k = k;
   A.ncls = P->ncls;
   A.kl_lds = kl_lds_bytes(P) <= (size_t)kKLLdsMax ? 1 : 0;
+  A.mode = P->eager_list ? kKLEager : kKLLazy;
   return A;
+}
+
+static size_t merge_lds_bytes(const Plan* P);
+
+// The event sort of the clouds in A's scope (every cloud in a run, the
+// deferred ones in a build).
+static void launch_list_sort(Plan* P, const KLArgs& A, hipStream_t st) {
+  const int B = P->B;
+  k_kl_rank_chunks<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
+  k_kl_nan_keys<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
+  const uint32_t mg = (P->nchunk + kMergeRuns - 1) / kMergeRuns;
+  if (P->nchunk <= (uint32_t)kMergeLdsChunks)
+    k_kl_merge<true><<<dim3(mg, B), kChunk * kMergeRuns, merge_lds_bytes(P), st>>>(A);
+  else
+    k_kl_merge<false><<<dim3(mg, B), kChunk * kMergeRuns, 0, st>>>(A);
+}
+
+// Builds the retained lists a lazy run deferred (no-op for the others).
+static int build_deferred_lists(Plan* P, hipStream_t st) {
+  if (P->eager_list) return NDNET_OK;
+  KLArgs A = kl_args(P, P->k, nullptr, nullptr, nullptr, nullptr, nullptr);
+  A.marks = nullptr;
+  A.mode = kKLBuild;
+  k_kl_events<<<dim3((6 * P->ndcap + 255) / 256, P->B), 256, 0, st>>>(A);
+  launch_list_sort(P, A, st);
+  k_kl_list_done<<<P->B, 256, 0, st>>>(A);
+  HIPCHK(hipGetLastError());
+  return NDNET_OK;
 }
 
 static size_t merge_lds_bytes(const Plan* P) { return 2 * (size_t)P->nchunk * kChunk * sizeof(unsigned long long); }
@@ -2146,13 +2229,7 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
   A.stats_out = stats_dst;
   k_kl_chains<<<dim3((P->ndcap + 255) / 256, B), 256, 0, st>>>(A);
   k_kl_events<<<dim3((6 * P->ndcap + 255) / 256, B), 256, 0, st>>>(A);
-  k_kl_rank_chunks<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
-  k_kl_nan_keys<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
-  const uint32_t mg = (P->nchunk + kMergeRuns - 1) / kMergeRuns;
-  if (P->nchunk <= (uint32_t)kMergeLdsChunks)
-    k_kl_merge<true><<<dim3(mg, B), kChunk * kMergeRuns, merge_lds_bytes(P), st>>>(A);
-  else
-    k_kl_merge<false><<<dim3(mg, B), kChunk * kMergeRuns, 0, st>>>(A);
+  launch_list_sort(P, A, st);
   k_kl<<<B, kKLThreads, A.kl_lds ? kl_lds_bytes(P) : 0, st>>>(A);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[6], st));
   HIPCHK(hipGetLastError());
@@ -2338,6 +2415,13 @@ int ndnet_ndt_set_exact_counts(void* plan, int on) {
   return NDNET_OK;
 }
 
+int ndnet_ndt_set_lazy_list(void* plan, int on) {
+  Plan* P = (Plan*)plan;
+  if (!P || on < 0 || on > 1) return NDNET_ERR_ARG;
+  P->eager_list = on ? 0 : 1;
+  return NDNET_OK;
+}
+
 int ndnet_ndt_get_path(void* plan) {
   Plan* P = (Plan*)plan;
   if (!P) return NDNET_ERR_ARG;
@@ -2398,6 +2482,8 @@ int ndnet_ndt_prune(void* plan, void* stream, uint64_t num_desired, float* d_out
   Plan* P = (Plan*)plan;
   if (!P || num_desired == 0) return NDNET_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
+  const int rc = build_deferred_lists(P, st);
+  if (rc != NDNET_OK) return rc;
   KLArgs A = kl_args(P, num_desired, d_out, d_out_classes, d_out_points, d_out_covariances, d_out_classes16);
   A.stats_out = d_stats;
   k_prune<<<P->B, kKLThreads, A.kl_lds ? kl_lds_bytes(P) : 0, st>>>(A);
@@ -2450,6 +2536,9 @@ int ndnet_ndt_debug_dump(void* plan, int cloud, uint32_t* nd_n, double* nd_mean,
   Plan* P = (Plan*)plan;
   if (!P || cloud < 0 || cloud >= P->B) return NDNET_ERR_ARG;
   CloudCtl c;
+  HIPCHK(hipDeviceSynchronize());
+  const int rc = build_deferred_lists(P, nullptr);
+  if (rc != NDNET_OK) return rc;
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(&c, P->ctl + cloud, sizeof(CloudCtl), hipMemcpyDeviceToHost));
   const size_t ob = (size_t)cloud * P->ndcap, eb = (size_t)cloud * P->ecap;

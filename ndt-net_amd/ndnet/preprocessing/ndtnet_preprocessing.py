@@ -68,6 +68,12 @@ class NdtPlan:
         (include/ndnet_amd.h ndnet_ndt_set_exact_counts; debug / parity)."""
         _lib.check(_lib.lib().ndnet_ndt_set_exact_counts(self.handle, 1 if on else 0), "ndnet_ndt_set_exact_counts")
 
+    def set_lazy_list(self, on: bool) -> None:
+        """Defer the retained KL list of clouds whose level-1 prune cannot read
+        it (num_nds <= k) until a prune or dump needs it (default on;
+        include/ndnet_amd.h ndnet_ndt_set_lazy_list)."""
+        _lib.check(_lib.lib().ndnet_ndt_set_lazy_list(self.handle, 1 if on else 0), "ndnet_ndt_set_lazy_list")
+
     @property
     def path(self) -> int:
         return int(_lib.lib().ndnet_ndt_get_path(self.handle))

@@ -128,6 +128,51 @@ def test_skipped_grids_change_nothing(name):
         assert sk == (V < k)
 
 
+@pytest.mark.parametrize("kind", ["U", "L"])
+def test_lazy_list_equals_eager(kind):
+    """Lazy retained list (default): clouds with num_nds <= k score and sort
+    no events in the run; a later prune level or dump builds the list on
+    demand.  Rows, stats, every dumped intermediate (the list entry for
+    entry) and two further prune levels equal the eager build's, bit for
+    bit.  U at k = 1000 has num_nds = k in every cloud (the deferred case),
+    L has num_nds > k (the list is built in the run either way)."""
+    import torch
+    from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
+    from ndnet.synthetic import make_batch
+    B, n, k = 4, 100_000, 1000
+    pts = torch.from_numpy(make_batch(kind, B, n)).cuda()
+    res = {}
+    for variant in ("eager", "lazy", "lazy_no_dump"):  # the last builds the list inside prune
+        plan = NdtPlan(B, n, k, -1)
+        plan.set_lazy_list(variant != "eager")
+        out = torch.empty((B, k, 12), dtype=torch.float32, device="cuda")
+        plan.run(pts, None, out, None)
+        torch.cuda.synchronize()
+        stats = plan.host_stats()
+        if kind == "U":
+            assert all(s.num_nds == k for s in stats)
+        dumps = None
+        if variant != "lazy_no_dump":
+            dumps = [_dump(plan, b, int(stats[b].num_nds), int(stats[b].num_events)) for b in range(B)]
+        levels = []
+        for k2 in (600, 300):
+            o2 = torch.empty((B, k2, 12), dtype=torch.float32, device="cuda")
+            plan.prune(k2, o2)
+            torch.cuda.synchronize()
+            levels.append((o2.cpu().numpy(), [bytes(s) for s in plan.host_stats()]))
+        res[variant] = (out.cpu().numpy(), [bytes(s) for s in stats], dumps, levels)
+    o0, s0, d0, l0 = res["eager"]
+    for variant in ("lazy", "lazy_no_dump"):
+        o1, s1, d1, l1 = res[variant]
+        assert np.array_equal(o0, o1) and s0 == s1, variant
+        if d1 is not None:
+            for b in range(B):
+                for key in d0[b]:
+                    assert np.array_equal(d0[b][key], d1[b][key], equal_nan=True), (b, key)
+        for (a0, t0), (a1, t1) in zip(l0, l1):
+            assert np.array_equal(a0, a1) and t0 == t1, variant
+
+
 def test_reference_driver_fixture():
     """Rows the reference's own ndt_preprocessing produced (over the oracle ABI)."""
     import torch
