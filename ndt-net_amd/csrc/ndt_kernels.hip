@@ -160,7 +160,7 @@ struct Plan {
   int exact_counts;           // k_front counts every bisection grid (ndnet_ndt_set_exact_counts)
   size_t wq_lds;              // k_welford_q dynamic LDS (labelled runs: class histograms)
   uint32_t wq_grid;           // k_welford_q workgroups: one per CU
-  uint32_t* wq_ctr;           // [2] k_welford_q dynamic item counter (re-armed by k_kl_chains)
+  uint32_t* wq_ctr;           // [2] k_welford_q dynamic item counter (re-armed by k_kl_rank_chunks)
   int eager_list;             // build every cloud's retained list in the run (ndnet_ndt_set_lazy_list(plan, 0))
 };
 
@@ -862,13 +862,42 @@ __device__ inline uint32_t wave_max_u32(uint32_t v) {
   return __builtin_amdgcn_readfirstlane(v);
 }
 
+// Event order of one ND's in-place LU chain (SURVEY A.5): the mutating events
+// it takes part in, by ascending key 6 * dense(v) + d.  Neighbours below it
+// (Z-, Y-, X-: smaller linear index) come first, as q; then its own six
+// directions, as p; then the neighbours above (X+, Y+, Z+), as q.  So the
+// chain position of an event is a popcount over a 12-slot mask:
+//   slot 0 Z-(q), 1 Y-(q), 2 X-(q), 3..8 own d = 0..5 (p), 9 X+(q), 10 Y+(q), 11 Z+(q)
+__device__ inline uint32_t chain_mask(uint32_t e) {  // e: 6 eligible-direction bits
+  return ((e >> 5) & 1u) | (((e >> 3) & 1u) << 1) | (((e >> 1) & 1u) << 2) | ((e & 0x3fu) << 3) |
+         ((e & 1u) << 9) | (((e >> 2) & 1u) << 10) | (((e >> 4) & 1u) << 11);
+}
+__device__ inline uint32_t qslot_of_dir(uint32_t d) {  // q-slot of the neighbour in direction d
+  return (0x0b1a29u >> (4 * d)) & 0xfu;  // {d0: 9, d1: 2, d2: 10, d3: 1, d4: 11, d5: 0}
+}
+
+// What k_welford_q writes for the KL stage after an ND's moments (the LU
+// chains, formerly their own kernel): neighbours, chain masks, the chain's
+// in-place LU states and the final (post-KL) covariance.
+struct WqChainArgs {
+  const uint32_t* vox;     // [B][ndcap] linear voxel of each ND
+  const uint32_t* dense;   // [B][vcap] dense id of each voxel (kInvalid: empty)
+  int32_t* nb;             // [B][ndcap][6]
+  uint32_t* nkeys;         // [B][ndcap] chain masks
+  double* chain;           // [B][108][ndcap] step-major LU states
+  uint32_t* chain_ps;      // [B][12][ndcap]
+  double* cov_post;        // [B][ndcap][9]
+  uint64_t vcap;
+};
+
 template <typename T>
 __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, int B, const T* __restrict__ nd_pts,
                                                           const uint16_t* __restrict__ nd_lbl,
                                                           const uint32_t* __restrict__ nd_n,
                                                           const uint32_t* __restrict__ nd_base, double* nd_mean,
                                                           double* nd_cov, uint16_t* nd_cls, uint32_t* hist_all,
-                                                          int ncls, uint64_t n, uint32_t ndcap, uint32_t* wq_ctr) {
+                                                          int ncls, uint64_t n, uint32_t ndcap, uint32_t* wq_ctr,
+                                                          WqChainArgs CA) {
   extern __shared__ __attribute__((aligned(16))) unsigned char wq_smem[];
   double* lrt = (double*)wq_smem;                                // [kWqRt] refined reciprocals of 1..kWqRt
   uint32_t* pre = (uint32_t*)(wq_smem + kWqRt * sizeof(double));  // [B + 1] first item of each cloud
@@ -892,7 +921,7 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
   // that finishes a light ND group takes the next one, so a heavy group is
   // never queued behind another.  A wave first reads the counter and only
   // increments it while items remain (one contended word takes ~11 ns per
-  // atomic: a thousand waves each adding would cost ~10 us).  k_kl_chains,
+  // atomic: a thousand waves each adding would cost ~10 us).  k_kl_rank_chunks,
   // the next kernel on the stream, re-arms it.
   const uint32_t nwaves = gridDim.x * (kWqThreads / 64);
   auto next_item = [&]() -> uint32_t {
@@ -922,6 +951,33 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
   const uint32_t jj = j < 3 ? j : 0u;
   const T* src = nd_pts + ((uint64_t)b * n + beg) * 3 + jj;
   const uint32_t mx = wave_max_u32(cnt);
+  // the ND's neighbours (voxel.c:116-175, directions X+, X-, Y+, Y-, Z+, Z-):
+  // lane j of the quad takes directions j and j + 4; their dense ids and
+  // counts are loaded before the fold, behind the first point loads
+  int32_t nw[2];
+  uint32_t ncn[2];
+  {
+    const uint32_t lx = ctl[b].len[0], ly = ctl[b].len[1], lz = ctl[b].len[2];
+    const uint32_t lin = CA.vox[o];
+    const uint32_t zc = lin / (lx * ly), yc = (lin % (lx * ly)) / lx, xc = lin % lx;
+    const uint32_t* dense = CA.dense + (uint64_t)b * CA.vcap;
+    uint32_t dn[2];
+    bool in[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const uint32_t dd = j + 4u * (uint32_t)k;
+      const uint32_t xx = xc + (dd == 0 ? 1u : dd == 1 ? ~0u : 0u);
+      const uint32_t yy = yc + (dd == 2 ? 1u : dd == 3 ? ~0u : 0u);
+      const uint32_t zz = zc + (dd == 4 ? 1u : dd == 5 ? ~0u : 0u);
+      in[k] = dd < 6u && xx < lx && yy < ly && zz < lz;
+      dn[k] = dense[in[k] ? zz * lx * ly + yy * lx + xx : lin];
+    }
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      nw[k] = (in[k] && dn[k] != kInvalid) ? (int32_t)dn[k] : -1;
+      ncn[k] = nd_n[(uint64_t)b * ndcap + (nw[k] >= 0 ? (uint32_t)nw[k] : (uint32_t)(o - (uint64_t)b * ndcap))];
+    }
+  }
 
   double mean = 0.0, m2 = 0.0, off = 0.0;
   bool bad = false;
@@ -1092,13 +1148,55 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
     }
     run(mx2, qbad, std::true_type{});
   }
+  const double vraw = m2 / (double)cnt;
+  const double vd = (vraw != vraw) ? 0.0 : vraw;
   if (live && j < 3) {
-    const double v = m2 / (double)cnt;
     nd_mean[3 * o + j] = mean;
-    nd_cov[9 * o + 4 * j] = (v != v) ? 0.0 : v;
+    nd_cov[9 * o + 4 * j] = vd;
     const uint32_t ia = j == 2 ? 0u : j, ib = j == 2 ? 2u : j + 1u;
     nd_cov[9 * o + 3 * ia + ib] = off;
     nd_cov[9 * o + 3 * ib + ia] = off;
+  }
+  // The ND's KL chain: eligible directions (a neighbour, and
+  // more than one sample on both sides), the chain mask, and every in-place
+  // LU state of the chain, stored step-major ([t][j][ND], coalesced across
+  // the wave's quads); lane 0 of the quad runs it on the covariance gathered
+  // from lanes 0..2.
+  {
+    uint32_t el = 0;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const uint32_t dd = j + 4u * (uint32_t)k;
+      if (live && dd < 6u) CA.nb[6 * o + dd] = nw[k];
+      if (nw[k] >= 0 && cnt > 1 && ncn[k] > 1) el |= 1u << dd;
+    }
+    el |= (uint32_t)__builtin_amdgcn_mov_dpp((int)el, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    el |= (uint32_t)__builtin_amdgcn_mov_dpp((int)el, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    double S[9];
+    S[0] = dpp_d<0x00>(vd);
+    S[4] = dpp_d<0x55>(vd);
+    S[8] = dpp_d<0xAA>(vd);
+    S[1] = S[3] = dpp_d<0x00>(off);
+    S[5] = S[7] = dpp_d<0x55>(off);
+    S[2] = S[6] = dpp_d<0xAA>(off);
+    if (live && j == 0) {
+      const uint32_t mask = chain_mask(el);
+      const int nT = __popc(mask);
+      CA.nkeys[o] = mask;
+      const uint64_t ob = (uint64_t)b * ndcap, u = o - ob;
+      double* chain = CA.chain + ob * 108 + u;
+      uint32_t* ps = CA.chain_ps + ob * 12 + u;
+      for (int t = 0; t < nT; t++) {
+        uint32_t perm;
+        int sg;
+        lu3(S, perm, sg);
+#pragma unroll
+        for (int q = 0; q < 9; q++) chain[(uint64_t)(9 * t + q) * ndcap] = S[q];
+        ps[(uint64_t)t * ndcap] = perm | (sg < 0 ? 0x100u : 0u);
+      }
+#pragma unroll
+      for (int q = 0; q < 9; q++) CA.cov_post[9 * o + q] = S[q];
+    }
   }
   if (live && j == 0) {
     uint16_t cls = 0;
@@ -1138,7 +1236,7 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
 struct KLArgs {
   unsigned long long* marks;  // [B][16] phase stamps of k_kl, or null
   CloudCtl* ctl;
-  uint32_t* wq_ctr;           // k_welford_q's item counter, re-armed by k_kl_chains
+  uint32_t* wq_ctr;           // k_welford_q's item counter, re-armed by k_kl_rank_chunks
   const uint32_t* dense_all;
   const uint32_t* vox_all;
   const uint32_t* nd_n;
@@ -1476,100 +1574,16 @@ __device__ void pad_class_rows(const KLArgs& A, int b, uint64_t k, uint32_t num_
   for (uint64_t r = num_out + threadIdx.x; r < k; r += blockDim.x) A.out_cls[w * ((uint64_t)b * k + r)] = 1.0f;
 }
 
-// Event order of one ND's in-place LU chain (SURVEY A.5): the mutating events
-// it takes part in, by ascending key 6 * dense(v) + d.  Neighbours below it
-// (Z-, Y-, X-: smaller linear index) come first, as q; then its own six
-// directions, as p; then the neighbours above (X+, Y+, Z+), as q.  So the
-// chain position of an event is a popcount over a 12-slot mask:
-//   slot 0 Z-(q), 1 Y-(q), 2 X-(q), 3..8 own d = 0..5 (p), 9 X+(q), 10 Y+(q), 11 Z+(q)
-__device__ inline uint32_t chain_mask(uint32_t e) {  // e: 6 eligible-direction bits
-  return ((e >> 5) & 1u) | (((e >> 3) & 1u) << 1) | (((e >> 1) & 1u) << 2) | ((e & 0x3fu) << 3) |
-         ((e & 1u) << 9) | (((e >> 2) & 1u) << 10) | (((e >> 4) & 1u) << 11);
-}
-__device__ inline uint32_t qslot_of_dir(uint32_t d) {  // q-slot of the neighbour in direction d
-  return (0x0b1a29u >> (4 * d)) & 0xfu;  // {d0: 9, d1: 2, d2: 10, d3: 1, d4: 11, d5: 0}
-}
-
-// Neighbours, chain masks and LU chains, one lane per ND.
-__global__ void __launch_bounds__(256) k_kl_chains(KLArgs A) {
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *A.wq_ctr = 0u;  // k_welford_q has finished
-  const int b = blockIdx.y;
-  const CloudCtl& c = A.ctl[b];
-  if (c.state != kAccepted) return;
-  const uint32_t nd = c.num_nds;
-  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-  if (u >= nd) return;
+// KL score of one (ND, direction) slot (kullback_leibler.c:129-202 calling
+// kl_divergence, :28-127) from the two chain states at the event's rank;
+// score = false only flags it.  Every load is issued unconditionally from
+// clamped indices, in three rounds (neighbour -> counts and chain masks -> LU
+// states).
+__device__ inline void kl_event(const KLArgs& A, int b, uint32_t s, bool score, uint32_t& flag, double& val) {
   const uint64_t ob = (uint64_t)b * A.ndcap;
-  const uint32_t* dense = A.dense_all + (uint64_t)b * A.vcap;
-  const uint32_t* vn = A.nd_n + ob;
-  const uint32_t lx = c.len[0], ly = c.len[1], lz = c.len[2];
-  const uint32_t lin = A.vox_all[ob + u];
-  const uint32_t z = lin / (lx * ly), y = (lin % (lx * ly)) / lx, x = lin % lx;
-  const uint32_t nu = vn[u];
-  // neighbours (voxel.c:116-175, directions X+, X-, Y+, Y-, Z+, Z-): every
-  // dense-id load, then every count load, issued unconditionally from
-  // clamped indices (a predicated load would serialise on its own wait)
-  uint32_t dn[6];
-  bool in[6];
-#pragma unroll
-  for (int d = 0; d < 6; d++) {
-    const uint32_t xx = x + (d == 0 ? 1u : d == 1 ? ~0u : 0u);
-    const uint32_t yy = y + (d == 2 ? 1u : d == 3 ? ~0u : 0u);
-    const uint32_t zz = z + (d == 4 ? 1u : d == 5 ? ~0u : 0u);
-    in[d] = xx < lx && yy < ly && zz < lz;
-    dn[d] = dense[in[d] ? zz * lx * ly + yy * lx + xx : lin];
-  }
-  uint32_t cn[6];
-#pragma unroll
-  for (int d = 0; d < 6; d++) cn[d] = vn[(in[d] && dn[d] != kInvalid) ? dn[d] : u];
-  uint32_t elig = 0;
-#pragma unroll
-  for (int d = 0; d < 6; d++) {
-    const int32_t w = (in[d] && dn[d] != kInvalid) ? (int32_t)dn[d] : -1;
-    A.nb_all[6 * ob + 6 * u + d] = w;
-    if (w >= 0 && nu > 1 && cn[d] > 1) elig |= 1u << d;
-  }
-  const uint32_t mask = chain_mask(elig);
-  const int T = __popc(mask);
-  A.nkeys_all[ob + u] = mask;
-  // every in-place LU state of the chain, stored step-major ([t][j][ND]) so a
-  // wave's stores are coalesced
-  double S[9];
-#pragma unroll
-  for (int j = 0; j < 9; j++) S[j] = A.nd_cov[9 * (ob + u) + j];
-  double* chain = A.chain_all + (uint64_t)b * 108 * A.ndcap + u;
-  uint32_t* ps = A.chain_ps_all + (uint64_t)b * 12 * A.ndcap + u;
-  for (int t = 0; t < T; t++) {
-    uint32_t perm;
-    int sg;
-    lu3(S, perm, sg);
-#pragma unroll
-    for (int j = 0; j < 9; j++) chain[(uint64_t)(9 * t + j) * A.ndcap] = S[j];
-    ps[(uint64_t)t * A.ndcap] = perm | (sg < 0 ? 0x100u : 0u);
-  }
-#pragma unroll
-  for (int j = 0; j < 9; j++) A.nd_cov_post[9 * (ob + u) + j] = S[j];
-}
-
-// KL score of every (voxel, direction) slot (kullback_leibler.c:28-127, 141-180).
-// KL score per (ND, direction) slot (kullback_leibler.c:129-202 calling
-// kl_divergence, :28-127) from the two chain states at the event's rank.
-// A lazy run only flags the events of a deferred cloud (no score).
-__global__ void __launch_bounds__(256) k_kl_events(KLArgs A) {
-  const int b = blockIdx.y;
-  const CloudCtl& c = A.ctl[b];
-  if (c.state != kAccepted) return;
-  if (A.mode == kKLBuild && !c.kl_deferred) return;
-  const bool score = !kl_list_deferrable(A, c);
-  const uint32_t nd = c.num_nds;
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= 6 * nd) return;
-  const uint64_t ob = (uint64_t)b * A.ndcap, eb = (uint64_t)b * A.ecap;
   const uint32_t u = s / 6, d = s % 6;
   const uint32_t* vn = A.nd_n + ob;
   const int32_t w = A.nb_all[6 * ob + s];
-  // every load issued unconditionally from clamped indices, in three rounds
-  // (neighbour -> counts and chain masks -> LU states)
   const uint32_t wu = w >= 0 ? (uint32_t)w : u;
   const uint32_t nu = vn[u], nw = vn[wu];
   const uint32_t mu = A.nkeys_all[ob + u], mw = A.nkeys_all[ob + wu];
@@ -1585,8 +1599,8 @@ __global__ void __launch_bounds__(256) k_kl_events(KLArgs A) {
     Lq[j] = chain[(uint64_t)(9 * rqc + j) * A.ndcap + wu];
   }
   const uint32_t psp = cps[(uint64_t)rpc * A.ndcap + u], psq = cps[(uint64_t)rqc * A.ndcap + wu];
-  uint32_t flag = 0;
-  double val = 0.0;
+  flag = 0;
+  val = 0.0;
   if (w >= 0) {
     if (nu <= 1 || nw <= 1) {
       flag = 1;  // kl_divergence returns -1 with div 0 and the entry is kept
@@ -1599,8 +1613,6 @@ __global__ void __launch_bounds__(256) k_kl_events(KLArgs A) {
       }
     }
   }
-  if (score) A.slot_val_all[eb + s] = val;
-  A.slot_flag_all[eb + s] = flag;
 }
 
 // ---- the reference's insertion order as one chip-wide sort ----
@@ -1618,7 +1630,8 @@ __global__ void __launch_bounds__(256) k_kl_events(KLArgs A) {
 // entries ahead of t; two NaNs keep slot order because m_s is non-increasing.
 // -0.0 is keyed as +0.0 (the reference compares with >, where they are equal).
 //
-// k_kl_rank_chunks sorts each kChunk-slot chunk (rank by counting in LDS);
+// k_kl_rank_chunks scores its chunk's slots and sorts them (rank by counting
+// in LDS);
 // k_kl_merge gives every event its global position: its rank in its chunk
 // plus, per other chunk, a binary search.  Chunks cover ordered, disjoint slot
 // ranges, so a tie against a chunk below counts and against a chunk above
@@ -1626,19 +1639,26 @@ __global__ void __launch_bounds__(256) k_kl_events(KLArgs A) {
 
 __device__ inline unsigned long long score_key(double v) { return ~ord_key(v + 0.0); }
 
+// A lazy run only flags the events of a deferred cloud (kl_list_deferrable).
 __global__ void __launch_bounds__(kChunk) k_kl_rank_chunks(KLArgs A) {
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *A.wq_ctr = 0u;  // k_welford_q has finished
   const int b = blockIdx.y;
   const CloudCtl& c = A.ctl[b];
-  if (c.state != kAccepted || kl_list_skipped(A, c)) return;
+  if (c.state != kAccepted) return;
+  if (A.mode == kKLBuild && !c.kl_deferred) return;
   const uint32_t nslots = 6 * c.num_nds;
   const uint32_t ch = blockIdx.x;
   if (ch * kChunk >= nslots) return;
   const uint64_t eb = (uint64_t)b * A.ecap, kb = (uint64_t)b * A.sortcap + (uint64_t)ch * kChunk;
   const uint32_t t = threadIdx.x;
   const uint32_t sl = ch * kChunk + t;
-  const uint32_t slc = sl < nslots ? sl : 0u;  // unconditional loads
-  const uint32_t fl = A.slot_flag_all[eb + slc];
-  const double vl = A.slot_val_all[eb + slc];
+  const bool deferred = kl_list_deferrable(A, c);
+  uint32_t fl = 0;
+  double vl = 0.0;
+  kl_event(A, b, sl < nslots ? sl : 0u, !deferred, fl, vl);  // the clamped slot's result is dropped
+  if (sl < nslots) A.slot_flag_all[eb + sl] = fl;
+  if (deferred) return;
+  if (sl < nslots) A.slot_val_all[eb + sl] = vl;
   const bool f = sl < nslots && fl;
   const double v = f ? vl : 0.0;
   const bool isn = f && v != v;
@@ -1839,25 +1859,65 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long dynk[];
   __shared__ uint32_t s_cnt[kMaxChunks];
   __shared__ uint32_t s_nb[kMaxChunks + 1];
+  __shared__ double s_pm[kMergeLdsChunks];
   __shared__ uint32_t s_own_num_slot[kMergeRuns][kChunk];
   __shared__ uint32_t s_own_nan_slot[kMergeRuns][kChunk];
   for (uint32_t c2 = tid; c2 < nch; c2 += blockDim.x) {
     s_cnt[c2] = A.chunk_cnt[cb + c2];
-    s_nb[c2] = A.chunk_nanbase[cb + c2];
+    if (kLds) s_pm[c2] = A.chunk_min[cb + c2];
+    else s_nb[c2] = A.chunk_nanbase[cb + c2];
   }
-  if (tid == 0) s_nb[nch] = A.chunk_nanbase[cb + nch - 1] + (A.chunk_cnt[cb + nch - 1] & 0xffffu);  // NaN total
+  if (!kLds && tid == 0) s_nb[nch] = A.chunk_nanbase[cb + nch - 1] + (A.chunk_cnt[cb + nch - 1] & 0xffffu);  // NaN total
   const unsigned long long* gK = A.sort_key_all + kb;
   const unsigned long long* gN = A.nan_key_all + eb;
   if (ch < nch) s_own_num_slot[lc][t] = A.sort_idx_all[kb + ch * kChunk + t];
   __syncthreads();
+  if (kLds) {
+    // the NaN bases and the min over earlier chunks (k_kl_nan_keys' scans),
+    // one lane per chunk (nch <= kMergeLdsChunks < 64)
+    if (tid < 64) {
+      uint32_t nn = tid < nch ? (s_cnt[tid] & 0xffffu) : 0u;
+      double cm = tid < nch ? s_pm[tid] : __builtin_inf();
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(nn, off, 64);
+        const double om = __shfl_up(cm, off, 64);
+        if ((int)tid >= off) {
+          nn += o;
+          cm = MinF64()(cm, om);
+        }
+      }
+      uint32_t ex = __shfl_up(nn, 1, 64);
+      double exm = __shfl_up(cm, 1, 64);
+      if (tid == 0) {
+        ex = 0;
+        exm = __builtin_inf();
+      }
+      if (tid < nch) {
+        s_nb[tid] = ex;
+        s_pm[tid] = exm;
+      }
+      if (tid + 1 == nch) s_nb[nch] = nn;
+    }
+    __syncthreads();
+  }
   const uint32_t nnan_tot = s_nb[nch];
   const uint32_t cc = ch < nch ? s_cnt[ch] : 0u;
   const uint32_t nnum = cc >> 16, nnan = cc & 0xffffu;
   const uint32_t nb0 = ch < nch ? s_nb[ch] : 0u;
-  if (t < nnan) s_own_nan_slot[lc][t] = A.nan_slot_all[eb + nb0 + t];
+  if (t < nnan) s_own_nan_slot[lc][t] = kLds ? A.nan_list_all[eb + ch * kChunk + t] : A.nan_slot_all[eb + nb0 + t];
   unsigned long long* lK = dynk;
   unsigned long long* lN = dynk + (uint64_t)nch * kChunk;
-  if (kLds) {  // stage the score runs and the NaN keys, eight 16-byte loads in flight per thread
+  if (kLds) {  // stage the score runs; the NaN keys are computed in place
+    for (uint32_t i = tid; i < nnan_tot; i += blockDim.x) {
+      // the chunk of NaN i: the last one whose base is <= i
+      uint32_t lo = 0, hi = nch;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_nb[mid] <= i) lo = mid;
+        else hi = mid;
+      }
+      lN[i] = score_key(MinF64()(s_pm[lo], A.ev_min_all[eb + lo * kChunk + (i - s_nb[lo])]));
+    }
     const uint32_t nv = nch * kChunk / 2;
     const ulonglong2* src = reinterpret_cast<const ulonglong2*>(gK);
     ulonglong2* dst = reinterpret_cast<ulonglong2*>(lK);
@@ -1873,19 +1933,6 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
       for (int u = 0; u < U; u++) {
         const uint32_t i = i0 + u * blockDim.x + tid;
         if (i < nv) dst[i] = v[u];
-      }
-    }
-    for (uint32_t i0 = 0; i0 < nnan_tot; i0 += U * blockDim.x) {
-      unsigned long long v[U];
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const uint32_t i = i0 + u * blockDim.x + tid;
-        v[u] = gN[i < nnan_tot ? i : 0];
-      }
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const uint32_t i = i0 + u * blockDim.x + tid;
-        if (i < nnan_tot) lN[i] = v[u];
       }
     }
   }
@@ -2137,12 +2184,13 @@ static size_t merge_lds_bytes(const Plan* P);
 static void launch_list_sort(Plan* P, const KLArgs& A, hipStream_t st) {
   const int B = P->B;
   k_kl_rank_chunks<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
-  k_kl_nan_keys<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
   const uint32_t mg = (P->nchunk + kMergeRuns - 1) / kMergeRuns;
-  if (P->nchunk <= (uint32_t)kMergeLdsChunks)
+  if (P->nchunk <= (uint32_t)kMergeLdsChunks) {  // the merge computes the NaN keys itself
     k_kl_merge<true><<<dim3(mg, B), kChunk * kMergeRuns, merge_lds_bytes(P), st>>>(A);
-  else
+  } else {
+    k_kl_nan_keys<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
     k_kl_merge<false><<<dim3(mg, B), kChunk * kMergeRuns, 0, st>>>(A);
+  }
 }
 
 // Builds the retained lists a lazy run deferred (no-op for the others).
@@ -2151,7 +2199,6 @@ static int build_deferred_lists(Plan* P, hipStream_t st) {
   KLArgs A = kl_args(P, P->k, nullptr, nullptr, nullptr, nullptr, nullptr);
   A.marks = nullptr;
   A.mode = kKLBuild;
-  k_kl_events<<<dim3((6 * P->ndcap + 255) / 256, P->B), 256, 0, st>>>(A);
   launch_list_sort(P, A, st);
   k_kl_list_done<<<P->B, 256, 0, st>>>(A);
   HIPCHK(hipGetLastError());
@@ -2223,12 +2270,11 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
   k_welford_q<T><<<P->wq_grid, kWqThreads, kWqRt * sizeof(double) + 4 * ((B + 1 + 3) & ~3) + (lbl ? P->wq_lds : 0),
                     st>>>(
       P->ctl, B, (const T*)P->nd_pts, lbl ? P->nd_lbl : nullptr, P->nd_n, P->nd_base, P->nd_mean, P->nd_cov,
-      P->nd_cls, P->hist, P->ncls, n, P->ndcap, P->wq_ctr);
+      P->nd_cls, P->hist, P->ncls, n, P->ndcap, P->wq_ctr,
+      WqChainArgs{P->vox, P->dense_of, P->nb, P->nkeys, P->chain, P->chain_ps, P->nd_cov_post, P->vcap});
   if (P->timing) HIPCHK(hipEventRecord(P->ev[5], st));
   KLArgs A = kl_args(P, P->k, out, out_cls, pc64, cov64, cls16);
   A.stats_out = stats_dst;
-  k_kl_chains<<<dim3((P->ndcap + 255) / 256, B), 256, 0, st>>>(A);
-  k_kl_events<<<dim3((6 * P->ndcap + 255) / 256, B), 256, 0, st>>>(A);
   launch_list_sort(P, A, st);
   k_kl<<<B, kKLThreads, A.kl_lds ? kl_lds_bytes(P) : 0, st>>>(A);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[6], st));
