@@ -143,3 +143,41 @@ def test_training_step_gpu_labelled_path():
         out, ref = m(p, c), m.forward_torch(p.contiguous(), c.contiguous())
     err = ((out - ref).abs() / ref.abs().clamp_min(1.0)).max().item()
     assert err < 1e-4, err
+
+
+@pytest.mark.gpu
+def test_adam_step_on_hip_nds_equals_oracle_nds():
+    """VERDICT r1 item 9 (reference tools/train.py:67-81): one Adam step on the
+    HIP-preprocessed labelled NDs against the same step on NDs the CPU oracle
+    produced from the same clouds.  The NDs (means, covariances, one-hot
+    classes) are bit-identical, and the parameters after the step agree within
+    1e-5 (same data; only the GPU's own reduction order may differ)."""
+    import copy
+    import oracle as O
+    from ndnet.preprocessing.ndtnet_preprocessing import ndt_preprocessing
+    from ndnet.synthetic import make_labelled_batch
+    dev = torch.device("cuda", 0)
+    B, n, k, C = 2, 20_000, 500, 28
+    pts, gt = make_labelled_batch(B, n, C, seed0=7)
+    p, c, g = ndt_preprocessing(k, torch.from_numpy(pts).to(dev), torch.from_numpy(gt).to(dev), C)
+    op = np.zeros((B, k, 3), np.float32)
+    oc = np.zeros((B, k, 9), np.float32)
+    og = np.zeros((B, k, C + 1), np.float32)
+    for b in range(B):
+        r = O.run(pts[b].astype(np.float64), k, classes=gt[b].argmax(axis=1), num_classes=C)
+        assert r.rc == 0
+        op[b] = np.nan_to_num(r.out_pc.astype(np.float32), nan=0.0, posinf=0.0, neginf=0.0)
+        oc[b] = np.nan_to_num(r.out_cov.astype(np.float32), nan=0.0, posinf=0.0, neginf=0.0)
+        og[b, np.arange(k), r.out_cls] = 1.0
+    assert np.array_equal(p.cpu().numpy(), op) and np.array_equal(c.cpu().numpy(), oc)
+    assert np.array_equal(g.cpu().numpy(), og)
+    m_hip = _model(F=768, C=C, seed=4)
+    m_orc = copy.deepcopy(m_hip)
+    t_hip = Trainer(m_hip, 1e-3, k, C, dev, ddp=False)
+    t_orc = Trainer(m_orc, 1e-3, k, C, dev, ddp=False)
+    l_hip, _ = t_hip.step_on_nds(p.contiguous(), c.contiguous(), g)
+    l_orc, _ = t_orc.step_on_nds(torch.from_numpy(op).to(dev), torch.from_numpy(oc).to(dev),
+                                 torch.from_numpy(og).to(dev))
+    assert abs(l_hip - l_orc) <= 1e-5 * max(1.0, abs(l_orc))
+    for (name, a), b in zip(m_hip.named_parameters(), m_orc.parameters()):
+        assert (a - b).abs().max().item() <= 1e-5, name
