@@ -463,6 +463,7 @@ def main() -> None:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": ("f64 NDT; PointNet fp32-accurate split-bf16x3 (6 products) on 7 layers, fp32 MFMA elsewhere"
+                      + ("; their weights streamed as fp32, split in registers" if pointnet_hip.WEIGHT_F32 else "")
                       if pointnet_hip.SPLIT_BF16 else "f64 NDT; PointNet fp32 MFMA"),
             "data": f"synthetic {args.kind} clouds (SURVEY 8d), random-init weights",
             "config": {"workload": (f"batch {B} x {n} pts -> {k} NDs, NDTNetSegmentation F={F} C={C} eval"

@@ -44,6 +44,15 @@ constexpr int kWaves = NDNET_PN_WAVES;
 constexpr int kThreads = 64 * kWaves;
 constexpr int kRowBlocks = kP / 16;  // 4 (kWaves / 2)
 constexpr int kFuseNC = 64;     // columns per chunk of a fused layer
+// LDS row pitch padding.  An A-fragment read (ds_read_b128, 16 B per lane at
+// row l & 15, column offset 16 B * (l >> 4)) is conflict-free when the row
+// pitch is 32 B mod 256 B (two 4-bank slots per row: the 16 lanes of each
+// ds_read_b128 lane group land on 16 distinct slots); a pitch of 16 B mod
+// 256 B (one slot per row) puts two lanes of every group on one slot and
+// doubles the read.  Activation widths are multiples of 64 (or 16 / 32 / 64
+// for the input tile), so width + kPadF floats / width + kPadB bf16 give it.
+constexpr int kPadF = 8;        // fp32 regions: pitch = width + 8 floats
+constexpr int kPadB = 16;       // bf16 planes: pitch = width + 16 bf16
 #ifndef NDNET_PN_DEPTH
 #define NDNET_PN_DEPTH 2
 #endif
@@ -52,6 +61,10 @@ constexpr int kDepth = NDNET_PN_DEPTH;  // weight k-groups in flight per wave
 #define NDNET_PN_DEPTH6 1
 #endif
 constexpr int kDepth6 = NDNET_PN_DEPTH6;  // the same for split-bf16 layers (3 fragment planes each)
+#ifndef NDNET_PN_DEPTH6F
+#define NDNET_PN_DEPTH6F 1
+#endif
+constexpr int kDepth6F = NDNET_PN_DEPTH6F;  // the same for prec 2 (fp32 weights split in registers)
 static_assert(kWaves % kRowBlocks == 0, "every row group has whole column groups");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -76,7 +89,8 @@ extern __shared__ __attribute__((aligned(16))) float g_smem[];
 // the weights stream from L2 straight into registers (no LDS staging, no
 // barrier inside a layer) and only the activations live in LDS.
 struct LayerCtx {
-  const f32x4* __restrict__ w;     // this cloud's fragments, offset by the lane (prec 0)
+  const f32x4* __restrict__ w;     // this cloud's fragments, offset by the lane (prec 0; prec 2: fp32
+                                   // split-bf16 fragments)
   const bf16x8* __restrict__ w6;   // split-bf16 fragments, offset by the lane (prec 1)
   const float* __restrict__ bias;
   int KG, N, relu, prec;           // KG: 16-row k-groups (prec 0) or 32-row (prec 1)
@@ -89,7 +103,7 @@ __device__ inline LayerCtx layer_ctx(const ndnet_pn_chain& A, int l, int b) {
   C.w6 = reinterpret_cast<const bf16x8*>(L.w + (int64_t)b * L.w_cloud_stride) + (threadIdx.x & 63);
   C.bias = L.bias + (int64_t)b * L.bias_cloud_stride;
   C.prec = L.prec;
-  C.KG = L.prec ? L.K / 32 : L.K / 16;
+  C.KG = L.prec ? L.K / 32 : L.K / 16;  // prec 1 and 2: 32-row k-groups
   C.N = L.N;
   C.relu = L.relu;
   return C;
@@ -239,7 +253,7 @@ __device__ __attribute__((always_inline)) inline void pool_cols(const f32x4 (&ac
 //
 // The layer's input activations are stored by the producing layer's epilogue
 // as three bf16 planes of the LDS region (plane p at p * kP * pitch, element
-// (row, k) at row * pitch + k, pitch = width + 8 bf16); lane l of a 16x16x32
+// (row, k) at row * pitch + k, pitch = width + kPadB bf16); lane l of a 16x16x32
 // A fragment reads row l & 15, k = 32 kg + 8 (l >> 4) .. + 7 with one
 // ds_read_b128 per plane.  The weights are fragment-major per 32-row k-group:
 // [column block][k-group][plane][lane][8 bf16], lane l holding
@@ -362,6 +376,77 @@ __device__ __attribute__((always_inline)) inline void run_tiles_x6(f32x4 (&acc)[
   }
 }
 
+// prec 2: the same products from fp32 weights, split into the three bf16
+// planes in registers when a step consumes them (h = bf16(w), m = bf16(w - h),
+// l = bf16(w - h - m): the split the host applies for prec 1, bit for bit).
+// 4 bytes per weight cross L2 -> CU instead of 6, and a prefetched step holds
+// 8 registers per column block instead of 12.  Layout: [column block][k-group]
+// [half][64 lanes][4] fp32, lane l's half h holding W^T[32 kg + 8 (l/16) + 4 h
+// + s][16 cb + l%16], s = 0..3 -- each half one coalesced 1 KB load per wave.
+__device__ __attribute__((always_inline)) inline void split_w8(const f32x4& lo, const f32x4& hi, bf16x8 (&o)[3]) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const float v = i < 4 ? lo[i] : hi[i - 4];
+    __bf16 h, m, l;
+    split3(v, h, m, l);
+    o[0][i] = h;
+    o[1][i] = m;
+    o[2][i] = l;
+  }
+}
+
+template <int RB, int NB, class Epi>
+__device__ __attribute__((always_inline)) inline void run_tiles_x6f(f32x4 (&acc)[RB][NB],
+                                                                    const f32x4* __restrict__ w, int KG, int kg0,
+                                                                    int nkg, int cb0, int cbs, int nchunk,
+                                                                    const __bf16* abase, int pitchb, Epi epi) {
+  const int T = nchunk * nkg;
+  const int plane = kP * pitchb;
+  const int64_t jstride = (int64_t)KG * 2 * 64;
+  const int64_t chunk_jump = ((int64_t)cbs * KG - (nkg - 1)) * 2 * 64;
+  const f32x4* lp = w + ((int64_t)cb0 * KG + kg0) * 2 * 64;
+  int lkk = 0, lleft = T;
+  auto load = [&](f32x4 (&raw)[NB][2]) {
+#pragma unroll
+    for (int j = 0; j < NB; j++)
+#pragma unroll
+      for (int h = 0; h < 2; h++) raw[j][h] = lp[j * jstride + h * 64];
+    if (lleft > 1) {
+      lleft--;
+      if (++lkk == nkg) {
+        lkk = 0;
+        lp += chunk_jump;
+      } else {
+        lp += 2 * 64;
+      }
+    }
+  };
+  int kk = 0, c = 0;
+  auto step = [&](const f32x4 (&raw)[NB][2]) {
+    bf16x8 bw[NB][3];
+#pragma unroll
+    for (int j = 0; j < NB; j++) split_w8(raw[j][0], raw[j][1], bw[j]);
+    mma_kgroup_x6<RB, NB>(acc, abase + 32 * kk, plane, 16 * pitchb, bw);
+    if (++kk == nkg) {
+      epi(acc, c);
+      kk = 0;
+      c++;
+    }
+  };
+  f32x4 rq[kDepth6F][NB][2];
+#pragma unroll
+  for (int i = 0; i < kDepth6F; i++) load(rq[i]);
+  for (int t = 0; t < T; t += kDepth6F) {
+#pragma unroll
+    for (int i = 0; i < kDepth6F; i++) {
+      if (t + i < T) {
+        step(rq[i]);
+        load(rq[i]);
+      }
+    }
+  }
+}
+
 // One layer: RB row blocks x NB column blocks per wave; 4 / RB row groups x
 // 4 RB column groups of waves; N in chunks of (column groups x NB x 16).
 template <int RB, int NB>
@@ -380,15 +465,16 @@ __device__ void plain_layer(const LayerCtx& C, int in, int pin, int out, int pou
   auto epi = [&](f32x4 (&a)[RB][NB], int c) {
     const int col0 = (c * CB + wc * NB) * 16;
     if (gmax) pool_cols<RB, NB>(a, C.bias, col0, C.relu, row0, rows_valid, gmax);
-    else if (out_planes) store_cols_planes<RB, NB>(a, C.bias, col0, C.relu, row0, out, C.N + 8, col0);
+    else if (out_planes) store_cols_planes<RB, NB>(a, C.bias, col0, C.relu, row0, out, C.N + kPadB, col0);
     else store_cols<RB, NB>(a, C.bias, col0, C.relu, row0, out, pout, col0);
     zero_acc(a);
   };
   const int nchunk = C.N < CB * 16 ? 1 : C.N / (CB * 16);
-  if (C.prec) {  // input: three bf16 planes of pitch K + 8 (the producer's N + 8)
-    const int pb = 32 * C.KG + 8;
+  if (C.prec) {  // input: three bf16 planes of pitch K + kPadB (the producer's N + kPadB)
+    const int pb = 32 * C.KG + kPadB;
     const __bf16* abase6 = reinterpret_cast<const __bf16*>(g_smem + in) + (row0 + cl) * pb + 8 * kq;
-    run_tiles_x6<RB, NB>(acc, C.w6, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase6, pb, epi);
+    if (C.prec == 2) run_tiles_x6f<RB, NB>(acc, C.w, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase6, pb, epi);
+    else run_tiles_x6<RB, NB>(acc, C.w6, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase6, pb, epi);
   } else {
     const float* abase = g_smem + in + (row0 + cl) * pin + 4 * kq;
     run_tiles<RB, NB>(acc, C.w, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase, pin, epi);
@@ -398,7 +484,7 @@ __device__ void plain_layer(const LayerCtx& C, int in, int pin, int out, int pou
 // Floats of the fused pair's double buffer: two 64-column chunks, fp32 or
 // (split-bf16 consumer) three bf16 planes of pitch 72.
 __host__ __device__ inline int fbuf_floats(int qprec) {
-  return qprec ? 2 * 3 * kP * (kFuseNC + 8) / 2 : 2 * kP * (kFuseNC + 4);
+  return qprec ? 2 * 3 * kP * (kFuseNC + kPadB) / 2 : 2 * kP * (kFuseNC + kPadF);
 }
 
 // A fused pair: layer P (K -> N1) produced 64 columns at a time into a
@@ -409,7 +495,7 @@ __host__ __device__ inline int fbuf_floats(int qprec) {
 template <int RB, int NB>
 __device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin, int fbuf, int out, int pout,
                            float* gmax, int rows_valid, bool out_planes) {
-  constexpr int kFP = kFuseNC + 4;
+  constexpr int kFP = kFuseNC + kPadF;
   constexpr int WR = kRowBlocks / RB, WC = kWaves / WR;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int kq = lane >> 4, cl = lane & 15;
@@ -417,7 +503,7 @@ __device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin
   constexpr int PWC = kWaves / kRowBlocks, PNB = 4 / PWC;
   const int prow0 = (wave / PWC) * 16, pwc = (wave % PWC) * PNB;
   const float* ain = g_smem + in + (prow0 + cl) * pin + 4 * kq;
-  const __bf16* ain6 = reinterpret_cast<const __bf16*>(g_smem + in) + (prow0 + cl) * (32 * P.KG + 8) + 8 * kq;
+  const __bf16* ain6 = reinterpret_cast<const __bf16*>(g_smem + in) + (prow0 + cl) * (32 * P.KG + kPadB) + 8 * kq;
   // Q: row group wave / WC, column group wave % WC
   const int qrow0 = (wave / WC) * RB * 16, qwc = wave % WC;
   const bool qidle = qwc * NB * 16 >= Q.N;
@@ -429,10 +515,11 @@ __device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin
     zero_acc(acc1);
     const int fb = fbuf + (f & 1) * fbsz;
     auto epi = [&](f32x4 (&a)[1][PNB], int) {
-      if (Q.prec) store_cols_planes<1, PNB>(a, P.bias, 64 * f + 16 * pwc, P.relu, prow0, fb, kFuseNC + 8, 16 * pwc);
+      if (Q.prec) store_cols_planes<1, PNB>(a, P.bias, 64 * f + 16 * pwc, P.relu, prow0, fb, kFuseNC + kPadB, 16 * pwc);
       else store_cols<1, PNB>(a, P.bias, 64 * f + 16 * pwc, P.relu, prow0, fb, kFP, 16 * pwc);
     };
-    if (P.prec) run_tiles_x6<1, PNB>(acc1, P.w6, P.KG, 0, P.KG, 4 * f + pwc, 0, 1, ain6, 32 * P.KG + 8, epi);
+    if (P.prec == 2) run_tiles_x6f<1, PNB>(acc1, P.w, P.KG, 0, P.KG, 4 * f + pwc, 0, 1, ain6, 32 * P.KG + kPadB, epi);
+    else if (P.prec) run_tiles_x6<1, PNB>(acc1, P.w6, P.KG, 0, P.KG, 4 * f + pwc, 0, 1, ain6, 32 * P.KG + kPadB, epi);
     else run_tiles<1, PNB>(acc1, P.w, P.KG, 0, P.KG, 4 * f + pwc, 0, 1, ain, pin, epi);
   };
   f32x4 acc2[RB][NB];
@@ -443,9 +530,13 @@ __device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin
     if (!qidle) {
       if (Q.prec) {
         const __bf16* af6 = reinterpret_cast<const __bf16*>(g_smem + fbuf + (f & 1) * fbsz) +
-                            (qrow0 + cl) * (kFuseNC + 8) + 8 * kq;
-        run_tiles_x6<RB, NB>(acc2, Q.w6, Q.KG, 2 * f, 2, qwc * NB, 0, 1, af6, kFuseNC + 8,
-                             [](f32x4 (&)[RB][NB], int) {});
+                            (qrow0 + cl) * (kFuseNC + kPadB) + 8 * kq;
+        if (Q.prec == 2)
+          run_tiles_x6f<RB, NB>(acc2, Q.w, Q.KG, 2 * f, 2, qwc * NB, 0, 1, af6, kFuseNC + kPadB,
+                                [](f32x4 (&)[RB][NB], int) {});
+        else
+          run_tiles_x6<RB, NB>(acc2, Q.w6, Q.KG, 2 * f, 2, qwc * NB, 0, 1, af6, kFuseNC + kPadB,
+                               [](f32x4 (&)[RB][NB], int) {});
       } else {
         const float* af = g_smem + fbuf + (f & 1) * fbsz + (qrow0 + cl) * kFP + 4 * kq;
         run_tiles<RB, NB>(acc2, Q.w, Q.KG, 4 * f, 4, qwc * NB, 0, 1, af, kFP, [](f32x4 (&)[RB][NB], int) {});
@@ -456,14 +547,14 @@ __device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin
   }
   if (qidle) return;
   if (gmax) pool_cols<RB, NB>(acc2, Q.bias, 16 * qwc * NB, Q.relu, qrow0, rows_valid, gmax);
-  else if (out_planes) store_cols_planes<RB, NB>(acc2, Q.bias, 16 * qwc * NB, Q.relu, qrow0, out, Q.N + 8, 16 * qwc * NB);
+  else if (out_planes) store_cols_planes<RB, NB>(acc2, Q.bias, 16 * qwc * NB, Q.relu, qrow0, out, Q.N + kPadB, 16 * qwc * NB);
   else store_cols<RB, NB>(acc2, Q.bias, 16 * qwc * NB, Q.relu, qrow0, out, pout, 16 * qwc * NB);
 }
 
-// Floats of LDS region r: fp32 activations (pitch width + 4) or, when it ever
+// Floats of LDS region r: fp32 activations (pitch width + kPadF) or, when it ever
 // holds a split-bf16 layer's input (planes bit r), three bf16 planes.
 __host__ __device__ inline int region_floats(int width, int planes) {
-  const int f32 = kP * (width + 4), b16 = 3 * kP * (width + 8) / 2;
+  const int f32 = kP * (width + kPadF), b16 = 3 * kP * (width + kPadB) / 2;
   return planes && b16 > f32 ? b16 : f32;
 }
 
@@ -471,7 +562,7 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
   const int b = blockIdx.y;
   const int p0 = blockIdx.x * kP;
   // LDS: activation region 0 | region 1 | [fused-chunk double buffer]
-  const int pitch0 = A.max_width + 4, pitch1 = A.max_width2 + 4;
+  const int pitch0 = A.max_width + kPadF, pitch1 = A.max_width2 + kPadF;
   const int reg[2] = {0, region_floats(A.max_width, planes & 1)};
   // fbuf (the fused pair's chunks): float offset chosen by the launcher
   // input tile, zero-filled to the first layer's K (a multiple of 16)
@@ -748,6 +839,42 @@ __global__ void __launch_bounds__(256) k_pn_fold64_x6(const float* __restrict__ 
     }
 }
 
+// The same fold in the prec-2 layout (fp32, K = 64: two 32-row k-groups):
+// out[b] = [N/16][2][2 halves][64 lanes][4] fp32.
+__global__ void __launch_bounds__(256) k_pn_fold64_x6f(const float* __restrict__ t2, const float* __restrict__ rhs,
+                                                       float* __restrict__ out, int N) {
+  __shared__ float s_a[64][65];
+  __shared__ float s_b[64][68];
+  const int b = blockIdx.y, j0 = blockIdx.x * 64;
+  const float* A = t2 + (int64_t)b * 4096;
+  for (int e = threadIdx.x; e < 4096; e += 256) {
+    s_a[e >> 6][e & 63] = A[e];
+    s_b[e >> 6][e & 63] = rhs[(int64_t)(e >> 6) * N + j0 + (e & 63)];
+  }
+  __syncthreads();
+  const int ti = (threadIdx.x >> 4) * 4, tj = (threadIdx.x & 15) * 4;
+  float acc[4][4] = {};
+  for (int k = 0; k < 64; k++) {
+    float av[4], bv[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) av[r] = s_a[ti + r][k];
+#pragma unroll
+    for (int c = 0; c < 4; c++) bv[c] = s_b[k][tj + c];
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+      for (int c = 0; c < 4; c++) acc[r][c] += av[r] * bv[c];
+  }
+  // rows ti..ti+3 are one lane's 4 consecutive values of one half: one float4 store per column
+  float* o = out + (int64_t)b * 64 * N;
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const int k = ti, n = j0 + tj + c;
+    const int64_t e = ((((int64_t)(n >> 4) * 2 + (k >> 5)) * 2 + ((k >> 2) & 1)) * 64 + ((k >> 3) & 3) * 16 + (n & 15)) * 4;
+    *reinterpret_cast<f32x4*>(o + e) = f32x4{acc[0][c], acc[1][c], acc[2][c], acc[3][c]};
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -781,6 +908,12 @@ int ndnet_pn_fold64_x6_run(const float* t2, const float* rhs, void* out6, int ba
   return hipGetLastError() == hipSuccess ? 0 : -21;
 }
 
+int ndnet_pn_fold64_x6f_run(const float* t2, const float* rhs, float* out, int batch, int N, void* stream) {
+  if (!t2 || !rhs || !out || batch <= 0 || N <= 0 || N % 64 || ((uintptr_t)out % 16)) return -20;
+  k_pn_fold64_x6f<<<dim3(N / 64, batch), 256, 0, (hipStream_t)stream>>>(t2, rhs, out, N);
+  return hipGetLastError() == hipSuccess ? 0 : -21;
+}
+
 int ndnet_pn_fold64_run(const float* t2, const float* rhs, float* out, int batch, int N, void* stream) {
   if (!t2 || !rhs || !out || batch <= 0 || N <= 0 || N % 64 || ((uintptr_t)out % 16)) return -20;
   k_pn_fold64<<<dim3(N / 64, batch), 256, 0, (hipStream_t)stream>>>(t2, rhs, out, N);
@@ -804,7 +937,7 @@ int ndnet_pn_chain_run(const ndnet_pn_chain* args, int batch, void* stream) {
         L.w_cloud_stride % 4)
       return -20;
     const bool fed = l > 0 && args->L[l - 1].fuse_next;
-    if (L.prec != 0 && L.prec != 1) return -20;
+    if (L.prec < 0 || L.prec > 2) return -20;
     if (L.prec) {  // split-bf16: reads planes its producer writes (into a region, or the fused chunks)
       if (l == 0 || L.K % 32 || args->L[l - 1].N != L.K) return -20;
       if (fed) qprec = 1;
@@ -837,8 +970,8 @@ int ndnet_pn_chain_run(const ndnet_pn_chain* args, int batch, void* stream) {
     int lf = 0;
     while (!args->L[lf].fuse_next) lf++;
     const int r = lf & 1, fb = fbuf_floats(qprec);
-    const int p_in = args->L[lf].prec ? 3 * kP * (args->L[lf].K + 8) / 2    // P's input: bf16 planes, pitch K + 8
-                                      : kP * ((r ? args->max_width2 : args->max_width) + 4);  // or fp32, region pitch
+    const int p_in = args->L[lf].prec ? 3 * kP * (args->L[lf].K + kPadB) / 2    // P's input: bf16 planes, pitch K + kPadB
+                                      : kP * ((r ? args->max_width2 : args->max_width) + kPadF);  // or fp32, region pitch
     const int inside = (r ? r0f : 0) + p_in;
     if (r == 1 || inside + fb <= r0f) fbuf_off = inside;
     total = fbuf_off + (size_t)fb > total ? fbuf_off + (size_t)fb : total;

@@ -139,6 +139,24 @@ def test_split_bf16_fragment_layout():
     assert torch.equal(rec, wT)
 
 
+def test_split_bf16_fp32_fragment_layout():
+    """_frag_x6f (prec 2): fp32 W^T at [cb][kg][half][lane][s] with
+    k = 32 kg + 8 (lane >> 4) + 4 half + s, n = 16 cb + (lane & 15)."""
+    from ndnet.models import pointnet_hip as ph
+    K, N = 64, 32
+    g = torch.Generator().manual_seed(1)
+    wT = torch.randn((K, N), generator=g)
+    f = ph._frag_x6f(wT).reshape(N // 16, K // 32, 2, 64, 4)
+    rec = torch.zeros((K, N))
+    for cb in range(N // 16):
+        for kg in range(K // 32):
+            for h in range(2):
+                for lane in range(64):
+                    for s_ in range(4):
+                        rec[32 * kg + 8 * (lane >> 4) + 4 * h + s_, 16 * cb + (lane & 15)] = f[cb, kg, h, lane, s_]
+    assert torch.equal(rec, wT)
+
+
 @pytest.mark.gpu
 def test_split_bf16_layers_are_fp32_accurate():
     """The split-bf16 ("x6") wide layers against a float64 evaluation of the
@@ -152,18 +170,20 @@ def test_split_bf16_layers_are_fp32_accurate():
     c = torch.randn((16, 1000, 9), device="cuda", generator=g)
     with torch.no_grad():
         ref64 = copy.deepcopy(m).double().forward_torch(p.double(), c.double())
-        saved = ph.SPLIT_BF16
+        saved = ph.PRECISION
+        outs = {}
         try:
-            ph.SPLIT_BF16 = True
-            m._hip = None
-            out_x6 = m(p, c).double()
-            ph.SPLIT_BF16 = False
-            m._hip = None
-            out_32 = m(p, c).double()
+            for mode in ("x6", "x6f", "fp32"):
+                ph.set_precision(mode)
+                m._hip = None
+                outs[mode] = m(p, c).double()
         finally:
-            ph.SPLIT_BF16 = saved
+            ph.set_precision(saved)
             m._hip = None
+        out_x6, out_32 = outs["x6"], outs["fp32"]
         out_t32 = m.forward_torch(p, c).double()
+    # prec 2 splits the fp32 weights in registers into the very planes prec 1 stores
+    assert torch.equal(outs["x6f"], out_x6)
     e_x6 = (out_x6 - ref64).abs().max().item()
     e_32 = (out_32 - ref64).abs().max().item()
     e_t32 = (out_t32 - ref64).abs().max().item()
