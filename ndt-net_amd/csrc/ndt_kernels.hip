@@ -2241,7 +2241,10 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
     F.G = P->fG;
     F.bpw = P->fbpw;
     F.rbs = P->frbs;
-    F.dbg_store = 0;
+#ifndef NDNET_FRONT_STORE
+#define NDNET_FRONT_STORE 0
+#endif
+    F.dbg_store = NDNET_FRONT_STORE;  // binning scatter stores: 0 plain, 1 nontemporal, 2 agent-scope atomic (A/B)
     F.eval_all = P->exact_counts;
     F.B = (uint32_t)B;
     F.nbins = P->nbins;
