@@ -303,6 +303,9 @@ __device__ __attribute__((always_inline)) inline void mma_kgroup_x6(f32x4 (&acc)
                                                                     int rstride, const bf16x8 (&bw)[NB][3]) {
   bf16x8 a[RB];
   auto ld = [&](int p) {
+#ifdef NDNET_PN_EXP_NOA  // timing experiment only (wrong results): A fragments from registers
+    if (p != 1) return;
+#endif
 #pragma unroll
     for (int rb = 0; rb < RB; rb++) a[rb] = *reinterpret_cast<const bf16x8*>(a0 + p * plane + rb * rstride);
   };
@@ -339,6 +342,9 @@ __device__ __attribute__((always_inline)) inline void run_tiles_x6(f32x4 (&acc)[
   const bf16x8* lp = w + ((int64_t)cb0 * KG + kg0) * 3 * 64;
   int lkk = 0, lleft = T;
   auto load = [&](bf16x8 (&bw)[NB][3]) {
+#ifdef NDNET_PN_EXP_NOB  // timing experiment only (wrong results): weights loaded once per layer
+    if (lleft == T)
+#endif
 #pragma unroll
     for (int j = 0; j < NB; j++)
 #pragma unroll
