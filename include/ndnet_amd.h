@@ -185,7 +185,7 @@ int ndnet_ndt_debug_dump(void *plan, int cloud, uint32_t *nd_n, double *nd_mean,
 int ndnet_ndt_debug_set_epoch(void *plan, uint32_t epoch);
 
 /* k_kl phase stamps of the last run at timing level 2: marks[cloud * 16 + i],
- * 100 MHz s_memrealtime ticks (0 start, 1 outputs zeroed, 2 event count,
+ * 100 MHz s_memrealtime ticks (0 start, 1 cloud state checked, 2 event count,
  * 5 list initialised, 6 first occurrences, 7 walk scan, 8 kills, 9 shift,
  * 10 rows emitted, 11 end; 3 and 4 unused); synchronises. */
 int ndnet_ndt_debug_kl_marks(void *plan, unsigned long long *marks);

@@ -1323,6 +1323,9 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
   uint8_t* alive;
   const uint32_t nv0 = c.num_valid, nkl0 = c.num_kl;
   const bool walk = k < nv0;  // the prune removes something: the walk reads the list
+  // no ND dead and none to remove: the survivors are every ND, the rows the
+  // NDs in order (the level-1 prune of a cloud with num_nds == k)
+  const bool identity = !walk && nv0 == nd;
   if constexpr (kLds) {
     first = kl_smem;                                       // [ndcap]
     tmp = kl_smem + A.ndcap;                               // [ecap]
@@ -1330,7 +1333,8 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
     alive = (uint8_t*)(kl_smem + A.ndcap + 2 * A.ecap);    // [ndcap]
     if (walk)
       for (uint32_t i = threadIdx.x; i < nkl0; i += blockDim.x) s_op[i] = g_op[i];
-    for (uint32_t u = threadIdx.x; u < nd; u += blockDim.x) alive[u] = g_alive[u];
+    if (!identity)
+      for (uint32_t u = threadIdx.x; u < nd; u += blockDim.x) alive[u] = g_alive[u];
     op = s_op;
     __syncthreads();
   } else {
@@ -1466,9 +1470,9 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
   // with every load issued unconditionally.
   const uint64_t kout = k;
   uint32_t* rowmap = tmp;  // the walk's scratch is free again
-  uint32_t carry = 0;
+  uint32_t carry = identity ? nd : 0u;
   constexpr int IT = 8;
-  for (uint32_t base = 0; base < nd; base += blockDim.x * IT) {
+  for (uint32_t base = 0; !identity && base < nd; base += blockDim.x * IT) {
     const uint32_t u0 = base + threadIdx.x * IT;
     uint32_t row[IT], live[IT];
 #pragma unroll
@@ -1484,11 +1488,12 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
   }
   __syncthreads();
   if constexpr (kLds) {  // the alive flags back to global (further prune levels, dumps)
-    for (uint32_t u = threadIdx.x; u < nd; u += blockDim.x) g_alive[u] = alive[u];
+    if (walk)
+      for (uint32_t u = threadIdx.x; u < nd; u += blockDim.x) g_alive[u] = alive[u];
   }
   const uint32_t nrows = carry < kout ? carry : (uint32_t)kout;
   for (uint32_t rw = threadIdx.x; rw < nrows; rw += blockDim.x) {
-    const uint32_t u = rowmap[rw];
+    const uint32_t u = identity ? rw : rowmap[rw];
     const uint64_t o = (uint64_t)b * kout + rw;
     const double* m = A.nd_mean + 3 * (ob + u);
     const double* cv = A.nd_cov_post + 9 * (ob + u);
@@ -1505,9 +1510,10 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
         r[q] = isfinite(f) ? f : 0.0f;  // nan_to_num(nan=0, posinf=0, neginf=0)
       }
     }
-    if (A.out_cls) {
+    if (A.out_cls) {  // the whole one-hot row (rows past the survivors: fill_tail)
       float* r = A.out_cls + (uint64_t)(A.ncls + 1) * o;
-      r[A.nd_cls[ob + u]] = 1.0f;
+      const uint32_t cl = A.nd_cls[ob + u];
+      for (int q = 0; q <= A.ncls; q++) r[q] = (uint32_t)q == cl ? 1.0f : 0.0f;
     }
     if (A.out_pc64) {
       for (int q = 0; q < 3; q++) A.out_pc64[3 * o + q] = v[q];
@@ -1565,6 +1571,25 @@ __device__ void zero_outputs(const KLArgs& A, int b, uint64_t k) {
   if (A.out_cls16)
     for (uint64_t i = threadIdx.x; i < k; i += blockDim.x) A.out_cls16[r0 + i] = 0;
   __syncthreads();
+}
+
+// Rows [r0, k) of cloud b past the survivors: zero (np.zeros in
+// ndt_legacy.py:126-143), the class one-hot class 0 (ndtnet_preprocessing.py:55-57).
+// The emission writes every row below r0 whole.
+__device__ void fill_tail(const KLArgs& A, int b, uint64_t k, uint32_t r0) {
+  const uint64_t rb = (uint64_t)b * k;
+  if (A.out)
+    for (uint64_t i = 12 * (uint64_t)r0 + threadIdx.x; i < 12 * k; i += blockDim.x) A.out[12 * rb + i] = 0.0f;
+  if (A.out_cls) {
+    const uint64_t w = (uint64_t)(A.ncls + 1);
+    for (uint64_t i = w * r0 + threadIdx.x; i < w * k; i += blockDim.x) A.out_cls[w * rb + i] = (i % w) == 0 ? 1.0f : 0.0f;
+  }
+  if (A.out_pc64) {
+    for (uint64_t i = 3 * (uint64_t)r0 + threadIdx.x; i < 3 * k; i += blockDim.x) A.out_pc64[3 * rb + i] = 0.0;
+    for (uint64_t i = 9 * (uint64_t)r0 + threadIdx.x; i < 9 * k; i += blockDim.x) A.out_cov64[9 * rb + i] = 0.0;
+  }
+  if (A.out_cls16)
+    for (uint64_t i = r0 + threadIdx.x; i < k; i += blockDim.x) A.out_cls16[rb + i] = 0;
 }
 
 // The class one-hot of rows past the survivors is class 0 (ndtnet_preprocessing.py:55-57).
@@ -2016,9 +2041,8 @@ __global__ void __launch_bounds__(kKLThreads) k_kl(KLArgs A) {
   CloudCtl& c = A.ctl[b];
   __shared__ uint32_t s_u32[16];
   KL_MARK(0);
-  zero_outputs(A, b, A.k);
-  KL_MARK(1);
   if (c.state != kAccepted) {
+    zero_outputs(A, b, A.k);
     if (threadIdx.x == 0) {
       c.num_out = 0;
       c.kl_deferred = 0;
@@ -2027,6 +2051,7 @@ __global__ void __launch_bounds__(kKLThreads) k_kl(KLArgs A) {
     pad_class_rows(A, b, A.k, 0);
     return;
   }
+  KL_MARK(1);
   const uint32_t nd = c.num_nds;
   const uint64_t ob = (uint64_t)b * A.ndcap, eb = (uint64_t)b * A.ecap;
   const uint32_t nch = (6 * nd + kChunk - 1) / kChunk;
@@ -2059,7 +2084,7 @@ __global__ void __launch_bounds__(kKLThreads) k_kl(KLArgs A) {
   KL_MARK(5);
   const uint32_t nout = A.kl_lds ? prune_and_emit<true>(A, b, A.k, s_u32, s_u32)
                                  : prune_and_emit<false>(A, b, A.k, s_u32, s_u32);
-  pad_class_rows(A, b, A.k, nout);
+  fill_tail(A, b, A.k, nout < A.k ? nout : (uint32_t)A.k);
   __syncthreads();
   if (threadIdx.x == 0) write_stats(A, b);
   KL_MARK(11);
@@ -2069,15 +2094,15 @@ __global__ void __launch_bounds__(kKLThreads) k_prune(KLArgs A) {
   const int b = blockIdx.x;
   CloudCtl& c = A.ctl[b];
   __shared__ uint32_t s_u32[16];
-  zero_outputs(A, b, A.k);
   if (c.state != kAccepted) {
+    zero_outputs(A, b, A.k);
     pad_class_rows(A, b, A.k, 0);
     if (threadIdx.x == 0) write_stats(A, b);
     return;
   }
   const uint32_t nout = A.kl_lds ? prune_and_emit<true>(A, b, A.k, s_u32, s_u32)
                                  : prune_and_emit<false>(A, b, A.k, s_u32, s_u32);
-  pad_class_rows(A, b, A.k, nout);
+  fill_tail(A, b, A.k, nout < A.k ? nout : (uint32_t)A.k);
   __syncthreads();
   if (threadIdx.x == 0) write_stats(A, b);
 }
