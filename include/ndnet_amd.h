@@ -179,6 +179,11 @@ int ndnet_ndt_debug_dump(void *plan, int cloud, uint32_t *nd_n, double *nd_mean,
                          double *nd_cov_post, uint32_t *vox, double *ord_val, uint32_t *ord_p, uint32_t *ord_q,
                          double *guesses, uint32_t *counts, uint32_t *iters, uint8_t *alive);
 
+/* k_front's cloud-barrier timeout in 100 MHz ticks for the plan's next runs
+ * (0 restores the default 2e8 = 2 s).  A workgroup that waits longer fails its
+ * cloud with NDNET_ERR_SYNC; tests shorten it to reach that path. */
+int ndnet_ndt_debug_set_sync_timeout(void *plan, uint64_t ticks);
+
 /* Sets every cloud's stamp epoch (synchronises).  The epoch advances once per
  * run and wraps after 2^26 - 1 runs, when the device clears the stale voxel
  * stamps itself; tests use this to reach the wrap. */

@@ -84,6 +84,7 @@ struct FrontArgs {
   uint32_t rbs;                 // points per rank bin (512 or 1024)
   int dbg_store;
   int eval_all;                 // 1: count every bisection grid (debug / parity); 0: skip grids too small to matter
+  uint64_t sync_ticks;          // cloud-barrier timeout in 100 MHz ticks (2e8 = 2 s; tests shorten it)
 };
 
 // The shared bisection state of one workgroup (every workgroup of a cloud
@@ -100,6 +101,7 @@ struct FrontState {
   int32_t rc;
   uint32_t cut[kWorkers];
   uint32_t sync_no;
+  uint64_t sync_ticks;              // barrier timeout, 100 MHz ticks (FrontArgs.sync_ticks)
   uint32_t puse[2];                 // uses of the two pass-sum slots
   unsigned long long psum_prev[2];  // their value after the previous use
   uint32_t ok;
@@ -167,7 +169,7 @@ __device__ inline bool cloud_sync(FrontState& s, uint32_t* bar, uint32_t G) {
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       while (ld_sc1(bar) < target) {
         __builtin_amdgcn_s_sleep(1);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 100 MHz clock: 2 s
+        if (__builtin_amdgcn_s_memrealtime() - t0 > s.sync_ticks) {  // 100 MHz clock (2 s by default)
           s.ok = 0;
           break;
         }
@@ -200,7 +202,7 @@ __device__ inline bool pass_sync(FrontState& s, uint32_t* bar, uint32_t G, uint3
     while ((v >> 48) < target) {
       __builtin_amdgcn_s_sleep(1);
       v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 100 MHz clock: 2 s
+      if (__builtin_amdgcn_s_memrealtime() - t0 > s.sync_ticks) {  // 100 MHz clock (2 s by default)
         s.ok = 0;
         break;
       }
@@ -305,6 +307,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
 
   if (t == 0) {
     s.sync_no = 0;
+    s.sync_ticks = A.sync_ticks;
     s.npass = 0;
     s.puse[0] = s.puse[1] = 0;
     s.psum_prev[0] = s.psum_prev[1] = 0;

@@ -28,6 +28,7 @@
 #include <stdio.h>
 #include <string.h>
 #include <type_traits>
+#include <vector>
 
 #include "ndt_device.h"
 #include "../../include/ndnet_amd.h"
@@ -83,6 +84,8 @@ struct CloudCtl {
   uint32_t last_k;
   uint32_t clear_stamps; // the epoch wrapped this run: k_limits zeroes the cloud's stamps
   uint32_t kl_deferred;  // the retained list was not built by the run (lazy list, num_nds <= k)
+  uint32_t list_off;     // physical index of the retained list's first entry (the prunes' pending
+                         // left shifts, ndt.c:69-72; always 0 on the global-memory prune path)
 };
 
 struct Plan {
@@ -162,6 +165,7 @@ struct Plan {
   uint32_t wq_grid;           // k_welford_q workgroups: one per CU
   uint32_t* wq_ctr;           // [2] k_welford_q dynamic item counter (re-armed by k_kl_rank_chunks)
   int eager_list;             // build every cloud's retained list in the run (ndnet_ndt_set_lazy_list(plan, 0))
+  uint64_t front_sync_ticks;  // k_front's cloud-barrier timeout (ndnet_ndt_debug_set_sync_timeout)
 };
 
 // ------------------------------------------------------------------ helpers
@@ -1322,6 +1326,7 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
   const uint32_t* op;
   uint8_t* alive;
   const uint32_t nv0 = c.num_valid, nkl0 = c.num_kl;
+  const uint32_t off = c.list_off, nphys = c.num_phys;
   const bool walk = k < nv0;  // the prune removes something: the walk reads the list
   // no ND dead and none to remove: the survivors are every ND, the rows the
   // NDs in order (the level-1 prune of a cloud with num_nds == k)
@@ -1331,8 +1336,10 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
     tmp = kl_smem + A.ndcap;                               // [ecap]
     uint32_t* s_op = kl_smem + A.ndcap + A.ecap;           // [ecap]
     alive = (uint8_t*)(kl_smem + A.ndcap + 2 * A.ecap);    // [ndcap]
+    // logical entry i is physical entry off + i; past the entries ever
+    // written it is poison (the reference's uninitialised tail)
     if (walk)
-      for (uint32_t i = threadIdx.x; i < nkl0; i += blockDim.x) s_op[i] = g_op[i];
+      for (uint32_t i = threadIdx.x; i < nkl0; i += blockDim.x) s_op[i] = i + off < nphys ? g_op[i + off] : kInvalid;
     if (!identity)
       for (uint32_t u = threadIdx.x; u < nd; u += blockDim.x) alive[u] = g_alive[u];
     op = s_op;
@@ -1429,7 +1436,14 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
     if (poisoned) rc = -8;
     else if (kills < to_remove) rc = -2;  // "Reached the end of the divergences array!"
     __syncthreads();
-    if (rc == 0 && to_remove > 0) {
+    if (rc == 0 && to_remove > 0 && kLds) {
+      // shift left by idx_to_remove = f_{to_remove} + 1 (ndt.c:69-72): kept
+      // pending as the list's offset (a further prune level or a dump applies it)
+      if (threadIdx.x == 0) {
+        c.list_off = off + s_kpos + 1;
+        c.num_kl = nkl0 - to_remove;
+      }
+    } else if (rc == 0 && to_remove > 0) {
       // shift left by idx_to_remove = f_{to_remove} + 1 (ndt.c:69-72)
       const uint32_t shift = s_kpos + 1;
       const uint32_t nkl1 = nkl0 - to_remove;
@@ -1882,6 +1896,22 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
   } while (0)
   MERGE_MARK(12);
   extern __shared__ __attribute__((aligned(16))) unsigned long long dynk[];
+  const unsigned long long* gK = A.sort_key_all + kb;
+  unsigned long long* lK = dynk;
+  unsigned long long* lN = dynk + (uint64_t)nch * kChunk;
+  // the score runs to stage in LDS: every load issued here, in the same
+  // round as the chunk counters below, written to LDS after them
+  constexpr int kStageU = (kMergeLdsChunks * kChunk / 2 + kChunk * kMergeRuns - 1) / (kChunk * kMergeRuns);
+  const uint32_t nv = kLds ? nch * kChunk / 2 : 0u;
+  ulonglong2 sv[kStageU];
+  if (kLds) {
+    const ulonglong2* src = reinterpret_cast<const ulonglong2*>(gK);
+#pragma unroll
+    for (int u = 0; u < kStageU; u++) {
+      const uint32_t i = u * blockDim.x + tid;
+      sv[u] = src[i < nv ? i : 0];
+    }
+  }
   __shared__ uint32_t s_cnt[kMaxChunks];
   __shared__ uint32_t s_nb[kMaxChunks + 1];
   __shared__ double s_pm[kMergeLdsChunks];
@@ -1893,9 +1923,16 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
     else s_nb[c2] = A.chunk_nanbase[cb + c2];
   }
   if (!kLds && tid == 0) s_nb[nch] = A.chunk_nanbase[cb + nch - 1] + (A.chunk_cnt[cb + nch - 1] & 0xffffu);  // NaN total
-  const unsigned long long* gK = A.sort_key_all + kb;
   const unsigned long long* gN = A.nan_key_all + eb;
   if (ch < nch) s_own_num_slot[lc][t] = A.sort_idx_all[kb + ch * kChunk + t];
+  if (kLds) {
+    ulonglong2* dst = reinterpret_cast<ulonglong2*>(lK);
+#pragma unroll
+    for (int u = 0; u < kStageU; u++) {
+      const uint32_t i = u * blockDim.x + tid;
+      if (i < nv) dst[i] = sv[u];
+    }
+  }
   __syncthreads();
   if (kLds) {
     // the NaN bases and the min over earlier chunks (k_kl_nan_keys' scans),
@@ -1930,9 +1967,7 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
   const uint32_t nnum = cc >> 16, nnan = cc & 0xffffu;
   const uint32_t nb0 = ch < nch ? s_nb[ch] : 0u;
   if (t < nnan) s_own_nan_slot[lc][t] = kLds ? A.nan_list_all[eb + ch * kChunk + t] : A.nan_slot_all[eb + nb0 + t];
-  unsigned long long* lK = dynk;
-  unsigned long long* lN = dynk + (uint64_t)nch * kChunk;
-  if (kLds) {  // stage the score runs; the NaN keys are computed in place
+  if (kLds) {  // the NaN keys, computed in place
     for (uint32_t i = tid; i < nnan_tot; i += blockDim.x) {
       // the chunk of NaN i: the last one whose base is <= i
       uint32_t lo = 0, hi = nch;
@@ -1942,23 +1977,6 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
         else hi = mid;
       }
       lN[i] = score_key(MinF64()(s_pm[lo], A.ev_min_all[eb + lo * kChunk + (i - s_nb[lo])]));
-    }
-    const uint32_t nv = nch * kChunk / 2;
-    const ulonglong2* src = reinterpret_cast<const ulonglong2*>(gK);
-    ulonglong2* dst = reinterpret_cast<ulonglong2*>(lK);
-    constexpr int U = 8;
-    for (uint32_t i0 = 0; i0 < nv; i0 += U * blockDim.x) {
-      ulonglong2 v[U];
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const uint32_t i = i0 + u * blockDim.x + tid;
-        v[u] = src[i < nv ? i : 0];
-      }
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const uint32_t i = i0 + u * blockDim.x + tid;
-        if (i < nv) dst[i] = v[u];
-      }
     }
   }
   __syncthreads();
@@ -2075,6 +2093,7 @@ __global__ void __launch_bounds__(kKLThreads) k_kl(KLArgs A) {
   for (uint32_t u = threadIdx.x; u < nd; u += blockDim.x) A.alive_all[ob + u] = 1;
   if (threadIdx.x == 0) {
     c.kl_deferred = deferred ? 1u : 0u;
+    c.list_off = 0;
     c.num_events = E;
     c.num_kl = E;
     c.num_phys = E;
@@ -2274,6 +2293,7 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
     F.B = (uint32_t)B;
     F.nbins = P->nbins;
     F.xcd_local = (B % 8) == 0 ? 1 : 0;
+    F.sync_ticks = P->front_sync_ticks;
     k_front<T><<<P->fG * B, kFrontThreads, P->flds, st>>>(pts, F);
     if (P->timing)
       for (int e = 1; e <= 4; e++) HIPCHK(hipEventRecord(P->ev[e], st));
@@ -2333,6 +2353,7 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   P->k = num_desired;
   P->ncls = num_classes;
   P->vcap = voxel_capacity ? voxel_capacity : (1ull << 22);
+  P->front_sync_ticks = 200000000ull;  // 2 s at the 100 MHz constant clock
   const double upper = (double)num_desired * (1 + 0.2);
   P->ndcap = (uint32_t)upper + 1;
   P->ecap = 6 * P->ndcap;
@@ -2594,6 +2615,13 @@ int ndnet_ndt_debug_front_wg_marks(void* plan, unsigned long long* marks, int* G
   return NDNET_OK;
 }
 
+int ndnet_ndt_debug_set_sync_timeout(void* plan, uint64_t ticks) {
+  Plan* P = (Plan*)plan;
+  if (!P) return NDNET_ERR_ARG;
+  P->front_sync_ticks = ticks ? ticks : 200000000ull;
+  return NDNET_OK;
+}
+
 int ndnet_ndt_debug_set_epoch(void* plan, uint32_t epoch) {
   Plan* P = (Plan*)plan;
   if (!P || epoch >= (1u << 26)) return NDNET_ERR_ARG;
@@ -2626,9 +2654,27 @@ int ndnet_ndt_debug_dump(void* plan, int cloud, uint32_t* nd_n, double* nd_mean,
   if (nd_cov_pre) HIPCHK(hipMemcpy(nd_cov_pre, P->nd_cov + 9 * ob, nd * 72, hipMemcpyDeviceToHost));
   if (nd_cov_post) HIPCHK(hipMemcpy(nd_cov_post, P->nd_cov_post + 9 * ob, nd * 72, hipMemcpyDeviceToHost));
   if (vox) HIPCHK(hipMemcpy(vox, P->vox + ob, nd * 4, hipMemcpyDeviceToHost));
-  if (ord_val) HIPCHK(hipMemcpy(ord_val, P->ord_val + eb, (size_t)c.num_events * 8, hipMemcpyDeviceToHost));
-  if (ord_p) HIPCHK(hipMemcpy(ord_p, P->ord_p + eb, (size_t)c.num_events * 4, hipMemcpyDeviceToHost));
-  if (ord_q) HIPCHK(hipMemcpy(ord_q, P->ord_q + eb, (size_t)c.num_events * 4, hipMemcpyDeviceToHost));
+  // the retained list as the reference holds it after its left shift
+  // (ndt.c:69-72): live entry i < num_kl = physical entry list_off + i, poison
+  // past the entries ever written (value 0, ids 0xFFFFFFFF); the entries past
+  // the live length are the ones the shift did not write (after one prune
+  // level: the run's list, as the reference's; after several: the run's list
+  // too, where the reference keeps what its earlier shifts left there)
+  if (ord_val || ord_p || ord_q) {
+    const size_t E = c.num_events, off = c.list_off, nphys = c.num_phys, nkl = c.num_kl;
+    std::vector<double> v(P->ecap);
+    std::vector<uint32_t> pp(P->ecap), qq(P->ecap);
+    HIPCHK(hipMemcpy(v.data(), P->ord_val + eb, (size_t)P->ecap * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(pp.data(), P->ord_p + eb, (size_t)P->ecap * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(qq.data(), P->ord_q + eb, (size_t)P->ecap * 4, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < E && i < P->ecap; i++) {
+      const size_t src = i < nkl ? i + off : i;
+      const bool ok = i < nkl ? src < nphys : true;
+      if (ord_val) ord_val[i] = ok ? v[src] : 0.0;
+      if (ord_p) ord_p[i] = ok ? pp[src] : kInvalid;
+      if (ord_q) ord_q[i] = ok ? qq[src] : kInvalid;
+    }
+  }
   if (alive) HIPCHK(hipMemcpy(alive, P->alive + ob, nd, hipMemcpyDeviceToHost));
   return NDNET_OK;
 }

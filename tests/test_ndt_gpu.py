@@ -415,3 +415,41 @@ def test_fullsize_fixture(cfg, kind):
         for b in range(B):
             assert _sha_rows(rows[b]) == sha[b, lv].tobytes(), f"{cfg} {kind} cloud {b} level {levels[lv]}"
     assert not z[f"{cfg}_{kind}_glibc_extra"].any() and not z[f"{cfg}_{kind}_columns_extra"].any()
+
+
+def test_front_barrier_timeout_fails_clouds_cleanly():
+    """VERDICT r1 (weak 8): the NDNET_ERR_SYNC path of k_front's cloud
+    barriers.  With a 1-tick timeout, a workgroup that reaches a barrier before
+    its siblings gives up at once and fails its cloud: such clouds report
+    rc -22 and all-zero rows, the launch still completes, and with the default
+    timeout restored the same plan (its barrier words re-armed by the last
+    workgroup out) runs the batch bit-exactly again."""
+    import torch
+    import oracle as O
+    from ndnet import _lib
+    from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
+    from ndnet.synthetic import make_batch
+    B, n, k = 4, 50_000, 500
+    pts = make_batch("U", B, n, seed0=31)
+    plan = NdtPlan(B, n, k, -1)
+    assert plan.path == 2
+    t = torch.from_numpy(pts).cuda()
+    out = torch.empty((B, k, 12), dtype=torch.float32, device="cuda")
+    assert _lib.lib().ndnet_ndt_debug_set_sync_timeout(plan.handle, 1) == 0
+    plan.run(t, None, out, None)
+    torch.cuda.synchronize()
+    st = plan.host_stats()
+    rcs = [s.rc for s in st]
+    assert -22 in rcs and set(rcs) <= {0, -22}, rcs
+    o = out.cpu().numpy()
+    for b in range(B):
+        if rcs[b] == -22:
+            assert not o[b].any()
+    assert _lib.lib().ndnet_ndt_debug_set_sync_timeout(plan.handle, 0) == 0
+    plan.run(t, None, out, None)
+    torch.cuda.synchronize()
+    assert all(s.rc == 0 for s in plan.host_stats())
+    o = out.cpu().numpy()
+    for b in range(B):
+        pc, cov, r = O.downsample_f32(pts[b], k)
+        assert r.rc == 0 and np.array_equal(o[b, :, :3], pc) and np.array_equal(o[b, :, 3:], cov)
