@@ -282,7 +282,8 @@ def main() -> None:
     # ---- stage timing (HIP events on the stream the kernels run on) ----
     plan = get_plan(B, n, k, -1, dev)
     _lib.lib().ndnet_ndt_set_timing(plan.handle, 1)
-    stage_names = ["reset+limits", "bisection (15 launches)", "dense ids", "binning", "welford", "kl (chains+events+order+prune)"]
+    stage_names = ["reset+limits", "bisection (15 launches)", "dense ids", "binning", "welford + LU chains",
+                   "kl (scores, order, prune, rows)"]
     stage_ms = np.zeros(6)
     fwd_ms = 0.0
     reps = max(3, min(args.steps, 10))
@@ -322,11 +323,12 @@ def main() -> None:
     # the NDT front (k_reset + k_front: limits, every bisection pass, dense ids
     # and binning in ONE launch) reads the f32 points once into registers and
     # writes them grouped by ND: 12 N in + 12 N out per cloud
-    front = bool(stage_ms[1:4].sum() < 0.25 * stage_ms[0])  # events with no kernel between them
+    front = plan.path == 2  # k_front: events 1-4 are recorded back to back after it
     if front:
-        stage_names = ["k_reset+k_front (limits, bisection, dense ids, binning)", "welford",
-                       "kl (chains+events+order+prune)"]
-        stage_ms = np.array([stage_ms[0:4].sum(), stage_ms[4], stage_ms[5]])
+        # events 1-4 follow k_front back to back: their intervals hold no kernel
+        stage_names = ["k_front (limits, bisection, dense ids, binning)", "welford + LU chains",
+                       "kl (scores, order, prune, rows)"]
+        stage_ms = np.array([stage_ms[0], stage_ms[4], stage_ms[5]])
     ndt_single = {  # stage index -> (kernel, algorithmic bytes per launch, what)
         0: ("k_front", 24.0 * n * B, "f32 xyz read once + written once grouped by ND (12 N + 12 N per cloud)")
            if front else ("k_limits", 12.0 * n * B, "f32 xyz read once (12 N per cloud)"),

@@ -169,8 +169,10 @@ int ndnet_ndt_prune(void *plan, void *stream, uint64_t num_desired, float *d_out
 
 /* Stage timing with HIP events on the run's stream (bench.py): after
  * ndnet_ndt_set_timing(plan, 1), each run records events around its stages;
- * ndnet_ndt_stage_ms fills ms[6] = reset+limits, 15 bisection passes, dense
- * ids, chunk sort, Welford, KL+prune of the last run (synchronises). */
+ * ndnet_ndt_stage_ms fills ms[6] of the last run (synchronises): path 1 =
+ * reset+limits, 15 bisection passes, dense ids, binning, Welford + LU chains,
+ * KL+prune+rows; path 2 = k_front, three empty intervals (events recorded
+ * back to back), Welford + LU chains, KL+prune+rows. */
 int ndnet_ndt_set_timing(void *plan, int enable);  /* 0 off, 1 stage events, 2 + k_kl phase stamps */
 int ndnet_ndt_stage_ms(void *plan, float *ms);
 
