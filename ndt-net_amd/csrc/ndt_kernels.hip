@@ -48,6 +48,7 @@ constexpr int kBitsWords = kBitsCap / 32;
 constexpr int kKLThreads = 1024;
 constexpr int kChunk = 256;          // slots per chunk of the chip-wide event sort
 constexpr int kMergeLdsChunks = 34;  // k_kl_merge stages score + NaN keys in LDS up to this many chunks (136 KB)
+constexpr int kMergeScoreChunks = 72; // ... and the score runs alone up to this many (144 KB; k <= 2440)
 constexpr int kMaxChunks = 6 * 16384 / kChunk;  // ndcap <= 16384
 
 enum State : uint32_t { kSearching = 0, kAccepted = 1, kFailed = 2 };
@@ -166,6 +167,7 @@ struct Plan {
   uint32_t* wq_ctr;           // [2] k_welford_q dynamic item counter (re-armed by k_kl_rank_chunks)
   int eager_list;             // build every cloud's retained list in the run (ndnet_ndt_set_lazy_list(plan, 0))
   uint64_t front_sync_ticks;  // k_front's cloud-barrier timeout (ndnet_ndt_debug_set_sync_timeout)
+  int lists_built;            // the deferred lists of the last run are built (no further build launches)
 };
 
 // ------------------------------------------------------------------ helpers
@@ -1286,6 +1288,7 @@ struct KLArgs {
   int ncls;
   int kl_lds;            // prune_and_emit keeps its per-cloud arrays in LDS (kl_lds_bytes)
   int mode;              // kKLEager, kKLLazy or kKLBuild (see kl_list_skipped)
+  uint32_t merge_lds_keys;  // k_kl_merge<1>: 64-bit keys its dynamic LDS holds (score runs, then NaN keys if they fit)
 };
 
 // The retained list (the reference's kl_divergences array, in insertion
@@ -1879,8 +1882,12 @@ __device__ inline uint32_t count_composite(KP K, SP S, uint32_t n, unsigned long
 constexpr int kMergeQ = NDNET_MERGE_Q;  // other runs searched together per probe round
 constexpr int kMergeRuns = 2;  // chunks merged per k_kl_merge workgroup (512 threads; ~one workgroup per CU at B = 16)
 
-template <bool kLds>
+// kMode 2: score runs and NaN keys in LDS, the NaN keys computed here (up to
+// kMergeLdsChunks chunks); 1: score runs in LDS, NaN keys from k_kl_nan_keys
+// (up to kMergeScoreChunks); 0: everything from global memory.
+template <int kMode>
 __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
+  constexpr bool kLds = kMode == 2;
   const int b = blockIdx.y;
   const CloudCtl& c = A.ctl[b];
   if (c.state != kAccepted || kl_list_skipped(A, c)) return;
@@ -1910,6 +1917,24 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
     for (int u = 0; u < kStageU; u++) {
       const uint32_t i = u * blockDim.x + tid;
       sv[u] = src[i < nv ? i : 0];
+    }
+  } else if (kMode == 1) {  // score runs only: eight 16-byte loads in flight per thread
+    const uint32_t nv1 = nch * kChunk / 2;
+    const ulonglong2* src = reinterpret_cast<const ulonglong2*>(gK);
+    ulonglong2* dst = reinterpret_cast<ulonglong2*>(lK);
+    constexpr int U = 8;
+    for (uint32_t i0 = 0; i0 < nv1; i0 += U * blockDim.x) {
+      ulonglong2 v[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint32_t i = i0 + u * blockDim.x + tid;
+        v[u] = src[i < nv1 ? i : 0];
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint32_t i = i0 + u * blockDim.x + tid;
+        if (i < nv1) dst[i] = v[u];
+      }
     }
   }
   __shared__ uint32_t s_cnt[kMaxChunks];
@@ -1967,6 +1992,11 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
   const uint32_t nnum = cc >> 16, nnan = cc & 0xffffu;
   const uint32_t nb0 = ch < nch ? s_nb[ch] : 0u;
   if (t < nnan) s_own_nan_slot[lc][t] = kLds ? A.nan_list_all[eb + ch * kChunk + t] : A.nan_slot_all[eb + nb0 + t];
+  // mode 1: the NaN keys (from k_kl_nan_keys) join the score runs in LDS when they fit
+  const bool nan_lds = kMode == 1 && (uint64_t)nch * kChunk + nnan_tot <= A.merge_lds_keys;
+  if (nan_lds) {
+    for (uint32_t i = tid; i < nnan_tot; i += blockDim.x) lN[i] = gN[i];
+  }
   if (kLds) {  // the NaN keys, computed in place
     for (uint32_t i = tid; i < nnan_tot; i += blockDim.x) {
       // the chunk of NaN i: the last one whose base is <= i
@@ -2025,6 +2055,9 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
     A.ord_q_all[eb + pos] = (uint32_t)A.nb_all[6 * (uint64_t)b * A.ndcap + sl];
   };
   if (kLds) body(static_cast<const unsigned long long*>(lK), static_cast<const unsigned long long*>(lN));
+  else if (kMode == 1 && nan_lds)
+    body(static_cast<const unsigned long long*>(lK), static_cast<const unsigned long long*>(lN));
+  else if (kMode == 1) body(static_cast<const unsigned long long*>(lK), gN);
   else body(gK, gN);
   MERGE_MARK(14);
 #undef MERGE_MARK
@@ -2218,6 +2251,7 @@ static KLArgs kl_args(Plan* P, uint64_t k, float* out, float* out_cls, double* p
   A.ncls = P->ncls;
   A.kl_lds = kl_lds_bytes(P) <= (size_t)kKLLdsMax ? 1 : 0;
   A.mode = P->eager_list ? kKLEager : kKLLazy;
+  A.merge_lds_keys = 0;
   return A;
 }
 
@@ -2230,16 +2264,23 @@ static void launch_list_sort(Plan* P, const KLArgs& A, hipStream_t st) {
   k_kl_rank_chunks<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
   const uint32_t mg = (P->nchunk + kMergeRuns - 1) / kMergeRuns;
   if (P->nchunk <= (uint32_t)kMergeLdsChunks) {  // the merge computes the NaN keys itself
-    k_kl_merge<true><<<dim3(mg, B), kChunk * kMergeRuns, merge_lds_bytes(P), st>>>(A);
+    k_kl_merge<2><<<dim3(mg, B), kChunk * kMergeRuns, merge_lds_bytes(P), st>>>(A);
+  } else if (P->nchunk <= (uint32_t)kMergeScoreChunks) {
+    k_kl_nan_keys<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
+    KLArgs A1 = A;
+    const size_t keys = kMergeScoreChunks * kChunk;  // the launch's dynamic LDS, in 64-bit keys (144 KB)
+    A1.merge_lds_keys = (uint32_t)keys;
+    k_kl_merge<1><<<dim3(mg, B), kChunk * kMergeRuns, keys * sizeof(unsigned long long), st>>>(A1);
   } else {
     k_kl_nan_keys<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
-    k_kl_merge<false><<<dim3(mg, B), kChunk * kMergeRuns, 0, st>>>(A);
+    k_kl_merge<0><<<dim3(mg, B), kChunk * kMergeRuns, 0, st>>>(A);
   }
 }
 
 // Builds the retained lists a lazy run deferred (no-op for the others).
 static int build_deferred_lists(Plan* P, hipStream_t st) {
-  if (P->eager_list) return NDNET_OK;
+  if (P->eager_list || P->lists_built) return NDNET_OK;
+  P->lists_built = 1;  // stream order: every later prune / dump of this run follows the build
   KLArgs A = kl_args(P, P->k, nullptr, nullptr, nullptr, nullptr, nullptr);
   A.marks = nullptr;
   A.mode = kKLBuild;
@@ -2258,6 +2299,7 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
   const uint64_t n = P->n;
   if (lbl && P->ncls < 0) return NDNET_ERR_ARG;
   if (P->timing) HIPCHK(hipEventRecord(P->ev[0], st));
+  P->lists_built = 0;
   // k_front re-arms its clouds itself (epoch, barrier words, list counters)
   if (!P->front) k_reset<<<(B + 63) / 64, 64, 0, st>>>(P->ctl, B, nullptr);
   P->calls++;
@@ -2477,8 +2519,11 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
     e = hipFuncSetAttribute((const void*)k_welford_q<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(kWqRt * sizeof(double) + 4 * ((batch + 1 + 3) & ~3) + kWqHistMax));
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_kl_merge<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    e = hipFuncSetAttribute((const void*)k_kl_merge<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(2 * kMergeLdsChunks * kChunk * sizeof(unsigned long long)));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_kl_merge<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(kMergeScoreChunks * kChunk * sizeof(unsigned long long)));
   if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_kl, hipFuncAttributeMaxDynamicSharedMemorySize, kKLLdsMax);
   if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_prune, hipFuncAttributeMaxDynamicSharedMemorySize, kKLLdsMax);
   if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_bin_count, hipFuncAttributeMaxDynamicSharedMemorySize,
