@@ -925,7 +925,7 @@ out:
     for (int i = 0; i < 7; i++) st_sc1(bar + i, 0u);
     c.epoch = epoch;
     c.clear_stamps = clear_stamps ? 1u : 0u;
-    c.num_valid = c.num_kl = c.num_phys = c.num_events = 0;
+    c.num_valid = c.num_kl = c.num_phys = c.num_events = c.flag_count = 0;
     c.prune_rc = 0;
     c.num_out = c.last_k = 0;
   }

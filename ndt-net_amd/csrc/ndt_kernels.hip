@@ -85,6 +85,7 @@ struct CloudCtl {
   uint32_t last_k;
   uint32_t clear_stamps; // the epoch wrapped this run: k_limits zeroes the cloud's stamps
   uint32_t kl_deferred;  // the retained list was not built by the run (lazy list, num_nds <= k)
+  uint32_t flag_count;   // events of a deferred cloud, counted by k_kl_rank_chunks (zeroed per run)
   uint32_t list_off;     // physical index of the retained list's first entry (the prunes' pending
                          // left shifts, ndt.c:69-72; always 0 on the global-memory prune path)
 };
@@ -291,6 +292,7 @@ __global__ void k_reset(CloudCtl* ctl, int B, uint32_t* bar) {
   c.num_kl = 0;
   c.num_phys = 0;
   c.num_events = 0;
+  c.flag_count = 0;
   c.prune_rc = 0;
   c.num_out = 0;
   c.last_k = 0;
@@ -1698,8 +1700,14 @@ __global__ void __launch_bounds__(kChunk) k_kl_rank_chunks(KLArgs A) {
   uint32_t fl = 0;
   double vl = 0.0;
   kl_event(A, b, sl < nslots ? sl : 0u, !deferred, fl, vl);  // the clamped slot's result is dropped
+  if (deferred) {  // count the cloud's events (stats num_events / num_kl), one atomic per wave
+    const unsigned long long bal = __ballot(sl < nslots && fl);
+    if ((t & 63) == 0 && bal)
+      __hip_atomic_fetch_add(&A.ctl[b].flag_count, (uint32_t)__popcll(bal), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
   if (sl < nslots) A.slot_flag_all[eb + sl] = fl;
-  if (deferred) return;
   if (sl < nslots) A.slot_val_all[eb + sl] = vl;
   const bool f = sl < nslots && fl;
   const double v = f ? vl : 0.0;
@@ -2107,12 +2115,9 @@ __global__ void __launch_bounds__(kKLThreads) k_kl(KLArgs A) {
   const uint64_t ob = (uint64_t)b * A.ndcap, eb = (uint64_t)b * A.ecap;
   const uint32_t nch = (6 * nd + kChunk - 1) / kChunk;
   const bool deferred = kl_list_deferrable(A, c);
-  // event count: from the chunk counters, or (deferred list) from the flags
+  // event count: from the chunk counters, or (deferred list) k_kl_rank_chunks' count
   uint32_t e_part = 0;
-  if (deferred) {
-    const uint32_t* fl = A.slot_flag_all + eb;
-    for (uint32_t s2 = threadIdx.x; s2 < 6 * nd; s2 += blockDim.x) e_part += fl[s2];
-  } else {
+  if (!deferred) {
     for (uint32_t c2 = threadIdx.x; c2 < nch; c2 += blockDim.x) {
       const uint32_t cc = A.chunk_cnt[(uint64_t)b * A.nchunk + c2];
       e_part += (cc >> 16) + (cc & 0xffffu);
@@ -2121,6 +2126,7 @@ __global__ void __launch_bounds__(kKLThreads) k_kl(KLArgs A) {
   uint32_t ev[1] = {e_part};
   uint32_t E;
   block_scan_items(ev, 0u, AddU32(), s_u32, E);
+  if (deferred) E = c.flag_count;
   KL_MARK(2);
   if (!deferred) kl_poison_tail(A, eb, E);
   for (uint32_t u = threadIdx.x; u < nd; u += blockDim.x) A.alive_all[ob + u] = 1;
