@@ -279,6 +279,45 @@ def main() -> None:
     assert all(s.rc == 0 for s in stats), [s.rc for s in stats]
     assert all(torch.isfinite(o).all() for o in (out if isinstance(out, list) else [out]))
 
+    # ---- BASELINE.json configs 2 and 3 as their own lines: the NDT stage alone
+    # (16 x 100k -> 1000 NDs) and the forward alone (16 x 1000 x 12-D NDs), each
+    # one HIP graph per step over the same resident inputs ----
+    config_lines = None
+    if not args.eager and not levels:
+        def graph_rate(fn):
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.no_grad(), torch.cuda.stream(side):
+                fn()
+                fn()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.no_grad(), torch.cuda.graph(g):
+                fn()
+            for _ in range(3):
+                g.replay()
+            torch.cuda.synchronize()
+            D.barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                g.replay()
+            torch.cuda.synchronize()
+            D.barrier()
+            return D.max_over_ranks(time.perf_counter() - t0)
+        t_ndt = graph_rate(lambda: ndt_preprocessing(k, pts))
+        rows_p, rows_c, _ = ndt_preprocessing(k, pts)
+        rows = torch.cat((rows_p, rows_c), dim=2).contiguous()
+        t_fwd = graph_rate(lambda: model(rows[..., :3], rows[..., 3:]))
+        config_lines = {
+            "C2_ndt_only": {"value": round(total_clouds / t_ndt, 2), "unit": "clouds/s",
+                            "ms_per_step": round(1e3 * t_ndt / args.steps, 4),
+                            "workload": f"batch {B} x {n} pts -> {k} NDs, ndt_preprocessing alone"},
+            "C3_forward_only": {"value": round(total_clouds / t_fwd, 2), "unit": "clouds/s",
+                                "ms_per_step": round(1e3 * t_fwd / args.steps, 4),
+                                "workload": f"batch {B} x {k} x 12-D NDs, NDTNetSegmentation F={F} C={C} eval forward alone"},
+        }
+
     # ---- stage timing (HIP events on the stream the kernels run on) ----
     plan = get_plan(B, n, k, -1, dev)
     _lib.lib().ndnet_ndt_set_timing(plan.handle, 1)
@@ -481,9 +520,13 @@ def main() -> None:
                            else "2 hip graphs alternating: NDT(batch i) || forward(batch i-1) on two streams "
                                 "(ndnet.pipeline.PipelinedSegmentation)"),
                        "global_batch": B * world, "points": n, "nds": k, "parallelism": f"dp{world} (clouds sharded)"},
-            "stages_ms": {nm: round(float(v), 4) for nm, v in zip(stage_names, stage_ms)} | {"pointnet_fwd": round(fwd_ms, 4)},
+            "stages_ms": {nm: round(float(v), 4) for nm, v in zip(stage_names, stage_ms)}
+                         | ({"pointnet_fwd": config_lines["C3_forward_only"]["ms_per_step"],
+                             "pointnet_fwd_eager": round(fwd_ms, 4)} if config_lines else
+                            {"pointnet_fwd": round(fwd_ms, 4)}),
             "roofline": roofline,
             "other_distribution": other,
+            "config_lines": config_lines,
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
         }
