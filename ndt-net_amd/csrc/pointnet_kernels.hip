@@ -614,17 +614,28 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
   if (A.mode == 1) {  // log_softmax over channels (ndtnet.py:239), [B][N][C+1] layout
     const int lg = reg[A.num_layers & 1];
     const int pl = (A.num_layers & 1) ? pitch1 : pitch0;
-    for (int r = threadIdx.x; r < kP; r += kThreads) {
+    // 16 lanes per point (a quarter wave): columns q, q + 16, ...; the max
+    // and the sum of exponentials meet in xor shuffles within the group
+    constexpr int kLpr = 16, kRpp = kThreads / kLpr;  // lanes per row, rows per pass
+    const int q = threadIdx.x % kLpr;
+    for (int r0 = 0; r0 < kP; r0 += kRpp) {
+      const int r = r0 + threadIdx.x / kLpr;
       const int p = p0 + r;
-      if (p >= A.num_points) continue;
-      const float* row = g_smem + lg + r * pl;
+      const bool live = r < kP && p < A.num_points;  // uniform per 16-lane group
+      const float* row = g_smem + lg + (r < kP ? r : 0) * pl;
       float m = -INFINITY;
-      for (int c = 0; c < A.out_cols; c++) m = fmaxf(m, row[c]);
-      float s = 0.0f;
-      for (int c = 0; c < A.out_cols; c++) s += expf(row[c] - m);
-      const float ls = logf(s);
-      float* o = A.out + ((int64_t)b * A.num_points + p) * A.out_cols;
-      for (int c = 0; c < A.out_cols; c++) o[c] = (row[c] - m) - ls;
+      for (int c = q; c < A.out_cols; c += kLpr) m = fmaxf(m, row[c]);
+#pragma unroll
+      for (int o = kLpr / 2; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+      float sum = 0.0f;
+      for (int c = q; c < A.out_cols; c += kLpr) sum += expf(row[c] - m);
+#pragma unroll
+      for (int o = kLpr / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+      const float ls = logf(sum);
+      if (live) {
+        float* out = A.out + ((int64_t)b * A.num_points + p) * A.out_cols;
+        for (int c = q; c < A.out_cols; c += kLpr) out[c] = (row[c] - m) - ls;
+      }
     }
   }
 }

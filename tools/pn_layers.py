@@ -85,3 +85,17 @@ for K, N in [(128, 1024), (128, 768), (128, 512), (128, 256), (64, 1024), (256, 
         print(f"{tag} {K:4d} -> {N:4d} (max-pool, minus producer) {us:7.1f} us  {flops / (us * 1e-6) / 1e12:6.1f} "
               f"TFLOP/s fp32-eq, bf16 MFMA {6 * flops / (us * 1e-6) / BF16_PEAK * 100:5.1f}% of peak   "
               f"(producer {base[K]:.1f} us)")
+
+# the seg head's fused pair in split-bf16 (64 -> 512 -> 256, as chain D runs it) and the whole D tail
+if "--no-d" not in sys.argv:
+    flops = 2.0 * B * n * (64 * 512 + 512 * 256)
+    us = time_chain([layer(16, 64), layer_x6(64, 512), layer_x6(512, 256)], (1, 1, 1), 0, gmax=gmax, fuse=(1,)) \
+        - base[64]
+    print(f"x6  64 -> 512 -> 256 fused (minus producer) {us:7.1f} us  {flops / (us * 1e-6) / 1e12:6.1f} TFLOP/s "
+          f"fp32-eq, bf16 MFMA {6 * flops / (us * 1e-6) / BF16_PEAK * 100:5.1f}% of peak")
+    flops = 2.0 * B * n * (64 * 512 + 512 * 256 + 256 * 128 + 128 * 32)
+    us = time_chain([layer(16, 64), layer_x6(64, 512), layer_x6(512, 256), layer_x6(256, 128), layer(128, 32)],
+                    (1, 1, 1, 1, 0), 1, out=out, out_cols=29, fuse=(1,)) - base[64]
+    print(f"D tail 64 -> 512 -> 256 -> 128 -> 32 + log_softmax (minus producer) {us:7.1f} us  "
+          f"{flops / (us * 1e-6) / 1e12:6.1f} TFLOP/s fp32-eq")
+
