@@ -453,3 +453,25 @@ def test_front_barrier_timeout_fails_clouds_cleanly():
     for b in range(B):
         pc, cov, r = O.downsample_f32(pts[b], k)
         assert r.rc == 0 and np.array_equal(o[b, :, :3], pc) and np.array_equal(o[b, :, 3:], cov)
+
+
+@pytest.mark.parametrize("k", [1300, 2600])
+def test_merge_paths_match_oracle(k):
+    """The three k_kl_merge forms by list size: k = 1000 runs the all-LDS merge
+    (every other test), k = 1300 the score-runs-in-LDS form with k_kl_nan_keys
+    (35-72 chunks), k = 2600 the global-memory form (> 72 chunks; its prune also takes the global-memory walk).  Rows,
+    event counts and the level-1 list against the oracle, on clouds whose
+    prune removes NDs."""
+    import torch
+    import oracle as O
+    from ndnet.preprocessing.ndtnet_preprocessing import ndt_preprocessing, last_stats
+    from ndnet.synthetic import make_batch
+    pts = make_batch("L", 2, 60_000, seed0=40)
+    p, c, _ = ndt_preprocessing(k, torch.from_numpy(pts).cuda())
+    p, c = p.cpu().numpy(), c.cpu().numpy()
+    stats = last_stats()
+    for b in range(2):
+        pc, cov, r = O.downsample_f32(pts[b], k)
+        assert stats[b].rc == r.rc == 0
+        assert stats[b].num_events == len(r.ord_div) and stats[b].num_out == r.nout
+        assert np.array_equal(p[b], pc) and np.array_equal(c[b], cov)
