@@ -149,9 +149,10 @@ class NDTNetSegmentation(nn.Module):
     def forward(self, points: torch.Tensor, covariances: torch.Tensor) -> torch.Tensor:
         if (not self.training and points.is_cuda and self.point_dim == 3
                 and not self._needs_autograd(points, covariances)):
+            # a cuda eval forward IS the HIP path: a missing library raises
+            # (ndnet._lib.lib()) instead of silently running the torch composition
             from . import pointnet_hip
-            if pointnet_hip.available():
-                return pointnet_hip.segmentation_forward(self, points, covariances)
+            return pointnet_hip.segmentation_forward(self, points, covariances)
         return self.forward_torch(points, covariances)
 
     def train(self, mode: bool = True):
