@@ -134,6 +134,14 @@ int ndnet_ndt_get_path(void *plan);
  * count with the reference's); default 0.  Path 1 always counts. */
 int ndnet_ndt_set_exact_counts(void *plan, int on);
 
+/* k_front's last phase writes every point to its ND's run (the grouped
+ * points k_welford_q reads).  on = 1 (default) places a workgroup's points in
+ * ND order in LDS first and stores them as consecutive dwords of its run
+ * segments; on = 0 stores each point from its own lane (12-byte pieces of
+ * random lines: ~2x the HBM write bytes).  Identical results either way;
+ * float input with the plan's shapes in LDS only (otherwise direct). */
+int ndnet_ndt_set_front_staged(void *plan, int on);
+
 /* The retained divergence list (kl_divergences, ndt.c:189-205) is read by the
  * level-1 prune only when it removes NDs.  A cloud with num_nds <= num_desired
  * keeps every ND (or fails with rc -1 before reading the list), so by default

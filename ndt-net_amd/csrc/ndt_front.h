@@ -83,6 +83,7 @@ struct FrontArgs {
   int xcd_local;                // 1: the G workgroups of a cloud share blockIdx % 8 (one XCD)
   uint32_t rbs;                 // points per rank bin (512 or 1024)
   int dbg_store;
+  int staged;                   // 1: scatter through LDS records in ND order (float input; host checks the fit)
   int eval_all;                 // 1: count every bisection grid (debug / parity); 0: skip grids too small to matter
   uint64_t sync_ticks;          // cloud-barrier timeout in 100 MHz ticks (2e8 = 2 s; tests shorten it)
 };
@@ -261,6 +262,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
   extern __shared__ __attribute__((aligned(16))) uint32_t f_smem[];
   __shared__ FrontState s;
   __shared__ uint32_t scratch[32];
+  __shared__ unsigned long long scratch64[16];
   __shared__ uint32_t s_bad[kWorkers];
   // Workgroup -> (cloud, g).  Blocks are dealt round-robin over the 8 XCDs
   // (MI355X_MICROARCH.md, speed only: the barriers below hold whatever the
@@ -818,11 +820,17 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
     FRONT_MARK(23);
     if (!cloud_sync(s, bar, G)) goto fail;
     FRONT_MARK(24);
-    // ND bases (scan of the per-ND totals over NDs) + earlier workgroups' counts
-    uint32_t carry = 0;
+    // ND bases (scan of the per-ND totals over NDs) + earlier workgroups'
+    // counts.  Staged scatter: the same scan also places my points in ND
+    // order (local position = my count prefix over NDs + the point's rank
+    // among my points of its ND); delta[d] = global - local is kept in the
+    // table region (free since the per-point NDs were found).
+    const bool staged = A.staged != 0;
+    uint32_t* delta = table;  // [ndcap] (staged: ndcap <= kFrontTable, host check)
+    uint32_t carry = 0, lcarry = 0;
     for (uint32_t base = 0; base < nd; base += kFrontThreads) {
       const uint32_t d = base + t;
-      uint32_t tot_d = 0, pre = 0;
+      uint32_t tot_d = 0, pre = 0, mine = 0;
       if (d < nd) {
         uint32_t gg = 0;
         for (; gg + 16 <= G; gg += 16) {  // 16 loads in flight: one memory round trip for G <= 16
@@ -832,6 +840,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
 #pragma unroll
           for (int q = 0; q < 16; q++) {
             if (gg + q < g) pre += x[q];
+            if (gg + q == g) mine = x[q];
             tot_d += x[q];
           }
         }
@@ -843,13 +852,26 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
           for (int q = 0; q < 16; q++) {
             if (gg + q < G) {
               if (gg + q < g) pre += x[q];
+              if (gg + q == g) mine = x[q];
               tot_d += x[q];
             }
           }
         }
       }
-      uint32_t tot;
-      const uint32_t start = carry + block_excl_scan(tot_d, 0u, AddU32(), scratch, tot);
+      uint32_t start;
+      if (staged) {  // both scans in one: the ND total in the high word, my count in the low
+        unsigned long long tot2;
+        const unsigned long long ex2 =
+            block_excl_scan(((unsigned long long)tot_d << 32) | mine, 0ull, AddU64(), scratch64, tot2);
+        start = carry + (uint32_t)(ex2 >> 32);
+        if (d < nd) delta[d] = start + pre - (lcarry + (uint32_t)ex2);
+        carry += (uint32_t)(tot2 >> 32);
+        lcarry += (uint32_t)tot2;
+      } else {
+        uint32_t tot;
+        start = carry + block_excl_scan(tot_d, 0u, AddU32(), scratch, tot);
+        carry += tot;
+      }
       if (d < nd) {
         if (g == 0) {
           A.nd_n[(uint64_t)b * ndcap + d] = tot_d;
@@ -867,13 +889,54 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
         }
         for (; r < nrb; r++) hist[(uint64_t)r * ndcap + d] += add;
       }
-      carry += tot;
     }
     __syncthreads();
     FRONT_MARK(25);
     // ---- scatter: every point to its ND's run, in index order ----
     T* out = (T*)A.nd_pts + (uint64_t)b * n * 3;
     const uint32_t rsub = t / rbs;  // my rank bin within a 1024-point bin
+    if constexpr (sizeof(T) == 4) {
+      if (staged) {
+        // Each workgroup's points form one contiguous segment of every ND's
+        // run (its bins are consecutive, ranks are in index order).  A point
+        // stored by its own lane is a 12-byte piece of a random line: 3.2x
+        // the bytes in L2 write-backs (tools/ubench/write_width.hip).  So the
+        // points are first placed in ND order in LDS (16-byte records: x, y,
+        // z, destination), then stored by consecutive lanes as consecutive
+        // dwords of those segments (1.3x).  Records for every local position
+        // fit the whole dynamic LDS (host check: 4 words per point), which is
+        // free once each thread holds its points' positions in registers.
+        uint32_t gd[kFrontR], lp[kFrontR];
+#pragma unroll
+        for (int j = 0; j < kFrontR; j++) {
+          gd[j] = kInvalid;
+          if ((uint32_t)j < bpw) {
+            const uint32_t bi = binfo[j * 1024 + t];
+            if (bi != kInvalid) {
+              const uint32_t d = bi >> 10;
+              gd[j] = hist[(uint64_t)(j * (1024 / rbs) + rsub) * ndcap + d] + (bi & 1023u);
+              lp[j] = gd[j] - delta[d];
+              if (A.nd_lbl) A.nd_lbl[(uint64_t)b * n + gd[j]] = (uint16_t)A.lbl[(uint64_t)b * n + (bin0 + j) * 1024 + t];
+            }
+          }
+        }
+        __syncthreads();  // binfo / hist / delta read: the records may overwrite them
+        float4* rec = reinterpret_cast<float4*>(f_smem);
+#pragma unroll
+        for (int j = 0; j < kFrontR; j++)
+          if (gd[j] != kInvalid)
+            rec[lp[j]] = make_float4((float)px[j], (float)py[j], (float)pz[j], __uint_as_float(gd[j]));
+        __syncthreads();
+        // lane l stores record l: 12 bytes (one global_store_dwordx3) right
+        // after lane l - 1's within a segment
+        float3* o3 = reinterpret_cast<float3*>(out);
+        for (uint32_t l = t; l < lcarry; l += kFrontThreads) {
+          const float4 r = rec[l];
+          o3[__float_as_uint(r.w)] = make_float3(r.x, r.y, r.z);
+        }
+      }
+    }
+    if (sizeof(T) != 4 || !staged) {
     auto put = [&](uint32_t j, uint64_t i, T x, T y, T z) {
       const uint32_t bi = binfo[j * 1024 + t];
       if (bi == kInvalid) return;
@@ -906,6 +969,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
         front_point(p, i, x, y, z);
         put(j, i, x, y, z);
       }
+    }
     }
     FRONT_MARK(26);
   }

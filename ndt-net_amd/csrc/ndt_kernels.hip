@@ -169,6 +169,7 @@ struct Plan {
   int eager_list;             // build every cloud's retained list in the run (ndnet_ndt_set_lazy_list(plan, 0))
   uint64_t front_sync_ticks;  // k_front's cloud-barrier timeout (ndnet_ndt_debug_set_sync_timeout)
   int lists_built;            // the deferred lists of the last run are built (no further build launches)
+  int front_staged;           // k_front's scatter through LDS records (ndnet_ndt_set_front_staged; default 1)
 };
 
 // ------------------------------------------------------------------ helpers
@@ -2337,6 +2338,10 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
 #define NDNET_FRONT_STORE 0
 #endif
     F.dbg_store = NDNET_FRONT_STORE;  // binning scatter stores: 0 plain, 1 nontemporal, 2 agent-scope atomic (A/B)
+    // staged scatter (float input): every point held in registers, delta[ndcap]
+    // in the table region, a 16-byte LDS record per point of the workgroup
+    F.staged = P->front_staged && F.dbg_store == 0 && sizeof(T) == 4 && P->fbpw <= (uint32_t)kFrontR &&
+               P->ndcap <= (uint32_t)kFrontTable && (size_t)16 * 1024 * P->fbpw <= P->flds;
     F.eval_all = P->exact_counts;
     F.B = (uint32_t)B;
     F.nbins = P->nbins;
@@ -2402,6 +2407,7 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   P->ncls = num_classes;
   P->vcap = voxel_capacity ? voxel_capacity : (1ull << 22);
   P->front_sync_ticks = 200000000ull;  // 2 s at the 100 MHz constant clock
+  P->front_staged = 1;
   const double upper = (double)num_desired * (1 + 0.2);
   P->ndcap = (uint32_t)upper + 1;
   P->ecap = 6 * P->ndcap;
@@ -2558,6 +2564,13 @@ int ndnet_ndt_set_exact_counts(void* plan, int on) {
   Plan* P = (Plan*)plan;
   if (!P || on < 0 || on > 1) return NDNET_ERR_ARG;
   P->exact_counts = on;
+  return NDNET_OK;
+}
+
+int ndnet_ndt_set_front_staged(void* plan, int on) {
+  Plan* P = (Plan*)plan;
+  if (!P || on < 0 || on > 1) return NDNET_ERR_ARG;
+  P->front_staged = on;
   return NDNET_OK;
 }
 

@@ -68,6 +68,11 @@ class NdtPlan:
         (include/ndnet_amd.h ndnet_ndt_set_exact_counts; debug / parity)."""
         _lib.check(_lib.lib().ndnet_ndt_set_exact_counts(self.handle, 1 if on else 0), "ndnet_ndt_set_exact_counts")
 
+    def set_front_staged(self, on: bool) -> None:
+        """k_front's scatter through LDS records in ND order (default on;
+        include/ndnet_amd.h ndnet_ndt_set_front_staged; identical results)."""
+        _lib.check(_lib.lib().ndnet_ndt_set_front_staged(self.handle, 1 if on else 0), "ndnet_ndt_set_front_staged")
+
     def set_lazy_list(self, on: bool) -> None:
         """Defer the retained KL list of clouds whose level-1 prune cannot read
         it (num_nds <= k) until a prune or dump needs it (default on;

@@ -475,3 +475,42 @@ def test_merge_paths_match_oracle(k):
         assert stats[b].rc == r.rc == 0
         assert stats[b].num_events == len(r.ord_div) and stats[b].num_out == r.nout
         assert np.array_equal(p[b], pc) and np.array_equal(c[b], cov)
+
+
+@pytest.mark.parametrize("case", ["U", "L", "labelled"])
+def test_front_staged_scatter_equals_direct(case):
+    """k_front's staged scatter (points placed in ND order in LDS, stored as
+    consecutive dwords) against the per-lane 12-byte stores: the grouped
+    points feed the order-dependent Welford, so equal means / covariances /
+    KL lists / rows / one-hot classes show the runs are identical."""
+    import torch
+    from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
+    from ndnet.synthetic import make_batch
+    kind = "L" if case == "labelled" else case
+    pts = make_batch(kind, 8, 60_000, seed0=31)
+    B, n, _ = pts.shape
+    k, ncls = 800, (27 if case == "labelled" else -1)
+    lbl = None
+    if case == "labelled":
+        lbl = torch.from_numpy(np.random.default_rng(3).integers(0, ncls + 1, size=(B, n)).astype(np.int32)).cuda()
+    res = {}
+    for staged in (True, False):
+        plan = NdtPlan(B, n, k, ncls)
+        plan.set_front_staged(staged)
+        assert plan.path == 2
+        out = torch.empty((B, k, 12), dtype=torch.float32, device="cuda")
+        oc = None if lbl is None else torch.empty((B, k, ncls + 1), dtype=torch.float32, device="cuda")
+        plan.run(torch.from_numpy(pts).cuda(), lbl, out, oc)
+        torch.cuda.synchronize()
+        stats = plan.host_stats()
+        dumps = [_dump(plan, b, int(stats[b].num_nds), int(stats[b].num_events)) for b in range(B)]
+        res[staged] = (out.cpu().numpy(), None if oc is None else oc.cpu().numpy(), stats, dumps)
+    (o1, c1, s1, d1), (o0, c0, s0, d0) = res[True], res[False]
+    assert np.array_equal(o1, o0)
+    if c1 is not None:
+        assert np.array_equal(c1, c0)
+    for b in range(B):
+        assert s1[b].rc == 0
+        assert bytes(s1[b]) == bytes(s0[b]), f"cloud {b} stats"
+        for key in d1[b]:
+            assert np.array_equal(d1[b][key], d0[b][key], equal_nan=True), (b, key)
