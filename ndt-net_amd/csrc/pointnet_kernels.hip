@@ -76,6 +76,37 @@ __device__ inline void atomic_max_f32(float* addr, float v) {
   else atomicMin(reinterpret_cast<unsigned int*>(addr), __float_as_uint(v));
 }
 
+// Output orientation of the MFMA tiles.  With the weights as the A operand
+// and the activations as B (NDNET_PN_SWAP = 1, default) a 16 x 16 tile comes
+// out transposed: lane (kq, cl) holds point cl, channels 4 kq .. 4 kq + 3 --
+// four consecutive channels of one point, which the epilogue stores as one
+// ds_write_b128 (fp32) or one ds_write_b64 per bf16 plane instead of 4 / 12
+// scalar stores, and max-pools over the 16 points of a lane row with DPP.
+// The operands' lane data are the same either way (the fragment layouts are
+// symmetric), so only the MFMA argument order and the epilogues change.
+// NDNET_PN_SWAP = 0: activations as A, lane (kq, cl) holds points 4 kq + r of
+// channel cl.
+#ifndef NDNET_PN_SWAP
+#define NDNET_PN_SWAP 1
+#endif
+
+// v of lane (lane ^ S) within a 16-lane row, through DPP (no LDS)
+template <int S>
+__device__ inline float xor_row(float v) {
+  const int x = __float_as_int(v);
+  if constexpr (S == 1) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
+  } else if constexpr (S == 2) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
+  } else if constexpr (S == 4) {
+    const int h = __builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, false);          // row_half_mirror: i ^ 7
+    return __int_as_float(__builtin_amdgcn_mov_dpp(h, 0x1B, 0xF, 0xF, false));  // quad_perm [3,2,1,0]: ^ 3
+  } else {
+    const int h = __builtin_amdgcn_mov_dpp(x, 0x140, 0xF, 0xF, false);           // row_mirror: i ^ 15
+    return __int_as_float(__builtin_amdgcn_mov_dpp(h, 0x141, 0xF, 0xF, false));  // row_half_mirror: ^ 7
+  }
+}
+
 // dynamic LDS of k_pn_chain: the two activation regions and the fused pair's
 // double buffer, addressed by float offsets so every access is a ds_* op
 extern __shared__ __attribute__((aligned(16))) float g_smem[];
@@ -126,7 +157,12 @@ __device__ __attribute__((always_inline)) inline void mma_kgroup(f32x4 (&acc)[RB
 #pragma unroll
     for (int rb = 0; rb < RB; rb++)
 #pragma unroll
-      for (int j = 0; j < NB; j++) acc[rb][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rb][s], bw[j][s], acc[rb][j], 0, 0, 0);
+      for (int j = 0; j < NB; j++)
+#if NDNET_PN_SWAP
+        acc[rb][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(bw[j][s], a[rb][s], acc[rb][j], 0, 0, 0);
+#else
+        acc[rb][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rb][s], bw[j][s], acc[rb][j], 0, 0, 0);
+#endif
 }
 
 // T = nchunk * nkg k-group steps.  Step t is k-group kg0 + t % nkg of column
@@ -200,6 +236,24 @@ __device__ __attribute__((always_inline)) inline void store_cols(const f32x4 (&a
                                                                  int row0, int out, int pout, int oc0) {
   const int lane = threadIdx.x & 63;
   const int kq = lane >> 4, cl = lane & 15;
+#if NDNET_PN_SWAP
+#pragma unroll
+  for (int j = 0; j < NB; j++) {
+    float bv[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) bv[r] = bias[col0 + 16 * j + 4 * kq + r];
+#pragma unroll
+    for (int rb = 0; rb < RB; rb++) {
+      f32x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        v[r] = acc[rb][j][r] + bv[r];
+        if (relu) v[r] = fmaxf(v[r], 0.0f);
+      }
+      *reinterpret_cast<f32x4*>(g_smem + out + (row0 + 16 * rb + cl) * pout + oc0 + 16 * j + 4 * kq) = v;
+    }
+  }
+#else
 #pragma unroll
   for (int j = 0; j < NB; j++) {
     const float bv = bias[col0 + 16 * j + cl];
@@ -212,6 +266,7 @@ __device__ __attribute__((always_inline)) inline void store_cols(const f32x4 (&a
         g_smem[out + (row0 + 16 * rb + 4 * kq + r) * pout + oc0 + 16 * j + cl] = v;
       }
   }
+#endif
 }
 
 // Bias + ReLU + max over this wave's valid rows, one float atomic max per
@@ -222,6 +277,32 @@ __device__ __attribute__((always_inline)) inline void pool_cols(const f32x4 (&ac
                                                                 int row0, int rows_valid, float* gmax) {
   const int lane = threadIdx.x & 63;
   const int kq = lane >> 4, cl = lane & 15;
+#if NDNET_PN_SWAP
+  // lane (kq, cl): point cl of each row block, channels 4 kq + r; the max over
+  // the 16 points of a lane row by DPP, then lane cl < 4 of the row takes
+  // channel 4 kq + cl's atomic
+#pragma unroll
+  for (int j = 0; j < NB; j++) {
+    float m[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const float bv = bias[col0 + 16 * j + 4 * kq + r];
+      m[r] = -INFINITY;
+#pragma unroll
+      for (int rb = 0; rb < RB; rb++) {
+        float v = acc[rb][j][r] + bv;
+        if (relu) v = fmaxf(v, 0.0f);
+        if (row0 + 16 * rb + cl < rows_valid) m[r] = fmaxf(m[r], v);
+      }
+      m[r] = fmaxf(m[r], xor_row<1>(m[r]));
+      m[r] = fmaxf(m[r], xor_row<2>(m[r]));
+      m[r] = fmaxf(m[r], xor_row<4>(m[r]));
+      m[r] = fmaxf(m[r], xor_row<8>(m[r]));
+    }
+    const float mm = cl == 0 ? m[0] : cl == 1 ? m[1] : cl == 2 ? m[2] : m[3];
+    if (cl < 4 && mm > -INFINITY) atomic_max_f32(gmax + col0 + 16 * j + 4 * kq + cl, mm);
+  }
+#else
 #pragma unroll
   for (int j = 0; j < NB; j++) {
     const float bv = bias[col0 + 16 * j + cl];
@@ -238,6 +319,7 @@ __device__ __attribute__((always_inline)) inline void pool_cols(const f32x4 (&ac
     m = fmaxf(m, __shfl_xor(m, 32, 64));
     if (lane < 16 && m > -INFINITY) atomic_max_f32(gmax + col0 + 16 * j + cl, m);
   }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -277,6 +359,33 @@ __device__ __attribute__((always_inline)) inline void store_cols_planes(const f3
   const int kq = lane >> 4, cl = lane & 15;
   __bf16* const base = reinterpret_cast<__bf16*>(g_smem + out);
   const int plane = kP * pitchb;
+#if NDNET_PN_SWAP
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int j = 0; j < NB; j++) {
+    float bv[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) bv[r] = bias[col0 + 16 * j + 4 * kq + r];
+#pragma unroll
+    for (int rb = 0; rb < RB; rb++) {
+      bf16x4 h4, m4, l4;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        float v = acc[rb][j][r] + bv[r];
+        if (relu) v = fmaxf(v, 0.0f);
+        __bf16 h, m, l;
+        split3(v, h, m, l);
+        h4[r] = h;
+        m4[r] = m;
+        l4[r] = l;
+      }
+      const int e = (row0 + 16 * rb + cl) * pitchb + oc0 + 16 * j + 4 * kq;  // 4 channels: 8 bytes
+      *reinterpret_cast<bf16x4*>(base + e) = h4;
+      *reinterpret_cast<bf16x4*>(base + plane + e) = m4;
+      *reinterpret_cast<bf16x4*>(base + 2 * plane + e) = l4;
+    }
+  }
+#else
 #pragma unroll
   for (int j = 0; j < NB; j++) {
     const float bv = bias[col0 + 16 * j + cl];
@@ -294,6 +403,7 @@ __device__ __attribute__((always_inline)) inline void store_cols_planes(const f3
         base[2 * plane + e] = l;
       }
   }
+#endif
 }
 
 // One 32-row k-group: the A planes are read one at a time (m, l, h) so only
@@ -314,7 +424,11 @@ __device__ __attribute__((always_inline)) inline void mma_kgroup_x6(f32x4 (&acc)
     for (int rb = 0; rb < RB; rb++)
 #pragma unroll
       for (int j = 0; j < NB; j++)
+#if NDNET_PN_SWAP
+        acc[rb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j][pb], a[rb], acc[rb][j], 0, 0, 0);
+#else
         acc[rb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], bw[j][pb], acc[rb][j], 0, 0, 0);
+#endif
   };
   ld(1);  // m: m*m, m*h
   mm(1);

@@ -67,6 +67,11 @@ def set_precision(mode: str) -> None:
 
 
 set_precision(os.environ.get("NDNET_PN_PRECISION", "x6"))
+# split-bf16 also on the narrower per-point layers with K >= 64 (TNet(3)'s
+# 64 -> 128, TNet(64)'s 64 -> 64 and 64 -> 128, the seg head's 128 -> C+1):
+# default on, measured -5 us per forward (chains A / B / D 3 / 2 / 1.5 us
+# faster); "0" keeps them on the fp32 MFMA.  Only the K = 16 first layers stay fp32.
+X6_NARROW = os.environ.get("NDNET_PN_X6_NARROW", "1") == "1"
 
 
 class _Layer(ctypes.Structure):
@@ -218,6 +223,8 @@ class _Folded:
             self.frag = {id(w): _frag(w) for w, _ in self.A + self.B_tail + [self.C_tail] + self.D_tail}
             # the wide pooled layers in split-bf16 form
             self.wide = [self.A[2][0], self.B_tail[2][0], self.C_tail[0], self.D_tail[0][0], self.D_tail[1][0]]
+            if X6_NARROW:  # the K >= 64 fp32-MFMA layers too (64 -> 128 of TNet(3) / TNet(64), 64 -> 64, 128 -> C+1)
+                self.wide += [self.A[1][0], self.B_tail[0][0], self.B_tail[1][0], self.D_tail[2][0]]
             self.frag6 = {id(w): (_frag_x6f(w) if WEIGHT_F32 else _frag_x6(w)) for w in self.wide}
             # the identity the TNet heads add (ndtnet.py:59), folded into fc3's bias
             self.t1["c3"] = self.t1["c3"] + torch.eye(3, device=dev).reshape(-1)
