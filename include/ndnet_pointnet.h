@@ -90,6 +90,12 @@ int ndnet_pn_chain_run(const ndnet_pn_chain *args, int batch, void *stream);
  * Same return codes as ndnet_pn_chain_run; graph-capturable. */
 int ndnet_pn_fc_run(const float *in, int ld_in, const float *W, const float *bias, float *out, int ld_out,
                     int batch, int K, int N, int relu, void *stream);
+/* The same FC layer on the fp32 MFMA (the default): Wf = W^T in the chain's
+ * fragment-major layout ([N/16][K/16][64 lanes][4], as ndnet_pn_layer.w with
+ * prec 0), K % 16 == 0, K <= 1024, N % 16 == 0; one launch of N / 16
+ * workgroups, each summing its waves' K-slices in a fixed order. */
+int ndnet_pn_fc_mfma_run(const float *in, int ld_in, const float *Wf, const float *bias, float *out, int ld_out,
+                         int batch, int K, int N, int relu, void *stream);
 int ndnet_pn_head3_run(const float *h2, int ld_h, const float *W3, const float *b3, const float *basis,
                        float *t1, float *w1f, int batch, int K, int kin, int nout, void *stream);
 int ndnet_pn_fold64_run(const float *t2, const float *rhs, float *out, int batch, int N, void *stream);

@@ -717,9 +717,23 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
       const int out = reg[(l + 1) & 1], pout = ((l + 1) & 1) ? pitch1 : pitch0;
       float* gm = (last && gmax_b) ? gmax_b : nullptr;
       const bool op = !last && A.L[l + 1].prec;  // the next layer reads bf16 planes
-      if (C.N % 256 == 0) plain_layer<4, 1>(C, in, pin, out, pout, gm, rows_valid, op);
-      else if (C.N % 128 == 0) plain_layer<2, 1>(C, in, pin, out, pout, gm, rows_valid, op);
-      else plain_layer<1, 1>(C, in, pin, out, pout, gm, rows_valid, op);  // N % 64 == 0, or N = 32 (half idle)
+      if constexpr (kWaves == 8) {
+        // 8 waves (2 per SIMD, up to 256 registers each): a wave takes up to
+        // four column blocks, so each A fragment feeds NB MFMAs per plane
+        // (tools/ubench/mfma_bf16_peak.hip b9 / b13 vs b3)
+#ifndef NDNET_PN_W8_NB4
+#define NDNET_PN_W8_NB4 1
+#endif
+        if (NDNET_PN_W8_NB4 && C.N % 512 == 0) plain_layer<4, 4>(C, in, pin, out, pout, gm, rows_valid, op);
+        else if (C.N % 256 == 0) plain_layer<4, 2>(C, in, pin, out, pout, gm, rows_valid, op);
+        else if (C.N % 128 == 0) plain_layer<4, 1>(C, in, pin, out, pout, gm, rows_valid, op);
+        else if (C.N % 64 == 0) plain_layer<2, 1>(C, in, pin, out, pout, gm, rows_valid, op);
+        else plain_layer<1, 1>(C, in, pin, out, pout, gm, rows_valid, op);  // N = 32
+      } else {
+        if (C.N % 256 == 0) plain_layer<4, 1>(C, in, pin, out, pout, gm, rows_valid, op);
+        else if (C.N % 128 == 0) plain_layer<2, 1>(C, in, pin, out, pout, gm, rows_valid, op);
+        else plain_layer<1, 1>(C, in, pin, out, pout, gm, rows_valid, op);  // N % 64 == 0, or N = 32 (half idle)
+      }
     }
     __syncthreads();
   }
@@ -795,6 +809,64 @@ __global__ void __launch_bounds__(256) k_pn_fc(const float* __restrict__ in, int
     v += bias[n];
     if (relu) v = fmaxf(v, 0.0f);
     out[(int64_t)lane * ld_out + n] = v;
+  }
+}
+
+// The same FC layer on the fp32 matrix cores: a 16-row GEMM (row = cloud,
+// b < B <= 16) with W^T fragment-major (the chain layout, [cb][kg][lane][4]).
+// One workgroup per 16-column block; its kFcWaves waves (8: measured best in the
+// pipelined step, 16 slowed it) split the K-groups,
+// each wave's weight fragments (1 KB each) and input pieces (a float4 of 4
+// consecutive k per lane) loaded up front -- one memory round trip per
+// launch -- then 4 MFMAs per k-group; the waves' 16 x 16 partial tiles are
+// summed in LDS in wave order (deterministic) and wave 0 adds the bias.
+// Products are exact and sums fp32, as torch's fp32 GEMM (another order).
+#ifndef NDNET_PN_FC_WAVES
+#define NDNET_PN_FC_WAVES 8
+#endif
+constexpr int kFcWaves = NDNET_PN_FC_WAVES, kFcMaxG = 64 / kFcWaves;  // K <= 16 * kFcWaves * kFcMaxG = 1024
+__global__ void __launch_bounds__(kFcWaves * 64) k_pn_fc_mfma(const float* __restrict__ in, int ld_in,
+                                                              const f32x4* __restrict__ wf,
+                                                              const float* __restrict__ bias, float* __restrict__ out,
+                                                              int ld_out, int B, int KG, int relu) {
+  __shared__ f32x4 part[kFcWaves][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kq = lane >> 4, cl = lane & 15;
+  const int cb = blockIdx.x;
+  const int kg0 = KG * wave / kFcWaves, ng = KG * (wave + 1) / kFcWaves - kg0;
+  const f32x4* wp = wf + ((int64_t)cb * KG + kg0) * 64 + lane;
+  const float* xr = in + (int64_t)(cl < B ? cl : 0) * ld_in + 16 * kg0 + 4 * kq;  // rows past B: discarded
+  f32x4 wv[kFcMaxG], xv[kFcMaxG];
+#pragma unroll
+  for (int i = 0; i < kFcMaxG; i++) {
+    if (i < ng) {
+      wv[i] = wp[i * 64];
+      xv[i] = *reinterpret_cast<const f32x4*>(xr + 16 * i);
+    }
+  }
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < kFcMaxG; i++)
+    if (i < ng)
+#pragma unroll
+      for (int s = 0; s < 4; s++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[i][s], wv[i][s], acc, 0, 0, 0);
+  part[wave][lane] = acc;
+  __syncthreads();
+  if (wave != 0) return;
+  f32x4 t = part[0][lane];
+#pragma unroll
+  for (int w = 1; w < kFcWaves; w++) t += part[w][lane];
+  // lane (kq, cl): clouds 4 kq + r of column 16 cb + cl
+  const int n = 16 * cb + cl;
+  const float bv = bias[n];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int b = 4 * kq + r;
+    if (b < B) {
+      float v = t[r] + bv;
+      if (relu) v = fmaxf(v, 0.0f);
+      out[(int64_t)b * ld_out + n] = v;
+    }
   }
 }
 
@@ -1009,6 +1081,16 @@ __global__ void __launch_bounds__(256) k_pn_fold64_x6f(const float* __restrict__
 }  // namespace
 
 extern "C" {
+
+int ndnet_pn_fc_mfma_run(const float* in, int ld_in, const float* Wf, const float* bias, float* out, int ld_out,
+                         int batch, int K, int N, int relu, void* stream) {
+  if (!in || !Wf || !bias || !out || batch <= 0 || batch > 16 || K <= 0 || K % 16 || K > 16 * kFcWaves * kFcMaxG ||
+      N <= 0 || N % 16 || ld_in % 4 || ld_in < K || ld_out < N || ((uintptr_t)in | (uintptr_t)Wf) % 16)
+    return -20;
+  k_pn_fc_mfma<<<N / 16, kFcWaves * 64, 0, (hipStream_t)stream>>>(in, ld_in, reinterpret_cast<const f32x4*>(Wf), bias,
+                                                                   out, ld_out, batch, K / 16, relu);
+  return hipGetLastError() == hipSuccess ? 0 : -21;
+}
 
 int ndnet_pn_fc_run(const float* in, int ld_in, const float* W, const float* bias, float* out, int ld_out, int batch,
                     int K, int N, int relu, void* stream) {

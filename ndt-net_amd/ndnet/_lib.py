@@ -110,6 +110,7 @@ POINTNET_EXPORTS: dict = {
     "ndnet_ply_count": (_I, [ctypes.c_char_p, _I, ctypes.POINTER(_U64)]),
     "ndnet_ply_read": (_I, [ctypes.c_char_p, _I, _I, _P, _P, _U64, ctypes.POINTER(_U64), _I]),
     "ndnet_pn_fc_run": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "ndnet_pn_fc_mfma_run": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "ndnet_pn_head3_run": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "ndnet_pn_fold64_run": (_I, [_P, _P, _P, _I, _I, _P]),
     "ndnet_pn_fold64_x6_run": (_I, [_P, _P, _P, _I, _I, _P]),

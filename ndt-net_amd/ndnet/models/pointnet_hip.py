@@ -226,6 +226,10 @@ class _Folded:
             if X6_NARROW:  # the K >= 64 fp32-MFMA layers too (64 -> 128 of TNet(3) / TNet(64), 64 -> 64, 128 -> C+1)
                 self.wide += [self.A[1][0], self.B_tail[0][0], self.B_tail[1][0], self.D_tail[2][0]]
             self.frag6 = {id(w): (_frag_x6f(w) if WEIGHT_F32 else _frag_x6(w)) for w in self.wide}
+            # the FC layers of the TNet heads and the seg head's global-feature
+            # bias, W^T fragment-major for the MFMA GEMV (ndnet_pn_fc_mfma_run)
+            self.fcf = {id(w): _frag(w.t().contiguous()) for w in
+                        (self.t1["f1"], self.t1["f2"], self.t2["f1"], self.t2["f2"], self.t2["f3"], self.s1g)}
             # the identity the TNet heads add (ndtnet.py:59), folded into fc3's bias
             self.t1["c3"] = self.t1["c3"] + torch.eye(3, device=dev).reshape(-1)
             self.t2["c3"] = self.t2["c3"] + torch.eye(64, device=dev).reshape(-1)
@@ -409,15 +413,29 @@ def _folded(model):
     return cache
 
 
-def _fc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: torch.Tensor, relu: bool) -> None:
-    """out = act(x @ w^T + b) on the HIP GEMV kernel (chunks of 16 clouds)."""
+# TNet / seg-bias FC layers: "mfma" (default: ndnet_pn_fc_mfma_run, 16-row
+# fp32-MFMA GEMM over fragment-major weights) or "gemv" (ndnet_pn_fc_run,
+# VALU dot products over row-major weights)
+FC_MFMA = os.environ.get("NDNET_PN_FC", "mfma") == "mfma"
+
+
+def _fc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: torch.Tensor, relu: bool, wf=None) -> None:
+    """out = act(x @ w^T + b) on a HIP kernel (chunks of 16 clouds); wf: W^T
+    fragment-major (the MFMA kernel), else the GEMV kernel on w."""
     B = x.shape[0]
     st = _lib.stream_ptr(x.device)
     for c0 in range(0, B, 16):
         n = min(16, B - c0)
-        rc = _lib.lib().ndnet_pn_fc_run(x[c0].data_ptr(), x.stride(0), w.data_ptr(), b.data_ptr(), out[c0].data_ptr(),
-                                        out.stride(0), n, w.shape[1], w.shape[0], 1 if relu else 0, st)
-        _lib.check(rc, "ndnet_pn_fc_run")
+        if FC_MFMA and wf is not None:
+            rc = _lib.lib().ndnet_pn_fc_mfma_run(x[c0].data_ptr(), x.stride(0), wf.data_ptr(), b.data_ptr(),
+                                                 out[c0].data_ptr(), out.stride(0), n, w.shape[1], w.shape[0],
+                                                 1 if relu else 0, st)
+            _lib.check(rc, "ndnet_pn_fc_mfma_run")
+        else:
+            rc = _lib.lib().ndnet_pn_fc_run(x[c0].data_ptr(), x.stride(0), w.data_ptr(), b.data_ptr(),
+                                            out[c0].data_ptr(), out.stride(0), n, w.shape[1], w.shape[0],
+                                            1 if relu else 0, st)
+            _lib.check(rc, "ndnet_pn_fc_run")
 
 
 def _glue_hip(W, ws, B: int):
@@ -425,10 +443,13 @@ def _glue_hip(W, ws, B: int):
     weight folds (t1 into conv1, t2 into conv2 / seg conv1)."""
     st = lambda: _lib.stream_ptr(ws.gbuf.device)  # noqa: E731
 
+    def fc(x, w, b, out, relu):  # with the layer's fragment-major weights (the MFMA kernel)
+        _fc(x, w, b, out, relu, W.fcf.get(id(w)))
+
     def head_a():
         t = W.t1
-        _fc(ws.g1, t["f1"], t["c1"], ws.h1, True)
-        _fc(ws.h1, t["f2"], t["c2"], ws.h2, True)
+        fc(ws.g1, t["f1"], t["c1"], ws.h1, True)
+        fc(ws.h1, t["f2"], t["c2"], ws.h2, True)
         for c0 in range(0, B, 16):
             n = min(16, B - c0)
             rc = _lib.lib().ndnet_pn_head3_run(ws.h2[c0].data_ptr(), ws.h2.stride(0), t["f3"].data_ptr(),
@@ -438,9 +459,9 @@ def _glue_hip(W, ws, B: int):
 
     def head_b():
         t = W.t2
-        _fc(ws.g2, t["f1"], t["c1"], ws.h1, True)
-        _fc(ws.h1, t["f2"], t["c2"], ws.h2, True)
-        _fc(ws.h2, t["f3"], t["c3"], ws.t2, False)
+        fc(ws.g2, t["f1"], t["c1"], ws.h1, True)
+        fc(ws.h1, t["f2"], t["c2"], ws.h2, True)
+        fc(ws.h2, t["f3"], t["c3"], ws.t2, False)
         if WEIGHT_F32:
             rc = _lib.lib().ndnet_pn_fold64_x6f_run(ws.t2.data_ptr(), W.t2_rhs.data_ptr(), ws.t2wf6.data_ptr(), B,
                                                     W.t2_rhs.shape[1], st())
@@ -455,7 +476,7 @@ def _glue_hip(W, ws, B: int):
             _lib.check(rc, "ndnet_pn_fold64_run")
 
     def seg_bias():
-        _fc(ws.g3[:, : W.F], W.s1g, W.s1b, ws.cvec, False)
+        fc(ws.g3[:, : W.F], W.s1g, W.s1b, ws.cvec, False)
 
     return head_a, head_b, seg_bias
 

@@ -110,6 +110,70 @@ __global__ void __launch_bounds__(1024) k_x6(float* out, const bf16x8* __restric
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// b8..: fewer waves, more column blocks per wave: WAVES waves per CU (one
+// workgroup), RB = 4 row blocks x NB column blocks of 16x16x32 per wave; the
+// three A planes of a k-group read up front (APRE) into their own registers,
+// the next k-group's B fragments prefetched one step ahead.
+template <int WAVES, int NB, bool APRE>
+__global__ void __launch_bounds__(WAVES * 64) k_x6w(float* out, const bf16x8* __restrict__ w, const float* __restrict__ rnd,
+                                                   int iters, int wmask) {
+  extern __shared__ bf16x8 lds[];
+  constexpr int pitch = 136, plane = 64 * pitch, RB = 4;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __bf16* l16 = reinterpret_cast<__bf16*>(lds);
+  for (int e = threadIdx.x; e < 3 * plane; e += blockDim.x) l16[e] = (__bf16)rnd[e & 1023];
+  __syncthreads();
+  const int wbase = (wave * 64 + lane);
+  const int arow = lane & 15, ak = 8 * (lane >> 4);
+  const int rstride = 16 * pitch;
+  f32x4 acc[RB][NB] = {};
+  bf16x8 bq[NB][3];
+  int off = 0;
+  auto loadb = [&]() {
+#pragma unroll
+    for (int j = 0; j < NB; j++)
+#pragma unroll
+      for (int p = 0; p < 3; p++) bq[j][p] = w[(wbase + ((off * NB + j) * 3 + p) * 1024) & wmask];
+    off++;
+  };
+  loadb();
+  for (int it = 0; it < iters; it++) {
+    const int kk = (it & 3) * 32;
+    const __bf16* a0 = l16 + arow * pitch + ak + kk;
+    bf16x8 bw[NB][3];
+#pragma unroll
+    for (int j = 0; j < NB; j++)
+#pragma unroll
+      for (int p = 0; p < 3; p++) bw[j][p] = bq[j][p];
+    loadb();
+    bf16x8 a3[3][RB];
+    bf16x8 a[RB];
+    if (APRE) {
+#pragma unroll
+      for (int p = 0; p < 3; p++)
+#pragma unroll
+        for (int rb = 0; rb < RB; rb++) a3[p][rb] = *reinterpret_cast<const bf16x8*>(a0 + p * plane + rb * rstride);
+    }
+    auto ld = [&](int p) {
+#pragma unroll
+      for (int rb = 0; rb < RB; rb++) a[rb] = APRE ? a3[p][rb] : *reinterpret_cast<const bf16x8*>(a0 + p * plane + rb * rstride);
+    };
+    auto mm = [&](int pb) {
+#pragma unroll
+      for (int rb = 0; rb < RB; rb++)
+#pragma unroll
+        for (int j = 0; j < NB; j++) acc[rb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j][pb], a[rb], acc[rb][j], 0, 0, 0);
+    };
+    ld(1); mm(1); mm(0);
+    ld(2); mm(0);
+    ld(0); mm(2); mm(1); mm(0);
+  }
+  float s = 0;
+  for (int rb = 0; rb < RB; rb++)
+    for (int j = 0; j < NB; j++) s += acc[rb][j][0] + acc[rb][j][3];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 int main() {
   float *out, *rnd;
   bf16x8* w;
@@ -163,5 +227,21 @@ int main() {
     const double per = v != 4 ? 24.0 * 16384 : 12.0 * 32768;
     report(names[v - 3], (double)grid * 16 * it_x6 * per);
   }
+  // b8..b13: waves per CU x column blocks per wave (the same FLOPs per CU per k-group round
+  // when WAVES * NB = 16)
+  auto wv = [&](const char* name, auto k, int waves, int nb) {
+    CHK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    k<<<grid, waves * 64, lds>>>(out, w, rnd, 16, wmask);
+    CHK(hipEventRecord(e0));
+    k<<<grid, waves * 64, lds>>>(out, w, rnd, it_x6, wmask);
+    CHK(hipEventRecord(e1));
+    report(name, (double)grid * waves * it_x6 * 24.0 * nb * 16384);
+  };
+  wv("b8  16 waves x NB 1, A planes up front", k_x6w<16, 1, true>, 16, 1);
+  wv("b9  8 waves x NB 2, A per plane", k_x6w<8, 2, false>, 8, 2);
+  wv("b10 8 waves x NB 2, A planes up front", k_x6w<8, 2, true>, 8, 2);
+  wv("b11 4 waves x NB 4, A per plane", k_x6w<4, 4, false>, 4, 4);
+  wv("b12 4 waves x NB 4, A planes up front", k_x6w<4, 4, true>, 4, 4);
+  wv("b13 8 waves x NB 4, A planes up front", k_x6w<8, 4, true>, 8, 4);
   return 0;
 }
