@@ -1029,10 +1029,7 @@ __global__ void __launch_bounds__(256) k_pn_fold64(const float* __restrict__ t2,
 }
 
 // The same fold written in the split-bf16 layout (K = 64: two 32-row
-// k-groups): out6[b] = [N/16][2][3 planes][64 lanes][8] bf16.  A thread
-// computes 8 consecutive k (one lane's 8 bf16 of a fragment) for 2 columns,
-// so each plane is stored as one 16-byte piece per column (the sums run over
-// j in order, as the fp32 fold's).
+// k-groups): out6[b] = [N/16][2][3 planes][64 lanes][8] bf16.
 __global__ void __launch_bounds__(256) k_pn_fold64_x6(const float* __restrict__ t2, const float* __restrict__ rhs,
                                                       __bf16* __restrict__ out6, int N) {
   __shared__ float s_a[64][65];
@@ -1044,37 +1041,32 @@ __global__ void __launch_bounds__(256) k_pn_fold64_x6(const float* __restrict__ 
     s_b[e >> 6][e & 63] = rhs[(int64_t)(e >> 6) * N + j0 + (e & 63)];
   }
   __syncthreads();
-  const int k0 = (threadIdx.x & 7) * 8, n0 = (threadIdx.x >> 3) * 2;
-  float acc[8][2] = {};
-  for (int j = 0; j < 64; j++) {
-    float av[8], bv[2];
+  const int ti = (threadIdx.x >> 4) * 4, tj = (threadIdx.x & 15) * 4;
+  float acc[4][4] = {};
+  for (int k = 0; k < 64; k++) {
+    float av[4], bv[4];
 #pragma unroll
-    for (int r = 0; r < 8; r++) av[r] = s_a[k0 + r][j];
+    for (int r = 0; r < 4; r++) av[r] = s_a[ti + r][k];
 #pragma unroll
-    for (int c = 0; c < 2; c++) bv[c] = s_b[j][n0 + c];
+    for (int c = 0; c < 4; c++) bv[c] = s_b[k][tj + c];
 #pragma unroll
-    for (int r = 0; r < 8; r++)
+    for (int r = 0; r < 4; r++)
 #pragma unroll
-      for (int c = 0; c < 2; c++) acc[r][c] += av[r] * bv[c];
+      for (int c = 0; c < 4; c++) acc[r][c] += av[r] * bv[c];
   }
   __bf16* o = out6 + (int64_t)b * 64 * N * 3;
 #pragma unroll
-  for (int c = 0; c < 2; c++) {
-    const int n = j0 + n0 + c;
-    const int64_t e = ((((int64_t)(n >> 4) * 2 + (k0 >> 5)) * 3) * 64 + ((k0 >> 3) & 3) * 16 + (n & 15)) * 8;
-    bf16x8 h8, m8, l8;
+  for (int r = 0; r < 4; r++)
 #pragma unroll
-    for (int r = 0; r < 8; r++) {
+    for (int c = 0; c < 4; c++) {
+      const int k = ti + r, n = j0 + tj + c;
+      const int64_t e = ((((int64_t)(n >> 4) * 2 + (k >> 5)) * 3) * 64 + ((k >> 3) & 3) * 16 + (n & 15)) * 8 + (k & 7);
       __bf16 h, m, l;
       split3(acc[r][c], h, m, l);
-      h8[r] = h;
-      m8[r] = m;
-      l8[r] = l;
+      o[e] = h;
+      o[e + 64 * 8] = m;
+      o[e + 2 * 64 * 8] = l;
     }
-    *reinterpret_cast<bf16x8*>(o + e) = h8;
-    *reinterpret_cast<bf16x8*>(o + e + 64 * 8) = m8;
-    *reinterpret_cast<bf16x8*>(o + e + 2 * 64 * 8) = l8;
-  }
 }
 
 
