@@ -15,13 +15,15 @@ with small per-cloud steps between them:
      ndtnet.py:227-230), -> 512 -> 256 -> 128 -> C+1, log_softmax
 
 Every BatchNorm (running statistics) is folded into the preceding 1x1 conv /
-linear layer.  The per-point GEMMs run on the matrix cores: seven layers
+linear layer.  The per-point GEMMs run on the matrix cores: eleven layers
 (the three 128 -> 1024 / F max-pooled convs, the t2-folded conv2, the seg
-head's 64 -> 512, 512 -> 256 and 256 -> 128) as fp32-accurate split-bf16
-products (``SPLIT_BF16`` below), the rest on the fp32 MFMA.  The per-cloud
-steps (TNet FC heads, the t1 / t2 weight folds, the seg head's global-feature
-bias) are HIP kernels on the same stream (``_glue_hip``); ``_glue_torch`` is
-their torch restatement for the tests.
+head's 64 -> 512, 512 -> 256, 256 -> 128 and 128 -> C+1, and the TNets'
+64 -> 64 / 64 -> 128; ``X6_NARROW``) as fp32-accurate split-bf16 products
+(``SPLIT_BF16`` below), the K = 16 first layers on the fp32 MFMA.  The
+per-cloud steps (TNet FC heads and the seg head's global-feature bias on the
+fp32 MFMA, ``ndnet_pn_fc_mfma_run``; the t1 / t2 weight folds) are HIP
+kernels on the same stream (``_glue_hip``); ``_glue_torch`` is their torch
+restatement for the tests.
 """
 from __future__ import annotations
 
