@@ -142,6 +142,13 @@ int ndnet_ndt_set_exact_counts(void *plan, int on);
  * float input with the plan's shapes in LDS only (otherwise direct). */
 int ndnet_ndt_set_front_staged(void *plan, int on);
 
+/* Split ndnet_ndt_run in two stream-ordered calls (a caller that overlaps the
+ * run with other work on another stream, e.g. ndnet.pipeline): part 1 runs the
+ * front only (k_front: limits, bisection, dense ids, binning), part 2 the rest
+ * (k_welford_q onwards) and must follow a part-1 call of the same plan in
+ * stream order, with the same arguments.  0 (default) = the whole run. */
+int ndnet_ndt_set_run_part(void *plan, int part);
+
 /* The retained divergence list (kl_divergences, ndt.c:189-205) is read by the
  * level-1 prune only when it removes NDs.  A cloud with num_nds <= num_desired
  * keeps every ND (or fails with rc -1 before reading the list), so by default

@@ -170,6 +170,7 @@ struct Plan {
   uint64_t front_sync_ticks;  // k_front's cloud-barrier timeout (ndnet_ndt_debug_set_sync_timeout)
   int lists_built;            // the deferred lists of the last run are built (no further build launches)
   int front_staged;           // k_front's scatter through LDS records (ndnet_ndt_set_front_staged; default 1)
+  int run_part;               // ndnet_ndt_set_run_part: 0 whole run, 1 front only, 2 from k_welford_q on
 };
 
 // ------------------------------------------------------------------ helpers
@@ -2305,6 +2306,7 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
   const int B = P->B;
   const uint64_t n = P->n;
   if (lbl && P->ncls < 0) return NDNET_ERR_ARG;
+  if (P->run_part == 2) goto welford;  // the front ran in an earlier call on this stream order
   if (P->timing) HIPCHK(hipEventRecord(P->ev[0], st));
   P->lists_built = 0;
   // k_front re-arms its clouds itself (epoch, barrier words, list counters)
@@ -2368,6 +2370,12 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
                                                                P->ndcap, P->nbins);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[4], st));
   }
+  if (P->run_part == 1) {
+    HIPCHK(hipGetLastError());
+    return NDNET_OK;
+  }
+welford:
+  P->lists_built = 0;
   k_welford_q<T><<<P->wq_grid, kWqThreads, kWqRt * sizeof(double) + 4 * ((B + 1 + 3) & ~3) + (lbl ? P->wq_lds : 0),
                     st>>>(
       P->ctl, B, (const T*)P->nd_pts, lbl ? P->nd_lbl : nullptr, P->nd_n, P->nd_base, P->nd_mean, P->nd_cov,
@@ -2571,6 +2579,13 @@ int ndnet_ndt_set_front_staged(void* plan, int on) {
   Plan* P = (Plan*)plan;
   if (!P || on < 0 || on > 1) return NDNET_ERR_ARG;
   P->front_staged = on;
+  return NDNET_OK;
+}
+
+int ndnet_ndt_set_run_part(void* plan, int part) {
+  Plan* P = (Plan*)plan;
+  if (!P || part < 0 || part > 2) return NDNET_ERR_ARG;
+  P->run_part = part;
   return NDNET_OK;
 }
 

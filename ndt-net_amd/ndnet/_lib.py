@@ -68,6 +68,7 @@ EXPORTS = {
     "ndnet_ndt_get_path": (_I, [_P]),
     "ndnet_ndt_set_exact_counts": (_I, [_P, _I]),
     "ndnet_ndt_set_front_staged": (_I, [_P, _I]),
+    "ndnet_ndt_set_run_part": (_I, [_P, _I]),
     "ndnet_ndt_set_lazy_list": (_I, [_P, _I]),
     "ndnet_ndt_debug_set_sync_timeout": (_I, [_P, ctypes.c_uint64]),
     "ndnet_ndt_run": (_I, [_P, _P, _P, _P, _P, _P, _P]),

@@ -17,12 +17,21 @@ the device (k_reset / k_limits), not by host bookkeeping.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
 
 from . import _lib
 from .preprocessing.ndtnet_preprocessing import ndt_multiscale, ndt_preprocessing, get_plan
+
+
+# PipelinedSegmentation step order: "free" (default) lets the two streams run
+# unordered; "front" runs k_front alone and starts the forward behind it, the
+# rest of the NDT stage beside the forward (measured 1.5% slower: Welford and
+# the chains cannot share a CU -- 164 and 4 x 128 VGPRs per SIMD -- so the two
+# still serialise, now with k_front's full-chip phase exposed)
+FRONT_FIRST = os.environ.get("NDNET_PIPE_ORDER", "free") == "front"
 
 
 class _Pinned:
@@ -153,6 +162,7 @@ class PipelinedSegmentation:
         # the forward's launches go first; stream priorities (either way) measured
         # 35-40% slower than none, so both streams keep the default priority
         self.s_ndt, self.s_fwd = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+        self.front_done = torch.cuda.Event()
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.no_grad(), torch.cuda.stream(side):
@@ -172,11 +182,26 @@ class PipelinedSegmentation:
         cur = torch.cuda.current_stream(self.device)
         self.s_ndt.wait_stream(cur)
         self.s_fwd.wait_stream(cur)
-        with torch.cuda.stream(self.s_fwd):
-            prev = self.rows[1 - j]
-            out = self.model(prev[..., :3], prev[..., 3:])
-        with torch.cuda.stream(self.s_ndt):
-            self.plan.run(self.inputs[j], None, self.rows[j], None)
+        if FRONT_FIRST:
+            # k_front needs every CU at once (its workgroups meet at cloud
+            # barriers), so it runs alone; the forward starts behind it and the
+            # rest of the NDT stage (Welford, KL: persistent / few-workgroup
+            # kernels) fills the forward's gaps
+            with torch.cuda.stream(self.s_ndt):
+                self.plan.run(self.inputs[j], None, self.rows[j], None, part=1)
+                self.front_done.record(self.s_ndt)
+            self.s_fwd.wait_event(self.front_done)
+            with torch.cuda.stream(self.s_fwd):
+                prev = self.rows[1 - j]
+                out = self.model(prev[..., :3], prev[..., 3:])
+            with torch.cuda.stream(self.s_ndt):
+                self.plan.run(self.inputs[j], None, self.rows[j], None, part=2)
+        else:
+            with torch.cuda.stream(self.s_fwd):
+                prev = self.rows[1 - j]
+                out = self.model(prev[..., :3], prev[..., 3:])
+            with torch.cuda.stream(self.s_ndt):
+                self.plan.run(self.inputs[j], None, self.rows[j], None)
         cur.wait_stream(self.s_ndt)
         cur.wait_stream(self.s_fwd)
         return out

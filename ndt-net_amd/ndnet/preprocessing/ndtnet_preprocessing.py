@@ -47,16 +47,22 @@ class NdtPlan:
             self.handle = None
 
     def run(self, points: torch.Tensor, labels: Optional[torch.Tensor], out: torch.Tensor,
-            out_classes: Optional[torch.Tensor]) -> None:
+            out_classes: Optional[torch.Tensor], part: int = 0) -> None:
+        """part: 0 the whole run; 1 the front only (k_front); 2 the rest, after a
+        part-1 call with the same arguments in stream order
+        (include/ndnet_amd.h ndnet_ndt_set_run_part)."""
         assert points.is_contiguous() and points.dtype == torch.float32 and points.device == self.device
         assert out.is_contiguous() and out.shape == (self.batch, self.num_nds, 12)
         st = _lib.stream_ptr(self.device)
+        _lib.check(_lib.lib().ndnet_ndt_set_run_part(self.handle, int(part)), "ndnet_ndt_set_run_part")
         rc = _lib.lib().ndnet_ndt_run(
             self.handle, st, points.data_ptr(),
             labels.data_ptr() if labels is not None else None,
             out.data_ptr(),
             out_classes.data_ptr() if out_classes is not None else None,
             self.stats.data_ptr())
+        if part:
+            _lib.lib().ndnet_ndt_set_run_part(self.handle, 0)
         _lib.check(rc, "ndnet_ndt_run")
 
     def set_path(self, path: int) -> None:
