@@ -514,3 +514,22 @@ def test_front_staged_scatter_equals_direct(case):
         assert bytes(s1[b]) == bytes(s0[b]), f"cloud {b} stats"
         for key in d1[b]:
             assert np.array_equal(d1[b][key], d0[b][key], equal_nan=True), (b, key)
+
+
+def test_run_parts_equal_whole_run():
+    """ndnet_ndt_set_run_part: the front (part 1) and the rest (part 2) as two
+    stream-ordered calls give the rows and stats of one whole run."""
+    import torch
+    from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
+    from ndnet.synthetic import make_batch
+    pts = torch.from_numpy(make_batch("L", 4, 40_000, seed0=41)).cuda()
+    res = []
+    for parts in ((0,), (1, 2)):
+        plan = NdtPlan(4, 40_000, 500, -1)
+        out = torch.empty((4, 500, 12), dtype=torch.float32, device="cuda")
+        for part in parts:
+            plan.run(pts, None, out, None, part=part)
+        torch.cuda.synchronize()
+        res.append((out.cpu().numpy(), [bytes(s) for s in plan.host_stats()]))
+    assert np.array_equal(res[0][0], res[1][0])
+    assert res[0][1] == res[1][1]
