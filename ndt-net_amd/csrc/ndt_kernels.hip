@@ -165,7 +165,7 @@ struct Plan {
   int exact_counts;           // k_front counts every bisection grid (ndnet_ndt_set_exact_counts)
   size_t wq_lds;              // k_welford_q dynamic LDS (labelled runs: class histograms)
   uint32_t wq_grid;           // k_welford_q workgroups: one per CU
-  uint32_t* wq_ctr;           // [2] k_welford_q dynamic item counter (re-armed by k_kl_rank_chunks)
+  uint32_t* wq_ctr;           // [8][16] k_welford_q dynamic item counters, one per XCD (re-armed by k_kl_rank_chunks)
   int eager_list;             // build every cloud's retained list in the run (ndnet_ndt_set_lazy_list(plan, 0))
   uint64_t front_sync_ticks;  // k_front's cloud-barrier timeout (ndnet_ndt_debug_set_sync_timeout)
   int lists_built;            // the deferred lists of the last run are built (no further build launches)
@@ -933,12 +933,23 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
   // increments it while items remain (one contended word takes ~11 ns per
   // atomic: a thousand waves each adding would cost ~10 us).  k_kl_rank_chunks,
   // the next kernel on the stream, re-arms it.
+  // The dynamic items are sharded over one counter per XCD (workgroups are
+  // dealt round-robin to the 8 XCDs, so blockIdx % 8 is the XCD): XCD x takes
+  // items nwaves + 8 c + x.  One shared word saturates at ~88 dequeues / us
+  // (MI355X_MICROARCH.md, dequeue), and when every wave finishes a uniform
+  // first round together (C5's 2000-ND level: 2400 items on 1024 waves) the
+  // ~1400 dequeues on it took ~15 us.
   const uint32_t nwaves = gridDim.x * (kWqThreads / 64);
+  const uint32_t nx = gridDim.x < 8u ? gridDim.x : 8u, xs = blockIdx.x % nx;
+  uint32_t* const ctr = wq_ctr + 16u * xs;  // one 64-byte line per shard
   auto next_item = [&]() -> uint32_t {
     uint32_t v = total;
     if (lane == 0) {
-      const uint32_t seen = __hip_atomic_load(wq_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (nwaves + seen < total) v = nwaves + __hip_atomic_fetch_add(wq_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t seen = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (nwaves + nx * seen + xs < total) {
+        const uint32_t it = nwaves + nx * __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + xs;
+        v = it < total ? it : total;
+      }
     }
     return __builtin_amdgcn_readfirstlane(v);
   };
@@ -1196,13 +1207,19 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
       const uint64_t ob = (uint64_t)b * ndcap, u = o - ob;
       double* chain = CA.chain + ob * 108 + u;
       uint32_t* ps = CA.chain_ps + ob * 12 + u;
+#ifdef NDNET_WQ_NOCHAIN  // timing experiment only (wrong results): no LU chain
+      for (int t = 0; t < 0; t++) {
+#else
       for (int t = 0; t < nT; t++) {
+#endif
         uint32_t perm;
         int sg;
         lu3(S, perm, sg);
+#ifndef NDNET_WQ_NOCHAINSTORE  // timing experiment only (wrong results): LU chain without its stores
 #pragma unroll
         for (int q = 0; q < 9; q++) chain[(uint64_t)(9 * t + q) * ndcap] = S[q];
         ps[(uint64_t)t * ndcap] = perm | (sg < 0 ? 0x100u : 0u);
+#endif
       }
 #pragma unroll
       for (int q = 0; q < 9; q++) CA.cov_post[9 * o + q] = S[q];
@@ -1687,7 +1704,7 @@ __device__ inline unsigned long long score_key(double v) { return ~ord_key(v + 0
 
 // A lazy run only flags the events of a deferred cloud (kl_list_deferrable).
 __global__ void __launch_bounds__(kChunk) k_kl_rank_chunks(KLArgs A) {
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *A.wq_ctr = 0u;  // k_welford_q has finished
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 8) A.wq_ctr[16 * threadIdx.x] = 0u;  // k_welford_q has finished
   const int b = blockIdx.y;
   const CloudCtl& c = A.ctl[b];
   if (c.state != kAccepted) return;
@@ -2477,7 +2494,7 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   A_(chunk_cnt, B * P->nchunk);
   A_(chunk_min, B * P->nchunk);
   A_(d_stats, B);
-  A_(wq_ctr, 2);
+  A_(wq_ctr, 128);
   // k_front: G workgroups per cloud, all resident together (G * B <= CUs);
   // each owns bpw bins, whose per-ND counts and ranks live in its LDS
   {
@@ -2523,14 +2540,19 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   if (e == hipSuccess) e = hipMemset(P->fbar, 0, B * kBarStride * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(P->stamps, 0, B * P->vcap * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(P->d_stats, 0, B * sizeof(ndnet_ndt_stats));
-  if (e == hipSuccess) e = hipMemset(P->wq_ctr, 0, 2 * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemset(P->wq_ctr, 0, 128 * sizeof(uint32_t));
   {
     const size_t hb = (size_t)kWqNDs * (size_t)nb * sizeof(uint32_t);
     P->wq_lds = num_classes >= 0 && hb <= (size_t)kWqHistMax ? hb : 0;
     int dv = 0, ncu = 0;
     if (e == hipSuccess) e = hipGetDevice(&dv);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dv);
-    P->wq_grid = ncu > 0 ? (uint32_t)ncu : 1u;
+#ifndef NDNET_WQ_WPC
+#define NDNET_WQ_WPC 2
+#endif
+    // NDNET_WQ_WPC workgroups per CU: a wave's Welford is a dependent FP64
+    // chain, so a second wave on each SIMD runs beside it instead of after it
+    P->wq_grid = ncu > 0 ? (uint32_t)ncu * NDNET_WQ_WPC : 1u;
   }
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_welford_q<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
