@@ -473,7 +473,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
     if (t < (uint32_t)kWorkers) s_bad[t] = kInvalid;
     __syncthreads();
 #ifndef NDNET_FRONT_BINMARKS
-    if (s.iter == 1) FRONT_MARK(27);
+    if (s.npass == 0) FRONT_MARK(27);
 #endif
     const double vs = s.guess, inv_vs = 1.0 / vs;
     double off[3] = {s.off[0], s.off[1], s.off[2]};
@@ -542,7 +542,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
     }
     __syncthreads();
 #ifndef NDNET_FRONT_BINMARKS
-    if (s.iter == 1) FRONT_MARK(28);
+    if (s.npass == 0) FRONT_MARK(28);
 #endif
     if (small) {  // byte map -> 32-voxel words, OR'd into the pass's global bitmap
       for (uint32_t w = t; w < words; w += kFrontThreads) {
@@ -560,11 +560,11 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
       for (uint32_t w = g * kFrontThreads + t; w < (uint32_t)kBitsWords; w += G * kFrontThreads) st_sc1(gn + w, 0u);
     }
 #ifndef NDNET_FRONT_BINMARKS
-    if (s.iter == 1) FRONT_MARK(29);
+    if (s.npass == 0) FRONT_MARK(29);
 #endif
     fresh = block_sum_u32(fresh, scratch);
 #ifndef NDNET_FRONT_BINMARKS
-    if (s.iter == 1) FRONT_MARK(30);
+    if (s.npass == 0) FRONT_MARK(30);
 #endif
     uint32_t* rec = A.rec + (((uint64_t)b * kFrontPhases + 1 + 2 * s.iter) * G) * kRecWords;
     uint32_t anyb = 0;
@@ -580,7 +580,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
     if (t < (uint32_t)kWorkers) s.cut[t] = kInvalid;
     __syncthreads();
 #ifndef NDNET_FRONT_BINMARKS
-    if (s.iter == 1) FRONT_MARK(31);
+    if (s.npass == 0) FRONT_MARK(31);
 #endif
     uint32_t mode = small ? parity : 2u;
     if (s.anybad) {
@@ -932,7 +932,14 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
         float3* o3 = reinterpret_cast<float3*>(out);
         for (uint32_t l = t; l < lcarry; l += kFrontThreads) {
           const float4 r = rec[l];
+#ifdef NDNET_FRONT_STAGED_NT  // A/B: streaming (nontemporal) stores
+          float* o = reinterpret_cast<float*>(o3 + __float_as_uint(r.w));
+          __builtin_nontemporal_store(r.x, o);
+          __builtin_nontemporal_store(r.y, o + 1);
+          __builtin_nontemporal_store(r.z, o + 2);
+#else
           o3[__float_as_uint(r.w)] = make_float3(r.x, r.y, r.z);
+#endif
         }
       }
     }
