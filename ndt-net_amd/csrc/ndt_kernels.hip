@@ -2548,10 +2548,11 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
     if (e == hipSuccess) e = hipGetDevice(&dv);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dv);
 #ifndef NDNET_WQ_WPC
-#define NDNET_WQ_WPC 2
+#define NDNET_WQ_WPC 1
 #endif
-    // NDNET_WQ_WPC workgroups per CU: a wave's Welford is a dependent FP64
-    // chain, so a second wave on each SIMD runs beside it instead of after it
+    // NDNET_WQ_WPC workgroups per CU (1, 2 and 3 measured equal on C2 and C5:
+    // profiles/r02c_welford_parts.txt -- the kernel is issue-bound, not
+    // latency-bound, so a second wave per SIMD shares the same issue slots)
     P->wq_grid = ncu > 0 ? (uint32_t)ncu * NDNET_WQ_WPC : 1u;
   }
   if (e == hipSuccess)
