@@ -68,6 +68,17 @@ typedef struct ndnet_pn_chain {
   float* out;             // mode 1
   float* clear;           // optional: set clear[0 .. clear_count) to -inf once the chain no longer
   int64_t clear_count;    // reads it (re-arms a max-pool buffer for the next forward), or NULL
+  // optional prologue (head_h2 != NULL; chain B): the TNet(3) tail of ndnet_pn_head3_run computed by
+  // every workgroup of a cloud before layer 0, which reads its result -- t1[b] = h2[b] @ W3^T + b3 (9
+  // outputs, the identity folded into b3) and conv1 with t1 folded, written fragment-major (K padded to
+  // 16) to L[0].w + b * L[0].w_cloud_stride (every workgroup writes the same bits); t1 to head_t1[b]
+  const float* head_h2;   // [B][head_ld]
+  int32_t head_ld, head_K;
+  const float* head_w3;   // [9][head_K]
+  const float* head_b3;   // [9]
+  const float* head_basis;  // [9][head_kin * head_nout]
+  int32_t head_kin, head_nout;
+  float* head_t1;         // [B][9]
 } ndnet_pn_chain;
 
 /* Runs one chain over `batch` clouds on `stream` (a hipStream_t; NULL = default

@@ -686,6 +686,60 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
   const int reg[2] = {0, region_floats(A.max_width, planes & 1)};
   // fbuf (the fused pair's chunks): float offset chosen by the launcher
   // input tile, zero-filled to the first layer's K (a multiple of 16)
+  if (A.head_h2) {
+    // TNet(3)'s tail for this cloud (ndnet_pn_head3_run's work, ndtnet.py:57-60):
+    // t1 = h2 @ W3^T + b3, then conv1 with t1 folded into layer 0's weights
+    float* const s_t1 = g_smem;  // [9]: the dynamic LDS is free until the input tile (no static LDS:
+                                 // a chain may use all 160 KB dynamically)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int M = A.head_kin * A.head_nout, total = 16 * A.head_nout;  // one k-group, K padded to 16
+    // this thread's fold element(s): basis values loaded ahead of the fc3 reduction
+    const int e0 = threadIdx.x;
+    const int cb0 = e0 >> 8, ln0 = (e0 >> 2) & 63, k0 = 4 * (ln0 >> 4) + (e0 & 3), n0 = 16 * cb0 + (ln0 & 15);
+    float bas[9];
+#pragma unroll
+    for (int a = 0; a < 9; a++) bas[a] = (e0 < total && k0 < A.head_kin) ? A.head_basis[a * M + k0 * A.head_nout + n0] : 0.0f;
+    const float* h = A.head_h2 + (int64_t)b * A.head_ld;
+    for (int o = wave; o < 9; o += kWaves) {  // one wave per output, lanes split K
+      float acc = 0.0f;
+      const float* wr = A.head_w3 + (int64_t)o * A.head_K;
+      if (A.head_K == 256) {  // one float4 of h and of the row per lane: one load round trip
+        const f32x4 hv = reinterpret_cast<const f32x4*>(h)[lane];
+        const f32x4 wv = reinterpret_cast<const f32x4*>(wr)[lane];
+        acc = (hv[0] * wv[0] + hv[1] * wv[1]) + (hv[2] * wv[2] + hv[3] * wv[3]);
+      } else {
+        for (int k = lane; k < A.head_K; k += 64) acc += h[k] * wr[k];
+      }
+      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+      if (lane == 0) {
+        s_t1[o] = acc + A.head_b3[o];
+        if (blockIdx.x == 0) A.head_t1[b * 9 + o] = acc + A.head_b3[o];
+      }
+    }
+    __syncthreads();
+    float* w1 = const_cast<float*>(A.L[0].w) + (int64_t)b * A.L[0].w_cloud_stride;
+    if (e0 < total) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int a = 0; a < 9; a++) acc += s_t1[a] * bas[a];
+      w1[e0] = acc;
+    }
+    for (int e = e0 + kThreads; e < total; e += kThreads) {
+      const int cb = e >> 8, ln = (e >> 2) & 63, k = 4 * (ln >> 4) + (e & 3), n = 16 * cb + (ln & 15);
+      float acc = 0.0f;
+      if (k < A.head_kin) {
+#pragma unroll
+        for (int a = 0; a < 9; a++) acc += s_t1[a] * A.head_basis[a * M + k * A.head_nout + n];
+      }
+      w1[e] = acc;
+    }
+    // layer 0 reads these weights back: __syncthreads' workgroup-scope release
+    // / acquire orders this workgroup's stores before its loads (same CU; no
+    // lines of them are cached here yet).  Every workgroup of the cloud stores
+    // the same bits.  (A device-scope __threadfence here writes back the L2:
+    // measured +60 us per launch.)
+    __syncthreads();
+  }
   const int K0 = A.L[0].K;
   for (int e = threadIdx.x; e < kP * K0; e += kThreads) {
     const int r = e / K0, c = e % K0;

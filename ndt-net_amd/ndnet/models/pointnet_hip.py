@@ -87,7 +87,10 @@ class _Chain(ctypes.Structure):
                 ("num_points", ctypes.c_int32), ("num_layers", ctypes.c_int32), ("L", _Layer * MAX_LAYERS),
                 ("mode", ctypes.c_int32), ("out_cols", ctypes.c_int32), ("gmax", ctypes.c_void_p),
                 ("gmax_ld", ctypes.c_int32), ("max_width", ctypes.c_int32), ("max_width2", ctypes.c_int32),
-                ("out", ctypes.c_void_p), ("clear", ctypes.c_void_p), ("clear_count", ctypes.c_int64)]
+                ("out", ctypes.c_void_p), ("clear", ctypes.c_void_p), ("clear_count", ctypes.c_int64),
+                ("head_h2", ctypes.c_void_p), ("head_ld", ctypes.c_int32), ("head_K", ctypes.c_int32),
+                ("head_w3", ctypes.c_void_p), ("head_b3", ctypes.c_void_p), ("head_basis", ctypes.c_void_p),
+                ("head_kin", ctypes.c_int32), ("head_nout", ctypes.c_int32), ("head_t1", ctypes.c_void_p)]
 
 
 
@@ -320,6 +323,7 @@ class _Workspace:
     an eval forward does no allocation but its output and no struct building."""
 
     def __init__(self, W: _Folded, B: int, N: int, dev) -> None:
+        self.W = W
         f32 = dict(dtype=torch.float32, device=dev)
         Fp = W.C_tail[0].shape[1]
         # the three max-pooled vectors, -inf before the atomic maxima (ReLU'd maxima are >= 0)
@@ -393,6 +397,12 @@ class _Workspace:
             # the last chain re-arms the max-pool buffer (-inf) for the next forward
             self.structs[3].clear = self.gbuf.data_ptr()
             self.structs[3].clear_count = self.gbuf.numel()
+            if HEAD3_IN_CHAIN:  # chain B computes t1 and its conv1 weights itself
+                W, cb = self.W, self.structs[1]
+                cb.head_h2, cb.head_ld, cb.head_K = self.h2.data_ptr(), self.h2.stride(0), self.h2.shape[1]
+                cb.head_w3, cb.head_b3 = W.t1["f3"].data_ptr(), W.t1["c3"].data_ptr()
+                cb.head_basis, cb.head_kin, cb.head_nout = W.t1_basis.data_ptr(), 12, 64
+                cb.head_t1 = self.t1.data_ptr()
         if chain_timing is not None:  # torch events on the launch stream (bench.py)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -414,6 +424,11 @@ def _folded(model):
         cache.update(sig=sig, W=_Folded(model), ws={})
     return cache
 
+
+# TNet(3)'s tail (fc3 + the t1 fold of conv1): "chain" (default) computes it in
+# chain B's prologue, per workgroup (ndnet_pn_chain.head_*: one launch and one
+# boundary fewer); "kernel" runs ndnet_pn_head3_run before chain B
+HEAD3_IN_CHAIN = os.environ.get("NDNET_PN_HEAD3", "chain") == "chain"
 
 # TNet / seg-bias FC layers: "mfma" (default: ndnet_pn_fc_mfma_run, 16-row
 # fp32-MFMA GEMM over fragment-major weights) or "gemv" (ndnet_pn_fc_run,
@@ -452,6 +467,8 @@ def _glue_hip(W, ws, B: int):
         t = W.t1
         fc(ws.g1, t["f1"], t["c1"], ws.h1, True)
         fc(ws.h1, t["f2"], t["c2"], ws.h2, True)
+        if HEAD3_IN_CHAIN:  # fc3 and the t1 fold run in chain B's prologue
+            return
         for c0 in range(0, B, 16):
             n = min(16, B - c0)
             rc = _lib.lib().ndnet_pn_head3_run(ws.h2[c0].data_ptr(), ws.h2.stride(0), t["f3"].data_ptr(),
