@@ -1348,6 +1348,7 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
   uint32_t* first;
   uint32_t* tmp;
   const uint32_t* op;
+  uint32_t* s_op = nullptr;  // kLds: the list's p column in LDS
   uint8_t* alive;
   const uint32_t nv0 = c.num_valid, nkl0 = c.num_kl;
   const uint32_t off = c.list_off, nphys = c.num_phys;
@@ -1358,12 +1359,9 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
   if constexpr (kLds) {
     first = kl_smem;                                       // [ndcap]
     tmp = kl_smem + A.ndcap;                               // [ecap]
-    uint32_t* s_op = kl_smem + A.ndcap + A.ecap;           // [ecap]
+    s_op = kl_smem + A.ndcap + A.ecap;                     // [ecap]
     alive = (uint8_t*)(kl_smem + A.ndcap + 2 * A.ecap);    // [ndcap]
-    // logical entry i is physical entry off + i; past the entries ever
-    // written it is poison (the reference's uninitialised tail)
-    if (walk)
-      for (uint32_t i = threadIdx.x; i < nkl0; i += blockDim.x) s_op[i] = i + off < nphys ? g_op[i + off] : kInvalid;
+    // (the list's p column is staged block by block by the walk below)
     if (!identity)
       for (uint32_t u = threadIdx.x; u < nd; u += blockDim.x) alive[u] = g_alive[u];
     op = s_op;
@@ -1388,23 +1386,37 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
     for (uint32_t u = threadIdx.x; u < nd; u += blockDim.x) first[u] = kInvalid;
     if (threadIdx.x == 0) { s_failc = kInvalid; s_kpos = kInvalid; s_poison = kInvalid; }
     __syncthreads();
-    // first occurrence of each live p (entries of dead p are skipped by the walk)
-    for (uint32_t i = threadIdx.x; i < nkl0; i += blockDim.x) {
-      const uint32_t pp = op[i];
-      if (pp == kInvalid) { atomicMin(&s_poison, i); continue; }
-      if (alive[pp]) atomicMin(&first[pp], i);
-    }
-    __syncthreads();
-    KL_MARK(6);
-    // walk order: the c-th first (1-based) at position f_c is killed iff
-    // f_c < nkl0 - (c-1) for it and for every earlier first.
+    // The walk, a block of the list at a time from the front: first
+    // occurrences of the live p within the prefix so far (entries of dead p
+    // are skipped by the walk), then their count (the c-th first, 1-based, at
+    // position f_c is killed iff f_c < nkl0 - (c-1) for it and every earlier
+    // first).  It stops at the block holding the to_remove-th first
+    // occurrence: the rest of the list cannot change the kills (a C5 level
+    // removes ~200 NDs, found in the first of two 8192-entry blocks).
     uint32_t carry = 0;
-    constexpr int IT = 8;
-    for (uint32_t base = 0; base < nkl0; base += blockDim.x * IT) {
-      const uint32_t i0 = base + threadIdx.x * IT;
-      uint32_t isf[IT];
+    KL_MARK(6);
+    // one block of ITB entries per thread: returns whether the
+    // to_remove-th first occurrence has been reached
+    auto walk_block = [&](auto itc, uint32_t base) -> bool {
+      constexpr int ITB = decltype(itc)::value;
+      const uint32_t bend = base + blockDim.x * ITB < nkl0 ? base + blockDim.x * ITB : nkl0;
+      if constexpr (kLds) {
+        // logical entry i is physical entry off + i; past the entries ever
+        // written it is poison (the reference's uninitialised tail)
+        for (uint32_t i = base + threadIdx.x; i < bend; i += blockDim.x)
+          s_op[i] = i + off < nphys ? g_op[i + off] : kInvalid;
+        __syncthreads();
+      }
+      for (uint32_t i = base + threadIdx.x; i < bend; i += blockDim.x) {
+        const uint32_t pp = op[i];
+        if (pp == kInvalid) { atomicMin(&s_poison, i); continue; }
+        if (alive[pp]) atomicMin(&first[pp], i);
+      }
+      __syncthreads();
+      const uint32_t i0 = base + threadIdx.x * ITB;
+      uint32_t isf[ITB];
 #pragma unroll
-      for (int j = 0; j < IT; j++) {
+      for (int j = 0; j < ITB; j++) {
         const uint32_t i = i0 + j;
         isf[j] = 0;
         if (i < nkl0) {
@@ -1412,13 +1424,13 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
           isf[j] = (pp != kInvalid && alive[pp] && first[pp] == i);
         }
       }
-      uint32_t pre[IT];
+      uint32_t pre[ITB];
 #pragma unroll
-      for (int j = 0; j < IT; j++) pre[j] = isf[j];
+      for (int j = 0; j < ITB; j++) pre[j] = isf[j];
       uint32_t tot;
       block_scan_items(pre, 0u, AddU32(), scratch, tot);
 #pragma unroll
-      for (int j = 0; j < IT; j++) {
+      for (int j = 0; j < ITB; j++) {
         const uint32_t i = i0 + j;
         if (i >= nkl0) continue;
         if (isf[j]) {
@@ -1431,8 +1443,14 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
         }
       }
       carry += tot;
-    }
-    __syncthreads();
+      __syncthreads();
+      return carry >= to_remove;  // uniform: carry is the block's total
+    };
+    // a first block of one entry per thread (the kills usually end there:
+    // ~120 of ~1120 NDs at C2-L, ~200 of ~2200 at C5), then 8 per thread
+    if (!walk_block(std::integral_constant<int, 1>{}, 0u))
+      for (uint32_t base = blockDim.x; base < nkl0; base += blockDim.x * 8)
+        if (walk_block(std::integral_constant<int, 8>{}, base)) break;
     KL_MARK(7);
     const uint32_t F = carry;
     uint32_t failc = s_failc;
