@@ -1926,11 +1926,18 @@ __device__ inline uint32_t count_composite(KP K, SP S, uint32_t n, unsigned long
 #endif
 constexpr int kMergeQ = NDNET_MERGE_Q;  // other runs searched together per probe round
 constexpr int kMergeRuns = 2;  // chunks merged per k_kl_merge workgroup (512 threads; ~one workgroup per CU at B = 16)
+// mode 1 (score runs staged whole per workgroup, 144 KB: one workgroup per
+// CU) merges 4 chunks per workgroup: C5's 57-chunk clouds then fit one round
+// of workgroups on the chip instead of two, and stage the runs half as often
+#ifndef NDNET_MERGE_RUNS1
+#define NDNET_MERGE_RUNS1 4
+#endif
+constexpr int kMergeRuns1 = NDNET_MERGE_RUNS1;
 
 // kMode 2: score runs and NaN keys in LDS, the NaN keys computed here (up to
 // kMergeLdsChunks chunks); 1: score runs in LDS, NaN keys from k_kl_nan_keys
 // (up to kMergeScoreChunks); 0: everything from global memory.
-template <int kMode>
+template <int kMode, int kMergeRuns = ::kMergeRuns>
 __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
   constexpr bool kLds = kMode == 2;
   const int b = blockIdx.y;
@@ -2313,7 +2320,8 @@ static void launch_list_sort(Plan* P, const KLArgs& A, hipStream_t st) {
     KLArgs A1 = A;
     const size_t keys = kMergeScoreChunks * kChunk;  // the launch's dynamic LDS, in 64-bit keys (144 KB)
     A1.merge_lds_keys = (uint32_t)keys;
-    k_kl_merge<1><<<dim3(mg, B), kChunk * kMergeRuns, keys * sizeof(unsigned long long), st>>>(A1);
+    const uint32_t mg1 = (P->nchunk + kMergeRuns1 - 1) / kMergeRuns1;
+    k_kl_merge<1, kMergeRuns1><<<dim3(mg1, B), kChunk * kMergeRuns1, keys * sizeof(unsigned long long), st>>>(A1);
   } else {
     k_kl_nan_keys<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
     k_kl_merge<0><<<dim3(mg, B), kChunk * kMergeRuns, 0, st>>>(A);
@@ -2583,7 +2591,7 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
     e = hipFuncSetAttribute((const void*)k_kl_merge<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(2 * kMergeLdsChunks * kChunk * sizeof(unsigned long long)));
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_kl_merge<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    e = hipFuncSetAttribute((const void*)k_kl_merge<1, kMergeRuns1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(kMergeScoreChunks * kChunk * sizeof(unsigned long long)));
   if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_kl, hipFuncAttributeMaxDynamicSharedMemorySize, kKLLdsMax);
   if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_prune, hipFuncAttributeMaxDynamicSharedMemorySize, kKLLdsMax);
