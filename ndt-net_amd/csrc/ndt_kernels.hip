@@ -1736,7 +1736,11 @@ __global__ void __launch_bounds__(kChunk) k_kl_rank_chunks(KLArgs A) {
   const bool deferred = kl_list_deferrable(A, c);
   uint32_t fl = 0;
   double vl = 0.0;
+#ifdef NDNET_RANK_NOSCORE  // timing experiment only (wrong results): flags without the KL scores
+  kl_event(A, b, sl < nslots ? sl : 0u, false, fl, vl);
+#else
   kl_event(A, b, sl < nslots ? sl : 0u, !deferred, fl, vl);  // the clamped slot's result is dropped
+#endif
   if (deferred) {  // count the cloud's events (stats num_events / num_kl), one atomic per wave
     const unsigned long long bal = __ballot(sl < nslots && fl);
     if ((t & 63) == 0 && bal)
