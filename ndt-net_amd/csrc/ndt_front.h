@@ -410,38 +410,39 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
 
   // ---- bisection passes ----
   for (;;) {
-    // grid of this guess (voxel.c:61-81), identical in every workgroup
+    // grid of this guess (voxel.c:61-81), identical in every workgroup.
+    // Thread 0 runs the passes a grid too small to count decides (hi = guess)
+    // back to back, without a workgroup barrier per pass; after each such
+    // pass the next guess's grid is computed, also when the pass ended the
+    // search (as the reference's loop would before it exits).
     if (t == 0) {
-      uint64_t V = 1;
-      for (int a = 0; a < 3; a++) {
-        const double d = s.lim[a] - s.lim[3 + a];
-        const double q = ceil(d / s.guess);
-        int li;
-        if (q >= -2147483648.0 && q < 2147483648.0) li = (int)q;
-        else li = (int)0x80000000;  // x86 cvttsd2si overflow value
-        s.len[a] = (uint32_t)li;
-        s.off[a] = s.lim[3 + a];
-        V *= (uint64_t)s.len[a];
-      }
-      s.V = V;
-      s.stamp = epoch * 32u + s.iter;
-      // A grid of fewer voxels than k (or than the n8 estimated points)
-      // cannot hold k occupied voxels: ndt.c:176-179 takes hi = guess
-      // whatever the count, so the pass is not run (eval_all: it is, for the
-      // parity tests that compare every count with the reference's).
-      const uint64_t bound = V < n8 ? V : n8;
-      s.skip = !A.eval_all && bound < A.k;
-      if (V > A.vcap) {  // the reference's malloc of V NDs would be the failure point
-        s.state = kFailed;
-        s.rc = -1;
-        s.vs = s.guess;
-        s.skip = 0;
-      }
-    }
-    __syncthreads();
-    if (s.state != kSearching) break;
-    if (s.skip) {
-      if (t == 0) {
+      for (;;) {
+        uint64_t V = 1;
+        for (int a = 0; a < 3; a++) {
+          const double d = s.lim[a] - s.lim[3 + a];
+          const double q = ceil(d / s.guess);
+          int li;
+          if (q >= -2147483648.0 && q < 2147483648.0) li = (int)q;
+          else li = (int)0x80000000;  // x86 cvttsd2si overflow value
+          s.len[a] = (uint32_t)li;
+          s.off[a] = s.lim[3 + a];
+          V *= (uint64_t)s.len[a];
+        }
+        s.V = V;
+        s.stamp = epoch * 32u + s.iter;
+        // A grid of fewer voxels than k (or than the n8 estimated points)
+        // cannot hold k occupied voxels: ndt.c:176-179 takes hi = guess
+        // whatever the count, so the pass is not run (eval_all: it is, for the
+        // parity tests that compare every count with the reference's).
+        const uint64_t bound = V < n8 ? V : n8;
+        s.skip = !A.eval_all && bound < A.k;
+        if (V > A.vcap) {  // the reference's malloc of V NDs would be the failure point
+          s.state = kFailed;
+          s.rc = -1;
+          s.vs = s.guess;
+          s.skip = 0;
+        }
+        if (s.state != kSearching || !s.skip) break;
         if (g == 0 && s.iter < 16) {
           c.guesses[s.iter] = s.guess;
           c.counts[s.iter] = kInvalid;  // not counted (< k)
@@ -456,9 +457,9 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
           s.vs = gn;
         }
       }
-      __syncthreads();
-      continue;
     }
+    __syncthreads();
+    if (s.state != kSearching) break;
     const uint64_t V = s.V;
     const bool small = V <= (uint64_t)kBitsCap;
     const uint32_t words = small ? (uint32_t)((V + 31) / 32) : 0u;
