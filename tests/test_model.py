@@ -189,3 +189,39 @@ def test_split_bf16_layers_are_fp32_accurate():
     e_t32 = (out_t32 - ref64).abs().max().item()
     print(f"max |err| vs fp64: x6 {e_x6:.3e}, fp32 MFMA {e_32:.3e}, torch fp32 {e_t32:.3e}")
     assert e_x6 <= 2.0 * max(e_32, e_t32) + 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,K,N,relu", [(16, 1024, 512, True), (5, 768, 512, False), (3, 256, 4096, False)])
+def test_fc_mfma_matches_torch(B, K, N, relu):
+    """ndnet_pn_fc_mfma_run (16-row fp32-MFMA GEMM over fragment-major W^T)
+    against torch fp32 addmm, row stride past K (the max-pool buffer's)."""
+    from ndnet.models import pointnet_hip as ph
+    g = torch.Generator().manual_seed(B * K + N)
+    xfull = torch.randn(B, K + 64, generator=g).cuda()
+    x = xfull[:, :K]
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).cuda()
+    b = torch.randn(N, generator=g).cuda()
+    out = torch.empty(B, N, device="cuda")
+    ph._fc(x, w, b, out, relu, ph._frag(w.t().contiguous()))
+    ref = torch.addmm(b, x, w.t())
+    if relu:
+        ref = ref.relu()
+    torch.cuda.synchronize()
+    assert (out - ref).abs().max().item() < 1e-5
+
+
+@pytest.mark.gpu
+def test_head3_in_chain_equals_head3_kernel(monkeypatch):
+    """TNet(3)'s fc3 + t1 fold in chain B's prologue (default) against the
+    separate k_pn_head3 launch: same log-probs within fp32 reduction order."""
+    from ndnet.models import pointnet_hip as ph
+    torch.manual_seed(7)
+    pts, cov = torch.randn(4, 300, 3).cuda(), torch.randn(4, 300, 9).cuda() * 0.1
+    outs = []
+    for flag in (True, False):
+        monkeypatch.setattr(ph, "HEAD3_IN_CHAIN", flag)
+        m = _model(768, 28, "cuda")
+        with torch.no_grad():
+            outs.append(m(pts, cov))
+    assert (outs[0] - outs[1]).abs().max().item() < 1e-5
