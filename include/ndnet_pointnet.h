@@ -86,6 +86,10 @@ typedef struct ndnet_pn_chain {
  * (layer sizes, LDS region widths) or NDNET_ERR_HIP (-21) on a launch failure.
  * No allocation, no synchronisation: graph-capturable. */
 int ndnet_pn_chain_run(const ndnet_pn_chain *args, int batch, void *stream);
+/* The same chain on 32-point tiles (8 waves per workgroup; same arguments,
+ * results within fp32 summation order): for batches whose 64-point tiles
+ * would leave CUs idle, e.g. 16 clouds of 500 points. */
+int ndnet_pn_chain_run_t32(const ndnet_pn_chain *args, int batch, void *stream);
 
 /* The per-cloud steps between the chains (TNet FC heads ndtnet.py:53-60 and
  * the weight folds of pointnet_hip.py), for batch <= 16 clouds:

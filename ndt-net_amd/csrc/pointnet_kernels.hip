@@ -36,13 +36,22 @@
 
 namespace {
 
-constexpr int kP = 64;          // points per workgroup
+// Tile size: 64 points (16 waves), or 32 points (8 waves) in the second build
+// of this file (-DNDNET_PN_TILE=32: pointnet_chain_t32.o, entry point
+// ndnet_pn_chain_run_t32) for batches whose 64-point tiles would leave CUs
+// idle (C5's 500-point level: 128 workgroups on 256 CUs).  Same wave-per-row-
+// block ratios, so every layer split below has the same shape per wave.
+#ifndef NDNET_PN_TILE
+#define NDNET_PN_TILE 64
+#endif
+constexpr int kP = NDNET_PN_TILE;  // points per workgroup
 #ifndef NDNET_PN_WAVES
-#define NDNET_PN_WAVES 16
+#define NDNET_PN_WAVES (NDNET_PN_TILE / 4)
 #endif
 constexpr int kWaves = NDNET_PN_WAVES;
 constexpr int kThreads = 64 * kWaves;
-constexpr int kRowBlocks = kP / 16;  // 4 (kWaves / 2)
+constexpr int kRowBlocks = kP / 16;  // 4 (2 for 32-point tiles)
+static_assert(kP == 64 || kP == 32, "64- or 32-point tiles");
 constexpr int kFuseNC = 64;     // columns per chunk of a fused layer
 // LDS row pitch padding.  An A-fragment read (ds_read_b128, 16 B per lane at
 // row l & 15, column offset 16 B * (l >> 4)) is conflict-free when the row
@@ -761,9 +770,14 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
       // Q is one chunk of its (RB, NB) split: NB = N2 / (16 * column groups)
       constexpr int kQ = 16 / kWaves > 0 ? 16 / kWaves : 1;
       const bool op = !last && A.L[l + 2].prec;  // the layer after Q reads bf16 planes
-      if (Q.N == 256) fused_pair<4, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op);
-      else if (Q.N > 64) fused_pair<2, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op);
-      else fused_pair<1, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op);
+      if constexpr (kP == 32) {  // two row blocks: each Q split with half the row groups
+        if (Q.N == 256) fused_pair<2, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op);
+        else fused_pair<1, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op);
+      } else {
+        if (Q.N == 256) fused_pair<4, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op);
+        else if (Q.N > 64) fused_pair<2, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op);
+        else fused_pair<1, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op);
+      }
       l++;
     } else {
       const LayerCtx C = layer_ctx(A, l, b);
@@ -771,7 +785,13 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
       const int out = reg[(l + 1) & 1], pout = ((l + 1) & 1) ? pitch1 : pitch0;
       float* gm = (last && gmax_b) ? gmax_b : nullptr;
       const bool op = !last && A.L[l + 1].prec;  // the next layer reads bf16 planes
-      if constexpr (kWaves == 8) {
+      if constexpr (kP == 32) {
+        // 32-point tiles, 8 waves: two row blocks, columns per wave as the
+        // 64-point form's (one row group, all waves across the columns)
+        if (C.N % 256 == 0) plain_layer<2, 2>(C, in, pin, out, pout, gm, rows_valid, op);
+        else if (C.N % 128 == 0) plain_layer<2, 1>(C, in, pin, out, pout, gm, rows_valid, op);
+        else plain_layer<1, 1>(C, in, pin, out, pout, gm, rows_valid, op);  // N % 64 == 0, or N = 32 (half idle)
+      } else if constexpr (kWaves == 8) {
         // 8 waves (2 per SIMD, up to 256 registers each): a wave takes up to
         // four column blocks, so each A fragment feeds NB MFMAs per plane
         // (tools/ubench/mfma_bf16_peak.hip b9 / b13 vs b3)
@@ -1164,6 +1184,7 @@ __global__ void __launch_bounds__(256) k_pn_fold64_x6f(const float* __restrict__
 
 extern "C" {
 
+#if NDNET_PN_TILE == 64  // the 32-point build exports only its chain entry point (below)
 int ndnet_pn_fc_mfma_run(const float* in, int ld_in, const float* Wf, const float* bias, float* out, int ld_out,
                          int batch, int K, int N, int relu, void* stream) {
   if (!in || !Wf || !bias || !out || batch <= 0 || batch > 16 || K <= 0 || K % 16 || K > 16 * kFcWaves * kFcMaxG ||
@@ -1216,7 +1237,13 @@ int ndnet_pn_fold64_run(const float* t2, const float* rhs, float* out, int batch
 }
 
 // One fused point-MLP chain over `batch` clouds on `stream` (see pointnet.h).
+#endif
+
+#if NDNET_PN_TILE == 64
 int ndnet_pn_chain_run(const ndnet_pn_chain* args, int batch, void* stream) {
+#else
+int ndnet_pn_chain_run_t32(const ndnet_pn_chain* args, int batch, void* stream) {
+#endif
   if (!args || batch <= 0 || args->num_layers < 1 || args->num_layers > NDNET_PN_MAX_LAYERS || args->num_points <= 0 ||
       args->in_cols < 1 || args->in_cols > args->L[0].K || args->in_cols > args->x_ld)
     return -20;

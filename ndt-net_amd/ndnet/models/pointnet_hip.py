@@ -293,10 +293,28 @@ def _build_chain(n: int, in_cols: int, layers, relus, mode: int, gmax=None, out_
     return ch
 
 
+# 32-point tiles (ndnet_pn_chain_run_t32) when 64-point tiles would fill at
+# most half the CUs (C5's 500-point level: 16 x 8 tiles on 256 CUs); "0" off
+TILE32 = os.environ.get("NDNET_PN_TILE32", "1") == "1"
+_cus = {}
+
+
+def _use_t32(B: int, n: int, device) -> bool:
+    if not TILE32:
+        return False
+    if device not in _cus:
+        _cus[device] = torch.cuda.get_device_properties(device).multi_processor_count
+    return 2 * B * ((n + 63) // 64) <= _cus[device]
+
+
 def _run_chain(ch: "_Chain", x: torch.Tensor, out=None) -> None:
     assert x.stride(1) == 12 and x.stride(2) == 1 and x.dtype == torch.float32
     ch.x = x.data_ptr()
     ch.out = out.data_ptr() if out is not None else None
+    if _use_t32(x.shape[0], x.shape[1], x.device):
+        rc = _lib.lib().ndnet_pn_chain_run_t32(ctypes.byref(ch), x.shape[0], _lib.stream_ptr(x.device))
+        _lib.check(rc, "ndnet_pn_chain_run_t32")
+        return
     rc = _lib.lib().ndnet_pn_chain_run(ctypes.byref(ch), x.shape[0], _lib.stream_ptr(x.device))
     _lib.check(rc, "ndnet_pn_chain_run")
 

@@ -225,3 +225,23 @@ def test_head3_in_chain_equals_head3_kernel(monkeypatch):
         with torch.no_grad():
             outs.append(m(pts, cov))
     assert (outs[0] - outs[1]).abs().max().item() < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,N", [(16, 500), (4, 77), (2, 1000)])
+def test_chain_t32_equals_t64(monkeypatch, B, N):
+    """The 32-point-tile chain build (ndnet_pn_chain_run_t32: 8 waves, two row
+    blocks) against the 64-point build on the same model and input: log-probs
+    within fp32 summation order, and both within the torch fp32 tolerance."""
+    from ndnet.models import pointnet_hip as ph
+    torch.manual_seed(11)
+    pts, cov = torch.randn(B, N, 3).cuda(), torch.randn(B, N, 9).cuda() * 0.1
+    outs = []
+    for force in (True, False):
+        monkeypatch.setattr(ph, "_use_t32", lambda b, n, d, f=force: f)
+        m = _model(768, 28, "cuda")
+        with torch.no_grad():
+            outs.append(m(pts, cov))
+    ref = m.forward_torch(pts, cov)
+    assert (outs[0] - outs[1]).abs().max().item() < 1e-5
+    assert (outs[0] - ref).abs().max().item() < TOL
