@@ -823,6 +823,23 @@ constexpr int kWqU = 16;                     // samples per prefetch block
 constexpr int kWqNB = 4;                     // register blocks in the prefetch ring
 constexpr int kWqRt = 4096;                  // reciprocals tabled in LDS (32 KB)
 constexpr int kWqHistMax = 64 * 1024;        // LDS class histograms up to this size, else global
+// Float input: a lane loads whole (x, y, z) records -- a quarter of its quad's
+// block, one dwordx3 each -- and the quad transposes them through LDS (lane j
+// then holds coordinate j of every sample): a quarter of the load
+// instructions per sample.  L's heaviest ND spent 16 of its 122 us on point
+// loads (23 with their issue); records took 6 us off it, and 2-3 us off C5's
+// welford (profiles/r02h_welford_loads.txt).  NDNET_WQ_VU = 2 (32-sample
+// blocks, 128 samples in flight -- the per-coordinate loads were capped by the
+// 63 outstanding loads a wave can count) gained 1 us more on L but lost 2 on
+// C2 and 3 on C5 (longer masked tails).
+#ifndef NDNET_WQ_VLOAD
+#define NDNET_WQ_VLOAD 1
+#endif
+constexpr int kWqStageQ = 100;               // LDS words per quad stage (96 + pad: conflict-free reads)
+template <typename T, bool kVec, int kU>
+struct WqBlk { T v[kU]; };                       // coordinate j of samples q0 .. q0 + kU - 1 (lane j)
+template <int kU>
+struct WqBlk<float, true, kU> { float3 v[kU / 4]; };  // records q0 + (kU / 4) j + i, i < kU / 4 (lane j)
 
 template <int CTRL>
 __device__ inline double dpp_d(double v) {
@@ -909,6 +926,8 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
                                                           int ncls, uint64_t n, uint32_t ndcap, uint32_t* wq_ctr,
                                                           WqChainArgs CA) {
   extern __shared__ __attribute__((aligned(16))) unsigned char wq_smem[];
+  __shared__ __attribute__((aligned(16))) float wq_stage[std::is_same<T, float>::value && NDNET_WQ_VLOAD ? kWqNDs : 1]
+                                                        [kWqStageQ];
   double* lrt = (double*)wq_smem;                                // [kWqRt] refined reciprocals of 1..kWqRt
   uint32_t* pre = (uint32_t*)(wq_smem + kWqRt * sizeof(double));  // [B + 1] first item of each cloud
   uint32_t* wq_hist = pre + ((B + 1 + 3) & ~3);                   // labelled runs: [kWqNDs][ncls + 1]
@@ -971,6 +990,12 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
   const uint32_t last = cnt ? cnt - 1u : 0u;
   const uint32_t jj = j < 3 ? j : 0u;
   const T* src = nd_pts + ((uint64_t)b * n + beg) * 3 + jj;
+  constexpr bool kVec = NDNET_WQ_VLOAD && std::is_same<T, float>::value;
+#ifndef NDNET_WQ_VU
+#define NDNET_WQ_VU 1
+#endif
+  constexpr int kU = kVec ? NDNET_WQ_VU * kWqU : kWqU;  // samples per ring block
+  float* const stg = kVec ? &wq_stage[threadIdx.x >> 2][0] : nullptr;
   const uint32_t mx = wave_max_u32(cnt);
   // the ND's neighbours (voxel.c:116-175, directions X+, X-, Y+, Y-, Z+, Z-):
   // lane j of the quad takes directions j and j + 4; their dense ids and
@@ -1002,29 +1027,42 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
 
   double mean = 0.0, m2 = 0.0, off = 0.0;
   bool bad = false;
-  // points: a ring of kWqNB register blocks of kWqU samples, kWqNB - 1 blocks
+  // points: a ring of kWqNB register blocks of kU samples, kWqNB - 1 blocks
   // in flight ahead of the one being folded (memory latency ~2 us under load
   // against ~0.5 us per block of compute)
-  T r0[kWqU], r1[kWqU], r2[kWqU], r3[kWqU];
-  auto load = [&](T (&r)[kWqU], uint32_t q0) __attribute__((always_inline)) {
+  using Blk = WqBlk<T, kVec, kU>;
+  Blk r0, r1, r2, r3;
+  auto load = [&](Blk& r, uint32_t q0) __attribute__((always_inline)) {
+    if constexpr (kVec) {
+      const float* rec = nd_pts + ((uint64_t)b * n + beg) * 3;
 #pragma unroll
-    for (int u = 0; u < kWqU; u++) {
-      const uint32_t q = q0 + (uint32_t)u;
+      for (int i = 0; i < kU / 4; i++) {
+        const uint32_t q = q0 + (uint32_t)(kU / 4) * j + (uint32_t)i;
+        const float* pq = rec + 3u * (q < last ? q : last);
+        r.v[i] = make_float3(pq[0], pq[1], pq[2]);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        const uint32_t q = q0 + (uint32_t)u;
 #ifdef NDNET_WQ_NOLOAD  // timing experiment only: no point loads (wrong results)
-      r[u] = (T)(1.0f + 0.001f * (float)(q & 7));
+        r.v[u] = (T)(1.0f + 0.001f * (float)(q & 7));
+#elif defined(NDNET_WQ_HOTLOAD)  // timing experiment only: loads of a few cached lines (wrong results)
+        r.v[u] = nd_pts[jj + 3u * (q & 7u)];
 #else
-      r[u] = src[3u * (q < last ? q : last)];
+        r.v[u] = src[3u * (q < last ? q : last)];
 #endif
+      }
     }
   };
   // the block's reciprocals: broadcast LDS reads, computed past the table
-  auto recips = [&](double (&cr)[kWqU], uint32_t q0) __attribute__((always_inline)) {
-    if (q0 + kWqU <= (uint32_t)kWqRt) {  // wave-uniform
+  auto recips = [&](double (&cr)[kU], uint32_t q0) __attribute__((always_inline)) {
+    if (q0 + kU <= (uint32_t)kWqRt) {  // wave-uniform
 #pragma unroll
-      for (int u = 0; u < kWqU; u++) cr[u] = lrt[q0 + u];
+      for (int u = 0; u < kU; u++) cr[u] = lrt[q0 + u];
     } else {
 #pragma unroll
-      for (int u = 0; u < kWqU; u++) cr[u] = recip_refined((double)(q0 + u + 1));
+      for (int u = 0; u < kU; u++) cr[u] = recip_refined((double)(q0 + u + 1));
     }
   };
   // One block of samples; kExact: IEEE divisions and the NaN -> 0 step.
@@ -1037,18 +1075,39 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
   // after each pair, so every head op finds its operand ready: the in-order
   // wave issues ~18 instructions per sample back to back instead of waiting
   // out each chain link.
-  auto fold = [&](const T (&r)[kWqU], uint32_t q0, bool act, auto exact_tag,
+  auto fold = [&](const Blk& rb, uint32_t q0, bool act, auto exact_tag,
                   auto masked_tag) __attribute__((always_inline)) {
     constexpr bool kExact = decltype(exact_tag)::value;
-    constexpr bool kMasked = decltype(masked_tag)::value;  // false: every live quad has >= q0 + kWqU samples
-    double cr[kWqU];
+    constexpr bool kMasked = decltype(masked_tag)::value;  // false: every live quad has >= q0 + kU samples
+    T r[kU];
+    if constexpr (kVec) {
+      // the quad's records to its LDS stage (word 3 s + c = coordinate c of
+      // sample s), then lane j reads coordinate jj of each sample; one wave's
+      // LDS operations complete in order, so the compiler barriers suffice
+#pragma unroll
+      for (int i = 0; i < kU / 4; i += 4) {
+        float4* d = reinterpret_cast<float4*>(stg + 3 * (kU / 4) * j + 3 * i);
+        const float3 a0 = rb.v[i], a1 = rb.v[i + 1], a2 = rb.v[i + 2], a3 = rb.v[i + 3];
+        d[0] = make_float4(a0.x, a0.y, a0.z, a1.x);
+        d[1] = make_float4(a1.y, a1.z, a2.x, a2.y);
+        d[2] = make_float4(a2.z, a3.x, a3.y, a3.z);
+      }
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < kU; u++) r[u] = stg[3 * u + jj];
+      asm volatile("" ::: "memory");
+    } else {
+#pragma unroll
+      for (int u = 0; u < kU; u++) r[u] = rb.v[u];
+    }
+    double cr[kU];
     if constexpr (!kExact) recips(cr, q0);
     double pt = 0.0, pu = 0.0, pcn = 1.0, prc = 1.0;       // the previous sample's head results
     unsigned long long plane = 0;
     if constexpr (kExact) {
       // the refold (never on ordinary data): plain order
 #pragma unroll
-      for (int u = 0; u < kWqU; u++) {
+      for (int u = 0; u < kU; u++) {
         const uint32_t q = q0 + (uint32_t)u;
         const unsigned long long lanes = __ballot(act && q < cnt);
         const double cn = (double)(q + 1u);
@@ -1072,19 +1131,19 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
       // m2 and the off-diagonal gain +0 -- an exact no-op (the sums start at +0
       // and never become -0), so one select on x replaces three on the state.
 #pragma unroll
-      for (int u = 0; u <= kWqU; u++) {  // u == kWqU: the last sample's tail alone
-        const bool head = u < kWqU, tail = u > 0;
+      for (int u = 0; u <= kU; u++) {  // u == kU: the last sample's tail alone
+        const bool head = u < kU, tail = u > 0;
         const uint32_t q = q0 + (uint32_t)u;
         const double cn = (double)(q + 1u);
-        const double rc = head ? cr[u < kWqU ? u : 0] : 0.0;
+        const double rc = head ? cr[u < kU ? u : 0] : 0.0;
         double x = 0.0, t = 0.0, q0v = 0.0, rem = 0.0, qq = 0.0, nm = 0.0, uu = 0.0;
         double pm = 0.0, ua = 0.0, tb = 0.0, pr = 0.0, q1 = 0.0, rm1 = 0.0, qq1 = 0.0;
         if constexpr (!std::is_same<T, float>::value) {
-          if (head) bad |= (!kMasked || (act && q < cnt)) && !wq_in_range(r[u < kWqU ? u : 0]);
+          if (head) bad |= (!kMasked || (act && q < cnt)) && !wq_in_range(r[u < kU ? u : 0]);
         }
         // pair 1: t | u_a
         if (head) {
-          x = (double)r[u < kWqU ? u : 0];
+          x = (double)r[u < kU ? u : 0];
           if constexpr (kMasked) x = sel_d(__ballot(act && q < cnt), x, mean);
           t = x - mean;
         }
@@ -1127,28 +1186,28 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
   };
   auto run = [&](uint32_t lim, bool act, auto exact_tag) __attribute__((always_inline)) {
     load(r0, 0);
-    load(r1, kWqU);
-    load(r2, 2 * kWqU);
-    load(r3, 3 * kWqU);
+    load(r1, kU);
+    load(r2, 2 * kU);
+    load(r3, 3 * kU);
     // blocks every live quad fills run without the per-sample selects
     // (the exact refold keeps the state of the quads it does not redo: always masked)
     const uint32_t full = decltype(exact_tag)::value ? 0u : wave_min_u32(live ? cnt : 0xffffffffu);
-    auto step = [&](const T (&r)[kWqU], uint32_t q0) __attribute__((always_inline)) {
-      if (q0 + kWqU <= full) fold(r, q0, act, exact_tag, std::false_type{});
+    auto step = [&](const Blk& r, uint32_t q0) __attribute__((always_inline)) {
+      if (q0 + kU <= full) fold(r, q0, act, exact_tag, std::false_type{});
       else fold(r, q0, act, exact_tag, std::true_type{});
     };
-    for (uint32_t q0 = 0; q0 < lim; q0 += kWqNB * kWqU) {  // every branch below is wave-uniform
+    for (uint32_t q0 = 0; q0 < lim; q0 += kWqNB * kU) {  // every branch below is wave-uniform
       step(r0, q0);
-      load(r0, q0 + 4 * kWqU);
-      if (q0 + kWqU >= lim) break;
-      step(r1, q0 + kWqU);
-      load(r1, q0 + 5 * kWqU);
-      if (q0 + 2 * kWqU >= lim) break;
-      step(r2, q0 + 2 * kWqU);
-      load(r2, q0 + 6 * kWqU);
-      if (q0 + 3 * kWqU >= lim) break;
-      step(r3, q0 + 3 * kWqU);
-      load(r3, q0 + 7 * kWqU);
+      load(r0, q0 + 4 * kU);
+      if (q0 + kU >= lim) break;
+      step(r1, q0 + kU);
+      load(r1, q0 + 5 * kU);
+      if (q0 + 2 * kU >= lim) break;
+      step(r2, q0 + 2 * kU);
+      load(r2, q0 + 6 * kU);
+      if (q0 + 3 * kU >= lim) break;
+      step(r3, q0 + 3 * kU);
+      load(r3, q0 + 7 * kU);
     }
   };
   run(mx, true, std::false_type{});
