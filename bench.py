@@ -460,7 +460,7 @@ def main() -> None:
         from concurrent.futures import ThreadPoolExecutor
         host = pts.cpu().numpy().astype(np.float64)
         nproc = os.cpu_count() or 1
-        cores = min(16, nproc)  # the GPU box's CPU share per GPU
+        cores = min(16, nproc)  # the GPU box's CPU share per GPU (labelled per_gpu_cpu_share)
         budget = args.cpu_baseline_seconds
         t_ref, done = 0.0, 0
         while done < B and t_ref < 0.45 * budget:
@@ -496,12 +496,15 @@ def main() -> None:
                          f"8 pthreads, mutex per voxel, -O0; {ref_cloud * 1e3:.1f} ms/cloud) + torch fp32 CPU "
                          f"forward ({cores} threads, {fwd * 1e3:.1f} ms/cloud)",
                "nproc": nproc,
-               "calibration": "cpu_ref / compiled reference estimate stage = 1.08 (U), 1.15 (L) in the build "
-                              "container (profiles/r02_cpu_ref_calibration.txt)",
-               "all_cores": {"value": round(1.0 / (all_cloud + fwd), 3), "unit": "clouds/s", "cores": cores,
-                             "sample": f"{len(jobs)} clouds through the -O2 oracle (oracle/ndt_oracle.c), one cloud "
-                                       f"per thread on {cores} threads ({all_cloud * 1e3:.2f} ms/cloud aggregate), "
-                                       f"+ the torch forward ({cores} threads per cloud)"}}
+               "calibration": "estimate stage only: cpu_ref / compiled reference estimate stage = 1.08 (U), "
+                              "1.15 (L) in the build container (profiles/r02_cpu_ref_calibration.txt); the KL leg "
+                              "(GSL calls, kullback_leibler.c:28-127) is uncalibrated: GSL is absent here",
+               "per_gpu_cpu_share": {"value": round(1.0 / (all_cloud + fwd), 3), "unit": "clouds/s", "cores": cores,
+                                     "sample": f"{len(jobs)} clouds through the -O2 oracle (oracle/ndt_oracle.c), one "
+                                               f"cloud per thread on {cores} threads ({all_cloud * 1e3:.2f} ms/cloud "
+                                               f"aggregate), + the torch forward ({cores} threads per cloud)",
+                                     "note": f"{cores} of the host's {nproc} CPUs: the CPU share the GPU box gives one "
+                                             f"GPU (gpurun: 16 per GPU), not every core of the host"}}
 
     if rank == 0:
         line = {

@@ -96,6 +96,11 @@ int to_point_cloud(void *nd_array,
 void free_nds(void *nd_array, unsigned long num_nds);
 void free_kl_divergences(void *kl_divergences);
 
+/* Replaces print_matrix (matrix.h:40, matrix.c:28-35): prints a rows x cols
+ * row-major double matrix to stdout, one row per line, "%f " per element.
+ * The reference's own library test binds it (ndnet/test/suites/libs.py:13-26). */
+void print_matrix(double *matrix, int rows, int cols);
+
 /* ---------------------------------------------------------------------------
  * 2. Batched device API (the ndt_preprocessing hot path,
  *    ndnet/preprocessing/ndtnet_preprocessing.py:6-73).

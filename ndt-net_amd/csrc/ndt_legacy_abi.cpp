@@ -204,4 +204,13 @@ void free_kl_divergences(void* kl_divergences) {
   delete t;
 }
 
+void print_matrix(double* matrix, int rows, int cols) {
+  if (!matrix) return;
+  for (int r = 0; r < rows; r++) {
+    for (int c = 0; c < cols; c++) printf("%f ", matrix[(size_t)r * cols + c]);
+    printf("\n");
+  }
+  fflush(stdout);
+}
+
 }  // extern "C"

@@ -61,6 +61,7 @@ EXPORTS = {
                             ctypes.c_double, ctypes.c_double, _PD, _PUL, _PD, _PUS]),
     "free_nds": (None, [_P, _UL]),
     "free_kl_divergences": (None, [_P]),
+    "print_matrix": (None, [_P, _I, _I]),  # matrix.h:40 (host only)
     # batched device API
     "ndnet_ndt_plan_create": (_I, [_I, _U64, _U64, _I, _U64, ctypes.POINTER(_P)]),
     "ndnet_ndt_plan_destroy": (None, [_P]),

@@ -43,3 +43,19 @@ def test_product_does_not_import_oracle():
             if f.endswith((".py", ".hip", ".cpp", ".h")):
                 txt = open(os.path.join(root, f)).read()
                 assert "import oracle" not in txt and "liboracle" not in txt, f
+
+
+def test_print_matrix_as_reference_libs_suite(capfd):
+    """The reference's own library suite (ndnet/test/suites/libs.py:13-26):
+    the symbol exists and prints a rows x cols double matrix ("%f " per
+    element, one row per line, matrix.c:28-35).  Host code, no GPU."""
+    import numpy as np
+    from ndnet import _lib
+    lib = _lib.lib()
+    assert hasattr(lib, "print_matrix")
+    m = np.arange(6, dtype=np.float64).reshape(2, 3) - 1.5
+    lib.print_matrix(m.ctypes.data, 2, 3)
+    out = capfd.readouterr().out
+    assert out == "-1.500000 -0.500000 0.500000 \n1.500000 2.500000 3.500000 \n"
+    lib.print_matrix(None, 3, 3)  # NULL: nothing printed, no crash
+    assert capfd.readouterr().out == ""
