@@ -39,6 +39,7 @@ sys.path.insert(0, os.path.join(REPO, "ndt-net_amd"))
 
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 FP32_MFMA_PEAK_TF = 157.3   # MI355X_MICROARCH.md: FP32 matrix 157.3 TF (dense)
+BF16_MFMA_PEAK_TF = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA ~2.5 PF dense (no sparsity)
 
 
 def pointnet_flops_per_cloud(n: int, F: int, C: int) -> float:
@@ -49,15 +50,33 @@ def pointnet_flops_per_cloud(n: int, F: int, C: int) -> float:
     return 2.0 * (pt * n + fc)
 
 
+def chain_layers(F: int, C: int) -> tuple:
+    """The per-point layers each k_pn_chain launch must compute, at their
+    unpadded sizes, with the matrix instruction they run on: ((K, N, kind),
+    ...) per chain, kind "x6" (fp32-accurate split-bf16: six
+    v_mfma_f32_16x16x32_bf16 products per fp32 MAC) or "f32"
+    (v_mfma_f32_16x16x4_f32).  The kernels' recomputation of conv1 / conv2 in
+    later chains and the zero padding are overhead, not counted."""
+    from ndnet.models import pointnet_hip as P
+    x6 = "x6" if P.SPLIT_BF16 else "f32"
+    nar = x6 if P.X6_NARROW else "f32"
+    return (((3, 64, "f32"), (64, 128, nar), (128, 1024, x6)),
+            ((12, 64, "f32"), (64, 64, nar), (64, 128, nar), (128, 1024, x6)),
+            ((64, 128, x6), (128, F, x6)),
+            ((64, 512, x6), (512, 256, x6), (256, 128, x6), (128, C + 1, nar)))
+
+
 def chain_flops_per_point(F: int, C: int) -> tuple:
-    """Algorithmic FLOPs per point of the four k_pn_chain launches: each layer
-    counted once at its unpadded size (the kernels' recomputation of conv1 /
-    conv2 in later chains and the zero padding are overhead, not counted)."""
-    a = 3 * 64 + 64 * 128 + 128 * 1024
-    b = 12 * 64 + 64 * 64 + 64 * 128 + 128 * 1024
-    c = 64 * 128 + 128 * F
-    d = 64 * 512 + 512 * 256 + 256 * 128 + 128 * (C + 1)
-    return tuple(2.0 * v for v in (a, b, c, d))
+    """Algorithmic FLOPs per point of the four k_pn_chain launches (2 K N per layer)."""
+    return tuple(2.0 * sum(K * N for K, N, _ in ch) for ch in chain_layers(F, C))
+
+
+def chain_ideal_s_per_point(F: int, C: int) -> tuple:
+    """Seconds per point of each chain at the dense peak of the instructions
+    its layers issue: x6 layers at BF16_MFMA_PEAK_TF / 6 (six bf16 products per
+    fp32 MAC), f32 layers at FP32_MFMA_PEAK_TF."""
+    peak = {"x6": BF16_MFMA_PEAK_TF * 1e12 / 6.0, "f32": FP32_MFMA_PEAK_TF * 1e12}
+    return tuple(sum(2.0 * K * N / peak[kind] for K, N, kind in ch) for ch in chain_layers(F, C))
 
 
 def _free_port() -> int:
@@ -125,6 +144,8 @@ def main() -> None:
                     help="config C5: comma-separated NDs per level, e.g. 2000,1000,500 (downsample, then prune; "
                          "a forward per level)")
     ap.add_argument("--no-other", action="store_true", help="skip the other-distribution (U <-> L) timing")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group of the timing barrier / max over ranks (nccl = RCCL)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / shard split / timing skeleton on CPU (gloo), no GPU work")
     args = ap.parse_args()
@@ -139,9 +160,14 @@ def main() -> None:
     if args.dry_run:
         _dry_run(args, rank, world)
         return
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    dist = D.init("nccl", dev)  # RCCL; used only for the barrier and the max-over-ranks time
+    # one GPU per rank; a box with fewer GPUs than ranks (a rehearsal of the
+    # multi-rank path on one card, --dist-backend gloo) wraps around
+    ndev = max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local % ndev)
+    dev = torch.device("cuda", local % ndev)
+    # RCCL ("nccl") carries only the barrier and the max-over-ranks time: no
+    # collective on the data path
+    dist = D.init(args.dist_backend, dev)
 
     from ndnet.models.ndtnet import NDTNetSegmentation
     from ndnet.models import pointnet_hip
@@ -333,6 +359,9 @@ def main() -> None:
         }
 
     # ---- stage timing (HIP events on the stream the kernels run on) ----
+    # Each timed region starts behind a ~2 ms device-side sleep on the same
+    # stream, so the host has queued every launch of the region before its
+    # first event fires: the events bracket kernel time, not Python launch gaps.
     plan = get_plan(B, n, k, -1, dev)
     _lib.lib().ndnet_ndt_set_timing(plan.handle, 1)
     stage_names = ["reset+limits", "bisection (15 launches)", "dense ids", "binning", "welford + LU chains",
@@ -340,14 +369,17 @@ def main() -> None:
     stage_ms = np.zeros(6)
     fwd_ms = 0.0
     reps = max(3, min(args.steps, 10))
+    sleep_cycles = int(5e6)
     pointnet_hip.chain_timing = []
     with torch.no_grad():
         for _ in range(reps):
+            torch.cuda._sleep(sleep_cycles)
             p, c, _ = ndt_preprocessing(k, pts)
             ms = np.zeros(6, np.float32)
             _lib.lib().ndnet_ndt_stage_ms(plan.handle, ms.ctypes.data)
             stage_ms += ms
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda._sleep(sleep_cycles)
             e0.record()
             model(p, c)
             e1.record()
@@ -362,17 +394,20 @@ def main() -> None:
     pointnet_hip.chain_timing = None
     ndt_ms = float(stage_ms.sum())
     hip_fwd = pointnet_hip.available()
-    # dominant stage -> roofline entry
     flops = pointnet_flops_per_cloud(k, F, C) * B
     ndt_bytes = (24.0 * n + 48.0 * k) * B  # fp64 xyz read once + fp32 12-D write
-    # The roofline entry is the dominant SINGLE kernel: the four k_pn_chain
-    # launches (each event-timed) and the NDT stages that are one kernel
-    # (k_limits after a 1-us reset, k_welford).  Multi-kernel stages (15
-    # bisection passes, binning, KL) are reported in stages_ms only.
+    # The roofline entry is the kernel that holds the most time per step (launch
+    # count x duration): the four k_pn_chain launches of a forward taken as one
+    # set (they are one kernel, launched once per chain), k_front, k_welford.
     cflops = np.array(chain_flops_per_point(F, C)) * k * B
+    cideal = np.array(chain_ideal_s_per_point(F, C)) * k * B  # seconds at the issued instructions' peak
     chains_info = {"ms": [round(float(v), 4) for v in chain_ms],
-                   "tflops": [round(float(f / (t * 1e-3) / 1e12), 2) if t > 0 else None
-                              for f, t in zip(cflops, chain_ms)]}
+                   "fp32_equiv_tflops": [round(float(f / (t * 1e-3) / 1e12), 2) if t > 0 else None
+                                         for f, t in zip(cflops, chain_ms)],
+                   "frac_of_issued_peak": [round(float(i / (t * 1e-3)), 4) if t > 0 else None
+                                           for i, t in zip(cideal, chain_ms)],
+                   "forward_other_ms": round(fwd_ms - float(chain_ms.sum()), 4),
+                   "forward_other": "per-cloud FC heads, weight folds and launch boundaries of the forward"}
     # the NDT front (k_reset + k_front: limits, every bisection pass, dense ids
     # and binning in ONE launch) reads the f32 points once into registers and
     # writes them grouped by ND: 12 N in + 12 N out per cloud
@@ -388,16 +423,33 @@ def main() -> None:
         (1 if front else 4): ("k_welford", 12.0 * n * B + (4 + 24 + 72) * k * B,
                               "grouped f32 xyz read once + count/mean/covariance write per ND"),
     }
-    cand = [("chain", i, float(chain_ms[i])) for i in range(4) if hip_fwd] + \
+    cand = ([("chains", -1, float(chain_ms.sum()))] if hip_fwd else []) + \
            [("ndt", i, float(stage_ms[i])) for i in ndt_single]
     kind, ci, ms = max(cand, key=lambda c: c[2])
-    if kind == "chain":
-        achieved = cflops[ci] / (ms * 1e-3) / 1e12
-        roofline = {"kernel": f"k_pn_chain {pointnet_hip.CHAIN_NAMES[ci]}", "bound": "mfma",
-                    "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                    "frac": round(achieved / FP32_MFMA_PEAK_TF, 4), "traffic": None,
-                    "algorithmic": f"{cflops[ci] / 1e9:.3f} GFLOP per launch ({B} clouds x {k} points)",
-                    "ms": round(ms, 4), "all_chains": chains_info}
+    pmc_path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    pmc = {}
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            pmc = json.load(f)
+    if kind == "chains":
+        # fp32-equivalent FLOP/s against the peak of the instructions issued:
+        # x6 layers at 2.5 PF / 6, f32 layers at 157.3 TF (chain_ideal_s_per_point)
+        achieved = float(cflops.sum()) / (ms * 1e-3) / 1e12
+        peak = float(cflops.sum()) / float(cideal.sum()) / 1e12
+        roofline = {"kernel": "k_pn_chain (4 launches per forward: chains A-D)", "bound": "mfma",
+                    "achieved": round(achieved, 3), "peak": round(peak, 2), "unit": "TFLOP/s",
+                    "frac": round(achieved / peak, 4), "traffic": None,
+                    "algorithmic": f"{cflops.sum() / 1e9:.3f} fp32-equivalent GFLOP per forward ({B} clouds x {k} "
+                                   f"points; 2 K N per point per layer at unpadded sizes)",
+                    "peak_basis": "the issued-instruction peak: split-bf16 (x6) layers at BF16 2500 TF / 6 products, "
+                                  "f32 layers at 157.3 TF, weighted by each layer's FLOPs",
+                    "ms": round(ms, 4), "ms_basis": "sum of the 4 chain launches (event-timed on the launch stream)",
+                    "all_chains": chains_info}
+        rows = [pmc.get(f"k_pn_chain {c}") for c in "ABCD"]
+        if all(r and "hbm_bytes" in r for r in rows):
+            roofline["traffic"] = round(sum(r["hbm_bytes"] for r in rows))
+            roofline["traffic_source"] = f"{pmc.get('_source', pmc_path)}: k_pn_chain A-D, sum over the 4 launches " \
+                f"of 2 x FETCH_SIZE + WRITE_SIZE"
     else:
         name, nbytes, what = ndt_single[ci]
         achieved = nbytes / (ms * 1e-3) / 1e9
@@ -405,24 +457,30 @@ def main() -> None:
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
                     "algorithmic": f"{nbytes / 1e6:.2f} MB per launch: {what}", "ms": round(ms, 4),
                     "all_chains": chains_info}
-    # HBM bytes per launch of that kernel from the committed rocprofv3 PMC
-    # passes (tools/pmc.sh -> tools/pmc_summary.py --json): FETCH_SIZE doubled
-    # per MI355X_MICROARCH.md's gfx950 correction, plus WRITE_SIZE
-    pmc_path = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_path):
-        with open(pmc_path) as f:
-            pmc = json.load(f)
+        # HBM bytes per launch of that kernel from the committed rocprofv3 PMC
+        # passes (tools/pmc.sh -> tools/pmc_summary.py --json): FETCH_SIZE doubled
+        # per MI355X_MICROARCH.md's gfx950 correction, plus WRITE_SIZE
         for kname, row in pmc.items():
             if kname != "_source" and roofline["kernel"].startswith(kname.split("<")[0]) and "hbm_bytes" in row:
                 roofline["traffic"] = round(row["hbm_bytes"])
                 roofline["traffic_source"] = f"{pmc.get('_source', pmc_path)}: {kname}, " \
                     f"2 x FETCH_SIZE {row['FETCH_SIZE']:.0f} KB + WRITE_SIZE {row['WRITE_SIZE']:.0f} KB per launch"
                 break
+    # the per-step time of each candidate, and the NDT single kernels beside it
+    roofline["per_step_ms"] = {("k_pn_chain x4" if kd == "chains" else ndt_single[i][0]): round(t, 4)
+                               for kd, i, t in cand}
+    if "k_front" in roofline["per_step_ms"] and front and stage_ms[0] > 0:
+        roofline["k_front"] = {"ms": round(float(stage_ms[0]), 4),
+                               "algorithmic_gbs": round(24.0 * n * B / (stage_ms[0] * 1e-3) / 1e9, 1),
+                               "frac_of_peak": round(24.0 * n * B / (stage_ms[0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        frow = next((r for kk, r in pmc.items() if kk.startswith("k_front")), None)
+        if frow and "hbm_bytes" in frow:
+            roofline["k_front"]["pmc_bytes"] = round(frow["hbm_bytes"])
     # the scatter-stage kernel (per-ND Welford over the grouped points) and the
     # MFMA-busy fraction of the four point-MLP chains, from the same PMC passes:
     # busy = SQ_VALU_MFMA_BUSY_CYCLES (MFMA cycles summed over SIMDs) /
     # (GRBM_GUI_ACTIVE (summed over the 8 XCDs) x 128 SIMDs per XCD)
-    if os.path.exists(pmc_path):
+    if pmc:
         wrow = next((r for kk, r in pmc.items() if kk.startswith("k_welford")), None)
         wi = 1 if front else 4
         if wrow and "hbm_bytes" in wrow and stage_ms[wi] > 0:
@@ -433,13 +491,19 @@ def main() -> None:
                                      "pmc_gbs": round(wrow["hbm_bytes"] / (stage_ms[wi] * 1e-3) / 1e9, 1),
                                      "frac_of_peak": round(wrow["hbm_bytes"] / (stage_ms[wi] * 1e-3) / 1e9
                                                            / HBM_PEAK_GBS, 4)}
-        busy = {}
+        busy, num, den = {}, 0.0, 0.0
         for c in "ABCD":
             row = pmc.get(f"k_pn_chain {c}")
             if row and row.get("GRBM_GUI_ACTIVE") and "SQ_VALU_MFMA_BUSY_CYCLES" in row:
                 busy[c] = round(row["SQ_VALU_MFMA_BUSY_CYCLES"] / (row["GRBM_GUI_ACTIVE"] * 128.0), 4)
+                num += row["SQ_VALU_MFMA_BUSY_CYCLES"]
+                den += row["GRBM_GUI_ACTIVE"] * 128.0
         if busy:
             roofline["all_chains"]["mfma_busy"] = busy
+            roofline["all_chains"]["mfma_busy_set"] = round(num / den, 4)
+            roofline["all_chains"]["mfma_busy_source"] = (
+                f"{pmc.get('_source', pmc_path)}: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x 128 SIMDs per XCD), "
+                f"summed over the 4 chains for the set")
     roofline["ndt_end_to_end"] = {"bytes": ndt_bytes, "ms": round(ndt_ms, 4),
                                   "gbs": round(ndt_bytes / (ndt_ms * 1e-3) / 1e9, 2),
                                   "unit": "SURVEY 8d: 24N+48k per cloud over the whole NDT stage"}
@@ -538,7 +602,9 @@ def main() -> None:
                            "hip graph per step (ndnet.pipeline.GraphedSegmentation)" if (levels or args.no_pipeline)
                            else "2 hip graphs alternating: NDT(batch i) || forward(batch i-1) on two streams "
                                 "(ndnet.pipeline.PipelinedSegmentation)"),
-                       "global_batch": B * world, "points": n, "nds": k, "parallelism": f"dp{world} (clouds sharded)"},
+                       "global_batch": B * world, "points": n, "nds": k, "parallelism": f"dp{world} (clouds sharded)",
+                       "dist_backend": args.dist_backend if world > 1 else None,
+                       **({"rehearsal": f"{world} ranks on {ndev} GPU(s)"} if world > ndev else {})},
             "stages_ms": {nm: round(float(v), 4) for nm, v in zip(stage_names, stage_ms)}
                          | ({"pointnet_fwd": config_lines["C3_forward_only"]["ms_per_step"],
                              "pointnet_fwd_eager": round(fwd_ms, 4)} if config_lines else

@@ -91,6 +91,12 @@ int ndnet_pn_chain_run(const ndnet_pn_chain *args, int batch, void *stream);
  * would leave CUs idle, e.g. 16 clouds of 500 points. */
 int ndnet_pn_chain_run_t32(const ndnet_pn_chain *args, int batch, void *stream);
 
+/* Timing builds only (-DNDNET_PN_STAMPS, tools/pn_stamps.py): the
+ * s_memrealtime stamps (100 MHz) of every workgroup of the last chain
+ * launch, [wgs][16] (0 start, 1 head prologue, 2 input tile, 3 + l after
+ * layer l, 15 end), copied to host memory.  The product build returns -20. */
+int ndnet_pn_debug_stamps(unsigned long long *host, int wgs);
+
 /* The per-cloud steps between the chains (TNet FC heads ndtnet.py:53-60 and
  * the weight folds of pointnet_hip.py), for batch <= 16 clouds:
  *   ndnet_pn_fc_run:     out[b][n] = act(bias[n] + sum_k in[b][k] W[n][k]),

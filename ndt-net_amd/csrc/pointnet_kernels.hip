@@ -120,6 +120,25 @@ __device__ inline float xor_row(float v) {
 // double buffer, addressed by float offsets so every access is a ds_* op
 extern __shared__ __attribute__((aligned(16))) float g_smem[];
 
+// Timing build only (-DNDNET_PN_STAMPS, tools/pn_stamps.py): s_memrealtime
+// (100 MHz) of every workgroup at its start (0), after chain B's head
+// prologue (1), after the input tile (2), after each layer's closing barrier
+// (3 + layer) and at its end (15), read back by ndnet_pn_debug_stamps.  The
+// product build compiles none of it.
+#ifdef NDNET_PN_STAMPS
+constexpr int kStampWgs = 1024;
+__device__ unsigned long long g_pn_stamps[kStampWgs][16];
+#define PN_STAMP(i)                                                                           \
+  do {                                                                                        \
+    const int w_ = blockIdx.y * gridDim.x + blockIdx.x;                                       \
+    if (threadIdx.x == 0 && w_ < kStampWgs) g_pn_stamps[w_][(i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define PN_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
+
 // Weights are fragment-major (include/ndnet_pointnet.h): the 16 x 16 block
 // (k-group kg, column block cb) of W^T is 64 lanes x float4, lane kq * 16 + cl
 // holding W^T[16 kg + 4 kq + s][16 cb + cl] for s = 0..3 -- the B operands of
@@ -690,6 +709,7 @@ __host__ __device__ inline int region_floats(int width, int planes) {
 __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int planes, int fbuf) {
   const int b = blockIdx.y;
   const int p0 = blockIdx.x * kP;
+  PN_STAMP(0);
   // LDS: activation region 0 | region 1 | [fused-chunk double buffer]
   const int pitch0 = A.max_width + kPadF, pitch1 = A.max_width2 + kPadF;
   const int reg[2] = {0, region_floats(A.max_width, planes & 1)};
@@ -748,6 +768,7 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
     // the same bits.  (A device-scope __threadfence here writes back the L2:
     // measured +60 us per launch.)
     __syncthreads();
+    PN_STAMP(1);
   }
   const int K0 = A.L[0].K;
   for (int e = threadIdx.x; e < kP * K0; e += kThreads) {
@@ -758,6 +779,7 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
     g_smem[r * pitch0 + c] = v;
   }
   __syncthreads();
+  PN_STAMP(2);
   const int rows_valid = A.num_points - p0;
   float* const gmax_b = A.mode == 0 ? A.gmax + (int64_t)b * A.gmax_ld : nullptr;
   for (int l = 0; l < A.num_layers; l++) {
@@ -810,6 +832,7 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
       }
     }
     __syncthreads();
+    PN_STAMP(3 + l);
   }
   if (A.clear && blockIdx.x == 0 && blockIdx.y == 0)
     for (int64_t i = threadIdx.x; i < A.clear_count; i += kThreads) A.clear[i] = -INFINITY;
@@ -840,6 +863,7 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
       }
     }
   }
+  PN_STAMP(15);
 }
 
 // ---------------------------------------------------------------------------
@@ -1237,6 +1261,20 @@ int ndnet_pn_fold64_run(const float* t2, const float* rhs, float* out, int batch
 }
 
 // One fused point-MLP chain over `batch` clouds on `stream` (see pointnet.h).
+
+// Timing builds (-DNDNET_PN_STAMPS): copies the stamps of the last chain
+// launch, [wgs][16] u64, to host memory; the product build returns -20.
+int ndnet_pn_debug_stamps(unsigned long long* host, int wgs) {
+#ifdef NDNET_PN_STAMPS
+  if (!host || wgs <= 0 || wgs > kStampWgs) return -20;
+  if (hipDeviceSynchronize() != hipSuccess) return -21;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pn_stamps), (size_t)wgs * 16 * sizeof(unsigned long long)) ==
+                 hipSuccess ? 0 : -21;
+#else
+  (void)host; (void)wgs;
+  return -20;
+#endif
+}
 #endif
 
 #if NDNET_PN_TILE == 64

@@ -533,3 +533,45 @@ def test_run_parts_equal_whole_run():
         res.append((out.cpu().numpy(), [bytes(s) for s in plan.host_stats()]))
     assert np.array_equal(res[0][0], res[1][0])
     assert res[0][1] == res[1][1]
+
+
+@pytest.mark.parametrize("num_classes", [28, 300])
+def test_full_size_labelled(num_classes):
+    """SURVEY 8(f)2 at the bench's size: 16 x 100k labelled L clouds -> 1000
+    NDs, every cloud's rows and one-hot classes against the oracle
+    (normal_distributions.c:107-121 first-max argmax; ndtnet_preprocessing.py:
+    22,55-57 one-hot).  28 classes: the training config, labels from
+    make_labelled_batch, through ndt_preprocessing's one-hot argmax (the
+    reference driver's path, ndtnet_preprocessing.py:34).  300 classes: 301
+    bins x 64 NDs per k_welford_q workgroup exceed the LDS histogram budget
+    (kWqHistMax, 64 KB), so the per-ND histograms live in global memory; labels
+    uniform over all 301 values, so the first-max tie rule decides many NDs."""
+    import torch
+    import oracle as O
+    from ndnet.preprocessing.ndtnet_preprocessing import ndt_preprocessing, last_stats
+    from ndnet.synthetic import make_labelled_batch
+    B, n, k = 16, 100_000, 1000
+    if num_classes == 28:
+        pts, onehot = make_labelled_batch(B, n, num_classes, seed0=0)
+        labels = onehot.argmax(axis=2)
+        p, c, g = ndt_preprocessing(k, torch.from_numpy(pts).cuda(), torch.from_numpy(onehot).cuda(), num_classes)
+        p, c, g = p.cpu().numpy(), c.cpu().numpy(), g.cpu().numpy()
+        stats = last_stats()
+    else:
+        pts, _ = make_labelled_batch(B, n, 1, seed0=0)
+        labels = np.random.default_rng(5).integers(0, num_classes + 1, (B, n))
+        plan, out, g = _run_plan(pts, k, labels, num_classes, exact_counts=False)
+        p, c = out[..., :3], out[..., 3:]
+        stats = plan.host_stats()
+    assert g.shape == (B, k, num_classes + 1)
+    for b in range(B):
+        r = O.run(pts[b].astype(np.float64), k, classes=labels[b], num_classes=num_classes)
+        assert stats[b].rc == r.rc == 0
+        rows = _f32_rows(r.out_pc, r.out_cov, k)
+        assert np.array_equal(p[b], rows[:, :3]), f"cloud {b} means"
+        assert np.array_equal(c[b], rows[:, 3:]), f"cloud {b} covariances"
+        onehot_ref = np.zeros((k, num_classes + 1), np.float32)
+        onehot_ref[np.arange(k), r.out_cls] = 1.0
+        assert np.array_equal(g[b], onehot_ref), f"cloud {b} classes"
+    if num_classes == 300:  # the tie rule and the wide histogram are exercised
+        assert len(np.unique(g.argmax(axis=2))) > 100
