@@ -96,6 +96,7 @@ int ndnet_pn_chain_run_t32(const ndnet_pn_chain *args, int batch, void *stream);
  * launch, [wgs][16] (0 start, 1 head prologue, 2 input tile, 3 + l after
  * layer l, 15 end), copied to host memory.  The product build returns -20. */
 int ndnet_pn_debug_stamps(unsigned long long *host, int wgs);
+int ndnet_pn_debug_stamps_clear(void);  /* zeroes them (timing builds; else -20) */
 
 /* The per-cloud steps between the chains (TNet FC heads ndtnet.py:53-60 and
  * the weight folds of pointnet_hip.py), for batch <= 16 clouds:

@@ -74,6 +74,11 @@ constexpr int kDepth6 = NDNET_PN_DEPTH6;  // the same for split-bf16 layers (3 f
 #define NDNET_PN_DEPTH6F 1
 #endif
 constexpr int kDepth6F = NDNET_PN_DEPTH6F;  // the same for prec 2 (fp32 weights split in registers)
+#ifdef NDNET_PN_NO_X6F  // A/B: a build without the prec-2 code paths (smaller kernel)
+constexpr bool kX6F = false;
+#else
+constexpr bool kX6F = true;
+#endif
 static_assert(kWaves % kRowBlocks == 0, "every row group has whole column groups");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -155,12 +160,22 @@ struct LayerCtx {
   int KG, N, relu, prec;           // KG: 16-row k-groups (prec 0) or 32-row (prec 1)
 };
 
-__device__ inline LayerCtx layer_ctx(const ndnet_pn_chain& A, int l, int b) {
+// bias: the layer's (this cloud's) bias, staged in LDS by the kernel's prologue
+// The first weight step of a layer, loaded by each wave before the barrier
+// that closes the previous layer (its latency hides behind the barrier wait;
+// 16-wave 64-point build, where every layer's wave tile is one column block):
+// w6 for prec 1, w[0] for prec 0, w[0..1] for prec 2.
+struct Pre {
+  bool on;
+  f32x4 r0, r1, r2;  // prec 1: bf16x8 planes h, m, l (bit_cast); prec 0: r0; prec 2: r0, r1
+};
+
+__device__ inline LayerCtx layer_ctx(const ndnet_pn_chain& A, int l, int b, const float* bias) {
   const ndnet_pn_layer& L = A.L[l];
   LayerCtx C;
   C.w = reinterpret_cast<const f32x4*>(L.w + (int64_t)b * L.w_cloud_stride) + (threadIdx.x & 63);
   C.w6 = reinterpret_cast<const bf16x8*>(L.w + (int64_t)b * L.w_cloud_stride) + (threadIdx.x & 63);
-  C.bias = L.bias + (int64_t)b * L.bias_cloud_stride;
+  C.bias = bias;
   C.prec = L.prec;
   C.KG = L.prec ? L.K / 32 : L.K / 16;  // prec 1 and 2: 32-row k-groups
   C.N = L.N;
@@ -201,15 +216,14 @@ __device__ __attribute__((always_inline)) inline void mma_kgroup(f32x4 (&acc)[RB
 template <int RB, int NB, class Epi>
 __device__ __attribute__((always_inline)) inline void run_tiles(f32x4 (&acc)[RB][NB], const f32x4* __restrict__ w,
                                                                 int KG, int kg0, int nkg, int cb0, int cbs,
-                                                                int nchunk, const float* abase, int pin, Epi epi) {
+                                                                int nchunk, const float* abase, int pin, Epi epi,
+                                                                Pre pre = {}) {
   const int T = nchunk * nkg;
   const int64_t jstride = (int64_t)KG * 64;
   const int64_t chunk_jump = ((int64_t)cbs * KG - (nkg - 1)) * 64;
   const f32x4* lp = w + ((int64_t)cb0 * KG + kg0) * 64;  // the next load's step
   int lkk = 0, lleft = T;
-  auto load = [&](f32x4 (&bw)[NB]) {
-#pragma unroll
-    for (int j = 0; j < NB; j++) bw[j] = lp[j * jstride];
+  auto advance = [&]() {
     if (lleft > 1) {
       lleft--;
       if (++lkk == nkg) {
@@ -219,6 +233,11 @@ __device__ __attribute__((always_inline)) inline void run_tiles(f32x4 (&acc)[RB]
         lp += 64;
       }
     }
+  };
+  auto load = [&](f32x4 (&bw)[NB]) {
+#pragma unroll
+    for (int j = 0; j < NB; j++) bw[j] = lp[j * jstride];
+    advance();
   };
   // A fragments are software-pipelined one step ahead too (the A region is
   // read-only during the layer, so the prefetch may run into the next chunk)
@@ -244,7 +263,14 @@ __device__ __attribute__((always_inline)) inline void run_tiles(f32x4 (&acc)[RB]
   load_a();
   f32x4 bq[kDepth][NB];
 #pragma unroll
-  for (int i = 0; i < kDepth; i++) load(bq[i]);
+  for (int i = 0; i < kDepth; i++) {
+    if (NB == 1 && i == 0 && pre.on) {  // the first step, prefetched by the caller
+      bq[0][0] = pre.r0;
+      advance();
+    } else {
+      load(bq[i]);
+    }
+  }
   for (int t = 0; t < T; t += kDepth) {
 #pragma unroll
     for (int i = 0; i < kDepth; i++) {
@@ -476,21 +502,15 @@ template <int RB, int NB, class Epi>
 __device__ __attribute__((always_inline)) inline void run_tiles_x6(f32x4 (&acc)[RB][NB],
                                                                    const bf16x8* __restrict__ w, int KG, int kg0,
                                                                    int nkg, int cb0, int cbs, int nchunk,
-                                                                   const __bf16* abase, int pitchb, Epi epi) {
+                                                                   const __bf16* abase, int pitchb, Epi epi,
+                                                                   Pre pre = {}) {
   const int T = nchunk * nkg;
   const int plane = kP * pitchb;
   const int64_t jstride = (int64_t)KG * 3 * 64;
   const int64_t chunk_jump = ((int64_t)cbs * KG - (nkg - 1)) * 3 * 64;
   const bf16x8* lp = w + ((int64_t)cb0 * KG + kg0) * 3 * 64;
   int lkk = 0, lleft = T;
-  auto load = [&](bf16x8 (&bw)[NB][3]) {
-#ifdef NDNET_PN_EXP_NOB  // timing experiment only (wrong results): weights loaded once per layer
-    if (lleft == T)
-#endif
-#pragma unroll
-    for (int j = 0; j < NB; j++)
-#pragma unroll
-      for (int p = 0; p < 3; p++) bw[j][p] = lp[j * jstride + p * 64];
+  auto advance = [&]() {
     if (lleft > 1) {
       lleft--;
       if (++lkk == nkg) {
@@ -500,6 +520,16 @@ __device__ __attribute__((always_inline)) inline void run_tiles_x6(f32x4 (&acc)[
         lp += 3 * 64;
       }
     }
+  };
+  auto load = [&](bf16x8 (&bw)[NB][3]) {
+#ifdef NDNET_PN_EXP_NOB  // timing experiment only (wrong results): weights loaded once per layer
+    if (lleft == T)
+#endif
+#pragma unroll
+    for (int j = 0; j < NB; j++)
+#pragma unroll
+      for (int p = 0; p < 3; p++) bw[j][p] = lp[j * jstride + p * 64];
+    advance();
   };
   int kk = 0, c = 0;
   auto step = [&](const bf16x8 (&bw)[NB][3]) {
@@ -512,7 +542,16 @@ __device__ __attribute__((always_inline)) inline void run_tiles_x6(f32x4 (&acc)[
   };
   bf16x8 bq[kDepth6][NB][3];
 #pragma unroll
-  for (int i = 0; i < kDepth6; i++) load(bq[i]);
+  for (int i = 0; i < kDepth6; i++) {
+    if (NB == 1 && i == 0 && pre.on) {  // the first step, prefetched by the caller
+      bq[0][0][0] = __builtin_bit_cast(bf16x8, pre.r0);
+      bq[0][0][1] = __builtin_bit_cast(bf16x8, pre.r1);
+      bq[0][0][2] = __builtin_bit_cast(bf16x8, pre.r2);
+      advance();
+    } else {
+      load(bq[i]);
+    }
+  }
   for (int t = 0; t < T; t += kDepth6) {
 #pragma unroll
     for (int i = 0; i < kDepth6; i++) {
@@ -547,18 +586,15 @@ template <int RB, int NB, class Epi>
 __device__ __attribute__((always_inline)) inline void run_tiles_x6f(f32x4 (&acc)[RB][NB],
                                                                     const f32x4* __restrict__ w, int KG, int kg0,
                                                                     int nkg, int cb0, int cbs, int nchunk,
-                                                                    const __bf16* abase, int pitchb, Epi epi) {
+                                                                    const __bf16* abase, int pitchb, Epi epi,
+                                                                    Pre pre = {}) {
   const int T = nchunk * nkg;
   const int plane = kP * pitchb;
   const int64_t jstride = (int64_t)KG * 2 * 64;
   const int64_t chunk_jump = ((int64_t)cbs * KG - (nkg - 1)) * 2 * 64;
   const f32x4* lp = w + ((int64_t)cb0 * KG + kg0) * 2 * 64;
   int lkk = 0, lleft = T;
-  auto load = [&](f32x4 (&raw)[NB][2]) {
-#pragma unroll
-    for (int j = 0; j < NB; j++)
-#pragma unroll
-      for (int h = 0; h < 2; h++) raw[j][h] = lp[j * jstride + h * 64];
+  auto advance = [&]() {
     if (lleft > 1) {
       lleft--;
       if (++lkk == nkg) {
@@ -568,6 +604,13 @@ __device__ __attribute__((always_inline)) inline void run_tiles_x6f(f32x4 (&acc)
         lp += 2 * 64;
       }
     }
+  };
+  auto load = [&](f32x4 (&raw)[NB][2]) {
+#pragma unroll
+    for (int j = 0; j < NB; j++)
+#pragma unroll
+      for (int h = 0; h < 2; h++) raw[j][h] = lp[j * jstride + h * 64];
+    advance();
   };
   int kk = 0, c = 0;
   auto step = [&](const f32x4 (&raw)[NB][2]) {
@@ -583,7 +626,15 @@ __device__ __attribute__((always_inline)) inline void run_tiles_x6f(f32x4 (&acc)
   };
   f32x4 rq[kDepth6F][NB][2];
 #pragma unroll
-  for (int i = 0; i < kDepth6F; i++) load(rq[i]);
+  for (int i = 0; i < kDepth6F; i++) {
+    if (NB == 1 && i == 0 && pre.on) {  // the first step, prefetched by the caller
+      rq[0][0][0] = pre.r0;
+      rq[0][0][1] = pre.r1;
+      advance();
+    } else {
+      load(rq[i]);
+    }
+  }
   for (int t = 0; t < T; t += kDepth6F) {
 #pragma unroll
     for (int i = 0; i < kDepth6F; i++) {
@@ -599,7 +650,7 @@ __device__ __attribute__((always_inline)) inline void run_tiles_x6f(f32x4 (&acc)
 // 4 RB column groups of waves; N in chunks of (column groups x NB x 16).
 template <int RB, int NB>
 __device__ void plain_layer(const LayerCtx& C, int in, int pin, int out, int pout, float* gmax, int rows_valid,
-                            bool out_planes) {
+                            bool out_planes, Pre pre = {}) {
   constexpr int WR = kRowBlocks / RB, WC = kWaves / WR, CB = WC * NB;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wr = wave / WC, wc = wave % WC;
@@ -621,11 +672,11 @@ __device__ void plain_layer(const LayerCtx& C, int in, int pin, int out, int pou
   if (C.prec) {  // input: three bf16 planes of pitch K + kPadB (the producer's N + kPadB)
     const int pb = 32 * C.KG + kPadB;
     const __bf16* abase6 = reinterpret_cast<const __bf16*>(g_smem + in) + (row0 + cl) * pb + 8 * kq;
-    if (C.prec == 2) run_tiles_x6f<RB, NB>(acc, C.w, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase6, pb, epi);
-    else run_tiles_x6<RB, NB>(acc, C.w6, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase6, pb, epi);
+    if (kX6F && C.prec == 2) run_tiles_x6f<RB, NB>(acc, C.w, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase6, pb, epi, pre);
+    else run_tiles_x6<RB, NB>(acc, C.w6, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase6, pb, epi, pre);
   } else {
     const float* abase = g_smem + in + (row0 + cl) * pin + 4 * kq;
-    run_tiles<RB, NB>(acc, C.w, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase, pin, epi);
+    run_tiles<RB, NB>(acc, C.w, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase, pin, epi, pre);
   }
 }
 
@@ -642,7 +693,7 @@ __host__ __device__ inline int fbuf_floats(int qprec) {
 // activation never needs LDS of its own.  One barrier per chunk.
 template <int RB, int NB>
 __device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin, int fbuf, int out, int pout,
-                           float* gmax, int rows_valid, bool out_planes) {
+                           float* gmax, int rows_valid, bool out_planes, Pre pre = {}) {
   constexpr int kFP = kFuseNC + kPadF;
   constexpr int WR = kRowBlocks / RB, WC = kWaves / WR;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -666,9 +717,11 @@ __device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin
       if (Q.prec) store_cols_planes<1, PNB>(a, P.bias, 64 * f + 16 * pwc, P.relu, prow0, fb, kFuseNC + kPadB, 16 * pwc);
       else store_cols<1, PNB>(a, P.bias, 64 * f + 16 * pwc, P.relu, prow0, fb, kFP, 16 * pwc);
     };
-    if (P.prec == 2) run_tiles_x6f<1, PNB>(acc1, P.w, P.KG, 0, P.KG, 4 * f + pwc, 0, 1, ain6, 32 * P.KG + kPadB, epi);
-    else if (P.prec) run_tiles_x6<1, PNB>(acc1, P.w6, P.KG, 0, P.KG, 4 * f + pwc, 0, 1, ain6, 32 * P.KG + kPadB, epi);
-    else run_tiles<1, PNB>(acc1, P.w, P.KG, 0, P.KG, 4 * f + pwc, 0, 1, ain, pin, epi);
+    Pre pf = pre;
+    if (f != 0) pf.on = false;
+    if (kX6F && P.prec == 2) run_tiles_x6f<1, PNB>(acc1, P.w, P.KG, 0, P.KG, 4 * f + pwc, 0, 1, ain6, 32 * P.KG + kPadB, epi, pf);
+    else if (P.prec) run_tiles_x6<1, PNB>(acc1, P.w6, P.KG, 0, P.KG, 4 * f + pwc, 0, 1, ain6, 32 * P.KG + kPadB, epi, pf);
+    else run_tiles<1, PNB>(acc1, P.w, P.KG, 0, P.KG, 4 * f + pwc, 0, 1, ain, pin, epi, pf);
   };
   f32x4 acc2[RB][NB];
   zero_acc(acc2);
@@ -679,7 +732,7 @@ __device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin
       if (Q.prec) {
         const __bf16* af6 = reinterpret_cast<const __bf16*>(g_smem + fbuf + (f & 1) * fbsz) +
                             (qrow0 + cl) * (kFuseNC + kPadB) + 8 * kq;
-        if (Q.prec == 2)
+        if (kX6F && Q.prec == 2)
           run_tiles_x6f<RB, NB>(acc2, Q.w, Q.KG, 2 * f, 2, qwc * NB, 0, 1, af6, kFuseNC + kPadB,
                                 [](f32x4 (&)[RB][NB], int) {});
         else
@@ -699,6 +752,55 @@ __device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin
   else store_cols<RB, NB>(acc2, Q.bias, 16 * qwc * NB, Q.relu, qrow0, out, pout, 16 * qwc * NB);
 }
 
+// Loads the first weight step this wave runs in layer l (the 16-wave 64-point
+// build; others leave pre off): the column block plain_layer<RB, 1> /
+// fused_pair's first chunk gives the wave, at k-group 0 -- the address
+// run_tiles* would load first.
+__device__ inline void prefetch_first(const ndnet_pn_chain& A, int l, int b, Pre& pre) {
+  pre.on = false;
+#ifndef NDNET_PN_PREFETCH  // off by default: measured 1-2 us slower per chain (profiles/r03e_stamps_ab.txt)
+  return;
+#endif
+  if constexpr (kP == 64 && kWaves == 16) {
+    const ndnet_pn_layer& L = A.L[l];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int cb0;
+    if (L.fuse_next) {
+      cb0 = wave % 4;  // fused_pair: PWC = 4 column groups of PNB = 1, chunk 0
+    } else {
+      const int WC = L.N % 256 == 0 ? 16 : L.N % 128 == 0 ? 8 : 4;  // plain_layer<4 | 2 | 1, 1>
+      cb0 = wave % WC;
+      if (L.N < WC * 16 && cb0 * 16 >= L.N) return;  // an idle wave of a narrow layer
+    }
+    const int KG = L.prec ? L.K / 32 : L.K / 16;
+    const float* wb = L.w + (int64_t)b * L.w_cloud_stride;
+    if (L.prec == 1) {
+      const bf16x8* q = reinterpret_cast<const bf16x8*>(wb) + lane + (int64_t)cb0 * KG * 3 * 64;
+      pre.r0 = __builtin_bit_cast(f32x4, q[0]);
+      pre.r1 = __builtin_bit_cast(f32x4, q[64]);
+      pre.r2 = __builtin_bit_cast(f32x4, q[128]);
+    } else if (L.prec == 2) {
+      const f32x4* q = reinterpret_cast<const f32x4*>(wb) + lane + (int64_t)cb0 * KG * 2 * 64;
+      pre.r0 = q[0];
+      pre.r1 = q[64];
+    } else {
+      pre.r0 = (reinterpret_cast<const f32x4*>(wb) + lane + (int64_t)cb0 * KG * 64)[0];
+    }
+    pre.on = true;
+  }
+}
+
+// The barrier between layers: LDS traffic retired, then s_barrier, with no
+// vmcnt drain (__syncthreads' fence waits for every vector-memory op, the
+// next layer's prefetched weights included; nothing between layers is a
+// global store -- the max-pool atomics come only in the last layer, which
+// closes with __syncthreads).
+__device__ inline void layer_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // Floats of LDS region r: fp32 activations (pitch width + kPadF) or, when it ever
 // holds a split-bf16 layer's input (planes bit r), three bf16 planes.
 __host__ __device__ inline int region_floats(int width, int planes) {
@@ -706,21 +808,100 @@ __host__ __device__ inline int region_floats(int width, int planes) {
   return planes && b16 > f32 ? b16 : f32;
 }
 
-__global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int planes, int fbuf) {
+// Layer 0 of the chains (conv1 of ndtnet.py:47 / :148, K = 3 or 12 inputs
+// padded to 16, N = 64) runs on the VALU straight from the input rows: each
+// thread computes 4 channels of one point from the point's 12 input floats
+// (three dwordx4 loads) and W0^T staged in LDS row-major ([16][64]) -- no
+// input tile, no MFMA fragment loads, one memory round trip for x, W0, every
+// layer's bias and (chain B) the TNet(3) tail.  The products are fp32 FMAs
+// (k ascending); the MFMA path computed the same sums in another order.
+__host__ __device__ inline bool valu_layer0(const ndnet_pn_chain& A) {
+#ifdef NDNET_PN_NO_VALU0  // A/B: layer 0 on the MFMA path from an LDS input tile
+  return false;
+#endif
+  return A.num_layers > 1 && A.L[0].K == 16 && A.L[0].N == 64 && A.L[0].prec == 0 && !A.L[0].fuse_next &&
+         A.in_cols <= 12 && A.x_ld % 4 == 0;
+}
+
+// LDS floats of the VALU layer-0 prologue scratch (W0^T [16][64] + bias [64]),
+// overlaid on activation region 0, which layer 0 neither reads nor writes.
+constexpr int kValu0Floats = 16 * 64 + 64;
+
+// Floats of activation region 0 (kernel and launcher): room for the layer-0
+// prologue's scratch (+ chain B's t1) when layer 0 runs on the VALU.
+__host__ __device__ inline int region0_floats(const ndnet_pn_chain& A, int planes) {
+  const int r = region_floats(A.max_width, planes & 1);
+  return valu_layer0(A) && r < kValu0Floats + 16 ? kValu0Floats + 16 : r;
+}
+
+__global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int planes, int fbuf, int bias_base) {
   const int b = blockIdx.y;
   const int p0 = blockIdx.x * kP;
   PN_STAMP(0);
-  // LDS: activation region 0 | region 1 | [fused-chunk double buffer]
+  // LDS: activation region 0 | region 1 | [fused-chunk double buffer] | biases of layers 1..
   const int pitch0 = A.max_width + kPadF, pitch1 = A.max_width2 + kPadF;
-  const int reg[2] = {0, region_floats(A.max_width, planes & 1)};
-  // fbuf (the fused pair's chunks): float offset chosen by the launcher
-  // input tile, zero-filled to the first layer's K (a multiple of 16)
+  const int reg[2] = {0, region0_floats(A, planes)};
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // every layer's bias (this cloud's) -> LDS at boff[l] (layer 0's into the
+  // prologue scratch when it runs on the VALU); the loads are issued together
+  // with the prologue's, so the epilogues never wait on a global bias read
+  int boff[NDNET_PN_MAX_LAYERS];
+  {
+    int o = bias_base;
+#pragma unroll
+    for (int l = 0; l < NDNET_PN_MAX_LAYERS; l++) {
+      boff[l] = o;
+      if (l < A.num_layers) o += A.L[l].N;
+    }
+    float bv[NDNET_PN_MAX_LAYERS][2];
+#pragma unroll
+    for (int l = 0; l < NDNET_PN_MAX_LAYERS; l++)
+#pragma unroll
+      for (int i = 0; i < 2; i++) {
+        const int e = threadIdx.x + i * kThreads;
+        bv[l][i] = (l < A.num_layers && e < A.L[l].N) ? A.L[l].bias[(int64_t)b * A.L[l].bias_cloud_stride + e] : 0.0f;
+      }
+#pragma unroll
+    for (int l = 0; l < NDNET_PN_MAX_LAYERS; l++)
+#pragma unroll
+      for (int i = 0; i < 2; i++) {
+        const int e = threadIdx.x + i * kThreads;
+        if (l < A.num_layers && e < A.L[l].N) g_smem[boff[l] + e] = bv[l][i];
+      }
+  }
+  const bool v0 = valu_layer0(A);
+  Pre pre;  // the next layer's first weight step (prefetched before each layer barrier)
+  prefetch_first(A, v0 ? 1 : 0, b, pre);
+  float* const s_w0 = g_smem;  // v0: W0^T [16][64] row-major, in region 0
+  // v0: this thread's point rows (t / 16 + pass * kThreads / 16) and 4 output
+  // channels (4 (t % 16) ..)
+  constexpr int kV0Pass = kP * 16 / kThreads;
+  static_assert(kV0Pass >= 1 && kV0Pass * kThreads == kP * 16, "whole layer-0 passes");
+  const int vq = threadIdx.x & 15;
+  f32x4 xin[kV0Pass][3] = {};
+  if (v0) {
+#pragma unroll
+    for (int ps = 0; ps < kV0Pass; ps++) {
+      const int vr = (threadIdx.x >> 4) + ps * (kThreads / 16);
+      const int p = p0 + vr;
+      if (p < A.num_points) {
+        const f32x4* xr = reinterpret_cast<const f32x4*>(A.x + ((int64_t)b * A.num_points + p) * A.x_ld);
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+          if (4 * i < A.in_cols) xin[ps][i] = xr[i];
+      }
+    }
+    if (!A.head_h2 && threadIdx.x < 256) {  // W0^T fragment-major [cb][kq][cl][s] -> row-major [k][n]
+      const f32x4 wv = reinterpret_cast<const f32x4*>(A.L[0].w + (int64_t)b * A.L[0].w_cloud_stride)[threadIdx.x];
+      const int cb = threadIdx.x >> 6, kq = (threadIdx.x >> 4) & 3, cl = threadIdx.x & 15;
+#pragma unroll
+      for (int s = 0; s < 4; s++) s_w0[(4 * kq + s) * 64 + 16 * cb + cl] = wv[s];
+    }
+  }
   if (A.head_h2) {
     // TNet(3)'s tail for this cloud (ndnet_pn_head3_run's work, ndtnet.py:57-60):
     // t1 = h2 @ W3^T + b3, then conv1 with t1 folded into layer 0's weights
-    float* const s_t1 = g_smem;  // [9]: the dynamic LDS is free until the input tile (no static LDS:
-                                 // a chain may use all 160 KB dynamically)
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float* const s_t1 = g_smem + (v0 ? kValu0Floats : 0);  // [9] (v0: past the scratch; region 0 is free until layer 1)
     const int M = A.head_kin * A.head_nout, total = 16 * A.head_nout;  // one k-group, K padded to 16
     // this thread's fold element(s): basis values loaded ahead of the fc3 reduction
     const int e0 = threadIdx.x;
@@ -747,45 +928,93 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
     }
     __syncthreads();
     float* w1 = const_cast<float*>(A.L[0].w) + (int64_t)b * A.L[0].w_cloud_stride;
-    if (e0 < total) {
-      float acc = 0.0f;
-#pragma unroll
-      for (int a = 0; a < 9; a++) acc += s_t1[a] * bas[a];
-      w1[e0] = acc;
-    }
-    for (int e = e0 + kThreads; e < total; e += kThreads) {
+    // v0: only the cloud's first workgroup publishes the fragment-major W0^T
+    // (chains C and D read it in later launches); every workgroup keeps its own
+    // copy in LDS.  Otherwise every workgroup stores it and its layer 0 reads it.
+    const bool publish = !v0 || blockIdx.x == 0;
+    for (int e = e0; e < total; e += kThreads) {
       const int cb = e >> 8, ln = (e >> 2) & 63, k = 4 * (ln >> 4) + (e & 3), n = 16 * cb + (ln & 15);
       float acc = 0.0f;
-      if (k < A.head_kin) {
+      if (e == e0) {
+#pragma unroll
+        for (int a = 0; a < 9; a++) acc += s_t1[a] * bas[a];
+      } else if (k < A.head_kin) {
 #pragma unroll
         for (int a = 0; a < 9; a++) acc += s_t1[a] * A.head_basis[a * M + k * A.head_nout + n];
       }
-      w1[e] = acc;
+      if (publish) w1[e] = acc;
+      if (v0) s_w0[k * 64 + n] = acc;
     }
-    // layer 0 reads these weights back: __syncthreads' workgroup-scope release
+    // !v0: layer 0 reads these weights back: __syncthreads' workgroup-scope release
     // / acquire orders this workgroup's stores before its loads (same CU; no
     // lines of them are cached here yet).  Every workgroup of the cloud stores
     // the same bits.  (A device-scope __threadfence here writes back the L2:
     // measured +60 us per launch.)
-    __syncthreads();
     PN_STAMP(1);
   }
-  const int K0 = A.L[0].K;
-  for (int e = threadIdx.x; e < kP * K0; e += kThreads) {
-    const int r = e / K0, c = e % K0;
-    const int p = p0 + r;
-    float v = 0.0f;
-    if (p < A.num_points && c < A.in_cols) v = A.x[((int64_t)b * A.num_points + p) * A.x_ld + c];
-    g_smem[r * pitch0 + c] = v;
+  __syncthreads();
+  if (v0) {
+    // layer 0: out = act(x W0^T + b0) for 4 channels of one point, into region 1
+    // as the next layer reads it (three bf16 planes, or fp32)
+#pragma unroll
+    for (int ps = 0; ps < kV0Pass; ps++) {
+      const int vr = (threadIdx.x >> 4) + ps * (kThreads / 16);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const float xs[12] = {xin[ps][0][0], xin[ps][0][1], xin[ps][0][2], xin[ps][0][3], xin[ps][1][0], xin[ps][1][1],
+                            xin[ps][1][2], xin[ps][1][3], xin[ps][2][0], xin[ps][2][1], xin[ps][2][2], xin[ps][2][3]};
+#pragma unroll
+      for (int k = 0; k < 12; k++) {
+        if (k < A.in_cols) {
+          const f32x4 w = *reinterpret_cast<const f32x4*>(s_w0 + k * 64 + 4 * vq);
+#pragma unroll
+          for (int j = 0; j < 4; j++) acc[j] = fmaf(xs[k], w[j], acc[j]);
+        }
+      }
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(g_smem + boff[0] + 4 * vq);
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        acc[j] += bb[j];
+        if (A.L[0].relu) acc[j] = fmaxf(acc[j], 0.0f);
+      }
+      const int out = reg[1];
+      if (A.L[1].prec) {  // three bf16 planes, pitch 64 + kPadB
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        const int pb = 64 + kPadB;
+        __bf16* const base = reinterpret_cast<__bf16*>(g_smem + out) + vr * pb + 4 * vq;
+        bf16x4 h4, m4, l4;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          __bf16 hh, mm, ll;
+          split3(acc[j], hh, mm, ll);
+          h4[j] = hh;
+          m4[j] = mm;
+          l4[j] = ll;
+        }
+        *reinterpret_cast<bf16x4*>(base) = h4;
+        *reinterpret_cast<bf16x4*>(base + kP * pb) = m4;
+        *reinterpret_cast<bf16x4*>(base + 2 * kP * pb) = l4;
+      } else {
+        *reinterpret_cast<f32x4*>(g_smem + out + vr * pitch1 + 4 * vq) = acc;
+      }
+    }
+  } else {
+    const int K0 = A.L[0].K;
+    for (int e = threadIdx.x; e < kP * K0; e += kThreads) {
+      const int r = e / K0, c = e % K0;
+      const int p = p0 + r;
+      float v = 0.0f;
+      if (p < A.num_points && c < A.in_cols) v = A.x[((int64_t)b * A.num_points + p) * A.x_ld + c];
+      g_smem[r * pitch0 + c] = v;
+    }
   }
   __syncthreads();
   PN_STAMP(2);
   const int rows_valid = A.num_points - p0;
   float* const gmax_b = A.mode == 0 ? A.gmax + (int64_t)b * A.gmax_ld : nullptr;
-  for (int l = 0; l < A.num_layers; l++) {
+  for (int l = v0 ? 1 : 0; l < A.num_layers; l++) {
     const int in = reg[l & 1], pin = (l & 1) ? pitch1 : pitch0;
     if (A.L[l].fuse_next) {  // layers l and l + 1 together; l + 1 writes region (l + 2) & 1
-      const LayerCtx P = layer_ctx(A, l, b), Q = layer_ctx(A, l + 1, b);
+      const LayerCtx P = layer_ctx(A, l, b, g_smem + boff[l]), Q = layer_ctx(A, l + 1, b, g_smem + boff[l + 1]);
       const bool last = l + 2 == A.num_layers;
       const int out = reg[(l + 2) & 1], pout = ((l + 2) & 1) ? pitch1 : pitch0;
       float* gm = (last && gmax_b) ? gmax_b : nullptr;
@@ -796,13 +1025,13 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
         if (Q.N == 256) fused_pair<2, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op);
         else fused_pair<1, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op);
       } else {
-        if (Q.N == 256) fused_pair<4, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op);
-        else if (Q.N > 64) fused_pair<2, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op);
-        else fused_pair<1, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op);
+        if (Q.N == 256) fused_pair<4, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op, pre);
+        else if (Q.N > 64) fused_pair<2, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op, pre);
+        else fused_pair<1, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op, pre);
       }
       l++;
     } else {
-      const LayerCtx C = layer_ctx(A, l, b);
+      const LayerCtx C = layer_ctx(A, l, b, g_smem + boff[l]);
       const bool last = l + 1 == A.num_layers;
       const int out = reg[(l + 1) & 1], pout = ((l + 1) & 1) ? pitch1 : pitch0;
       float* gm = (last && gmax_b) ? gmax_b : nullptr;
@@ -826,12 +1055,21 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
         else if (C.N % 64 == 0) plain_layer<2, 1>(C, in, pin, out, pout, gm, rows_valid, op);
         else plain_layer<1, 1>(C, in, pin, out, pout, gm, rows_valid, op);  // N = 32
       } else {
-        if (C.N % 256 == 0) plain_layer<4, 1>(C, in, pin, out, pout, gm, rows_valid, op);
-        else if (C.N % 128 == 0) plain_layer<2, 1>(C, in, pin, out, pout, gm, rows_valid, op);
-        else plain_layer<1, 1>(C, in, pin, out, pout, gm, rows_valid, op);  // N % 64 == 0, or N = 32 (half idle)
+        if (C.N % 256 == 0) plain_layer<4, 1>(C, in, pin, out, pout, gm, rows_valid, op, pre);
+        else if (C.N % 128 == 0) plain_layer<2, 1>(C, in, pin, out, pout, gm, rows_valid, op, pre);
+        else plain_layer<1, 1>(C, in, pin, out, pout, gm, rows_valid, op, pre);  // N % 64 == 0, or N = 32 (half idle)
       }
     }
+#ifdef NDNET_PN_PREFETCH
+    if (l + 1 < A.num_layers) {
+      prefetch_first(A, l + 1, b, pre);
+      layer_barrier();
+    } else {
+      __syncthreads();
+    }
+#else
     __syncthreads();
+#endif
     PN_STAMP(3 + l);
   }
   if (A.clear && blockIdx.x == 0 && blockIdx.y == 0)
@@ -1262,6 +1500,16 @@ int ndnet_pn_fold64_run(const float* t2, const float* rhs, float* out, int batch
 
 // One fused point-MLP chain over `batch` clouds on `stream` (see pointnet.h).
 
+// Timing builds: zeroes the stamp array (before a launch whose stamps are read)
+int ndnet_pn_debug_stamps_clear(void) {
+#ifdef NDNET_PN_STAMPS
+  static unsigned long long zeros[kStampWgs][16];
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_pn_stamps), zeros, sizeof(zeros)) == hipSuccess ? 0 : -21;
+#else
+  return -20;
+#endif
+}
+
 // Timing builds (-DNDNET_PN_STAMPS): copies the stamps of the last chain
 // launch, [wgs][16] u64, to host memory; the product build returns -20.
 int ndnet_pn_debug_stamps(unsigned long long* host, int wgs) {
@@ -1323,7 +1571,8 @@ int ndnet_pn_chain_run_t32(const ndnet_pn_chain* args, int batch, void* stream) 
   // LDS: region 0 | region 1, then the fused pair's chunks.  Q writes the
   // region P reads, after its last chunk, so the chunks may start right after
   // P's input inside that region (and run past its end when it is region 1)
-  const int r0f = region_floats(args->max_width, planes & 1), r1f = region_floats(args->max_width2, planes & 2);
+  const int r0f = region0_floats(*args, planes);
+  const int r1f = region_floats(args->max_width2, planes & 2);
   int fbuf_off = r0f + r1f;
   size_t total = (size_t)r0f + r1f;
   if (has_fuse) {
@@ -1336,6 +1585,15 @@ int ndnet_pn_chain_run_t32(const ndnet_pn_chain* args, int batch, void* stream) 
     if (r == 1 || inside + fb <= r0f) fbuf_off = inside;
     total = fbuf_off + (size_t)fb > total ? fbuf_off + (size_t)fb : total;
   }
+  // every layer's bias after the other regions (layer 0's too: the prologue
+  // reads it there when layer 0 runs on the MFMA path)
+  const int bias_base = (int)((total + 3) & ~(size_t)3);
+  int nbias = 0;
+  for (int l = 0; l < args->num_layers; l++) {
+    if (args->L[l].N > 2 * kThreads) return -20;  // the prologue stages <= 2 bias values per thread and layer
+    nbias += args->L[l].N;
+  }
+  total = (size_t)bias_base + nbias;
   const size_t lds = sizeof(float) * total;
   static bool attr_set = false;
   if (!attr_set) {
@@ -1346,7 +1604,7 @@ int ndnet_pn_chain_run_t32(const ndnet_pn_chain* args, int batch, void* stream) 
   }
   if (lds > 160 * 1024) return -20;
   dim3 grid((args->num_points + kP - 1) / kP, batch);
-  k_pn_chain<<<grid, kThreads, lds, (hipStream_t)stream>>>(*args, planes, fbuf_off);
+  k_pn_chain<<<grid, kThreads, lds, (hipStream_t)stream>>>(*args, planes, fbuf_off, bias_base);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     fprintf(stderr, "ndnet_amd: k_pn_chain launch failed: %s\n", hipGetErrorString(e));

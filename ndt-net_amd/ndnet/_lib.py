@@ -110,6 +110,7 @@ POINTNET_EXPORTS: dict = {
     "ndnet_pn_chain_run": (_I, [_P, _I, _P]),
     "ndnet_pn_chain_run_t32": (_I, [_P, _I, _P]),
     "ndnet_pn_debug_stamps": (_I, [_P, _I]),
+    "ndnet_pn_debug_stamps_clear": (_I, []),
     # include/ndnet_ingest.h (host code: the ASCII-PLY reader)
     "ndnet_ply_count": (_I, [ctypes.c_char_p, _I, ctypes.POINTER(_U64)]),
     "ndnet_ply_read": (_I, [ctypes.c_char_p, _I, _I, _P, _P, _U64, ctypes.POINTER(_U64), _I]),

@@ -534,16 +534,49 @@ def _glue_torch(W, ws, B: int):
     return head_a, head_b, seg_bias
 
 
+# Workspace slot of the forwards launched from now on (``workspace_slot``).
+_slot = 0
+
+
+class workspace_slot:
+    """``with workspace_slot(i):`` -- forwards launched inside use workspace
+    slot ``i`` of their shape.  A forward's workspace (the max-pool buffer
+    that chain D re-arms, the FC-head intermediates, the per-cloud folded
+    weights and the prebuilt argument blocks) is cached per (batch, points,
+    device, slot) and is written by every forward of that key, so forwards
+    that may run CONCURRENTLY -- launched on different streams with no order
+    between them, e.g. two halves of a batch captured on two streams of one
+    graph -- must use different slots; forwards in stream order may share one
+    (the default slot 0).  This was the hazard behind round 2's crashed
+    two-stream capture: both halves shared one slot, so one half's chain D
+    re-armed the max-pool buffer the other half was still reducing into."""
+
+    def __init__(self, slot: int) -> None:
+        self.slot, self.prev = int(slot), None
+
+    def __enter__(self):
+        global _slot
+        self.prev, _slot = _slot, self.slot
+        return self
+
+    def __exit__(self, *exc):
+        global _slot
+        _slot = self.prev
+        return False
+
+
 def segmentation_forward(model, points: torch.Tensor, covariances: torch.Tensor, chain=None) -> torch.Tensor:
     """model(points [B,N,3], covariances [B,N,9]) -> log-probs [B,N,C+1], eval mode.
 
     ``chain``: None runs every step on the HIP kernels; a chain emulator
-    (``_chain_torch``) runs the chains and the per-cloud steps as torch ops."""
+    (``_chain_torch``) runs the chains and the per-cloud steps as torch ops.
+    Concurrent forwards (different streams, no order) need different
+    ``workspace_slot``s."""
     cache = _folded(model)
     W = cache["W"]
     B, N, _ = points.shape
     dev = points.device
-    key = (B, N, dev)
+    key = (B, N, dev, _slot)
     ws = cache["ws"].get(key)
     if ws is None:
         ws = cache["ws"][key] = _Workspace(W, B, N, dev)

@@ -206,3 +206,53 @@ def test_legacy_entry_points_run_concurrently():
         pc, cov = ref.downsample(500)
         assert np.array_equal(res[i][0], pc) and np.array_equal(res[i][1], cov, equal_nan=True)
         ref.cleanup()
+
+
+def test_two_stream_forward_capture_matches_eager():
+    """two forwards captured on two streams of one graph
+    (the two halves of a batch, forked from and joined back into the capture
+    stream), each in its own workspace slot, replay to exactly the eager
+    forwards of the halves.  Concurrent forwards in ONE slot share the
+    max-pool buffer, FC-head intermediates and folded weights (the round-2
+    crash): pointnet_hip.workspace_slot keeps them apart."""
+    import torch
+    from ndnet.models import pointnet_hip
+    from ndnet.preprocessing.ndtnet_preprocessing import ndt_preprocessing
+    from ndnet.synthetic import make_batch
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(1)
+    m = _model(F=768, C=28, seed=5)
+    B, n, k = 8, 20_000, 400
+    with torch.no_grad():
+        p, c, _ = ndt_preprocessing(k, torch.from_numpy(make_batch("L", B, n, seed0=3)).to(dev))
+        rows = torch.cat((p, c), 2).contiguous()
+        halves = [rows[: B // 2].contiguous(), rows[B // 2:].contiguous()]
+        eager = [m(h[..., :3], h[..., 3:]).clone() for h in halves]
+    streams = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]
+
+    def step():
+        cur = torch.cuda.current_stream(dev)
+        outs = []
+        for i, (h, s) in enumerate(zip(halves, streams)):
+            s.wait_stream(cur)
+            with torch.cuda.stream(s), pointnet_hip.workspace_slot(i):
+                outs.append(m(h[..., :3], h[..., 3:]))
+        for s in streams:
+            cur.wait_stream(s)
+        return outs
+
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.no_grad(), torch.cuda.stream(side):
+        for _ in range(2):  # warm-up: both slots' workspaces exist before capture
+            step()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.no_grad(), torch.cuda.graph(g):
+        outs = step()
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        for o, e in zip(outs, eager):
+            assert torch.equal(o, e)

@@ -38,7 +38,7 @@ with torch.no_grad():
     model(x[..., :3], x[..., 3:])
     torch.cuda.synchronize()
 cache = ph._folded(model)
-ws = cache["ws"][(B, n, dev)]
+ws = cache["ws"][(B, n, dev, 0)]
 tiles = (n + 63) // 64
 wgs = B * tiles
 buf = np.zeros((wgs, 16), np.uint64)
@@ -49,6 +49,8 @@ for i, name in enumerate(ph.CHAIN_NAMES):
         if a.cold:
             junk.fill_(1.0)
         torch.cuda.synchronize()
+        buf[:] = 0
+        _lib.lib().ndnet_pn_debug_stamps_clear()
         out = torch.empty((B, n, 29), device=dev) if i == 3 else None
         with torch.no_grad():
             ws.chain(i, x, out=out)
@@ -59,7 +61,7 @@ for i, name in enumerate(ph.CHAIN_NAMES):
         s = buf.astype(np.int64)
         t0 = s[:, 0].min()
         spans.append((s[:, 15].max() - t0) * 10e-3)
-        idx = [j for j in range(16) if (s[:, j] > 0).all()]
+        idx = [j for j in range(16) if (s[:, j] > 0).all()]  # stamps this launch wrote
         phases.append((idx, s[:, idx] - t0))
     idx, rel = phases[-1]
     print(f"chain {name}: launch span median {np.median(spans):.2f} us (first start -> last end, reps {a.reps})")
