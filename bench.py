@@ -587,7 +587,6 @@ def main() -> None:
             "vs_baseline": None,
             "dtype": (f"f64 NDT; PointNet fp32-accurate split-bf16x3 (6 products) on {11 if pointnet_hip.X6_NARROW else 7}"
                       " per-point layers, fp32 MFMA on the K=16 first layers and the TNet / seg-bias FC layers"
-                      + ("; their weights streamed as fp32, split in registers" if pointnet_hip.WEIGHT_F32 else "")
                       if pointnet_hip.SPLIT_BF16 else "f64 NDT; PointNet fp32 MFMA"),
             "data": f"synthetic {args.kind} clouds (SURVEY 8d), random-init weights",
             "config": {"workload": (f"batch {B} x {n} pts -> {k} NDs, NDTNetSegmentation F={F} C={C} eval"

@@ -40,9 +40,6 @@ typedef struct ndnet_pn_layer {
                           //    `w` = bf16 [N/16][K/32][3 planes][64 lanes][8] with W^T = h + m + l and
                           //    lane l's 8 values W^T[32 kg + 8 (l/16) + j][16 cb + l%16]; the layer's
                           //    producer must be the previous, unfused layer (it stores bf16 planes)
-                          // 2: the same products from fp32 weights split into h + m + l in registers:
-                          //    `w` = fp32 [N/16][K/32][2 halves][64 lanes][4], lane l's half h holding
-                          //    W^T[32 kg + 8 (l/16) + 4 h + s][16 cb + l%16], s = 0..3
   int32_t fuse_next;      // 1: this layer's output (N % 64 == 0) is produced in 64-column chunks, each
                           // consumed at once by the next layer (whose N is 64, 128 or 256) -- the
                           // activation never occupies LDS whole
@@ -124,8 +121,6 @@ int ndnet_pn_fold64_run(const float *t2, const float *rhs, float *out, int batch
 /* The same fold in the split-bf16 layout (prec = 1 layers, K = 64): out6[b] =
  * bf16 [N/16][2][3 planes][64 lanes][8] (3 * 64 * N bf16 per cloud). */
 int ndnet_pn_fold64_x6_run(const float *t2, const float *rhs, void *out6, int batch, int N, void *stream);
-/* The same fold in the prec = 2 layout: out[b] = fp32 [N/16][2][2 halves][64 lanes][4]. */
-int ndnet_pn_fold64_x6f_run(const float *t2, const float *rhs, float *out, int batch, int N, void *stream);
 
 #ifdef __cplusplus
 }

@@ -2651,7 +2651,10 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
     // NDNET_WQ_WPC workgroups per CU (1, 2 and 3 measured equal on C2 and C5:
     // profiles/r02c_welford_parts.txt -- the kernel is issue-bound, not
     // latency-bound, so a second wave per SIMD shares the same issue slots)
-    P->wq_grid = ncu > 0 ? (uint32_t)ncu * NDNET_WQ_WPC : 1u;
+#ifndef NDNET_WQ_CU_SHARE  // A/B (pipelined step): k_welford_q on CUs / share of the CUs
+#define NDNET_WQ_CU_SHARE 1
+#endif
+    P->wq_grid = ncu > 0 ? (uint32_t)(ncu / NDNET_WQ_CU_SHARE) * NDNET_WQ_WPC : 1u;
   }
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_welford_q<float>, hipFuncAttributeMaxDynamicSharedMemorySize,

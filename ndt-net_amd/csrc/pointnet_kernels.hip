@@ -70,15 +70,10 @@ constexpr int kDepth = NDNET_PN_DEPTH;  // weight k-groups in flight per wave
 #define NDNET_PN_DEPTH6 1
 #endif
 constexpr int kDepth6 = NDNET_PN_DEPTH6;  // the same for split-bf16 layers (3 fragment planes each)
-#ifndef NDNET_PN_DEPTH6F
-#define NDNET_PN_DEPTH6F 1
+#ifndef NDNET_PN_CHUNK_ROT
+#define NDNET_PN_CHUNK_ROT 1
 #endif
-constexpr int kDepth6F = NDNET_PN_DEPTH6F;  // the same for prec 2 (fp32 weights split in registers)
-#ifdef NDNET_PN_NO_X6F  // A/B: a build without the prec-2 code paths (smaller kernel)
-constexpr bool kX6F = false;
-#else
-constexpr bool kX6F = true;
-#endif
+constexpr bool kChunkRot = NDNET_PN_CHUNK_ROT;  // per-workgroup chunk order (run_tiles_x6 rot)
 static_assert(kWaves % kRowBlocks == 0, "every row group has whole column groups");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -153,8 +148,7 @@ __device__ unsigned long long g_pn_stamps[kStampWgs][16];
 // the weights stream from L2 straight into registers (no LDS staging, no
 // barrier inside a layer) and only the activations live in LDS.
 struct LayerCtx {
-  const f32x4* __restrict__ w;     // this cloud's fragments, offset by the lane (prec 0; prec 2: fp32
-                                   // split-bf16 fragments)
+  const f32x4* __restrict__ w;     // this cloud's fragments, offset by the lane (prec 0)
   const bf16x8* __restrict__ w6;   // split-bf16 fragments, offset by the lane (prec 1)
   const float* __restrict__ bias;
   int KG, N, relu, prec;           // KG: 16-row k-groups (prec 0) or 32-row (prec 1)
@@ -164,10 +158,10 @@ struct LayerCtx {
 // The first weight step of a layer, loaded by each wave before the barrier
 // that closes the previous layer (its latency hides behind the barrier wait;
 // 16-wave 64-point build, where every layer's wave tile is one column block):
-// w6 for prec 1, w[0] for prec 0, w[0..1] for prec 2.
+// r0..r2 = the three bf16x8 planes for prec 1, r0 for prec 0.
 struct Pre {
   bool on;
-  f32x4 r0, r1, r2;  // prec 1: bf16x8 planes h, m, l (bit_cast); prec 0: r0; prec 2: r0, r1
+  f32x4 r0, r1, r2;  // prec 1: bf16x8 planes h, m, l (bit_cast); prec 0: r0
 };
 
 __device__ inline LayerCtx layer_ctx(const ndnet_pn_chain& A, int l, int b, const float* bias) {
@@ -333,20 +327,25 @@ __device__ __attribute__((always_inline)) inline void pool_cols(const f32x4 (&ac
   const int kq = lane >> 4, cl = lane & 15;
 #if NDNET_PN_SWAP
   // lane (kq, cl): point cl of each row block, channels 4 kq + r; the max over
-  // the 16 points of a lane row by DPP, then lane cl < 4 of the row takes
+  // the tile's valid points first (RB values in the lane, then the 16 lanes of
+  // a lane row by DPP), then bias + ReLU once on the maximum -- exact, as
+  // fl(a + b) and ReLU are monotonic in a -- and lane cl < 4 of the row takes
   // channel 4 kq + cl's atomic
+  const bool full = row0 + 16 * RB <= rows_valid;  // wave-uniform: every row of the wave's tile is a point
 #pragma unroll
   for (int j = 0; j < NB; j++) {
     float m[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-      const float bv = bias[col0 + 16 * j + 4 * kq + r];
-      m[r] = -INFINITY;
+      if (full) {
+        m[r] = acc[0][j][r];
 #pragma unroll
-      for (int rb = 0; rb < RB; rb++) {
-        float v = acc[rb][j][r] + bv;
-        if (relu) v = fmaxf(v, 0.0f);
-        if (row0 + 16 * rb + cl < rows_valid) m[r] = fmaxf(m[r], v);
+        for (int rb = 1; rb < RB; rb++) m[r] = fmaxf(m[r], acc[rb][j][r]);
+      } else {
+        m[r] = -INFINITY;
+#pragma unroll
+        for (int rb = 0; rb < RB; rb++)
+          if (row0 + 16 * rb + cl < rows_valid) m[r] = fmaxf(m[r], acc[rb][j][r]);
       }
       m[r] = fmaxf(m[r], xor_row<1>(m[r]));
       m[r] = fmaxf(m[r], xor_row<2>(m[r]));
@@ -354,7 +353,11 @@ __device__ __attribute__((always_inline)) inline void pool_cols(const f32x4 (&ac
       m[r] = fmaxf(m[r], xor_row<8>(m[r]));
     }
     const float mm = cl == 0 ? m[0] : cl == 1 ? m[1] : cl == 2 ? m[2] : m[3];
-    if (cl < 4 && mm > -INFINITY) atomic_max_f32(gmax + col0 + 16 * j + 4 * kq + cl, mm);
+    if (cl < 4 && mm > -INFINITY) {
+      float v = mm + bias[col0 + 16 * j + 4 * kq + cl];
+      if (relu) v = fmaxf(v, 0.0f);
+      atomic_max_f32(gmax + col0 + 16 * j + 4 * kq + cl, v);
+    }
   }
 #else
 #pragma unroll
@@ -503,19 +506,28 @@ __device__ __attribute__((always_inline)) inline void run_tiles_x6(f32x4 (&acc)[
                                                                    const bf16x8* __restrict__ w, int KG, int kg0,
                                                                    int nkg, int cb0, int cbs, int nchunk,
                                                                    const __bf16* abase, int pitchb, Epi epi,
-                                                                   Pre pre = {}) {
+                                                                   Pre pre = {}, int rot = 0) {
+  // rot: the chunks run in the order rot, rot + 1, .. (mod nchunk), so that
+  // workgroups in lockstep do not all stream the same weight fragments at
+  // once (different chunks hit different L2 lines); each chunk's columns and
+  // sums are unchanged
   const int T = nchunk * nkg;
   const int plane = kP * pitchb;
   const int64_t jstride = (int64_t)KG * 3 * 64;
   const int64_t chunk_jump = ((int64_t)cbs * KG - (nkg - 1)) * 3 * 64;
-  const bf16x8* lp = w + ((int64_t)cb0 * KG + kg0) * 3 * 64;
-  int lkk = 0, lleft = T;
+  const int64_t wrap = (int64_t)nchunk * cbs * KG * 3 * 64;
+  const bf16x8* lp = w + ((int64_t)(cb0 + rot * cbs) * KG + kg0) * 3 * 64;
+  int lkk = 0, lleft = T, lc = rot;
   auto advance = [&]() {
     if (lleft > 1) {
       lleft--;
       if (++lkk == nkg) {
         lkk = 0;
         lp += chunk_jump;
+        if (++lc == nchunk) {
+          lc = 0;
+          lp -= wrap;
+        }
       } else {
         lp += 3 * 64;
       }
@@ -531,13 +543,13 @@ __device__ __attribute__((always_inline)) inline void run_tiles_x6(f32x4 (&acc)[
       for (int p = 0; p < 3; p++) bw[j][p] = lp[j * jstride + p * 64];
     advance();
   };
-  int kk = 0, c = 0;
+  int kk = 0, c = rot;
   auto step = [&](const bf16x8 (&bw)[NB][3]) {
     mma_kgroup_x6<RB, NB>(acc, abase + 32 * kk, plane, 16 * pitchb, bw);
     if (++kk == nkg) {
       epi(acc, c);
       kk = 0;
-      c++;
+      if (++c == nchunk) c = 0;
     }
   };
   bf16x8 bq[kDepth6][NB][3];
@@ -558,89 +570,6 @@ __device__ __attribute__((always_inline)) inline void run_tiles_x6(f32x4 (&acc)[
       if (t + i < T) {
         step(bq[i]);
         load(bq[i]);
-      }
-    }
-  }
-}
-
-// prec 2: the same products from fp32 weights, split into the three bf16
-// planes in registers when a step consumes them (h = bf16(w), m = bf16(w - h),
-// l = bf16(w - h - m): the split the host applies for prec 1, bit for bit).
-// 4 bytes per weight cross L2 -> CU instead of 6, and a prefetched step holds
-// 8 registers per column block instead of 12.  Layout: [column block][k-group]
-// [half][64 lanes][4] fp32, lane l's half h holding W^T[32 kg + 8 (l/16) + 4 h
-// + s][16 cb + l%16], s = 0..3 -- each half one coalesced 1 KB load per wave.
-__device__ __attribute__((always_inline)) inline void split_w8(const f32x4& lo, const f32x4& hi, bf16x8 (&o)[3]) {
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const float v = i < 4 ? lo[i] : hi[i - 4];
-    __bf16 h, m, l;
-    split3(v, h, m, l);
-    o[0][i] = h;
-    o[1][i] = m;
-    o[2][i] = l;
-  }
-}
-
-template <int RB, int NB, class Epi>
-__device__ __attribute__((always_inline)) inline void run_tiles_x6f(f32x4 (&acc)[RB][NB],
-                                                                    const f32x4* __restrict__ w, int KG, int kg0,
-                                                                    int nkg, int cb0, int cbs, int nchunk,
-                                                                    const __bf16* abase, int pitchb, Epi epi,
-                                                                    Pre pre = {}) {
-  const int T = nchunk * nkg;
-  const int plane = kP * pitchb;
-  const int64_t jstride = (int64_t)KG * 2 * 64;
-  const int64_t chunk_jump = ((int64_t)cbs * KG - (nkg - 1)) * 2 * 64;
-  const f32x4* lp = w + ((int64_t)cb0 * KG + kg0) * 2 * 64;
-  int lkk = 0, lleft = T;
-  auto advance = [&]() {
-    if (lleft > 1) {
-      lleft--;
-      if (++lkk == nkg) {
-        lkk = 0;
-        lp += chunk_jump;
-      } else {
-        lp += 2 * 64;
-      }
-    }
-  };
-  auto load = [&](f32x4 (&raw)[NB][2]) {
-#pragma unroll
-    for (int j = 0; j < NB; j++)
-#pragma unroll
-      for (int h = 0; h < 2; h++) raw[j][h] = lp[j * jstride + h * 64];
-    advance();
-  };
-  int kk = 0, c = 0;
-  auto step = [&](const f32x4 (&raw)[NB][2]) {
-    bf16x8 bw[NB][3];
-#pragma unroll
-    for (int j = 0; j < NB; j++) split_w8(raw[j][0], raw[j][1], bw[j]);
-    mma_kgroup_x6<RB, NB>(acc, abase + 32 * kk, plane, 16 * pitchb, bw);
-    if (++kk == nkg) {
-      epi(acc, c);
-      kk = 0;
-      c++;
-    }
-  };
-  f32x4 rq[kDepth6F][NB][2];
-#pragma unroll
-  for (int i = 0; i < kDepth6F; i++) {
-    if (NB == 1 && i == 0 && pre.on) {  // the first step, prefetched by the caller
-      rq[0][0][0] = pre.r0;
-      rq[0][0][1] = pre.r1;
-      advance();
-    } else {
-      load(rq[i]);
-    }
-  }
-  for (int t = 0; t < T; t += kDepth6F) {
-#pragma unroll
-    for (int i = 0; i < kDepth6F; i++) {
-      if (t + i < T) {
-        step(rq[i]);
-        load(rq[i]);
       }
     }
   }
@@ -672,8 +601,8 @@ __device__ void plain_layer(const LayerCtx& C, int in, int pin, int out, int pou
   if (C.prec) {  // input: three bf16 planes of pitch K + kPadB (the producer's N + kPadB)
     const int pb = 32 * C.KG + kPadB;
     const __bf16* abase6 = reinterpret_cast<const __bf16*>(g_smem + in) + (row0 + cl) * pb + 8 * kq;
-    if (kX6F && C.prec == 2) run_tiles_x6f<RB, NB>(acc, C.w, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase6, pb, epi, pre);
-    else run_tiles_x6<RB, NB>(acc, C.w6, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase6, pb, epi, pre);
+    run_tiles_x6<RB, NB>(acc, C.w6, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase6, pb, epi, pre,
+                              kChunkRot ? (int)((blockIdx.x + blockIdx.y) % nchunk) : 0);
   } else {
     const float* abase = g_smem + in + (row0 + cl) * pin + 4 * kq;
     run_tiles<RB, NB>(acc, C.w, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase, pin, epi, pre);
@@ -719,8 +648,7 @@ __device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin
     };
     Pre pf = pre;
     if (f != 0) pf.on = false;
-    if (kX6F && P.prec == 2) run_tiles_x6f<1, PNB>(acc1, P.w, P.KG, 0, P.KG, 4 * f + pwc, 0, 1, ain6, 32 * P.KG + kPadB, epi, pf);
-    else if (P.prec) run_tiles_x6<1, PNB>(acc1, P.w6, P.KG, 0, P.KG, 4 * f + pwc, 0, 1, ain6, 32 * P.KG + kPadB, epi, pf);
+    if (P.prec) run_tiles_x6<1, PNB>(acc1, P.w6, P.KG, 0, P.KG, 4 * f + pwc, 0, 1, ain6, 32 * P.KG + kPadB, epi, pf);
     else run_tiles<1, PNB>(acc1, P.w, P.KG, 0, P.KG, 4 * f + pwc, 0, 1, ain, pin, epi, pf);
   };
   f32x4 acc2[RB][NB];
@@ -732,12 +660,8 @@ __device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin
       if (Q.prec) {
         const __bf16* af6 = reinterpret_cast<const __bf16*>(g_smem + fbuf + (f & 1) * fbsz) +
                             (qrow0 + cl) * (kFuseNC + kPadB) + 8 * kq;
-        if (kX6F && Q.prec == 2)
-          run_tiles_x6f<RB, NB>(acc2, Q.w, Q.KG, 2 * f, 2, qwc * NB, 0, 1, af6, kFuseNC + kPadB,
-                                [](f32x4 (&)[RB][NB], int) {});
-        else
-          run_tiles_x6<RB, NB>(acc2, Q.w6, Q.KG, 2 * f, 2, qwc * NB, 0, 1, af6, kFuseNC + kPadB,
-                               [](f32x4 (&)[RB][NB], int) {});
+        run_tiles_x6<RB, NB>(acc2, Q.w6, Q.KG, 2 * f, 2, qwc * NB, 0, 1, af6, kFuseNC + kPadB,
+                             [](f32x4 (&)[RB][NB], int) {});
       } else {
         const float* af = g_smem + fbuf + (f & 1) * fbsz + (qrow0 + cl) * kFP + 4 * kq;
         run_tiles<RB, NB>(acc2, Q.w, Q.KG, 4 * f, 4, qwc * NB, 0, 1, af, kFP, [](f32x4 (&)[RB][NB], int) {});
@@ -779,10 +703,6 @@ __device__ inline void prefetch_first(const ndnet_pn_chain& A, int l, int b, Pre
       pre.r0 = __builtin_bit_cast(f32x4, q[0]);
       pre.r1 = __builtin_bit_cast(f32x4, q[64]);
       pre.r2 = __builtin_bit_cast(f32x4, q[128]);
-    } else if (L.prec == 2) {
-      const f32x4* q = reinterpret_cast<const f32x4*>(wb) + lane + (int64_t)cb0 * KG * 2 * 64;
-      pre.r0 = q[0];
-      pre.r1 = q[64];
     } else {
       pre.r0 = (reinterpret_cast<const f32x4*>(wb) + lane + (int64_t)cb0 * KG * 64)[0];
     }
@@ -1406,42 +1326,6 @@ __global__ void __launch_bounds__(256) k_pn_fold64_x6(const float* __restrict__ 
 }
 
 
-// The same fold in the prec-2 layout (fp32, K = 64: two 32-row k-groups):
-// out[b] = [N/16][2][2 halves][64 lanes][4] fp32.
-__global__ void __launch_bounds__(256) k_pn_fold64_x6f(const float* __restrict__ t2, const float* __restrict__ rhs,
-                                                       float* __restrict__ out, int N) {
-  __shared__ float s_a[64][65];
-  __shared__ float s_b[64][68];
-  const int b = blockIdx.y, j0 = blockIdx.x * 64;
-  const float* A = t2 + (int64_t)b * 4096;
-  for (int e = threadIdx.x; e < 4096; e += 256) {
-    s_a[e >> 6][e & 63] = A[e];
-    s_b[e >> 6][e & 63] = rhs[(int64_t)(e >> 6) * N + j0 + (e & 63)];
-  }
-  __syncthreads();
-  const int ti = (threadIdx.x >> 4) * 4, tj = (threadIdx.x & 15) * 4;
-  float acc[4][4] = {};
-  for (int k = 0; k < 64; k++) {
-    float av[4], bv[4];
-#pragma unroll
-    for (int r = 0; r < 4; r++) av[r] = s_a[ti + r][k];
-#pragma unroll
-    for (int c = 0; c < 4; c++) bv[c] = s_b[k][tj + c];
-#pragma unroll
-    for (int r = 0; r < 4; r++)
-#pragma unroll
-      for (int c = 0; c < 4; c++) acc[r][c] += av[r] * bv[c];
-  }
-  // rows ti..ti+3 are one lane's 4 consecutive values of one half: one float4 store per column
-  float* o = out + (int64_t)b * 64 * N;
-#pragma unroll
-  for (int c = 0; c < 4; c++) {
-    const int k = ti, n = j0 + tj + c;
-    const int64_t e = ((((int64_t)(n >> 4) * 2 + (k >> 5)) * 2 + ((k >> 2) & 1)) * 64 + ((k >> 3) & 3) * 16 + (n & 15)) * 4;
-    *reinterpret_cast<f32x4*>(o + e) = f32x4{acc[0][c], acc[1][c], acc[2][c], acc[3][c]};
-  }
-}
-
 }  // namespace
 
 extern "C" {
@@ -1483,12 +1367,6 @@ int ndnet_pn_head3_run(const float* h2, int ld_h, const float* W3, const float* 
 int ndnet_pn_fold64_x6_run(const float* t2, const float* rhs, void* out6, int batch, int N, void* stream) {
   if (!t2 || !rhs || !out6 || batch <= 0 || N <= 0 || N % 64) return -20;
   k_pn_fold64_x6<<<dim3(N / 64, batch), 256, 0, (hipStream_t)stream>>>(t2, rhs, (__bf16*)out6, N);
-  return hipGetLastError() == hipSuccess ? 0 : -21;
-}
-
-int ndnet_pn_fold64_x6f_run(const float* t2, const float* rhs, float* out, int batch, int N, void* stream) {
-  if (!t2 || !rhs || !out || batch <= 0 || N <= 0 || N % 64 || ((uintptr_t)out % 16)) return -20;
-  k_pn_fold64_x6f<<<dim3(N / 64, batch), 256, 0, (hipStream_t)stream>>>(t2, rhs, out, N);
   return hipGetLastError() == hipSuccess ? 0 : -21;
 }
 
@@ -1545,7 +1423,7 @@ int ndnet_pn_chain_run_t32(const ndnet_pn_chain* args, int batch, void* stream) 
         L.w_cloud_stride % 4)
       return -20;
     const bool fed = l > 0 && args->L[l - 1].fuse_next;
-    if (L.prec < 0 || L.prec > 2) return -20;
+    if (L.prec < 0 || L.prec > 1) return -20;
     if (L.prec) {  // split-bf16: reads planes its producer writes (into a region, or the fused chunks)
       if (l == 0 || L.K % 32 || args->L[l - 1].N != L.K) return -20;
       if (fed) qprec = 1;

@@ -45,27 +45,25 @@ chain_timing = None
 # 128 -> 1024 / 768, 90% of chains A-C's FLOPs) and the seg head's 512 -> 256
 # (fed chunk by chunk from the fused 64 -> 512), the 64 -> 512 itself, 256 -> 128
 # and NDTNet's t2-folded conv2 run as split-bf16 "x6" GEMMs
-# (include/ndnet_pointnet.h prec = 1 / 2): fp32-accurate (operands split into
+# (include/ndnet_pointnet.h prec = 1): fp32-accurate (operands split into
 # three bf16, six exact partial products accumulated in fp32) on the bf16
-# matrix cores.  NDNET_PN_PRECISION: "x6" (default) stores the three bf16 planes
-# (prec 1), "x6f" streams those layers'
-# weights as fp32 and splits them in registers (prec 2: 4 bytes per weight
-# from L2 instead of 6, the same bits; measured 20-25% slower per layer:
-# the split costs more issue slots than the bytes save),
-# "fp32" keeps every layer on the fp32 MFMA.
-PRECISION = SPLIT_BF16 = WEIGHT_F32 = X6_PREC = None
+# matrix cores.  NDNET_PN_PRECISION: "x6" (default), or "fp32" to keep every
+# layer on the fp32 MFMA.  (Round 2's "x6f" -- fp32 weights split in
+# registers, measured 20-25% slower per layer -- was removed in round 3: its
+# code paths alone cost the kernel registers and scratch,
+# profiles/r03l_stamps_depth.txt.)
+PRECISION = SPLIT_BF16 = X6_PREC = None
 
 
 def set_precision(mode: str) -> None:
-    """"x6f", "x6" or "fp32" for models folded from now on (a model re-folds
-    when its ``_hip`` cache is cleared)."""
-    global PRECISION, SPLIT_BF16, WEIGHT_F32, X6_PREC
-    if mode not in ("x6f", "x6", "fp32"):
+    """"x6" or "fp32" for models folded from now on (a model re-folds when its
+    ``_hip`` cache is cleared)."""
+    global PRECISION, SPLIT_BF16, X6_PREC
+    if mode not in ("x6", "fp32"):
         raise ValueError(f"unknown PointNet precision mode {mode!r}")
     PRECISION = mode
     SPLIT_BF16 = mode != "fp32"
-    WEIGHT_F32 = mode == "x6f"
-    X6_PREC = 2 if WEIGHT_F32 else 1
+    X6_PREC = 1
 
 
 set_precision(os.environ.get("NDNET_PN_PRECISION", "x6"))
@@ -152,16 +150,6 @@ def _frag_x6(wT: torch.Tensor) -> torch.Tensor:
     return v.permute(4, 1, 0, 2, 5, 3).reshape(-1).contiguous()        # cb, kg, plane, kq, cl, j
 
 
-def _frag_x6f(wT: torch.Tensor) -> torch.Tensor:
-    """Plain W^T [K, N] (K % 32 == 0, N % 16 == 0) -> the prec-2 layout of
-    include/ndnet_pointnet.h, flattened fp32: [cb][kg][half][kq][cl][s] with
-    k = 32 kg + 8 kq + 4 half + s, n = 16 cb + cl (the kernel splits each
-    weight into h + m + l as _frag_x6 does)."""
-    K, N = wT.shape
-    v = wT.float().reshape(K // 32, 4, 2, 4, N // 16, 16)            # kg, kq, half, s, cb, cl
-    return v.permute(4, 0, 2, 1, 5, 3).reshape(-1).contiguous()       # cb, kg, half, kq, cl, s
-
-
 def _bpad(b: torch.Tensor, npad: int) -> torch.Tensor:
     out = torch.zeros(npad, dtype=torch.float32, device=b.device)
     out[: b.shape[0]] = b
@@ -230,7 +218,7 @@ class _Folded:
             self.wide = [self.A[2][0], self.B_tail[2][0], self.C_tail[0], self.D_tail[0][0], self.D_tail[1][0]]
             if X6_NARROW:  # the K >= 64 fp32-MFMA layers too (64 -> 128 of TNet(3) / TNet(64), 64 -> 64, 128 -> C+1)
                 self.wide += [self.A[1][0], self.B_tail[0][0], self.B_tail[1][0], self.D_tail[2][0]]
-            self.frag6 = {id(w): (_frag_x6f(w) if WEIGHT_F32 else _frag_x6(w)) for w in self.wide}
+            self.frag6 = {id(w): _frag_x6(w) for w in self.wide}
             # the FC layers of the TNet heads and the seg head's global-feature
             # bias, W^T fragment-major for the MFMA GEMV (ndnet_pn_fc_mfma_run)
             self.fcf = {id(w): _frag(w.t().contiguous()) for w in
@@ -359,12 +347,10 @@ class _Workspace:
         # column blocks are outermost, so conv2's 8 blocks precede seg conv1a's 32
         self.w1f = torch.empty((B, 16 * 64), **f32)
         self.t2wf = torch.empty((B, 64 * 640), **f32)
-        # t2-folded conv2 / seg conv1a also in the split-bf16 layout ([cb][kg][plane][lane][8]),
-        # or its fp32 form ([cb][kg][half][lane][4]) for prec 2
+        # t2-folded conv2 / seg conv1a also in the split-bf16 layout ([cb][kg][plane][lane][8])
         self.t2wf6 = None
         if SPLIT_BF16:
-            self.t2wf6 = (torch.empty((B, 64 * 640), **f32) if WEIGHT_F32 else
-                          torch.empty((B, 3 * 64 * 640), dtype=torch.bfloat16, device=dev))
+            self.t2wf6 = torch.empty((B, 3 * 64 * 640), dtype=torch.bfloat16, device=dev)
         self.specs = [  # torch emulation: (in_cols, [(W^T, bias)], relus, mode, kwargs)
             (3, W.A, (1, 1, 1), 0, dict(gmax=self.g1)),
             (12, [(self.w1T, W.c1b)] + W.B_tail, (0, 1, 1, 1), 0, dict(gmax=self.g2)),
@@ -381,11 +367,7 @@ class _Workspace:
             return (W.frag[id(w)], 0, b, w.shape[0], w.shape[1])
 
         L1 = (self.w1f, self.w1f.stride(0), W.c1b, 16, 64)
-        if WEIGHT_F32:  # per-cloud stride in floats; conv2's 8 column blocks (1024 floats each) come first
-            s6 = self.t2wf6.stride(0)
-            L2 = (self.t2wf6, s6, W.c2b, 64, 128, 2)
-            Ls = (self.t2wf6[:, 8 * 1024:], s6, self.cvec, 64, 512, 2)
-        elif SPLIT_BF16:  # per-cloud stride in floats (bf16 pairs); conv2's 8 column blocks come first
+        if SPLIT_BF16:  # per-cloud stride in floats (bf16 pairs); conv2's 8 column blocks come first
             s6 = self.t2wf6.stride(0) // 2
             L2 = (self.t2wf6, s6, W.c2b, 64, 128, 1)
             Ls = (self.t2wf6[:, 8 * 2 * 3 * 64 * 8:], s6, self.cvec, 64, 512, 1)
@@ -499,11 +481,7 @@ def _glue_hip(W, ws, B: int):
         fc(ws.g2, t["f1"], t["c1"], ws.h1, True)
         fc(ws.h1, t["f2"], t["c2"], ws.h2, True)
         fc(ws.h2, t["f3"], t["c3"], ws.t2, False)
-        if WEIGHT_F32:
-            rc = _lib.lib().ndnet_pn_fold64_x6f_run(ws.t2.data_ptr(), W.t2_rhs.data_ptr(), ws.t2wf6.data_ptr(), B,
-                                                    W.t2_rhs.shape[1], st())
-            _lib.check(rc, "ndnet_pn_fold64_x6f_run")
-        elif ws.t2wf6 is not None:
+        if ws.t2wf6 is not None:
             rc = _lib.lib().ndnet_pn_fold64_x6_run(ws.t2.data_ptr(), W.t2_rhs.data_ptr(), ws.t2wf6.data_ptr(), B,
                                                    W.t2_rhs.shape[1], st())
             _lib.check(rc, "ndnet_pn_fold64_x6_run")

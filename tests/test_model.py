@@ -139,22 +139,6 @@ def test_split_bf16_fragment_layout():
     assert torch.equal(rec, wT)
 
 
-def test_split_bf16_fp32_fragment_layout():
-    """_frag_x6f (prec 2): fp32 W^T at [cb][kg][half][lane][s] with
-    k = 32 kg + 8 (lane >> 4) + 4 half + s, n = 16 cb + (lane & 15)."""
-    from ndnet.models import pointnet_hip as ph
-    K, N = 64, 32
-    g = torch.Generator().manual_seed(1)
-    wT = torch.randn((K, N), generator=g)
-    f = ph._frag_x6f(wT).reshape(N // 16, K // 32, 2, 64, 4)
-    rec = torch.zeros((K, N))
-    for cb in range(N // 16):
-        for kg in range(K // 32):
-            for h in range(2):
-                for lane in range(64):
-                    for s_ in range(4):
-                        rec[32 * kg + 8 * (lane >> 4) + 4 * h + s_, 16 * cb + (lane & 15)] = f[cb, kg, h, lane, s_]
-    assert torch.equal(rec, wT)
 
 
 @pytest.mark.gpu
@@ -173,7 +157,7 @@ def test_split_bf16_layers_are_fp32_accurate():
         saved = ph.PRECISION
         outs = {}
         try:
-            for mode in ("x6", "x6f", "fp32"):
+            for mode in ("x6", "fp32"):
                 ph.set_precision(mode)
                 m._hip = None
                 outs[mode] = m(p, c).double()
@@ -182,8 +166,6 @@ def test_split_bf16_layers_are_fp32_accurate():
             m._hip = None
         out_x6, out_32 = outs["x6"], outs["fp32"]
         out_t32 = m.forward_torch(p, c).double()
-    # prec 2 splits the fp32 weights in registers into the very planes prec 1 stores
-    assert torch.equal(outs["x6f"], out_x6)
     e_x6 = (out_x6 - ref64).abs().max().item()
     e_32 = (out_32 - ref64).abs().max().item()
     e_t32 = (out_t32 - ref64).abs().max().item()

@@ -70,9 +70,6 @@ def layer_x6(K, N):
     return (ph._frag_x6(w), 0, torch.zeros(N, device=dev), K, N, 1)
 
 
-def layer_x6f(K, N):
-    w = torch.randn(K, N, device=dev) * 0.05
-    return (ph._frag_x6f(w), 0, torch.zeros(N, device=dev), K, N, 2)
 
 
 BF16_PEAK = 2.5e15
@@ -80,7 +77,7 @@ for K, N in [(128, 1024), (128, 768), (128, 512), (128, 256), (64, 1024), (256, 
     flops = 2.0 * B * n * K * N
     if K not in base:
         base[K] = time_chain([layer(16, K)], (1,), 0, gmax=gmax)
-    for tag, fn in (("x6 ", layer_x6), ("x6f", layer_x6f)):
+    for tag, fn in (("x6 ", layer_x6),):
         us = time_chain([layer(16, K), fn(K, N)], (1, 1), 0, gmax=gmax) - base[K]
         print(f"{tag} {K:4d} -> {N:4d} (max-pool, minus producer) {us:7.1f} us  {flops / (us * 1e-6) / 1e12:6.1f} "
               f"TFLOP/s fp32-eq, bf16 MFMA {6 * flops / (us * 1e-6) / BF16_PEAK * 100:5.1f}% of peak   "
