@@ -131,6 +131,15 @@ void ndnet_ndt_plan_destroy(void *plan);
 int ndnet_ndt_set_path(void *plan, int path);
 int ndnet_ndt_get_path(void *plan);
 
+/* CU share of the plan's two widest kernels: k_front runs CUs / (share * batch)
+ * workgroups per cloud and k_welford_q CUs / share workgroups, so a run
+ * leaves (share - 1) / share of the CUs to kernels on other streams
+ * (ndnet.pipeline.PipelinedSegmentation overlaps the NDT stage with the
+ * PointNet forward that way).  Default 1 (every CU).  Results are identical
+ * for every share.  NDNET_ERR_ARG when k_front does not fit the share (the
+ * previous share is kept). */
+int ndnet_ndt_set_cu_share(void *plan, int share);
+
 /* The bisection (ndt.c:144-187) takes hi = guess whenever a grid has fewer
  * voxels (or the cloud fewer estimated points) than num_desired: such a grid
  * cannot reach k occupied voxels, so path 2 does not count it and the debug

@@ -164,7 +164,9 @@ struct Plan {
   unsigned long long* fmarks; // [B][kFrontMarkStride]: k_front phase stamps of WG 0 + start/end of every WG (timing level 2)
   int exact_counts;           // k_front counts every bisection grid (ndnet_ndt_set_exact_counts)
   size_t wq_lds;              // k_welford_q dynamic LDS (labelled runs: class histograms)
-  uint32_t wq_grid;           // k_welford_q workgroups: one per CU
+  uint32_t wq_grid;           // k_welford_q workgroups: one per CU (of the plan's CU share)
+  int cus;                    // the device's CUs
+  int cu_share;               // k_front / k_welford_q use CUs / cu_share (ndnet_ndt_set_cu_share)
   uint32_t* wq_ctr;           // [8][16] k_welford_q dynamic item counters, one per XCD (re-armed by k_kl_rank_chunks)
   int eager_list;             // build every cloud's retained list in the run (ndnet_ndt_set_lazy_list(plan, 0))
   uint64_t front_sync_ticks;  // k_front's cloud-barrier timeout (ndnet_ndt_debug_set_sync_timeout)
@@ -2517,6 +2519,51 @@ __global__ void k_set_epoch(CloudCtl* ctl, int B, uint32_t epoch) {
 
 extern "C" {
 
+}  // extern "C" (reopened below)
+
+namespace {
+
+// k_front's geometry for a CU share: G = CUs / (share * B) workgroups per
+// cloud (at most the plan's bins), bpw bins per workgroup, rank-bin size and
+// dynamic LDS; front_ok when the shape fits (LDS, residency).  At share 1
+// every CU runs a k_front workgroup (B = 16: G = 16); a larger share leaves
+// CUs to work on another stream (PipelinedSegmentation) at the cost of more
+// bins per workgroup.
+hipError_t front_config(Plan* P, int share) {
+  const uint32_t B = (uint32_t)P->B;
+  const int cus = P->cus;
+  const uint32_t gt = (uint32_t)(cus / (share * (int)B) > 0 ? cus / (share * (int)B) : 1);
+  const uint32_t G = gt < P->nbins ? gt : P->nbins;
+  const uint32_t bpw = (P->nbins + G - 1) / G;
+  // rank bins of 512 points when that keeps every wave busy and fits
+  auto lds_of = [&](uint32_t rbs) {
+    return sizeof(uint32_t) * ((size_t)kFrontTable + (size_t)bpw * 1024 + (size_t)bpw * (1024 / rbs) * P->ndcap);
+  };
+  const uint32_t rbs = (2 * bpw <= (uint32_t)kFrontWaves && lds_of(512) <= 150 * 1024) ? 512u : 1024u;
+  const size_t lds = lds_of(rbs);
+  hipError_t e = hipSuccess;
+  int ok = lds <= 150 * 1024 && (G == 1 || (uint64_t)G * B <= (uint64_t)cus);
+  if (ok) e = hipFuncSetAttribute((const void*)k_front<float>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+  if (ok && e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_front<double>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+  if (ok && e == hipSuccess) {
+    int nb = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_front<double>, kFrontThreads, lds);
+    if (e == hipSuccess && nb < 1) ok = 0;
+  }
+  P->fG = G;
+  P->fbpw = bpw;
+  P->frbs = rbs;
+  P->flds = lds;
+  P->front_ok = e == hipSuccess && ok;
+  P->cu_share = share;
+  return e;
+}
+
+}  // namespace
+
+extern "C" {
+
 int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, int num_classes,
                           uint64_t voxel_capacity, void** plan_out) {
   if (!plan_out || batch <= 0 || num_points == 0 || num_desired == 0 || num_points >= (1ull << 31))
@@ -2594,40 +2641,16 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   A_(d_stats, B);
   A_(wq_ctr, 128);
   // k_front: G workgroups per cloud, all resident together (G * B <= CUs);
-  // each owns bpw bins, whose per-ND counts and ranks live in its LDS
+  // each owns bpw bins, whose per-ND counts and ranks live in its LDS.  The
+  // per-workgroup buffers are sized for the largest G (CU share 1).
   {
     int dev = 0, cus = 0;
     if (e == hipSuccess) e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-#ifndef NDNET_FRONT_CU_SHARE
-#define NDNET_FRONT_CU_SHARE 1
-#endif
-    const uint32_t gt = (uint32_t)(cus / (NDNET_FRONT_CU_SHARE * batch) > 0 ? cus / (NDNET_FRONT_CU_SHARE * batch) : 1);
-    // G workgroups per cloud (every CU busy at B = 16), the cloud's bins split
-    // as evenly as G allows: bpw = the most bins a workgroup holds
-    uint32_t G = gt < P->nbins ? gt : P->nbins;
-    uint32_t bpw = (P->nbins + G - 1) / G;
-    // rank bins of 512 points when that keeps every wave busy and fits
-    auto lds_of = [&](uint32_t rbs) {
-      return sizeof(uint32_t) * ((size_t)kFrontTable + (size_t)bpw * 1024 + (size_t)bpw * (1024 / rbs) * P->ndcap);
-    };
-    const uint32_t rbs = (2 * bpw <= (uint32_t)kFrontWaves && lds_of(512) <= 150 * 1024) ? 512u : 1024u;
-    const size_t lds = lds_of(rbs);
-    P->fG = G;
-    P->fbpw = bpw;
-    P->frbs = rbs;
-    P->flds = lds;
-    P->front_ok = e == hipSuccess && lds <= 150 * 1024 && (G == 1 || (uint64_t)G * batch <= (uint64_t)cus);
-    if (P->front_ok && e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)k_front<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (P->front_ok && e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)k_front<double>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (P->front_ok && e == hipSuccess) {
-      int nb = 0;
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_front<double>, kFrontThreads, lds);
-      if (e == hipSuccess && nb < 1) P->front_ok = 0;
-    }
+    P->cus = cus;
+    if (e == hipSuccess) e = front_config(P, 1);
     P->front = P->front_ok;
+    const uint32_t G = P->fG;
     A_(flims, B * G * 6);
     A_(frec, B * kFrontPhases * G * kRecWords);
     A_(fwgcnt, B * G * nd);
@@ -2651,10 +2674,7 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
     // NDNET_WQ_WPC workgroups per CU (1, 2 and 3 measured equal on C2 and C5:
     // profiles/r02c_welford_parts.txt -- the kernel is issue-bound, not
     // latency-bound, so a second wave per SIMD shares the same issue slots)
-#ifndef NDNET_WQ_CU_SHARE  // A/B (pipelined step): k_welford_q on CUs / share of the CUs
-#define NDNET_WQ_CU_SHARE 1
-#endif
-    P->wq_grid = ncu > 0 ? (uint32_t)(ncu / NDNET_WQ_CU_SHARE) * NDNET_WQ_WPC : 1u;
+    P->wq_grid = ncu > 0 ? (uint32_t)ncu * NDNET_WQ_WPC : 1u;
   }
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_welford_q<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2689,6 +2709,21 @@ int ndnet_ndt_set_path(void* plan, int path) {
   if (!P || path < 0 || path > 2) return NDNET_ERR_ARG;
   if (path == 2 && !P->front_ok) return NDNET_ERR_ARG;
   P->front = path == 1 ? 0 : P->front_ok;
+  return NDNET_OK;
+}
+
+int ndnet_ndt_set_cu_share(void* plan, int share) {
+  Plan* P = (Plan*)plan;
+  if (!P || share < 1 || share > P->cus) return NDNET_ERR_ARG;
+  const int prev = P->cu_share;
+  const bool on_front = P->front != 0;  // path 2 in use (not forced to path 1)
+  if (front_config(P, share) != hipSuccess) return NDNET_ERR_HIP;
+  if (!P->front_ok) {  // k_front does not fit this share: keep the previous one
+    front_config(P, prev);
+    return NDNET_ERR_ARG;
+  }
+  P->front = on_front ? 1 : 0;
+  P->wq_grid = (uint32_t)(P->cus / share > 0 ? P->cus / share : 1) * NDNET_WQ_WPC;
   return NDNET_OK;
 }
 

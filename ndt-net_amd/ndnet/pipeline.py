@@ -23,7 +23,7 @@ from typing import Optional
 import torch
 
 from . import _lib
-from .preprocessing.ndtnet_preprocessing import ndt_multiscale, ndt_preprocessing, get_plan
+from .preprocessing.ndtnet_preprocessing import NdtPlan, ndt_multiscale, ndt_preprocessing, get_plan
 
 
 # PipelinedSegmentation step order: "free" (default) lets the two streams run
@@ -35,6 +35,13 @@ FRONT_FIRST = os.environ.get("NDNET_PIPE_ORDER", "free") == "front"
 # "ndt": unordered, but the NDT stage's launches captured ahead of the
 # forward's (measured 2.5% slower: 62.0-62.5k vs 63.7-64.1k clouds/s)
 NDT_FIRST = os.environ.get("NDNET_PIPE_ORDER", "free") == "ndt"
+# CU share of the pipelined NDT stage (ndnet_ndt_set_cu_share): k_front and
+# k_welford_q take CUs / share, leaving the rest to the forward's kernels on
+# the other stream.  Measured on C2 (profiles/r03n_cu_share.txt): share 2
+# 69.8k clouds/s against 64.1k at share 1, although the NDT stage alone
+# slows from 100 to 136 us -- at share 1 k_front needs every CU at once and
+# the two streams serialise.
+PIPE_CU_SHARE = int(os.environ.get("NDNET_PIPE_CU_SHARE", "2"))
 
 
 class _Pinned:
@@ -150,7 +157,7 @@ class PipelinedSegmentation:
     """
 
     def __init__(self, model, num_nds: int, batch: int, num_points: int,
-                 device: Optional[torch.device] = None, warmup: int = 2) -> None:
+                 device: Optional[torch.device] = None, warmup: int = 2, cu_share: Optional[int] = None) -> None:
         _lib.require_gpu()
         if model.training:
             raise ValueError("PipelinedSegmentation needs an eval-mode model")
@@ -161,7 +168,16 @@ class PipelinedSegmentation:
         self.done = [torch.cuda.Event(), torch.cuda.Event()]    # graph j finished (its input is free)
         self.copied = [torch.cuda.Event(), torch.cuda.Event()]  # input j holds the streamed batch
         self.rows = [torch.zeros((batch, self.num_nds, 12), dtype=torch.float32, device=dev) for _ in range(2)]
-        self.plan = get_plan(batch, num_points, self.num_nds, -1, dev)
+        # a plan of its own (not ndt_preprocessing's cached one): its CU share
+        # is a property of the pipeline
+        self.plan = NdtPlan(batch, num_points, self.num_nds, -1, device=dev)
+        if cu_share is None:
+            cu_share = PIPE_CU_SHARE
+        if cu_share > 1 and self.plan.path == 2:
+            try:
+                self.plan.set_cu_share(cu_share)
+            except RuntimeError:  # k_front does not fit that share for this shape
+                pass
         # the forward's launches go first; stream priorities (either way) measured
         # 35-40% slower than none, so both streams keep the default priority
         self.s_ndt, self.s_fwd = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)

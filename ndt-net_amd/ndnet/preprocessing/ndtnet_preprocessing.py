@@ -69,6 +69,11 @@ class NdtPlan:
         """1: one launch per stage; 2: the fused front kernel (k_front); 0: 2 where allowed."""
         _lib.check(_lib.lib().ndnet_ndt_set_path(self.handle, int(path)), "ndnet_ndt_set_path")
 
+    def set_cu_share(self, share: int) -> None:
+        """k_front / k_welford_q on CUs / share (include/ndnet_amd.h
+        ndnet_ndt_set_cu_share): leaves CUs to another stream; identical results."""
+        _lib.check(_lib.lib().ndnet_ndt_set_cu_share(self.handle, int(share)), "ndnet_ndt_set_cu_share")
+
     def set_exact_counts(self, on: bool) -> None:
         """Count every bisection grid, also those with fewer voxels than k
         (include/ndnet_amd.h ndnet_ndt_set_exact_counts; debug / parity)."""

@@ -575,3 +575,31 @@ def test_full_size_labelled(num_classes):
         assert np.array_equal(g[b], onehot_ref), f"cloud {b} classes"
     if num_classes == 300:  # the tie rule and the wide histogram are exercised
         assert len(np.unique(g.argmax(axis=2))) > 100
+
+
+@pytest.mark.parametrize("share", [2])
+def test_cu_share_results_identical(share):
+    """ndnet_ndt_set_cu_share: k_front on CUs / (share B) workgroups per cloud
+    and k_welford_q on CUs / share give the same rows and stats, bit for bit,
+    as the whole-chip plan (C2 U and L clouds, 16 x 100k -> 1000).  A share
+    whose k_front does not fit (4: 25 bins per workgroup exceed its LDS) is
+    refused and the plan keeps its previous share."""
+    import torch
+    from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
+    from ndnet.synthetic import make_batch
+    B, n, k = 16, 100_000, 1000
+    for kind in ("U", "L"):
+        pts = torch.from_numpy(make_batch(kind, B, n)).cuda()
+        res = []
+        for s in (1, share):
+            plan = NdtPlan(B, n, k, -1)
+            assert plan.path == 2
+            if s > 1:
+                plan.set_cu_share(s)
+                with pytest.raises(RuntimeError):
+                    plan.set_cu_share(4)
+            out = torch.empty((B, k, 12), dtype=torch.float32, device="cuda")
+            plan.run(pts, None, out, None)
+            torch.cuda.synchronize()
+            res.append((out.cpu().numpy(), [bytes(st) for st in plan.host_stats()]))
+        assert np.array_equal(res[0][0], res[1][0]) and res[0][1] == res[1][1], kind
