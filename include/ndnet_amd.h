@@ -131,14 +131,14 @@ void ndnet_ndt_plan_destroy(void *plan);
 int ndnet_ndt_set_path(void *plan, int path);
 int ndnet_ndt_get_path(void *plan);
 
-/* CU share of the plan's two widest kernels: k_front runs CUs / (share * batch)
- * workgroups per cloud and k_welford_q CUs / share workgroups, so a run
- * leaves (share - 1) / share of the CUs to kernels on other streams
- * (ndnet.pipeline.PipelinedSegmentation overlaps the NDT stage with the
- * PointNet forward that way).  Default 1 (every CU).  Results are identical
- * for every share.  NDNET_ERR_ARG when k_front does not fit the share (the
- * previous share is kept). */
-int ndnet_ndt_set_cu_share(void *plan, int share);
+/* CU shares of the plan's two widest kernels: k_front runs
+ * CUs / (front_share * batch) workgroups per cloud and k_welford_q
+ * CUs / welford_share workgroups, leaving the other CUs to kernels on other
+ * streams (ndnet.pipeline.PipelinedSegmentation overlaps the NDT stage with the
+ * PointNet forward that way).  Default 1, 1 (every CU).  Results are identical
+ * for every share.  NDNET_ERR_ARG when k_front does not fit front_share (the
+ * previous shares are kept). */
+int ndnet_ndt_set_cu_share(void *plan, int front_share, int welford_share);
 
 /* The bisection (ndt.c:144-187) takes hi = guess whenever a grid has fewer
  * voxels (or the cloud fewer estimated points) than num_desired: such a grid

@@ -2712,18 +2712,19 @@ int ndnet_ndt_set_path(void* plan, int path) {
   return NDNET_OK;
 }
 
-int ndnet_ndt_set_cu_share(void* plan, int share) {
+int ndnet_ndt_set_cu_share(void* plan, int front_share, int welford_share) {
   Plan* P = (Plan*)plan;
-  if (!P || share < 1 || share > P->cus) return NDNET_ERR_ARG;
+  if (!P || front_share < 1 || front_share > P->cus || welford_share < 1 || welford_share > P->cus)
+    return NDNET_ERR_ARG;
   const int prev = P->cu_share;
   const bool on_front = P->front != 0;  // path 2 in use (not forced to path 1)
-  if (front_config(P, share) != hipSuccess) return NDNET_ERR_HIP;
+  if (front_config(P, front_share) != hipSuccess) return NDNET_ERR_HIP;
   if (!P->front_ok) {  // k_front does not fit this share: keep the previous one
     front_config(P, prev);
     return NDNET_ERR_ARG;
   }
   P->front = on_front ? 1 : 0;
-  P->wq_grid = (uint32_t)(P->cus / share > 0 ? P->cus / share : 1) * NDNET_WQ_WPC;
+  P->wq_grid = (uint32_t)(P->cus / welford_share > 0 ? P->cus / welford_share : 1) * NDNET_WQ_WPC;
   return NDNET_OK;
 }
 

@@ -975,7 +975,11 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
         else if (C.N % 64 == 0) plain_layer<2, 1>(C, in, pin, out, pout, gm, rows_valid, op);
         else plain_layer<1, 1>(C, in, pin, out, pout, gm, rows_valid, op);  // N = 32
       } else {
-        if (C.N % 256 == 0) plain_layer<4, 1>(C, in, pin, out, pout, gm, rows_valid, op, pre);
+#ifndef NDNET_PN_NB2  // two column blocks per wave on the 1024-wide x6 layers (-5% per layer, r03q)
+#define NDNET_PN_NB2 1
+#endif
+        if (NDNET_PN_NB2 && C.N % 512 == 0 && C.prec) plain_layer<4, 2>(C, in, pin, out, pout, gm, rows_valid, op, pre);
+        else if (C.N % 256 == 0) plain_layer<4, 1>(C, in, pin, out, pout, gm, rows_valid, op, pre);
         else if (C.N % 128 == 0) plain_layer<2, 1>(C, in, pin, out, pout, gm, rows_valid, op, pre);
         else plain_layer<1, 1>(C, in, pin, out, pout, gm, rows_valid, op, pre);  // N % 64 == 0, or N = 32 (half idle)
       }

@@ -42,6 +42,9 @@ NDT_FIRST = os.environ.get("NDNET_PIPE_ORDER", "free") == "ndt"
 # slows from 100 to 136 us -- at share 1 k_front needs every CU at once and
 # the two streams serialise.
 PIPE_CU_SHARE = int(os.environ.get("NDNET_PIPE_CU_SHARE", "2"))
+# k_welford_q keeps every CU: front 2 / welford 1 measured 70.5k clouds/s
+# against 68.8-70.2k for 2 / 2 and 62.8k for 2 / 4 (profiles/r03n_cu_share.txt)
+PIPE_WQ_SHARE = int(os.environ.get("NDNET_PIPE_WQ_SHARE", "1"))
 
 
 class _Pinned:
@@ -175,7 +178,7 @@ class PipelinedSegmentation:
             cu_share = PIPE_CU_SHARE
         if cu_share > 1 and self.plan.path == 2:
             try:
-                self.plan.set_cu_share(cu_share)
+                self.plan.set_cu_share(cu_share, PIPE_WQ_SHARE)
             except RuntimeError:  # k_front does not fit that share for this shape
                 pass
         # the forward's launches go first; stream priorities (either way) measured

@@ -69,10 +69,12 @@ class NdtPlan:
         """1: one launch per stage; 2: the fused front kernel (k_front); 0: 2 where allowed."""
         _lib.check(_lib.lib().ndnet_ndt_set_path(self.handle, int(path)), "ndnet_ndt_set_path")
 
-    def set_cu_share(self, share: int) -> None:
-        """k_front / k_welford_q on CUs / share (include/ndnet_amd.h
-        ndnet_ndt_set_cu_share): leaves CUs to another stream; identical results."""
-        _lib.check(_lib.lib().ndnet_ndt_set_cu_share(self.handle, int(share)), "ndnet_ndt_set_cu_share")
+    def set_cu_share(self, front_share: int, welford_share: Optional[int] = None) -> None:
+        """k_front on CUs / front_share, k_welford_q on CUs / welford_share
+        (default: front_share) -- include/ndnet_amd.h ndnet_ndt_set_cu_share:
+        leaves CUs to another stream; identical results."""
+        ws = front_share if welford_share is None else welford_share
+        _lib.check(_lib.lib().ndnet_ndt_set_cu_share(self.handle, int(front_share), int(ws)), "ndnet_ndt_set_cu_share")
 
     def set_exact_counts(self, on: bool) -> None:
         """Count every bisection grid, also those with fewer voxels than k
