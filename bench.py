@@ -204,17 +204,26 @@ def main() -> None:
     else:
         # the same kernels, launched from one captured HIP graph per step
         from ndnet.pipeline import GraphedSegmentation
-        if levels or args.no_pipeline:
+        if args.no_pipeline:
             graphed = GraphedSegmentation(model, k, B, n, device=dev, levels=levels)
         else:
-            # step i: NDT of batch i on one stream || forward of batch i - 1 on another
+            # step i: NDT of batch i on one stream || forward(s) of batch i - 1 on another
             from ndnet.pipeline import PipelinedSegmentation
-            graphed = PipelinedSegmentation(model, k, B, n, device=dev)
+            graphed = PipelinedSegmentation(model, k, B, n, device=dev, levels=levels)
         if hasattr(graphed, "load_resident"):
             graphed.load_resident(pts)
         else:
             graphed.points.copy_(pts)
         step = graphed.replay
+
+    def run_steps(k: int):
+        """k steps: the pipeline's event-ordered replays where it has them, else k replays."""
+        if not args.eager and hasattr(graphed, "replay_steps"):
+            return graphed.replay_steps(k)
+        out = None
+        for _ in range(k):
+            out = step()
+        return out
 
     def run_plan():
         """The NDT plan the timed steps ran (the pipeline's own, else the cached one)."""
@@ -230,18 +239,15 @@ def main() -> None:
         t_settle = time.perf_counter()
         n_settle = 0
         while args.settle_ms > 0 and (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
-            for _ in range(8):
-                out = step()
-            n_settle += 8
+            out = run_steps(12)
+            n_settle += 12
             torch.cuda.synchronize()
-        for _ in range(args.warmup):
-            out = step()
+        out = run_steps(args.warmup)
         torch.cuda.synchronize()
         D.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            out = step()
+        out = run_steps(args.steps)
         torch.cuda.synchronize()
         D.barrier()
         torch.cuda.synchronize()
@@ -261,13 +267,11 @@ def main() -> None:
         else:
             graphed.points.copy_(opts)
         with torch.no_grad():
-            for _ in range(max(2, args.warmup)):
-                step()
+            run_steps(max(2, args.warmup))
             torch.cuda.synchronize()
             D.barrier()
             t0 = time.perf_counter()
-            for _ in range(args.steps):
-                step()
+            run_steps(args.steps)
             torch.cuda.synchronize()
             D.barrier()
             t_o = D.max_over_ranks(time.perf_counter() - t0)
@@ -319,7 +323,7 @@ def main() -> None:
                 t_ov = D.max_over_ranks(time.perf_counter() - t0)
             pcie["overlapped"] = {"value": round(total_clouds / t_ov, 2),
                                   "ms_per_step": round(1e3 * t_ov / args.steps, 4),
-                                  "how": "PipelinedSegmentation.replay_streamed: double-buffered inputs, copy stream"}
+                                  "how": "PipelinedSegmentation.replay_streamed: ring of 3 input buffers, copy stream"}
     stats = run_plan().host_stats()
     assert all(s.rc == 0 for s in stats), [s.rc for s in stats]
     assert all(torch.isfinite(o).all() for o in (out if isinstance(out, list) else [out]))
@@ -603,9 +607,10 @@ def main() -> None:
                                     f"{' -> '.join(map(str, levels[1:]))}, NDTNetSegmentation F={F} C={C} eval "
                                     f"per level"),
                        "launch": "eager" if args.eager else (
-                           "hip graph per step (ndnet.pipeline.GraphedSegmentation)" if (levels or args.no_pipeline)
-                           else "2 hip graphs alternating: NDT(batch i) || forward(batch i-1) on two streams "
-                                "(ndnet.pipeline.PipelinedSegmentation)"),
+                           "hip graph per step (ndnet.pipeline.GraphedSegmentation)" if args.no_pipeline
+                           else "NDT(batch i) || forward(batch i-1): a hip graph per stage and ring slot (3 "
+                                "buffers) on two streams ordered by events only, joined once per timed region "
+                                "(ndnet.pipeline.PipelinedSegmentation.replay_steps)"),
                        "global_batch": B * world, "points": n, "nds": k, "parallelism": f"dp{world} (clouds sharded)",
                        "dist_backend": args.dist_backend if world > 1 else None,
                        **({"rehearsal": f"{world} ranks on {ndev} GPU(s)"} if world > ndev else {})},

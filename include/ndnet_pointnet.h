@@ -76,6 +76,13 @@ typedef struct ndnet_pn_chain {
   const float* head_basis;  // [9][head_kin * head_nout]
   int32_t head_kin, head_nout;
   float* head_t1;         // [B][9]
+  // optional prologue (fold_t2 != NULL; chains C and D, layer 0 on the VALU): TNet(64)'s feature
+  // transform applied through layer 0 -- x_t2 = t2[b]^T (W0 x + b0) (ndtnet.py:150-157: bmm of the
+  // bn1(conv1) rows with t2, no ReLU between) -- as the per-cloud layer W0' = W0^T t2[b], b0' = b0^T t2[b],
+  // computed by every workgroup in LDS before layer 0; t2[b] = fold_t2 + b * fold_ld, 64 x 64 row-major
+  // (row = the input channel of conv1's output).  Layer 0 must be 64 wide; its relu flag is applied after.
+  const float* fold_t2;
+  int32_t fold_ld;
 } ndnet_pn_chain;
 
 /* Runs one chain over `batch` clouds on `stream` (a hipStream_t; NULL = default
@@ -96,7 +103,7 @@ int ndnet_pn_debug_stamps(unsigned long long *host, int wgs);
 int ndnet_pn_debug_stamps_clear(void);  /* zeroes them (timing builds; else -20) */
 
 /* The per-cloud steps between the chains (TNet FC heads ndtnet.py:53-60 and
- * the weight folds of pointnet_hip.py), for batch <= 16 clouds:
+ * the t1 weight fold of pointnet_hip.py), for batch <= 16 clouds:
  *   ndnet_pn_fc_run:     out[b][n] = act(bias[n] + sum_k in[b][k] W[n][k]),
  *                        W row-major [N][K], K % 4 == 0, act = ReLU if relu
  *                        (Linear + folded BatchNorm1d + ReLU, ndtnet.py:55-56)
@@ -105,7 +112,6 @@ int ndnet_pn_debug_stamps_clear(void);  /* zeroes them (timing builds; else -20)
  *                        w1f[b] = t1[b] @ basis ([9][kin * nout] row-major) --
  *                        conv1 with t1 folded, written fragment-major with K
  *                        padded to 16 (16 * nout floats per cloud)
- *   ndnet_pn_fold64_run: out[b] (64 x N, fragment-major) = t2[b] (64 x 64) @ rhs (64 x N)
  * Same return codes as ndnet_pn_chain_run; graph-capturable. */
 int ndnet_pn_fc_run(const float *in, int ld_in, const float *W, const float *bias, float *out, int ld_out,
                     int batch, int K, int N, int relu, void *stream);
@@ -117,10 +123,6 @@ int ndnet_pn_fc_mfma_run(const float *in, int ld_in, const float *Wf, const floa
                          int batch, int K, int N, int relu, void *stream);
 int ndnet_pn_head3_run(const float *h2, int ld_h, const float *W3, const float *b3, const float *basis,
                        float *t1, float *w1f, int batch, int K, int kin, int nout, void *stream);
-int ndnet_pn_fold64_run(const float *t2, const float *rhs, float *out, int batch, int N, void *stream);
-/* The same fold in the split-bf16 layout (prec = 1 layers, K = 64): out6[b] =
- * bf16 [N/16][2][3 planes][64 lanes][8] (3 * 64 * N bf16 per cloud). */
-int ndnet_pn_fold64_x6_run(const float *t2, const float *rhs, void *out6, int batch, int N, void *stream);
 
 #ifdef __cplusplus
 }

@@ -872,6 +872,37 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
     // measured +60 us per launch.)
     PN_STAMP(1);
   }
+  if (A.fold_t2) {
+    // TNet(64)'s transform through layer 0 (chains C, D; v0 only, checked on
+    // the host): x_t2 = t2^T (W0 x + b0) = (W0^T t2)^T x + t2^T b0, so layer 0
+    // runs on W0' = W0^T t2 (its 12 used rows) and b0' = b0^T t2 -- 64-term
+    // fp32 dot products over t2 staged in region 1, which layer 0 has not
+    // written yet (the launcher keeps the biases past it)
+    float* const s_t2 = g_smem + reg[1];
+    const f32x4* t2b = reinterpret_cast<const f32x4*>(A.fold_t2 + (int64_t)b * A.fold_ld);
+    for (int e = threadIdx.x; e < 1024; e += kThreads) reinterpret_cast<f32x4*>(s_t2)[e] = t2b[e];
+    __syncthreads();  // + s_w0 (W0^T row-major) and layer 0's bias at boff[0]
+    constexpr int kFold = 13 * 64, kFoldPer = (kFold + kThreads - 1) / kThreads;
+    float fv[kFoldPer];
+#pragma unroll
+    for (int r = 0; r < kFoldPer; r++) {
+      const int e = threadIdx.x + r * kThreads;
+      fv[r] = 0.0f;
+      if (e < kFold) {
+        const int k = e >> 6, nn = e & 63;  // row k of W0^T, or (k == 12) the bias
+        const float* arow = k < 12 ? s_w0 + k * 64 : g_smem + boff[0];
+#pragma unroll 8
+        for (int i = 0; i < 64; i++) fv[r] = fmaf(arow[i], s_t2[i * 64 + nn], fv[r]);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kFoldPer; r++) {
+      const int e = threadIdx.x + r * kThreads;
+      if (e < 12 * 64) s_w0[e] = fv[r];
+      else if (e < kFold) g_smem[boff[0] + (e - 12 * 64)] = fv[r];
+    }
+  }
   __syncthreads();
   if (v0) {
     // layer 0: out = act(x W0^T + b0) for 4 channels of one point, into region 1
@@ -1254,82 +1285,6 @@ __global__ void __launch_bounds__(256) k_pn_head3(const float* __restrict__ h2, 
   }
 }
 
-// TNet(64) fold: out[b] (64 x N, fragment-major, 4 k-groups) = t2[b] (64 x 64)
-// @ rhs (64 x N row-major), N % 64 == 0.  Workgroup (column tile of 64,
-// cloud): both operand tiles in LDS, 4 x 4 outputs per thread; the 4 rows of
-// one column are the 4 consecutive floats of one fragment lane.
-__global__ void __launch_bounds__(256) k_pn_fold64(const float* __restrict__ t2, const float* __restrict__ rhs,
-                                                   float* __restrict__ out, int N) {
-  __shared__ float s_a[64][65];
-  __shared__ float s_b[64][68];
-  const int b = blockIdx.y, j0 = blockIdx.x * 64;
-  const float* A = t2 + (int64_t)b * 4096;
-  for (int e = threadIdx.x; e < 4096; e += 256) {
-    s_a[e >> 6][e & 63] = A[e];
-    s_b[e >> 6][e & 63] = rhs[(int64_t)(e >> 6) * N + j0 + (e & 63)];
-  }
-  __syncthreads();
-  const int ti = (threadIdx.x >> 4) * 4, tj = (threadIdx.x & 15) * 4;
-  float acc[4][4] = {};
-  for (int k = 0; k < 64; k++) {
-    float av[4], bv[4];
-#pragma unroll
-    for (int r = 0; r < 4; r++) av[r] = s_a[ti + r][k];
-#pragma unroll
-    for (int c = 0; c < 4; c++) bv[c] = s_b[k][tj + c];
-#pragma unroll
-    for (int r = 0; r < 4; r++)
-#pragma unroll
-      for (int c = 0; c < 4; c++) acc[r][c] += av[r] * bv[c];
-  }
-  float* o = out + (int64_t)b * 64 * N;
-#pragma unroll
-  for (int c = 0; c < 4; c++)
-    *reinterpret_cast<f32x4*>(o + frag_index(ti, j0 + tj + c, 4)) = f32x4{acc[0][c], acc[1][c], acc[2][c], acc[3][c]};
-}
-
-// The same fold written in the split-bf16 layout (K = 64: two 32-row
-// k-groups): out6[b] = [N/16][2][3 planes][64 lanes][8] bf16.
-__global__ void __launch_bounds__(256) k_pn_fold64_x6(const float* __restrict__ t2, const float* __restrict__ rhs,
-                                                      __bf16* __restrict__ out6, int N) {
-  __shared__ float s_a[64][65];
-  __shared__ float s_b[64][68];
-  const int b = blockIdx.y, j0 = blockIdx.x * 64;
-  const float* A = t2 + (int64_t)b * 4096;
-  for (int e = threadIdx.x; e < 4096; e += 256) {
-    s_a[e >> 6][e & 63] = A[e];
-    s_b[e >> 6][e & 63] = rhs[(int64_t)(e >> 6) * N + j0 + (e & 63)];
-  }
-  __syncthreads();
-  const int ti = (threadIdx.x >> 4) * 4, tj = (threadIdx.x & 15) * 4;
-  float acc[4][4] = {};
-  for (int k = 0; k < 64; k++) {
-    float av[4], bv[4];
-#pragma unroll
-    for (int r = 0; r < 4; r++) av[r] = s_a[ti + r][k];
-#pragma unroll
-    for (int c = 0; c < 4; c++) bv[c] = s_b[k][tj + c];
-#pragma unroll
-    for (int r = 0; r < 4; r++)
-#pragma unroll
-      for (int c = 0; c < 4; c++) acc[r][c] += av[r] * bv[c];
-  }
-  __bf16* o = out6 + (int64_t)b * 64 * N * 3;
-#pragma unroll
-  for (int r = 0; r < 4; r++)
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const int k = ti + r, n = j0 + tj + c;
-      const int64_t e = ((((int64_t)(n >> 4) * 2 + (k >> 5)) * 3) * 64 + ((k >> 3) & 3) * 16 + (n & 15)) * 8 + (k & 7);
-      __bf16 h, m, l;
-      split3(acc[r][c], h, m, l);
-      o[e] = h;
-      o[e + 64 * 8] = m;
-      o[e + 2 * 64 * 8] = l;
-    }
-}
-
-
 }  // namespace
 
 extern "C" {
@@ -1368,18 +1323,6 @@ int ndnet_pn_head3_run(const float* h2, int ld_h, const float* W3, const float* 
   return hipGetLastError() == hipSuccess ? 0 : -21;
 }
 
-int ndnet_pn_fold64_x6_run(const float* t2, const float* rhs, void* out6, int batch, int N, void* stream) {
-  if (!t2 || !rhs || !out6 || batch <= 0 || N <= 0 || N % 64) return -20;
-  k_pn_fold64_x6<<<dim3(N / 64, batch), 256, 0, (hipStream_t)stream>>>(t2, rhs, (__bf16*)out6, N);
-  return hipGetLastError() == hipSuccess ? 0 : -21;
-}
-
-int ndnet_pn_fold64_run(const float* t2, const float* rhs, float* out, int batch, int N, void* stream) {
-  if (!t2 || !rhs || !out || batch <= 0 || N <= 0 || N % 64 || ((uintptr_t)out % 16)) return -20;
-  k_pn_fold64<<<dim3(N / 64, batch), 256, 0, (hipStream_t)stream>>>(t2, rhs, out, N);
-  return hipGetLastError() == hipSuccess ? 0 : -21;
-}
-
 // One fused point-MLP chain over `batch` clouds on `stream` (see pointnet.h).
 
 // Timing builds: zeroes the stamp array (before a launch whose stamps are read)
@@ -1407,6 +1350,13 @@ int ndnet_pn_debug_stamps(unsigned long long* host, int wgs) {
 }
 #endif
 
+// an inconsistent argument block: NDNET_ERR_ARG, with the failing check's line on stderr
+#define PN_ARG_FAIL()                                                                          \
+  do {                                                                                         \
+    fprintf(stderr, "ndnet_amd: chain launch: invalid argument (pointnet_kernels.hip:%d)\n", __LINE__); \
+    return -20;                                                                                \
+  } while (0)
+
 #if NDNET_PN_TILE == 64
 int ndnet_pn_chain_run(const ndnet_pn_chain* args, int batch, void* stream) {
 #else
@@ -1414,7 +1364,7 @@ int ndnet_pn_chain_run_t32(const ndnet_pn_chain* args, int batch, void* stream) 
 #endif
   if (!args || batch <= 0 || args->num_layers < 1 || args->num_layers > NDNET_PN_MAX_LAYERS || args->num_points <= 0 ||
       args->in_cols < 1 || args->in_cols > args->L[0].K || args->in_cols > args->x_ld)
-    return -20;
+    PN_ARG_FAIL();
   // activation regions: layer l reads region l & 1 (or the fused-chunk buffer
   // after a fused layer) and writes region (l + 1) & 1
   int w[2] = {args->L[0].K, 0};
@@ -1425,31 +1375,31 @@ int ndnet_pn_chain_run_t32(const ndnet_pn_chain* args, int batch, void* stream) 
     if (!L.w || !L.bias || L.K <= 0 || L.K % 16 || L.N <= 0 || L.N % 32 || (L.N > 32 && L.N % 64) ||
         ((uintptr_t)L.w % 16) ||
         L.w_cloud_stride % 4)
-      return -20;
+      PN_ARG_FAIL();
     const bool fed = l > 0 && args->L[l - 1].fuse_next;
-    if (L.prec < 0 || L.prec > 1) return -20;
+    if (L.prec < 0 || L.prec > 1) PN_ARG_FAIL();
     if (L.prec) {  // split-bf16: reads planes its producer writes (into a region, or the fused chunks)
-      if (l == 0 || L.K % 32 || args->L[l - 1].N != L.K) return -20;
+      if (l == 0 || L.K % 32 || args->L[l - 1].N != L.K) PN_ARG_FAIL();
       if (fed) qprec = 1;
       else planes |= 1 << (l & 1);
     }
     if (fed) {
-      if (L.K != args->L[l - 1].N || (L.N != 64 && L.N != 128 && L.N != 256) || L.fuse_next) return -20;
+      if (L.K != args->L[l - 1].N || (L.N != 64 && L.N != 128 && L.N != 256) || L.fuse_next) PN_ARG_FAIL();
     } else if (l > 0 && L.K > w[l & 1]) {
-      return -20;
+      PN_ARG_FAIL();
     }
     if (L.fuse_next) {
-      if (l + 1 >= args->num_layers || L.N % kFuseNC) return -20;
+      if (l + 1 >= args->num_layers || L.N % kFuseNC) PN_ARG_FAIL();
       has_fuse = true;
       continue;  // not stored in a region
     }
     const bool stored = l + 1 < args->num_layers || args->mode == 1;
     if (stored && L.N > w[(l + 1) & 1]) w[(l + 1) & 1] = L.N;
   }
-  if (args->max_width < w[0] || args->max_width2 < w[1] || args->max_width % 8 || args->max_width2 % 8) return -20;
+  if (args->max_width < w[0] || args->max_width2 < w[1] || args->max_width % 8 || args->max_width2 % 8) PN_ARG_FAIL();
   if (args->mode == 1 && (!args->out || args->out_cols <= 0 || args->out_cols > args->L[args->num_layers - 1].N))
-    return -20;
-  if (args->mode == 0 && !args->gmax) return -20;
+    PN_ARG_FAIL();
+  if (args->mode == 0 && !args->gmax) PN_ARG_FAIL();
   // LDS: region 0 | region 1, then the fused pair's chunks.  Q writes the
   // region P reads, after its last chunk, so the chunks may start right after
   // P's input inside that region (and run past its end when it is region 1)
@@ -1467,12 +1417,17 @@ int ndnet_pn_chain_run_t32(const ndnet_pn_chain* args, int batch, void* stream) 
     if (r == 1 || inside + fb <= r0f) fbuf_off = inside;
     total = fbuf_off + (size_t)fb > total ? fbuf_off + (size_t)fb : total;
   }
+  if (args->fold_t2) {  // the t2 fold runs in layer 0's VALU prologue, t2 staged at region 1
+    if (!valu_layer0(*args) || args->head_h2 || args->fold_ld < 4096 || args->fold_ld % 4 || (uintptr_t)args->fold_t2 % 16)
+      PN_ARG_FAIL();
+    if (total < (size_t)r0f + 4096) total = (size_t)r0f + 4096;
+  }
   // every layer's bias after the other regions (layer 0's too: the prologue
   // reads it there when layer 0 runs on the MFMA path)
   const int bias_base = (int)((total + 3) & ~(size_t)3);
   int nbias = 0;
   for (int l = 0; l < args->num_layers; l++) {
-    if (args->L[l].N > 2 * kThreads) return -20;  // the prologue stages <= 2 bias values per thread and layer
+    if (args->L[l].N > 2 * kThreads) PN_ARG_FAIL();  // the prologue stages <= 2 bias values per thread and layer
     nbias += args->L[l].N;
   }
   total = (size_t)bias_base + nbias;
@@ -1484,7 +1439,7 @@ int ndnet_pn_chain_run_t32(const ndnet_pn_chain* args, int batch, void* stream) 
       return -21;
     attr_set = true;
   }
-  if (lds > 160 * 1024) return -20;
+  if (lds > 160 * 1024) PN_ARG_FAIL();
   dim3 grid((args->num_points + kP - 1) / kP, batch);
   k_pn_chain<<<grid, kThreads, lds, (hipStream_t)stream>>>(*args, planes, fbuf_off, bias_base);
   hipError_t e = hipGetLastError();

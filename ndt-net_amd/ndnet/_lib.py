@@ -118,8 +118,6 @@ POINTNET_EXPORTS: dict = {
     "ndnet_pn_fc_run": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "ndnet_pn_fc_mfma_run": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "ndnet_pn_head3_run": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
-    "ndnet_pn_fold64_run": (_I, [_P, _P, _P, _I, _I, _P]),
-    "ndnet_pn_fold64_x6_run": (_I, [_P, _P, _P, _I, _I, _P]),
 }
 
 

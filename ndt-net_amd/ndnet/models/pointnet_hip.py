@@ -88,7 +88,8 @@ class _Chain(ctypes.Structure):
                 ("out", ctypes.c_void_p), ("clear", ctypes.c_void_p), ("clear_count", ctypes.c_int64),
                 ("head_h2", ctypes.c_void_p), ("head_ld", ctypes.c_int32), ("head_K", ctypes.c_int32),
                 ("head_w3", ctypes.c_void_p), ("head_b3", ctypes.c_void_p), ("head_basis", ctypes.c_void_p),
-                ("head_kin", ctypes.c_int32), ("head_nout", ctypes.c_int32), ("head_t1", ctypes.c_void_p)]
+                ("head_kin", ctypes.c_int32), ("head_nout", ctypes.c_int32), ("head_t1", ctypes.c_void_p),
+                ("fold_t2", ctypes.c_void_p), ("fold_ld", ctypes.c_int32)]
 
 
 
@@ -198,10 +199,11 @@ class _Folded:
             self.D_tail = [(_wT(self.s2w, 512, 256), self.s2b), (_wT(self.s3w, 256, 128), self.s3b),
                            (_wT(self.s4w, 128, _npad(self.C1)), _bpad(self.s4b, _npad(self.C1)))]
             self.c1wT = self.c1w.t().contiguous()         # [12, 64]
-            self.c2wT = self.c2w.t().contiguous()         # [64, 128]
-            self.s1aT = self.s1a.t().contiguous()         # [64, 512]
-            # x_t2 = t2^T x1 feeds conv2 and the seg head: one bmm t2 @ [W2^T | Ws1a^T]
-            self.t2_rhs = torch.cat((self.c2wT, self.s1aT), dim=1).contiguous()  # [64, 640]
+            # x_t2 = t2^T x1 (ndtnet.py:152-157) feeds conv2 and the seg head's
+            # conv1a; t2 is folded into chains C / D's layer 0 (their prologue,
+            # ndnet_pn_chain.fold_t2), so both layers keep shared weights
+            self.C_mid = (_wT(self.c2w, 64, 128), self.c2b)          # conv2 W^T [64, 128]
+            self.s1aT = _wT(self.s1a, 64, 512)                        # seg conv1a W^T [64, 512]
             # conv1 of the t1-transformed input: (W1 M(t1))^T = sum_ac t1[a,c] E_ac^T W1^T,
             # M(t1) = blockdiag(t1, kron(t1, I3)) (p' = t1 p, C' = t1 C)
             dev = self.c1wT.device
@@ -213,9 +215,11 @@ class _Folded:
                         E[3 * a + c, 3 + 3 * a + j, 3 + 3 * c + j] = 1.0
             self.t1_basis = torch.matmul(E.transpose(1, 2), self.c1wT).reshape(9, 12 * 64).contiguous()
             # fragment-major copies of the shared per-point layers (the HIP chains)
-            self.frag = {id(w): _frag(w) for w, _ in self.A + self.B_tail + [self.C_tail] + self.D_tail}
-            # the wide pooled layers in split-bf16 form
-            self.wide = [self.A[2][0], self.B_tail[2][0], self.C_tail[0], self.D_tail[0][0], self.D_tail[1][0]]
+            self.frag = {id(w): _frag(w) for w, _ in
+                         self.A + self.B_tail + [self.C_mid, self.C_tail, (self.s1aT, None)] + self.D_tail}
+            # the wide pooled layers, conv2 and the seg head's conv1a in split-bf16 form
+            self.wide = [self.A[2][0], self.B_tail[2][0], self.C_tail[0], self.D_tail[0][0], self.D_tail[1][0],
+                         self.C_mid[0], self.s1aT]
             if X6_NARROW:  # the K >= 64 fp32-MFMA layers too (64 -> 128 of TNet(3) / TNet(64), 64 -> 64, 128 -> C+1)
                 self.wide += [self.A[1][0], self.B_tail[0][0], self.B_tail[1][0], self.D_tail[2][0]]
             self.frag6 = {id(w): _frag_x6(w) for w in self.wide}
@@ -341,22 +345,17 @@ class _Workspace:
         self.cvec = torch.empty((B, 512), **f32)        # per-cloud bias of the seg head
         # per-cloud folded weights: plain W^T for the torch emulation ...
         self.w1T = torch.empty((B, 12, 64), **f32)      # (W1 M(t1))^T per cloud
-        self.t2w = torch.empty((B, 64, 640), **f32)     # t2 @ [W2^T | Ws1a^T]
-        self.w2T, self.sT = self.t2w[:, :, :128], self.t2w[:, :, 128:]
+        self.w1t2 = torch.empty((B, 12, 64), **f32)     # (W1 M(t1))^T t2: layer 0 of chains C / D
+        self.b1t2 = torch.empty((B, 64), **f32)         # b1^T t2
         # ... and fragment-major for the HIP chains (K of conv1 padded 12 -> 16);
-        # column blocks are outermost, so conv2's 8 blocks precede seg conv1a's 32
+        # the HIP chains C / D fold t2 in their prologue (fold_t2)
         self.w1f = torch.empty((B, 16 * 64), **f32)
-        self.t2wf = torch.empty((B, 64 * 640), **f32)
-        # t2-folded conv2 / seg conv1a also in the split-bf16 layout ([cb][kg][plane][lane][8])
-        self.t2wf6 = None
-        if SPLIT_BF16:
-            self.t2wf6 = torch.empty((B, 3 * 64 * 640), dtype=torch.bfloat16, device=dev)
         self.specs = [  # torch emulation: (in_cols, [(W^T, bias)], relus, mode, kwargs)
             (3, W.A, (1, 1, 1), 0, dict(gmax=self.g1)),
             (12, [(self.w1T, W.c1b)] + W.B_tail, (0, 1, 1, 1), 0, dict(gmax=self.g2)),
-            (12, [(self.w1T, W.c1b), (self.w2T, W.c2b), W.C_tail], (0, 0, 0), 0, dict(gmax=self.g3)),
+            (12, [(self.w1t2, self.b1t2), W.C_mid, W.C_tail], (0, 0, 0), 0, dict(gmax=self.g3)),
             # the 512-wide seg conv1 output feeds conv2 chunk by chunk (never stored whole)
-            (12, [(self.w1T, W.c1b), (self.sT, self.cvec)] + W.D_tail, (0, 1, 1, 1, 0), 1,
+            (12, [(self.w1t2, self.b1t2), (W.s1aT, self.cvec)] + W.D_tail, (0, 1, 1, 1, 0), 1,
              dict(out_cols=W.C1, fuse=(1,))),
         ]
 
@@ -367,18 +366,11 @@ class _Workspace:
             return (W.frag[id(w)], 0, b, w.shape[0], w.shape[1])
 
         L1 = (self.w1f, self.w1f.stride(0), W.c1b, 16, 64)
-        if SPLIT_BF16:  # per-cloud stride in floats (bf16 pairs); conv2's 8 column blocks come first
-            s6 = self.t2wf6.stride(0) // 2
-            L2 = (self.t2wf6, s6, W.c2b, 64, 128, 1)
-            Ls = (self.t2wf6[:, 8 * 2 * 3 * 64 * 8:], s6, self.cvec, 64, 512, 1)
-        else:
-            L2 = (self.t2wf, self.t2wf.stride(0), W.c2b, 64, 128)
-            Ls = (self.t2wf[:, 64 * 128:], self.t2wf.stride(0), self.cvec, 64, 512)
         self.hip_layers = [
             [shared(x) for x in W.A],
             [L1] + [shared(x) for x in W.B_tail],
-            [L1, L2, shared(W.C_tail)],
-            [L1, Ls] + [shared(x) for x in W.D_tail],
+            [L1, shared(W.C_mid), shared(W.C_tail)],
+            [L1, shared((W.s1aT, self.cvec))] + [shared(x) for x in W.D_tail],
         ]
         self.N = N
         self.structs = None
@@ -403,6 +395,8 @@ class _Workspace:
                 cb.head_w3, cb.head_b3 = W.t1["f3"].data_ptr(), W.t1["c3"].data_ptr()
                 cb.head_basis, cb.head_kin, cb.head_nout = W.t1_basis.data_ptr(), 12, 64
                 cb.head_t1 = self.t1.data_ptr()
+            for cd in self.structs[2:]:  # chains C / D: t2 through layer 0 (prologue fold)
+                cd.fold_t2, cd.fold_ld = self.t2.data_ptr(), self.t2.stride(0)
         if chain_timing is not None:  # torch events on the launch stream (bench.py)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -480,15 +474,7 @@ def _glue_hip(W, ws, B: int):
         t = W.t2
         fc(ws.g2, t["f1"], t["c1"], ws.h1, True)
         fc(ws.h1, t["f2"], t["c2"], ws.h2, True)
-        fc(ws.h2, t["f3"], t["c3"], ws.t2, False)
-        if ws.t2wf6 is not None:
-            rc = _lib.lib().ndnet_pn_fold64_x6_run(ws.t2.data_ptr(), W.t2_rhs.data_ptr(), ws.t2wf6.data_ptr(), B,
-                                                   W.t2_rhs.shape[1], st())
-            _lib.check(rc, "ndnet_pn_fold64_x6_run")
-        else:
-            rc = _lib.lib().ndnet_pn_fold64_run(ws.t2.data_ptr(), W.t2_rhs.data_ptr(), ws.t2wf.data_ptr(), B,
-                                                W.t2_rhs.shape[1], st())
-            _lib.check(rc, "ndnet_pn_fold64_run")
+        fc(ws.h2, t["f3"], t["c3"], ws.t2, False)  # t2: folded into chains C / D's layer 0 by their prologue
 
     def seg_bias():
         fc(ws.g3[:, : W.F], W.s1g, W.s1b, ws.cvec, False)
@@ -504,7 +490,8 @@ def _glue_torch(W, ws, B: int):
 
     def head_b():
         t2 = _fc_head(ws.g2, W.t2, 64, ws.h1, ws.h2, ws.t2)
-        torch.matmul(t2, W.t2_rhs, out=ws.t2w)
+        torch.matmul(ws.w1T, t2, out=ws.w1t2)
+        torch.matmul(W.c1b[None, None, :], t2, out=ws.b1t2.view(B, 1, 64))
 
     def seg_bias():
         torch.addmm(W.s1b, ws.g3[:, : W.F], W.s1bT, out=ws.cvec)

@@ -26,15 +26,6 @@ from . import _lib
 from .preprocessing.ndtnet_preprocessing import NdtPlan, ndt_multiscale, ndt_preprocessing, get_plan
 
 
-# PipelinedSegmentation step order: "free" (default) lets the two streams run
-# unordered; "front" runs k_front alone and starts the forward behind it, the
-# rest of the NDT stage beside the forward (measured 1.5% slower: Welford and
-# the chains cannot share a CU -- 164 and 4 x 128 VGPRs per SIMD -- so the two
-# still serialise, now with k_front's full-chip phase exposed)
-FRONT_FIRST = os.environ.get("NDNET_PIPE_ORDER", "free") == "front"
-# "ndt": unordered, but the NDT stage's launches captured ahead of the
-# forward's (measured 2.5% slower: 62.0-62.5k vs 63.7-64.1k clouds/s)
-NDT_FIRST = os.environ.get("NDNET_PIPE_ORDER", "free") == "ndt"
 # CU share of the pipelined NDT stage (ndnet_ndt_set_cu_share): k_front and
 # k_welford_q take CUs / share, leaving the rest to the forward's kernels on
 # the other stream.  Measured on C2 (profiles/r03n_cu_share.txt): share 2
@@ -141,7 +132,7 @@ class GraphedSegmentation:
 class PipelinedSegmentation:
     """Two-stage pipeline over consecutive batches: step i runs the NDT stage
     of batch i on one stream while the forward of batch i - 1 runs on
-    another, from two alternating HIP graphs (the NDT rows double-buffered).
+    another, over a ring of R = 3 input / row buffers.
 
     The NDT stage is latency-bound (dependent bisection passes with chip-level
     barriers, one-workgroup-per-cloud prune walks, small KL launches) and the
@@ -150,27 +141,49 @@ class PipelinedSegmentation:
     forward of step i returns the log-probs of the batch of step i - 1 (the
     first step's forward runs on the warm-up batch).
 
-    The two graphs read alternating input buffers: ``points`` is the buffer
-    the NEXT ``replay()`` reads (fill it, then replay); ``load_resident(pts)``
-    fills both.  ``replay_streamed(host_next)`` replays the next step and, on
-    a copy stream overlapped with it, copies ``host_next`` (pinned host
-    memory) into the buffer of the step after it -- the PCIe-inclusive
-    serving loop.  ``replay()`` returns the static ``[B, num_nds, C+1]``
-    output of that step's forward.
+    Each stage of each ring slot is its own HIP graph, captured on its own
+    stream (``g_ndt[j]`` on the NDT stream, ``g_fwd[j]`` on the forward
+    stream).  Step i (slot j = i % R) reads input j, writes rows j, and its
+    forward reads rows j - 1.  The streams are ordered by events only: the
+    forward of step i waits for the NDT of step i - 1 (the rows it reads), the
+    NDT of step i for the forward of step i - 2 (the last reader of the rows
+    it overwrites).  ``replay()`` runs one step joined with the caller's
+    stream at both ends (its output is ready in stream order);
+    ``replay_steps(k)`` runs k steps joined only at the ends, so the NDT
+    stream runs up to a step ahead of the forward stream and no per-step
+    join separates the graphs.  (One graph holding several steps crashed
+    hipStreamEndCapture on this ROCm, profiles/r03t_pipeline.txt.)
+
+    ``points`` is the buffer the NEXT step reads (fill it, then replay);
+    ``load_resident(pts)`` fills every buffer.  ``replay_streamed(host_next)``
+    replays the next step and, on a copy stream overlapped with it, copies
+    ``host_next`` (pinned host memory) into the buffer of the step after it --
+    the PCIe-inclusive serving loop.
+
+    ``levels`` (config C5): the NDT stage is ndt_multiscale (downsample to
+    levels[0], prune to each further level) and the forward stage one forward
+    per level; the output is then the list of per-level log-probs.
     """
 
+    R = 3  # ring depth of the input / row buffers
+
     def __init__(self, model, num_nds: int, batch: int, num_points: int,
-                 device: Optional[torch.device] = None, warmup: int = 2, cu_share: Optional[int] = None) -> None:
+                 device: Optional[torch.device] = None, warmup: int = 2, cu_share: Optional[int] = None,
+                 levels=None) -> None:
         _lib.require_gpu()
         if model.training:
             raise ValueError("PipelinedSegmentation needs an eval-mode model")
         dev = torch.device(device) if device is not None else next(model.parameters()).device
+        self.levels = tuple(int(k) for k in levels) if levels else None
+        if self.levels:
+            if any(b >= a for a, b in zip(self.levels, self.levels[1:])):
+                raise ValueError(f"levels must be strictly decreasing, got {self.levels}")
+            num_nds = self.levels[0]
         self.model, self.num_nds, self.device = model, int(num_nds), dev
-        self.inputs = [torch.zeros((batch, num_points, 3), dtype=torch.float32, device=dev) for _ in range(2)]
-        self.s_copy = torch.cuda.Stream(device=dev)
-        self.done = [torch.cuda.Event(), torch.cuda.Event()]    # graph j finished (its input is free)
-        self.copied = [torch.cuda.Event(), torch.cuda.Event()]  # input j holds the streamed batch
-        self.rows = [torch.zeros((batch, self.num_nds, 12), dtype=torch.float32, device=dev) for _ in range(2)]
+        R = self.R
+        self.inputs = [torch.zeros((batch, num_points, 3), dtype=torch.float32, device=dev) for _ in range(R)]
+        self.rows = [[torch.zeros((batch, k, 12), dtype=torch.float32, device=dev)
+                      for k in (self.levels or (self.num_nds,))] for _ in range(R)]
         # a plan of its own (not ndt_preprocessing's cached one): its CU share
         # is a property of the pipeline
         self.plan = NdtPlan(batch, num_points, self.num_nds, -1, device=dev)
@@ -181,88 +194,113 @@ class PipelinedSegmentation:
                 self.plan.set_cu_share(cu_share, PIPE_WQ_SHARE)
             except RuntimeError:  # k_front does not fit that share for this shape
                 pass
-        # the forward's launches go first; stream priorities (either way) measured
-        # 35-40% slower than none, so both streams keep the default priority
+        # stream priorities (either way) measured 35-40% slower than none
         self.s_ndt, self.s_fwd = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
-        self.front_done = torch.cuda.Event()
-        side = torch.cuda.Stream(device=dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.no_grad(), torch.cuda.stream(side):
-            for i in range(max(2, warmup)):
-                self._step(i & 1)
-        torch.cuda.current_stream(dev).wait_stream(side)
+        self.s_copy = torch.cuda.Stream(device=dev)
+        self.ndt_done = [torch.cuda.Event() for _ in range(R)]  # NDT of slot j finished (rows j, input j free)
+        self.fwd_done = [torch.cuda.Event() for _ in range(R)]  # forward of slot j finished (rows j - 1 free)
+        self.copied = [torch.cuda.Event() for _ in range(R)]    # input j holds the streamed batch
+        cur = torch.cuda.current_stream(dev)
+        self.s_ndt.wait_stream(cur)
+        self.s_fwd.wait_stream(cur)
+        with torch.no_grad():  # plan / workspace creation, kernel attributes
+            for i in range(max(R, warmup)):
+                with torch.cuda.stream(self.s_ndt):
+                    self._ndt(i % R)
+                with torch.cuda.stream(self.s_fwd):
+                    self._fwd(i % R)
         torch.cuda.synchronize(dev)
-        self.graphs = [torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()]
-        self.out = [None, None]
-        for j in range(2):
-            with torch.no_grad(), torch.cuda.graph(self.graphs[j]):
-                self.out[j] = self._step(j)
+        self.g_ndt, self.g_fwd, self.out = [], [], []
+        for j in range(R):
+            g = torch.cuda.CUDAGraph()
+            with torch.no_grad(), torch.cuda.graph(g, stream=self.s_ndt):
+                self._ndt(j)
+            self.g_ndt.append(g)
+            g = torch.cuda.CUDAGraph()
+            with torch.no_grad(), torch.cuda.graph(g, stream=self.s_fwd):
+                self.out.append(self._fwd(j))
+            self.g_fwd.append(g)
+        torch.cuda.synchronize(dev)
         self._pinned = _Pinned(model, [self.plan])
         self.i = 0
 
-    def _step(self, j: int) -> torch.Tensor:
+    def _ndt(self, j: int) -> None:
+        """The NDT stage of ring slot j on the current stream."""
+        rows = self.rows[j]
+        self.plan.run(self.inputs[j], None, rows[0], None)
+        for k, blk in zip(self.levels[1:] if self.levels else (), rows[1:]):
+            self.plan.prune(k, blk)
+
+    def _fwd(self, j: int):
+        """The forward stage of ring slot j: the rows of slot j - 1."""
+        outs = [self.model(r[..., :3], r[..., 3:]) for r in self.rows[(j - 1) % self.R]]
+        return outs if self.levels else outs[0]
+
+    def _enqueue(self) -> int:
+        """Launches the next step's two graphs, ordered by events only."""
+        R, j = self.R, self.i % self.R
+        self.s_fwd.wait_event(self.ndt_done[(j - 1) % R])   # its rows: the previous step's NDT
+        with torch.cuda.stream(self.s_fwd):
+            self.g_fwd[j].replay()
+        self.fwd_done[j].record(self.s_fwd)
+        self.s_ndt.wait_event(self.fwd_done[(j - 2) % R])   # rows j: last read by the forward of step i - 2
+        self.s_ndt.wait_event(self.copied[j])               # no-op unless a streamed copy targets input j
+        with torch.cuda.stream(self.s_ndt):
+            self.g_ndt[j].replay()
+        self.ndt_done[j].record(self.s_ndt)
+        self.i += 1
+        return j
+
+    def _fork(self) -> None:
         cur = torch.cuda.current_stream(self.device)
         self.s_ndt.wait_stream(cur)
         self.s_fwd.wait_stream(cur)
-        if FRONT_FIRST:
-            # k_front needs every CU at once (its workgroups meet at cloud
-            # barriers), so it runs alone; the forward starts behind it and the
-            # rest of the NDT stage (Welford, KL: persistent / few-workgroup
-            # kernels) fills the forward's gaps
-            with torch.cuda.stream(self.s_ndt):
-                self.plan.run(self.inputs[j], None, self.rows[j], None, part=1)
-                self.front_done.record(self.s_ndt)
-            self.s_fwd.wait_event(self.front_done)
-            with torch.cuda.stream(self.s_fwd):
-                prev = self.rows[1 - j]
-                out = self.model(prev[..., :3], prev[..., 3:])
-            with torch.cuda.stream(self.s_ndt):
-                self.plan.run(self.inputs[j], None, self.rows[j], None, part=2)
-        elif NDT_FIRST:
-            with torch.cuda.stream(self.s_ndt):
-                self.plan.run(self.inputs[j], None, self.rows[j], None)
-            with torch.cuda.stream(self.s_fwd):
-                prev = self.rows[1 - j]
-                out = self.model(prev[..., :3], prev[..., 3:])
-        else:
-            with torch.cuda.stream(self.s_fwd):
-                prev = self.rows[1 - j]
-                out = self.model(prev[..., :3], prev[..., 3:])
-            with torch.cuda.stream(self.s_ndt):
-                self.plan.run(self.inputs[j], None, self.rows[j], None)
-        cur.wait_stream(self.s_ndt)
-        cur.wait_stream(self.s_fwd)
-        return out
+
+    def _join(self, j: int) -> None:
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_event(self.fwd_done[j])
+        cur.wait_event(self.ndt_done[j])
 
     @property
     def points(self) -> torch.Tensor:
-        """The input buffer the next ``replay()`` reads."""
-        return self.inputs[self.i & 1]
+        """The input buffer the next step reads."""
+        return self.inputs[self.i % self.R]
 
     def load_resident(self, points: torch.Tensor) -> None:
-        """Fill both input buffers (every later step re-reads this batch)."""
+        """Fill every input buffer (every later step re-reads this batch)."""
         for buf in self.inputs:
             buf.copy_(points)
 
-    def replay(self) -> torch.Tensor:
+    def replay(self):
+        """One step, ordered after the caller's stream and before its later work."""
         self._pinned.check()
-        j = self.i & 1
-        cur = torch.cuda.current_stream(self.device)
-        cur.wait_event(self.copied[j])  # no-op unless a streamed copy targets input j
-        self.graphs[j].replay()
-        self.done[j].record(cur)
-        self.i += 1
+        self._fork()
+        j = self._enqueue()
+        self._join(j)
         return self.out[j]
 
-    def replay_streamed(self, host_next: torch.Tensor) -> torch.Tensor:
+    def replay_steps(self, k: int):
+        """k steps with the streams joined to the caller's only at the ends;
+        returns the last step's output."""
+        self._pinned.check()
+        self._fork()
+        j = None
+        for _ in range(k):
+            j = self._enqueue()
+        if j is None:
+            return None
+        self._join(j)
+        return self.out[j]
+
+    def replay_streamed(self, host_next: torch.Tensor):
         """``replay()`` with the H2D copy of the batch after it overlapped."""
-        j = self.i & 1
+        nxt = (self.i + 1) % self.R
         out = self.replay()
-        # input 1-j was last read by the previous step's graph
-        self.s_copy.wait_event(self.done[1 - j])
+        # input nxt: last read by the NDT of step i + 1 - R, finished before this step's join
+        self.s_copy.wait_event(self.ndt_done[nxt])
         with torch.cuda.stream(self.s_copy):
-            self.inputs[1 - j].copy_(host_next, non_blocking=True)
-            self.copied[1 - j].record(self.s_copy)
+            self.inputs[nxt].copy_(host_next, non_blocking=True)
+            self.copied[nxt].record(self.s_copy)
         return out
 
     def stats(self) -> list:

@@ -106,6 +106,66 @@ def test_pipelined_steps_equal_sequential_batches():
         assert torch.equal(outs[i + 1], expect[i]), f"batch {i}"
 
 
+def test_pipelined_free_running_steps_equal_sequential_batches():
+    """replay_steps: the two stage streams ordered by events only (the NDT
+    stream up to a step ahead, no per-step join) give every step the forward
+    of the batch before it, bit-equal to the one-graph-per-step path;
+    single-step replays before it keep the ring position."""
+    import torch
+    from ndnet.models.ndtnet import NDTNetSegmentation
+    from ndnet.pipeline import GraphedSegmentation, PipelinedSegmentation
+    from ndnet.synthetic import make_batch
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    m = NDTNetSegmentation(3, 28, 768).to(dev).eval()
+    batches = [torch.from_numpy(make_batch("L", 4, 20_000, seed0=10 * i + 1)).to(dev) for i in range(3)]
+    ref = GraphedSegmentation(m, 400, 4, 20_000, device=dev)
+    expect = [ref(b).clone() for b in batches]
+    pipe = PipelinedSegmentation(m, 400, 4, 20_000, device=dev)
+    for j, b in enumerate(batches):  # step s reads input s % 3
+        pipe.inputs[j].copy_(b)
+    for _ in range(3):
+        pipe.replay()                        # steps 0..2
+    for rnd in range(2):
+        last = pipe.replay_steps(3 + 3 * rnd)  # steps 3..5, then 6..11
+        torch.cuda.synchronize()
+        for j in range(3):  # slot j's last step s = j mod 3: the forward of batch (s - 1) % 3
+            assert torch.equal(pipe.out[j], expect[(j - 1) % 3]), f"round {rnd} slot {j}"
+        assert last.data_ptr() == pipe.out[2].data_ptr()
+    out = pipe.replay()                      # step 12 (slot 0)
+    torch.cuda.synchronize()
+    assert torch.equal(out, expect[2])
+
+
+def test_pipelined_levels_equal_graphed_levels():
+    """C5-shaped pipeline (downsample + two prune levels, a forward per level):
+    every step's per-level outputs, single-step and free-running, bit-equal the
+    one-graph multiscale path on the batch before it."""
+    import torch
+    from ndnet.models.ndtnet import NDTNetSegmentation
+    from ndnet.pipeline import GraphedSegmentation, PipelinedSegmentation
+    from ndnet.synthetic import make_batch
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    m = NDTNetSegmentation(3, 28, 768).to(dev).eval()
+    levels = (400, 200, 100)
+    batches = [torch.from_numpy(make_batch("L", 4, 20_000, seed0=7 * i + 2)).to(dev) for i in range(3)]
+    ref = GraphedSegmentation(m, levels[0], 4, 20_000, device=dev, levels=levels)
+    expect = [[o.clone() for o in ref(b)] for b in batches]
+    pipe = PipelinedSegmentation(m, levels[0], 4, 20_000, device=dev, levels=levels)
+    for j, b in enumerate(batches):
+        pipe.inputs[j].copy_(b)
+    outs = [[o.clone() for o in pipe.replay()] for _ in range(3)]   # steps 0..2
+    pipe.replay_steps(3)                                              # steps 3..5, free-running
+    torch.cuda.synchronize()
+    for s in (1, 2):
+        for lv in range(3):
+            assert torch.equal(outs[s][lv], expect[s - 1][lv]), f"step {s} level {lv}"
+    for j in range(3):  # step 3 + j (slot j): batch (j - 1) % 3
+        for lv in range(3):
+            assert torch.equal(pipe.out[j][lv], expect[(j - 1) % 3][lv]), f"slot {j} level {lv}"
+
+
 def test_pipelined_streamed_host_batches():
     """replay_streamed: host batches copied on a copy stream one step ahead
     (double-buffered inputs) give the same outputs as the one-graph path."""

@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""The training step of tools/train.py:67-81, timed by stage
+on one GPU: labelled NDT on HIP (16 x 100k points -> 1000 NDs, 28 classes,
+one-hot) -> NDTNetSegmentation train-mode forward (BatchNorm batch
+statistics) -> NLL loss -> backward -> Adam.  The forward / backward are
+torch autograd (hipBLASLt / MIOpen kernels); the eval forward of the same
+batch on the HIP chains is timed beside them for the gap.
+
+    python tools/bench_train.py [--steps 20] [--warmup 5] [--batch 16]
+
+Prints one JSON line: ms per stage (HIP events on the step's stream) and
+clouds/s of the whole step.
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "ndt-net_amd"))
+from ndnet.models.ndtnet import NDTNetSegmentation  # noqa: E402
+from ndnet.preprocessing.ndtnet_preprocessing import ndt_preprocessing  # noqa: E402
+from ndnet.synthetic import make_labelled_batch  # noqa: E402
+from ndnet.training import Trainer, segmentation_loss  # noqa: E402
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--points", type=int, default=100_000)
+    ap.add_argument("--nds", type=int, default=1000)
+    ap.add_argument("--classes", type=int, default=28)
+    ap.add_argument("--feature-dim", type=int, default=768)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    pts, gt = make_labelled_batch(a.batch, a.points, a.classes, seed0=0)
+    pts, gt = torch.from_numpy(pts).to(dev), torch.from_numpy(gt).to(dev)
+    model = NDTNetSegmentation(3, a.classes, a.feature_dim)
+    tr = Trainer(model, 1e-3, a.nds, a.classes, dev, ddp=False)
+    names = ("ndt_labelled", "forward_train", "loss", "backward", "adam", "forward_eval_hip")
+    tot = {n: 0.0 for n in names}
+    st = torch.cuda.current_stream(dev)
+    for it in range(a.warmup + a.steps):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)]
+        ev[0].record(st)
+        pcl, covs, g1 = ndt_preprocessing(a.nds, pts, gt, a.classes)
+        ev[1].record(st)
+        model.train()
+        pred = tr.net(pcl, covs)
+        ev[2].record(st)
+        loss = segmentation_loss(pred, g1)
+        ev[3].record(st)
+        tr.opt.zero_grad(set_to_none=True)
+        loss.backward()
+        ev[4].record(st)
+        tr.opt.step()
+        ev[5].record(st)
+        model.eval()
+        with torch.no_grad():
+            model(pcl, covs)
+        ev[6].record(st)
+        torch.cuda.synchronize()
+        if it >= a.warmup:
+            for i, n in enumerate(names):
+                tot[n] += ev[i].elapsed_time(ev[i + 1])
+    ms = {n: round(v / a.steps, 4) for n, v in tot.items()}
+    step = sum(v for n, v in ms.items() if n != "forward_eval_hip")
+    print(json.dumps({"what": "training step (tools/train.py:67-81): HIP labelled NDT + torch train "
+                              "forward/backward + Adam", "batch": a.batch, "points": a.points, "nds": a.nds,
+                      "classes": a.classes, "F": a.feature_dim, "steps": a.steps, "ms": ms,
+                      "step_ms": round(step, 4), "clouds_per_s": round(a.batch / step * 1e3, 1),
+                      "train_forward_vs_hip_eval": round(ms["forward_train"] / ms["forward_eval_hip"], 2)}))
+
+
+if __name__ == "__main__":
+    main()
