@@ -83,6 +83,11 @@ typedef struct ndnet_pn_chain {
   // (row = the input channel of conv1's output).  Layer 0 must be 64 wide; its relu flag is applied after.
   const float* fold_t2;
   int32_t fold_ld;
+  // optional with fold_t2: the cloud's first workgroup also writes W0' fragment-major (K = 16, rows
+  // 12..15 untouched: zero-initialise them) to fold_out_w + b * 1024 and b0' to fold_out_b + b * 64,
+  // so a later chain runs the same transformed layer 0 as a plain per-cloud layer (chain D)
+  float* fold_out_w;
+  float* fold_out_b;
 } ndnet_pn_chain;
 
 /* Runs one chain over `batch` clouds on `stream` (a hipStream_t; NULL = default

@@ -129,6 +129,7 @@ struct Plan {
   uint32_t* nkeys;     // [B][ndcap]
   double* chain;       // [B][ndcap][12][9]
   uint32_t* chain_ps;  // [B][ndcap][12] perm | (signum < 0) << 8
+  uint32_t* chain_ok;  // [B][ndcap] bit t: LU state t has det != 0 and sgndet != 0 (lazy clouds only)
   double* slot_val;    // [B][ecap]
   uint32_t* slot_flag; // [B][ecap]
   double* ev_val;      // [B][ecap]
@@ -917,6 +918,13 @@ struct WqChainArgs {
   uint32_t* chain_ps;      // [B][12][ndcap]
   double* cov_post;        // [B][ndcap][9]
   uint64_t vcap;
+  // lazy run (KLArgs.mode kKLLazy): a cloud with num_nds <= lazy_k defers its
+  // list (kl_list_deferrable), so its events are only flagged: it stores, per
+  // ND, which LU states have a non-zero determinant (chain_ok) instead of the
+  // states themselves (k_kl_chains recomputes them if the list is ever built).
+  // 0: every cloud stores its states.
+  uint64_t lazy_k;
+  uint32_t* chain_ok;      // [B][ndcap]
 };
 
 template <typename T>
@@ -1268,6 +1276,8 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
       const uint64_t ob = (uint64_t)b * ndcap, u = o - ob;
       double* chain = CA.chain + ob * 108 + u;
       uint32_t* ps = CA.chain_ps + ob * 12 + u;
+      const bool flags_only = CA.lazy_k && nd <= CA.lazy_k;  // a deferred cloud (wave-uniform)
+      uint32_t okb = 0;
 #ifdef NDNET_WQ_NOCHAIN  // timing experiment only (wrong results): no LU chain
       for (int t = 0; t < 0; t++) {
 #else
@@ -1276,12 +1286,17 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
         uint32_t perm;
         int sg;
         lu3(S, perm, sg);
+        if (flags_only) {  // what kl_event's flag reads of the state (kullback_leibler.c:57-70)
+          okb |= (lu3_det(S, sg) != 0 && lu3_sgndet(S, sg) != 0 ? 1u : 0u) << t;
+          continue;
+        }
 #ifndef NDNET_WQ_NOCHAINSTORE  // timing experiment only (wrong results): LU chain without its stores
 #pragma unroll
         for (int q = 0; q < 9; q++) chain[(uint64_t)(9 * t + q) * ndcap] = S[q];
         ps[(uint64_t)t * ndcap] = perm | (sg < 0 ? 0x100u : 0u);
 #endif
       }
+      if (flags_only) CA.chain_ok[o] = okb;
 #pragma unroll
       for (int q = 0; q < 9; q++) CA.cov_post[9 * o + q] = S[q];
     }
@@ -1337,6 +1352,7 @@ struct KLArgs {
   uint32_t* nkeys_all;
   double* chain_all;
   uint32_t* chain_ps_all;
+  uint32_t* chain_ok_all;
   double* slot_val_all;
   uint32_t* slot_flag_all;
   double* ev_val_all;
@@ -1721,6 +1737,21 @@ __device__ void pad_class_rows(const KLArgs& A, int b, uint64_t k, uint32_t num_
 // score = false only flags it.  Every load is issued unconditionally from
 // clamped indices, in three rounds (neighbour -> counts and chain masks -> LU
 // states).
+// The flag of an event of a deferred cloud from the chains' determinant bits
+// (k_welford_q's chain_ok): the same rules as kl_event without the states.
+__device__ inline uint32_t kl_event_flag(const KLArgs& A, int b, uint32_t s) {
+  const uint64_t ob = (uint64_t)b * A.ndcap;
+  const uint32_t u = s / 6, d = s % 6;
+  const int32_t w = A.nb_all[6 * ob + s];
+  if (w < 0) return 0;
+  const uint32_t wu = (uint32_t)w;
+  if (A.nd_n[ob + u] <= 1 || A.nd_n[ob + wu] <= 1) return 1;  // kl_divergence returns -1, the entry is kept
+  const uint32_t mu = A.nkeys_all[ob + u], mw = A.nkeys_all[ob + wu];
+  const int rp = __popc(mu & ((1u << (3 + d)) - 1u));
+  const int rq = __popc(mw & ((1u << qslot_of_dir(d ^ 1u)) - 1u));
+  return (A.chain_ok_all[ob + u] >> rp) & (A.chain_ok_all[ob + wu] >> rq) & 1u;
+}
+
 __device__ inline void kl_event(const KLArgs& A, int b, uint32_t s, bool score, uint32_t& flag, double& val) {
   const uint64_t ob = (uint64_t)b * A.ndcap;
   const uint32_t u = s / 6, d = s % 6;
@@ -1797,11 +1828,15 @@ __global__ void __launch_bounds__(kChunk) k_kl_rank_chunks(KLArgs A) {
   const bool deferred = kl_list_deferrable(A, c);
   uint32_t fl = 0;
   double vl = 0.0;
+  if (deferred) {
+    fl = kl_event_flag(A, b, sl < nslots ? sl : 0u);
+  } else {
 #ifdef NDNET_RANK_NOSCORE  // timing experiment only (wrong results): flags without the KL scores
-  kl_event(A, b, sl < nslots ? sl : 0u, false, fl, vl);
+    kl_event(A, b, sl < nslots ? sl : 0u, false, fl, vl);
 #else
-  kl_event(A, b, sl < nslots ? sl : 0u, !deferred, fl, vl);  // the clamped slot's result is dropped
+    kl_event(A, b, sl < nslots ? sl : 0u, true, fl, vl);  // the clamped slot's result is dropped
 #endif
+  }
   if (deferred) {  // count the cloud's events (stats num_events / num_kl), one atomic per wave
     const unsigned long long bal = __ballot(sl < nslots && fl);
     if ((t & 63) == 0 && bal)
@@ -2308,7 +2343,7 @@ static void plan_free(Plan* P) {
   void* bufs[] = {P->flims, P->frec, P->fwgcnt, P->fbar, P->ctl, P->stamps, P->dense_of, P->vox, P->gbits, P->pkeys, P->did, P->bin_cnt, P->nd_base,
                   P->nd_pts, P->nd_lbl, P->nd_n,
                   P->nd_mean, P->nd_cov, P->nd_cov_post, P->nd_cls, P->hist, P->nb, P->keys, P->nkeys,
-                  P->chain, P->chain_ps, P->slot_val, P->slot_flag, P->ev_val, P->ev_p, P->ev_q, P->ev_min,
+                  P->chain, P->chain_ps, P->chain_ok, P->slot_val, P->slot_flag, P->ev_val, P->ev_p, P->ev_q, P->ev_min,
                   P->sort_key, P->sort_idx, P->nan_list, P->nan_key, P->nan_slot, P->chunk_nanbase, P->ord_val, P->ord_p, P->ord_q,
                   P->first_occ, P->tmp_u32, P->alive, P->d_stats, P->chunk_cnt, P->chunk_min, P->wq_ctr};
   for (void* b : bufs)
@@ -2339,6 +2374,7 @@ static KLArgs kl_args(Plan* P, uint64_t k, float* out, float* out_cls, double* p
   A.nkeys_all = P->nkeys;
   A.chain_all = P->chain;
   A.chain_ps_all = P->chain_ps;
+  A.chain_ok_all = P->chain_ok;
   A.slot_val_all = P->slot_val;
   A.slot_flag_all = P->slot_flag;
   A.ev_val_all = P->ev_val;
@@ -2383,6 +2419,32 @@ static size_t merge_lds_bytes(const Plan* P);
 
 // The event sort of the clouds in A's scope (every cloud in a run, the
 // deferred ones in a build).
+// The LU chain states of a deferred cloud (k_welford_q stored only their
+// determinant bits): from the pre-KL covariance and the chain mask, the same
+// in-place lu3 sequence as k_welford_q's epilogue, one thread per ND.
+__global__ void __launch_bounds__(256) k_kl_chains(KLArgs A) {
+  const int b = blockIdx.y;
+  const CloudCtl& c = A.ctl[b];
+  if (c.state != kAccepted || !c.kl_deferred) return;
+  const uint32_t u = blockIdx.x * 256 + threadIdx.x;
+  if (u >= c.num_nds) return;
+  const uint64_t ob = (uint64_t)b * A.ndcap;
+  double S[9];
+#pragma unroll
+  for (int q = 0; q < 9; q++) S[q] = A.nd_cov[9 * (ob + u) + q];
+  const int nT = __popc(A.nkeys_all[ob + u]);
+  double* chain = A.chain_all + ob * 108 + u;
+  uint32_t* ps = A.chain_ps_all + ob * 12 + u;
+  for (int t = 0; t < nT; t++) {
+    uint32_t perm;
+    int sg;
+    lu3(S, perm, sg);
+#pragma unroll
+    for (int q = 0; q < 9; q++) chain[(uint64_t)(9 * t + q) * A.ndcap] = S[q];
+    ps[(uint64_t)t * A.ndcap] = perm | (sg < 0 ? 0x100u : 0u);
+  }
+}
+
 static void launch_list_sort(Plan* P, const KLArgs& A, hipStream_t st) {
   const int B = P->B;
   k_kl_rank_chunks<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
@@ -2409,6 +2471,7 @@ static int build_deferred_lists(Plan* P, hipStream_t st) {
   KLArgs A = kl_args(P, P->k, nullptr, nullptr, nullptr, nullptr, nullptr);
   A.marks = nullptr;
   A.mode = kKLBuild;
+  k_kl_chains<<<dim3((P->ndcap + 255) / 256, P->B), 256, 0, st>>>(A);  // the states k_welford_q did not store
   launch_list_sort(P, A, st);
   k_kl_list_done<<<P->B, 256, 0, st>>>(A);
   HIPCHK(hipGetLastError());
@@ -2497,7 +2560,8 @@ welford:
                     st>>>(
       P->ctl, B, (const T*)P->nd_pts, lbl ? P->nd_lbl : nullptr, P->nd_n, P->nd_base, P->nd_mean, P->nd_cov,
       P->nd_cls, P->hist, P->ncls, n, P->ndcap, P->wq_ctr,
-      WqChainArgs{P->vox, P->dense_of, P->nb, P->nkeys, P->chain, P->chain_ps, P->nd_cov_post, P->vcap});
+      WqChainArgs{P->vox, P->dense_of, P->nb, P->nkeys, P->chain, P->chain_ps, P->nd_cov_post, P->vcap,
+                  P->eager_list ? 0ull : (uint64_t)P->k, P->chain_ok});
   if (P->timing) HIPCHK(hipEventRecord(P->ev[5], st));
   KLArgs A = kl_args(P, P->k, out, out_cls, pc64, cov64, cls16);
   A.stats_out = stats_dst;
@@ -2618,6 +2682,7 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   A_(nkeys, B * nd);
   A_(chain, B * nd * 108);
   A_(chain_ps, B * nd * 12);
+  A_(chain_ok, B * nd);
   A_(slot_val, B * ec);
   A_(slot_flag, B * ec);
   A_(ev_val, B * ec);

@@ -875,32 +875,45 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
   if (A.fold_t2) {
     // TNet(64)'s transform through layer 0 (chains C, D; v0 only, checked on
     // the host): x_t2 = t2^T (W0 x + b0) = (W0^T t2)^T x + t2^T b0, so layer 0
-    // runs on W0' = W0^T t2 (its 12 used rows) and b0' = b0^T t2 -- 64-term
-    // fp32 dot products over t2 staged in region 1, which layer 0 has not
-    // written yet (the launcher keeps the biases past it)
+    // runs on W0' = W0^T t2 (its 12 used rows) and b0' = b0^T t2: a 16 x 64 x 64
+    // GEMM (rows 0..11 W0^T, row 12 the bias, 13..15 zero) on the fp32 MFMA,
+    // waves 0..3 one 16-column block each, t2 staged in region 1 (layer 0 has
+    // not written it yet; the launcher keeps the biases past it)
     float* const s_t2 = g_smem + reg[1];
     const f32x4* t2b = reinterpret_cast<const f32x4*>(A.fold_t2 + (int64_t)b * A.fold_ld);
     for (int e = threadIdx.x; e < 1024; e += kThreads) reinterpret_cast<f32x4*>(s_t2)[e] = t2b[e];
     __syncthreads();  // + s_w0 (W0^T row-major) and layer 0's bias at boff[0]
-    constexpr int kFold = 13 * 64, kFoldPer = (kFold + kThreads - 1) / kThreads;
-    float fv[kFoldPer];
+    f32x4 fo = {0.f, 0.f, 0.f, 0.f};
+    const int fr = lane & 15, fk = lane >> 4;  // operand row / k within a 4-step
+    if (wave < 4) {
 #pragma unroll
-    for (int r = 0; r < kFoldPer; r++) {
-      const int e = threadIdx.x + r * kThreads;
-      fv[r] = 0.0f;
-      if (e < kFold) {
-        const int k = e >> 6, nn = e & 63;  // row k of W0^T, or (k == 12) the bias
-        const float* arow = k < 12 ? s_w0 + k * 64 : g_smem + boff[0];
-#pragma unroll 8
-        for (int i = 0; i < 64; i++) fv[r] = fmaf(arow[i], s_t2[i * 64 + nn], fv[r]);
+      for (int st = 0; st < 16; st++) {
+        const int i = 4 * st + fk;
+        const float av = fr < 12 ? s_w0[fr * 64 + i] : fr == 12 ? g_smem[boff[0] + i] : 0.0f;
+        const float bv = s_t2[i * 64 + 16 * wave + fr];
+        fo = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, fo, 0, 0, 0);
       }
     }
     __syncthreads();
+    if (wave < 4) {  // lane (fk, fr): rows 4 fk + r, column 16 wave + fr
+      const int n = 16 * wave + fr;
 #pragma unroll
-    for (int r = 0; r < kFoldPer; r++) {
-      const int e = threadIdx.x + r * kThreads;
-      if (e < 12 * 64) s_w0[e] = fv[r];
-      else if (e < kFold) g_smem[boff[0] + (e - 12 * 64)] = fv[r];
+      for (int r = 0; r < 4; r++) {
+        const int row = 4 * fk + r;
+        if (row < 12) s_w0[row * 64 + n] = fo[r];
+        else if (row == 12) g_smem[boff[0] + n] = fo[r];
+      }
+      // the cloud's first workgroup publishes W0' (fragment-major, K = 16, rows
+      // 12..15 left zero) and b0' for a later chain's plain layer 0 (chain D)
+      if (A.fold_out_w && blockIdx.x == 0) {
+        float* ow = A.fold_out_w + (int64_t)b * 1024;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int row = 4 * fk + r;
+          if (row < 12) ow[(((n >> 4) * 64 + ((row >> 2) & 3) * 16 + (n & 15)) << 2) + (row & 3)] = fo[r];
+          else if (row == 12) A.fold_out_b[(int64_t)b * 64 + n] = fo[r];
+        }
+      }
     }
   }
   __syncthreads();
@@ -1417,6 +1430,8 @@ int ndnet_pn_chain_run_t32(const ndnet_pn_chain* args, int batch, void* stream) 
     if (r == 1 || inside + fb <= r0f) fbuf_off = inside;
     total = fbuf_off + (size_t)fb > total ? fbuf_off + (size_t)fb : total;
   }
+  if ((args->fold_out_w || args->fold_out_b) && (!args->fold_t2 || !args->fold_out_w || !args->fold_out_b))
+    PN_ARG_FAIL();
   if (args->fold_t2) {  // the t2 fold runs in layer 0's VALU prologue, t2 staged at region 1
     if (!valu_layer0(*args) || args->head_h2 || args->fold_ld < 4096 || args->fold_ld % 4 || (uintptr_t)args->fold_t2 % 16)
       PN_ARG_FAIL();

@@ -89,7 +89,8 @@ class _Chain(ctypes.Structure):
                 ("head_h2", ctypes.c_void_p), ("head_ld", ctypes.c_int32), ("head_K", ctypes.c_int32),
                 ("head_w3", ctypes.c_void_p), ("head_b3", ctypes.c_void_p), ("head_basis", ctypes.c_void_p),
                 ("head_kin", ctypes.c_int32), ("head_nout", ctypes.c_int32), ("head_t1", ctypes.c_void_p),
-                ("fold_t2", ctypes.c_void_p), ("fold_ld", ctypes.c_int32)]
+                ("fold_t2", ctypes.c_void_p), ("fold_ld", ctypes.c_int32), ("fold_out_w", ctypes.c_void_p),
+                ("fold_out_b", ctypes.c_void_p)]
 
 
 
@@ -350,6 +351,7 @@ class _Workspace:
         # ... and fragment-major for the HIP chains (K of conv1 padded 12 -> 16);
         # the HIP chains C / D fold t2 in their prologue (fold_t2)
         self.w1f = torch.empty((B, 16 * 64), **f32)
+        self.w1t2f = torch.zeros((B, 16 * 64), **f32)   # chain C publishes (W1 M(t1))^T t2 here for chain D
         self.specs = [  # torch emulation: (in_cols, [(W^T, bias)], relus, mode, kwargs)
             (3, W.A, (1, 1, 1), 0, dict(gmax=self.g1)),
             (12, [(self.w1T, W.c1b)] + W.B_tail, (0, 1, 1, 1), 0, dict(gmax=self.g2)),
@@ -370,7 +372,8 @@ class _Workspace:
             [shared(x) for x in W.A],
             [L1] + [shared(x) for x in W.B_tail],
             [L1, shared(W.C_mid), shared(W.C_tail)],
-            [L1, shared((W.s1aT, self.cvec))] + [shared(x) for x in W.D_tail],
+            [(self.w1t2f, self.w1t2f.stride(0), self.b1t2, 16, 64), shared((W.s1aT, self.cvec))] +
+            [shared(x) for x in W.D_tail],
         ]
         self.N = N
         self.structs = None
@@ -395,8 +398,10 @@ class _Workspace:
                 cb.head_w3, cb.head_b3 = W.t1["f3"].data_ptr(), W.t1["c3"].data_ptr()
                 cb.head_basis, cb.head_kin, cb.head_nout = W.t1_basis.data_ptr(), 12, 64
                 cb.head_t1 = self.t1.data_ptr()
-            for cd in self.structs[2:]:  # chains C / D: t2 through layer 0 (prologue fold)
-                cd.fold_t2, cd.fold_ld = self.t2.data_ptr(), self.t2.stride(0)
+            # chain C: t2 through layer 0 (prologue fold), published for chain D's layer 0
+            cc = self.structs[2]
+            cc.fold_t2, cc.fold_ld = self.t2.data_ptr(), self.t2.stride(0)
+            cc.fold_out_w, cc.fold_out_b = self.w1t2f.data_ptr(), self.b1t2.data_ptr()
         if chain_timing is not None:  # torch events on the launch stream (bench.py)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
