@@ -33,28 +33,30 @@ def main():
         print(f"{k:34s} {len(v):5d} {np.median(v):10.1f} {np.percentile(v, 10):8.1f} {np.percentile(v, 90):8.1f}")
 
 
-def timeline(d, anchor="k_front", which=-2):
+def timeline(d, anchor="k_front", which=-2, span=1):
     f = glob.glob(os.path.join(d, "*kernel_trace.csv"))[0]
     rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
     idx = [i for i, r in enumerate(rows) if anchor in r["Kernel_Name"]]
-    if len(idx) < 2:
+    if len(idx) < span + 1:
         return
-    a, b = idx[which], idx[which + 1]
+    a, b = idx[which], idx[min(which + span, len(idx) - 1)]
     t0 = int(rows[a]["Start_Timestamp"])
     prev_end = None
-    print(f"{'kernel':34s} {'start':>8s} {'dur':>7s} {'gap':>7s}")
+    q = "Queue_Id" if "Queue_Id" in rows[0] else None
+    print(f"{'kernel':34s} {'start':>8s} {'dur':>7s} {'gap':>7s}" + ("  queue" if q else ""))
     for r in rows[a:b]:
         s_, e_ = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
         m = re.search(r"(k_\w+(?:<[^>]*>)?)", r["Kernel_Name"])
         k = m.group(1) if m else r["Kernel_Name"][:34]
         gap = "" if prev_end is None else f"{(s_ - prev_end) / 1000:7.1f}"
-        print(f"{k:34s} {(s_ - t0) / 1000:8.1f} {(e_ - s_) / 1000:7.1f} {gap:>7s}")
+        print(f"{k:34s} {(s_ - t0) / 1000:8.1f} {(e_ - s_) / 1000:7.1f} {gap:>7s}" + (f"  {r[q]}" if q else ""))
         prev_end = e_ if prev_end is None else max(prev_end, e_)
 
 
 if __name__ == "__main__":
     if "--timeline" in sys.argv:
         w = int(sys.argv[sys.argv.index("--step") + 1]) if "--step" in sys.argv else -2
-        timeline(sys.argv[1], which=w)
+        n = int(sys.argv[sys.argv.index("--span") + 1]) if "--span" in sys.argv else 1
+        timeline(sys.argv[1], which=w, span=n)
         sys.exit(0)
     main()
