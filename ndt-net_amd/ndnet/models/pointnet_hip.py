@@ -431,7 +431,10 @@ HEAD3_IN_CHAIN = os.environ.get("NDNET_PN_HEAD3", "chain") == "chain"
 
 # TNet / seg-bias FC layers: "mfma" (default: ndnet_pn_fc_mfma_run, 16-row
 # fp32-MFMA GEMM over fragment-major weights) or "gemv" (ndnet_pn_fc_run,
-# VALU dot products over row-major weights)
+# VALU dot products over row-major weights).  Round 3 also tried a TNet head's
+# 2-3 layers in ONE launch handing off through an in-memory counter (stage
+# workgroups polling, sc1 stores / loads): the forward's non-chain time rose
+# from 46 to 63 us (profiles/r03z_fc_ab.txt), so every layer stays a launch.
 FC_MFMA = os.environ.get("NDNET_PN_FC", "mfma") == "mfma"
 
 
@@ -479,7 +482,7 @@ def _glue_hip(W, ws, B: int):
         t = W.t2
         fc(ws.g2, t["f1"], t["c1"], ws.h1, True)
         fc(ws.h1, t["f2"], t["c2"], ws.h2, True)
-        fc(ws.h2, t["f3"], t["c3"], ws.t2, False)  # t2: folded into chains C / D's layer 0 by their prologue
+        fc(ws.h2, t["f3"], t["c3"], ws.t2, False)  # t2: folded into chains C / D's layer 0 by chain C's prologue
 
     def seg_bias():
         fc(ws.g3[:, : W.F], W.s1g, W.s1b, ws.cvec, False)

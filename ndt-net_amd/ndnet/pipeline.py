@@ -36,6 +36,10 @@ PIPE_CU_SHARE = int(os.environ.get("NDNET_PIPE_CU_SHARE", "2"))
 # k_welford_q keeps every CU: front 2 / welford 1 measured 70.5k clouds/s
 # against 68.8-70.2k for 2 / 2 and 62.8k for 2 / 4 (profiles/r03n_cu_share.txt)
 PIPE_WQ_SHARE = int(os.environ.get("NDNET_PIPE_WQ_SHARE", "1"))
+# Forward streams of PipelinedSegmentation: 2 lets consecutive forwards
+# overlap (each in its own workspace slot), one's TNet heads and chain
+# prologues beside the other's chains
+PIPE_FWD_STREAMS = int(os.environ.get("NDNET_PIPE_FWD_STREAMS", "1"))
 
 
 class _Pinned:
@@ -165,11 +169,9 @@ class PipelinedSegmentation:
     per level; the output is then the list of per-level log-probs.
     """
 
-    R = 3  # ring depth of the input / row buffers
-
     def __init__(self, model, num_nds: int, batch: int, num_points: int,
                  device: Optional[torch.device] = None, warmup: int = 2, cu_share: Optional[int] = None,
-                 levels=None) -> None:
+                 levels=None, fwd_streams: Optional[int] = None) -> None:
         _lib.require_gpu()
         if model.training:
             raise ValueError("PipelinedSegmentation needs an eval-mode model")
@@ -180,7 +182,11 @@ class PipelinedSegmentation:
                 raise ValueError(f"levels must be strictly decreasing, got {self.levels}")
             num_nds = self.levels[0]
         self.model, self.num_nds, self.device = model, int(num_nds), dev
-        R = self.R
+        # F forward streams: step i's forward runs on stream i % F in workspace
+        # slot i % F; a ring of R = F + 2 buffers keeps the rows of every
+        # forward in flight apart from the one the NDT stream writes
+        self.F = F = max(1, int(fwd_streams if fwd_streams is not None else PIPE_FWD_STREAMS))
+        self.R = R = F + 2
         self.inputs = [torch.zeros((batch, num_points, 3), dtype=torch.float32, device=dev) for _ in range(R)]
         self.rows = [[torch.zeros((batch, k, 12), dtype=torch.float32, device=dev)
                       for k in (self.levels or (self.num_nds,))] for _ in range(R)]
@@ -195,19 +201,18 @@ class PipelinedSegmentation:
             except RuntimeError:  # k_front does not fit that share for this shape
                 pass
         # stream priorities (either way) measured 35-40% slower than none
-        self.s_ndt, self.s_fwd = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+        self.s_ndt = torch.cuda.Stream(device=dev)
+        self.s_fwds = [torch.cuda.Stream(device=dev) for _ in range(F)]
         self.s_copy = torch.cuda.Stream(device=dev)
         self.ndt_done = [torch.cuda.Event() for _ in range(R)]  # NDT of slot j finished (rows j, input j free)
         self.fwd_done = [torch.cuda.Event() for _ in range(R)]  # forward of slot j finished (rows j - 1 free)
         self.copied = [torch.cuda.Event() for _ in range(R)]    # input j holds the streamed batch
-        cur = torch.cuda.current_stream(dev)
-        self.s_ndt.wait_stream(cur)
-        self.s_fwd.wait_stream(cur)
+        self._fork()
         with torch.no_grad():  # plan / workspace creation, kernel attributes
             for i in range(max(R, warmup)):
                 with torch.cuda.stream(self.s_ndt):
                     self._ndt(i % R)
-                with torch.cuda.stream(self.s_fwd):
+                with torch.cuda.stream(self.s_fwds[i % R % F]):
                     self._fwd(i % R)
         torch.cuda.synchronize(dev)
         self.g_ndt, self.g_fwd, self.out = [], [], []
@@ -217,7 +222,7 @@ class PipelinedSegmentation:
                 self._ndt(j)
             self.g_ndt.append(g)
             g = torch.cuda.CUDAGraph()
-            with torch.no_grad(), torch.cuda.graph(g, stream=self.s_fwd):
+            with torch.no_grad(), torch.cuda.graph(g, stream=self.s_fwds[j % F]):
                 self.out.append(self._fwd(j))
             self.g_fwd.append(g)
         torch.cuda.synchronize(dev)
@@ -232,18 +237,23 @@ class PipelinedSegmentation:
             self.plan.prune(k, blk)
 
     def _fwd(self, j: int):
-        """The forward stage of ring slot j: the rows of slot j - 1."""
-        outs = [self.model(r[..., :3], r[..., 3:]) for r in self.rows[(j - 1) % self.R]]
+        """The forward stage of ring slot j: the rows of slot j - 1, in
+        workspace slot j % F (forwards on different streams run concurrently)."""
+        from .models import pointnet_hip
+        with pointnet_hip.workspace_slot(j % self.F):
+            outs = [self.model(r[..., :3], r[..., 3:]) for r in self.rows[(j - 1) % self.R]]
         return outs if self.levels else outs[0]
 
     def _enqueue(self) -> int:
         """Launches the next step's two graphs, ordered by events only."""
         R, j = self.R, self.i % self.R
-        self.s_fwd.wait_event(self.ndt_done[(j - 1) % R])   # its rows: the previous step's NDT
-        with torch.cuda.stream(self.s_fwd):
+        s_fwd = self.s_fwds[j % self.F]
+        s_fwd.wait_event(self.ndt_done[(j - 1) % R])         # its rows: the previous step's NDT
+        with torch.cuda.stream(s_fwd):
             self.g_fwd[j].replay()
-        self.fwd_done[j].record(self.s_fwd)
-        self.s_ndt.wait_event(self.fwd_done[(j - 2) % R])   # rows j: last read by the forward of step i - 2
+        self.fwd_done[j].record(s_fwd)
+        # rows j: last read by the forward of step i - R + 1
+        self.s_ndt.wait_event(self.fwd_done[(j + 1) % R])
         self.s_ndt.wait_event(self.copied[j])               # no-op unless a streamed copy targets input j
         with torch.cuda.stream(self.s_ndt):
             self.g_ndt[j].replay()
@@ -253,12 +263,14 @@ class PipelinedSegmentation:
 
     def _fork(self) -> None:
         cur = torch.cuda.current_stream(self.device)
-        self.s_ndt.wait_stream(cur)
-        self.s_fwd.wait_stream(cur)
+        for st in [self.s_ndt] + self.s_fwds:
+            st.wait_stream(cur)
 
     def _join(self, j: int) -> None:
+        """The caller's stream waits for the last step's NDT and the last F forwards."""
         cur = torch.cuda.current_stream(self.device)
-        cur.wait_event(self.fwd_done[j])
+        for t in range(self.F):
+            cur.wait_event(self.fwd_done[(j - t) % self.R])
         cur.wait_event(self.ndt_done[j])
 
     @property

@@ -106,9 +106,11 @@ def test_pipelined_steps_equal_sequential_batches():
         assert torch.equal(outs[i + 1], expect[i]), f"batch {i}"
 
 
-def test_pipelined_free_running_steps_equal_sequential_batches():
-    """replay_steps: the two stage streams ordered by events only (the NDT
-    stream up to a step ahead, no per-step join) give every step the forward
+@pytest.mark.parametrize("fwd_streams", [1, 2])
+def test_pipelined_free_running_steps_equal_sequential_batches(fwd_streams):
+    """replay_steps: the stage streams ordered by events only (the NDT stream
+    up to a step ahead, no per-step join; with 2 forward streams consecutive
+    forwards overlap in separate workspace slots) give every step the forward
     of the batch before it, bit-equal to the one-graph-per-step path;
     single-step replays before it keep the ring position."""
     import torch
@@ -118,23 +120,25 @@ def test_pipelined_free_running_steps_equal_sequential_batches():
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     m = NDTNetSegmentation(3, 28, 768).to(dev).eval()
-    batches = [torch.from_numpy(make_batch("L", 4, 20_000, seed0=10 * i + 1)).to(dev) for i in range(3)]
+    pipe = PipelinedSegmentation(m, 400, 4, 20_000, device=dev, fwd_streams=fwd_streams)
+    R = pipe.R
+    assert R == fwd_streams + 2
+    batches = [torch.from_numpy(make_batch("L", 4, 20_000, seed0=10 * i + 1)).to(dev) for i in range(R)]
     ref = GraphedSegmentation(m, 400, 4, 20_000, device=dev)
     expect = [ref(b).clone() for b in batches]
-    pipe = PipelinedSegmentation(m, 400, 4, 20_000, device=dev)
-    for j, b in enumerate(batches):  # step s reads input s % 3
+    for j, b in enumerate(batches):  # step s reads input s % R
         pipe.inputs[j].copy_(b)
-    for _ in range(3):
-        pipe.replay()                        # steps 0..2
+    for _ in range(R):
+        pipe.replay()                        # steps 0 .. R - 1
     for rnd in range(2):
-        last = pipe.replay_steps(3 + 3 * rnd)  # steps 3..5, then 6..11
+        last = pipe.replay_steps(R + R * rnd)  # then R, then 2 R steps
         torch.cuda.synchronize()
-        for j in range(3):  # slot j's last step s = j mod 3: the forward of batch (s - 1) % 3
-            assert torch.equal(pipe.out[j], expect[(j - 1) % 3]), f"round {rnd} slot {j}"
-        assert last.data_ptr() == pipe.out[2].data_ptr()
-    out = pipe.replay()                      # step 12 (slot 0)
+        for j in range(R):  # slot j's last step s = j mod R: the forward of batch (s - 1) % R
+            assert torch.equal(pipe.out[j], expect[(j - 1) % R]), f"round {rnd} slot {j}"
+        assert last.data_ptr() == pipe.out[R - 1].data_ptr()
+    out = pipe.replay()                      # slot 0
     torch.cuda.synchronize()
-    assert torch.equal(out, expect[2])
+    assert torch.equal(out, expect[R - 1])
 
 
 def test_pipelined_levels_equal_graphed_levels():
