@@ -323,7 +323,7 @@ def main() -> None:
                 t_ov = D.max_over_ranks(time.perf_counter() - t0)
             pcie["overlapped"] = {"value": round(total_clouds / t_ov, 2),
                                   "ms_per_step": round(1e3 * t_ov / args.steps, 4),
-                                  "how": "PipelinedSegmentation.replay_streamed: ring of 3 input buffers, copy stream"}
+                                  "how": "PipelinedSegmentation.replay_streamed: ring of input buffers, copy stream"}
     stats = run_plan().host_stats()
     assert all(s.rc == 0 for s in stats), [s.rc for s in stats]
     assert all(torch.isfinite(o).all() for o in (out if isinstance(out, list) else [out]))
@@ -608,9 +608,10 @@ def main() -> None:
                                     f"per level"),
                        "launch": "eager" if args.eager else (
                            "hip graph per step (ndnet.pipeline.GraphedSegmentation)" if args.no_pipeline
-                           else "NDT(batch i) || forward(batch i-1): a hip graph per stage and ring slot (3 "
-                                "buffers) on two streams ordered by events only, joined once per timed region "
-                                "(ndnet.pipeline.PipelinedSegmentation.replay_steps)"),
+                           else f"NDT(batch i) || forward(batch i-1): a hip graph per stage and ring slot "
+                                f"({graphed.R} buffers), one NDT stream + {graphed.F} forward streams (step i's "
+                                f"forward on stream i % {graphed.F}) ordered by events only, joined once per timed "
+                                f"region (ndnet.pipeline.PipelinedSegmentation.replay_steps)"),
                        "global_batch": B * world, "points": n, "nds": k, "parallelism": f"dp{world} (clouds sharded)",
                        "dist_backend": args.dist_backend if world > 1 else None,
                        **({"rehearsal": f"{world} ranks on {ndev} GPU(s)"} if world > ndev else {})},

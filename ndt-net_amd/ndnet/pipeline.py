@@ -36,10 +36,13 @@ PIPE_CU_SHARE = int(os.environ.get("NDNET_PIPE_CU_SHARE", "2"))
 # k_welford_q keeps every CU: front 2 / welford 1 measured 70.5k clouds/s
 # against 68.8-70.2k for 2 / 2 and 62.8k for 2 / 4 (profiles/r03n_cu_share.txt)
 PIPE_WQ_SHARE = int(os.environ.get("NDNET_PIPE_WQ_SHARE", "1"))
-# Forward streams of PipelinedSegmentation: 2 lets consecutive forwards
-# overlap (each in its own workspace slot), one's TNet heads and chain
-# prologues beside the other's chains
-PIPE_FWD_STREAMS = int(os.environ.get("NDNET_PIPE_FWD_STREAMS", "1"))
+# Forward streams of PipelinedSegmentation: more than one lets consecutive
+# forwards overlap (each in its own workspace slot), one's TNet heads and
+# chain prologues beside the other's chains.  C2: 1 stream 74.9-75.0k, 2
+# streams 74.8-78.8k, 3 streams (default) 81.7k clouds/s; C5 20.7k -> 23.7-24.4k
+# with 2 or 3 (profiles/r03aa_fwd_streams.txt, r03ab_fwd_streams.txt).  With the
+# NDT stream that is 4 streams, the hardware queues a process gets by default.
+PIPE_FWD_STREAMS = int(os.environ.get("NDNET_PIPE_FWD_STREAMS", "3"))
 
 
 class _Pinned:
