@@ -153,21 +153,22 @@ def test_pipelined_levels_equal_graphed_levels():
     torch.manual_seed(0)
     m = NDTNetSegmentation(3, 28, 768).to(dev).eval()
     levels = (400, 200, 100)
-    batches = [torch.from_numpy(make_batch("L", 4, 20_000, seed0=7 * i + 2)).to(dev) for i in range(3)]
+    pipe = PipelinedSegmentation(m, levels[0], 4, 20_000, device=dev, levels=levels)
+    R = pipe.R
+    batches = [torch.from_numpy(make_batch("L", 4, 20_000, seed0=7 * i + 2)).to(dev) for i in range(R)]
     ref = GraphedSegmentation(m, levels[0], 4, 20_000, device=dev, levels=levels)
     expect = [[o.clone() for o in ref(b)] for b in batches]
-    pipe = PipelinedSegmentation(m, levels[0], 4, 20_000, device=dev, levels=levels)
     for j, b in enumerate(batches):
         pipe.inputs[j].copy_(b)
-    outs = [[o.clone() for o in pipe.replay()] for _ in range(3)]   # steps 0..2
-    pipe.replay_steps(3)                                              # steps 3..5, free-running
+    outs = [[o.clone() for o in pipe.replay()] for _ in range(R)]   # steps 0 .. R - 1
+    pipe.replay_steps(R)                                              # steps R .. 2 R - 1, free-running
     torch.cuda.synchronize()
-    for s in (1, 2):
+    for s in range(1, R):
         for lv in range(3):
             assert torch.equal(outs[s][lv], expect[s - 1][lv]), f"step {s} level {lv}"
-    for j in range(3):  # step 3 + j (slot j): batch (j - 1) % 3
+    for j in range(R):  # step R + j (slot j): batch (j - 1) % R
         for lv in range(3):
-            assert torch.equal(pipe.out[j][lv], expect[(j - 1) % 3][lv]), f"slot {j} level {lv}"
+            assert torch.equal(pipe.out[j][lv], expect[(j - 1) % R][lv]), f"slot {j} level {lv}"
 
 
 def test_pipelined_streamed_host_batches():
