@@ -291,7 +291,12 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
   uint32_t* table = f_smem;                                   // kFrontTable words
   uint8_t* bytemap = (uint8_t*)f_smem;                        // small grids: one byte per voxel
   uint32_t* binfo = f_smem + kFrontTable;                     // [bpw][1024]: key, then did << 10 | rank
-  uint32_t* hist = binfo + (uint64_t)bpw * 1024;              // [nrb][ndcap]
+  // [nrb][ndcap] u16: per rank bin and ND a count (<= 1024), then the
+  // workgroup-local prefix over rank bins (< 65536: a workgroup that fits
+  // its LDS holds fewer points); the ND's global base goes to a per-ND word
+  // in the table region (addv), so the u16 array halves the LDS that bounds
+  // bins per workgroup (k = 2000 fits 8 workgroups per cloud)
+  uint16_t* hist = reinterpret_cast<uint16_t*>(binfo + (uint64_t)bpw * 1024);
   uint32_t* stamps = A.stamps + (uint64_t)b * A.vcap;
   // my bins: [bin0, bin0 + nbw), nbw <= bpw (the bins of a cloud split as evenly as G allows)
   const uint64_t bin0 = (uint64_t)g * A.nbins / G;
@@ -765,7 +770,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
     const uint32_t nbits = __builtin_amdgcn_readfirstlane(32u - (uint32_t)__clz((int)(ndcap > 1 ? ndcap - 1 : 1)));
     const unsigned long long below = (1ull << lane) - 1ull;
     for (uint32_t r = wave; r < nrb; r += kFrontWaves) {
-      uint32_t* hr = hist + (uint64_t)r * ndcap;
+      uint16_t* hr = hist + (uint64_t)r * ndcap;
       uint32_t* br = binfo + (uint64_t)r * rbs;
       for (uint32_t st = 0; st < rbs / 64; st++) {
         const uint32_t d = br[st * 64 + lane];
@@ -786,7 +791,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
           const uint32_t rank = (uint32_t)__popcll(m & below), cnt = (uint32_t)__popcll(m);
           const uint32_t cur = hr[d];  // read by every lane of the set before its last lane writes
           br[st * 64 + lane] = (d << 10) | (cur + rank);
-          if (rank + 1 == cnt) hr[d] = cur + cnt;
+          if (rank + 1 == cnt) hr[d] = (uint16_t)(cur + cnt);
         }
       }
     }
@@ -807,13 +812,13 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
         for (int q = 0; q < 4; q++) x[q] = hist[(uint64_t)(r + q) * ndcap + d];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-          hist[(uint64_t)(r + q) * ndcap + d] = run;
+          hist[(uint64_t)(r + q) * ndcap + d] = (uint16_t)run;
           run += x[q];
         }
       }
       for (; r < nrb; r++) {
         const uint32_t x = hist[(uint64_t)r * ndcap + d];
-        hist[(uint64_t)r * ndcap + d] = run;
+        hist[(uint64_t)r * ndcap + d] = (uint16_t)run;
         run += x;
       }
       st_sc1(wg + (uint64_t)g * ndcap + d, run);
@@ -827,7 +832,8 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
     // among my points of its ND); delta[d] = global - local is kept in the
     // table region (free since the per-point NDs were found).
     const bool staged = A.staged != 0;
-    uint32_t* delta = table;  // [ndcap] (staged: ndcap <= kFrontTable, host check)
+    uint32_t* addv = table;           // [ndcap]: the ND's global base + earlier workgroups' counts
+    uint32_t* delta = table + ndcap;  // [ndcap] (staged: 2 ndcap <= kFrontTable, host check)
     uint32_t carry = 0, lcarry = 0;
     for (uint32_t base = 0; base < nd; base += kFrontThreads) {
       const uint32_t d = base + t;
@@ -878,17 +884,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
           A.nd_n[(uint64_t)b * ndcap + d] = tot_d;
           A.nd_base[(uint64_t)b * ndcap + d] = start;
         }
-        // four rank bins per LDS round trip (loads, then stores)
-        const uint32_t add = start + pre;
-        uint32_t r = 0;
-        for (; r + 4 <= nrb; r += 4) {
-          uint32_t x[4];
-#pragma unroll
-          for (int q = 0; q < 4; q++) x[q] = hist[(uint64_t)(r + q) * ndcap + d];
-#pragma unroll
-          for (int q = 0; q < 4; q++) hist[(uint64_t)(r + q) * ndcap + d] = x[q] + add;
-        }
-        for (; r < nrb; r++) hist[(uint64_t)r * ndcap + d] += add;
+        addv[d] = start + pre;  // a point's destination: addv[d] + hist[r][d] + its rank
       }
     }
     __syncthreads();
@@ -915,7 +911,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
             const uint32_t bi = binfo[j * 1024 + t];
             if (bi != kInvalid) {
               const uint32_t d = bi >> 10;
-              gd[j] = hist[(uint64_t)(j * (1024 / rbs) + rsub) * ndcap + d] + (bi & 1023u);
+              gd[j] = addv[d] + hist[(uint64_t)(j * (1024 / rbs) + rsub) * ndcap + d] + (bi & 1023u);
               lp[j] = gd[j] - delta[d];
               if (A.nd_lbl) A.nd_lbl[(uint64_t)b * n + gd[j]] = (uint16_t)A.lbl[(uint64_t)b * n + (bin0 + j) * 1024 + t];
             }
@@ -950,7 +946,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
       if (bi == kInvalid) return;
       const uint32_t d = bi >> 10;
       const uint32_t r = j * (1024 / rbs) + rsub;
-      const uint32_t dst = hist[(uint64_t)r * ndcap + d] + (bi & 1023u);
+      const uint32_t dst = addv[d] + hist[(uint64_t)r * ndcap + d] + (bi & 1023u);
       T* o = out + (uint64_t)dst * 3;
       if (A.dbg_store == 1) {
         __builtin_nontemporal_store(x, o);

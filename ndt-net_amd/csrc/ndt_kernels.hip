@@ -2523,7 +2523,7 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
     // staged scatter (float input): every point held in registers, delta[ndcap]
     // in the table region, a 16-byte LDS record per point of the workgroup
     F.staged = P->front_staged && F.dbg_store == 0 && sizeof(T) == 4 && P->fbpw <= (uint32_t)kFrontR &&
-               P->ndcap <= (uint32_t)kFrontTable && (size_t)16 * 1024 * P->fbpw <= P->flds;
+               2 * P->ndcap <= (uint32_t)kFrontTable && (size_t)16 * 1024 * P->fbpw <= P->flds;
     F.eval_all = P->exact_counts;
     F.B = (uint32_t)B;
     F.nbins = P->nbins;
@@ -2600,13 +2600,15 @@ hipError_t front_config(Plan* P, int share) {
   const uint32_t G = gt < P->nbins ? gt : P->nbins;
   const uint32_t bpw = (P->nbins + G - 1) / G;
   // rank bins of 512 points when that keeps every wave busy and fits
-  auto lds_of = [&](uint32_t rbs) {
-    return sizeof(uint32_t) * ((size_t)kFrontTable + (size_t)bpw * 1024 + (size_t)bpw * (1024 / rbs) * P->ndcap);
+  auto lds_of = [&](uint32_t rbs) {  // table + binfo (u32) + the rank-bin ND histograms (u16)
+    return sizeof(uint32_t) * ((size_t)kFrontTable + (size_t)bpw * 1024) +
+           ((sizeof(uint16_t) * (size_t)bpw * (1024 / rbs) * P->ndcap + 3) & ~(size_t)3);
   };
   const uint32_t rbs = (2 * bpw <= (uint32_t)kFrontWaves && lds_of(512) <= 150 * 1024) ? 512u : 1024u;
   const size_t lds = lds_of(rbs);
   hipError_t e = hipSuccess;
-  int ok = lds <= 150 * 1024 && (G == 1 || (uint64_t)G * B <= (uint64_t)cus);
+  // (addv, the per-ND base words of the binning, live in the table region)
+  int ok = lds <= 150 * 1024 && (G == 1 || (uint64_t)G * B <= (uint64_t)cus) && P->ndcap <= (uint32_t)kFrontTable;
   if (ok) e = hipFuncSetAttribute((const void*)k_front<float>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
   if (ok && e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_front<double>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);

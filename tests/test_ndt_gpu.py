@@ -577,17 +577,18 @@ def test_full_size_labelled(num_classes):
         assert len(np.unique(g.argmax(axis=2))) > 100
 
 
-@pytest.mark.parametrize("share", [2])
-def test_cu_share_results_identical(share):
+@pytest.mark.parametrize("share,k", [(2, 1000), (2, 2000)])
+def test_cu_share_results_identical(share, k):
     """ndnet_ndt_set_cu_share: k_front on CUs / (share B) workgroups per cloud
     and k_welford_q on CUs / share give the same rows and stats, bit for bit,
-    as the whole-chip plan (C2 U and L clouds, 16 x 100k -> 1000).  A share
-    whose k_front does not fit (4: 25 bins per workgroup exceed its LDS) is
-    refused and the plan keeps its previous share."""
+    as the whole-chip plan (U and L clouds, 16 x 100k -> 1000 (C2) and -> 2000
+    (C5's first level: 13 bins per workgroup, which fit since the rank-bin
+    histograms are u16)).  A share whose k_front does not fit (4: 25 bins per
+    workgroup exceed its LDS) is refused and the plan keeps its previous share."""
     import torch
     from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
     from ndnet.synthetic import make_batch
-    B, n, k = 16, 100_000, 1000
+    B, n = 16, 100_000
     for kind in ("U", "L"):
         pts = torch.from_numpy(make_batch(kind, B, n)).cuda()
         res = []
