@@ -287,18 +287,16 @@ def _build_chain(n: int, in_cols: int, layers, relus, mode: int, gmax=None, out_
 
 
 # 32-point tiles (ndnet_pn_chain_run_t32) when 64-point tiles would fill at
-# most half the CUs (C5's 500-point level: 16 x 8 tiles on 256 CUs); "0" off,
-# "force" always (8-wave workgroups, two per CU)
-TILE32_MODE = os.environ.get("NDNET_PN_TILE32", "1")
-TILE32 = TILE32_MODE != "0"
+# most half the CUs (C5's 500-point level: 16 x 8 tiles on 256 CUs); "0" off.
+# Always taking them (8-wave workgroups, two per CU, beside other forwards'
+# kernels) measured 71-74k against 81k clouds/s (profiles/r03af_t32_ab.txt).
+TILE32 = os.environ.get("NDNET_PN_TILE32", "1") == "1"
 _cus = {}
 
 
 def _use_t32(B: int, n: int, device) -> bool:
     if not TILE32:
         return False
-    if TILE32_MODE == "force":
-        return True
     if device not in _cus:
         _cus[device] = torch.cuda.get_device_properties(device).multi_processor_count
     return 2 * B * ((n + 63) // 64) <= _cus[device]
