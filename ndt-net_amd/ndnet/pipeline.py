@@ -17,6 +17,7 @@ the device (k_reset / k_limits), not by host bookkeeping.
 """
 from __future__ import annotations
 
+import math
 import os
 from typing import Optional
 
@@ -43,6 +44,12 @@ PIPE_WQ_SHARE = int(os.environ.get("NDNET_PIPE_WQ_SHARE", "1"))
 # with 2 or 3 (profiles/r03aa_fwd_streams.txt, r03ab_fwd_streams.txt).  With the
 # NDT stream that is 4 streams, the hardware queues a process gets by default.
 PIPE_FWD_STREAMS = int(os.environ.get("NDNET_PIPE_FWD_STREAMS", "3"))
+# NDT streams, each with its own plan (workspace): 2 lets the NDT stage of
+# consecutive batches overlap, for clouds whose NDT stage outlasts a forward
+# (L: k_welford_q's heaviest ND alone takes ~90 us).  Measured: L 47.6k ->
+# 53.2k clouds/s, but U 83k -> 79k and C5 26.0k -> 25.7k, so 1 by default
+# (profiles/r03ah_ndt_streams.txt)
+PIPE_NDT_STREAMS = int(os.environ.get("NDNET_PIPE_NDT_STREAMS", "1"))
 
 
 class _Pinned:
@@ -174,7 +181,7 @@ class PipelinedSegmentation:
 
     def __init__(self, model, num_nds: int, batch: int, num_points: int,
                  device: Optional[torch.device] = None, warmup: int = 2, cu_share: Optional[int] = None,
-                 levels=None, fwd_streams: Optional[int] = None) -> None:
+                 levels=None, fwd_streams: Optional[int] = None, ndt_streams: Optional[int] = None) -> None:
         _lib.require_gpu()
         if model.training:
             raise ValueError("PipelinedSegmentation needs an eval-mode model")
@@ -186,25 +193,31 @@ class PipelinedSegmentation:
             num_nds = self.levels[0]
         self.model, self.num_nds, self.device = model, int(num_nds), dev
         # F forward streams: step i's forward runs on stream i % F in workspace
-        # slot i % F; a ring of R = F + 2 buffers keeps the rows of every
-        # forward in flight apart from the one the NDT stream writes
+        # slot i % F; N NDT streams: step i's NDT stage on stream i % N with
+        # plan i % N.  A ring of R >= F + N + 1 buffers (a multiple of F and N)
+        # keeps the rows of every forward in flight apart from those the NDT
+        # streams write
         self.F = F = max(1, int(fwd_streams if fwd_streams is not None else PIPE_FWD_STREAMS))
-        self.R = R = F + 2
+        self.N = N = max(1, int(ndt_streams if ndt_streams is not None else PIPE_NDT_STREAMS))
+        lcm = F * N // math.gcd(F, N)
+        self.R = R = -(-(F + N + 1) // lcm) * lcm
         self.inputs = [torch.zeros((batch, num_points, 3), dtype=torch.float32, device=dev) for _ in range(R)]
         self.rows = [[torch.zeros((batch, k, 12), dtype=torch.float32, device=dev)
                       for k in (self.levels or (self.num_nds,))] for _ in range(R)]
-        # a plan of its own (not ndt_preprocessing's cached one): its CU share
+        # plans of its own (not ndt_preprocessing's cached one): their CU share
         # is a property of the pipeline
-        self.plan = NdtPlan(batch, num_points, self.num_nds, -1, device=dev)
+        self.plans = [NdtPlan(batch, num_points, self.num_nds, -1, device=dev) for _ in range(N)]
+        self.plan = self.plans[0]
         if cu_share is None:
             cu_share = PIPE_CU_SHARE
-        if cu_share > 1 and self.plan.path == 2:
-            try:
-                self.plan.set_cu_share(cu_share, PIPE_WQ_SHARE)
-            except RuntimeError:  # k_front does not fit that share for this shape
-                pass
+        for plan in self.plans:
+            if cu_share > 1 and plan.path == 2:
+                try:
+                    plan.set_cu_share(cu_share, PIPE_WQ_SHARE)
+                except RuntimeError:  # k_front does not fit that share for this shape
+                    pass
         # stream priorities (either way) measured 35-40% slower than none
-        self.s_ndt = torch.cuda.Stream(device=dev)
+        self.s_ndts = [torch.cuda.Stream(device=dev) for _ in range(N)]
         self.s_fwds = [torch.cuda.Stream(device=dev) for _ in range(F)]
         self.s_copy = torch.cuda.Stream(device=dev)
         self.ndt_done = [torch.cuda.Event() for _ in range(R)]  # NDT of slot j finished (rows j, input j free)
@@ -213,7 +226,7 @@ class PipelinedSegmentation:
         self._fork()
         with torch.no_grad():  # plan / workspace creation, kernel attributes
             for i in range(max(R, warmup)):
-                with torch.cuda.stream(self.s_ndt):
+                with torch.cuda.stream(self.s_ndts[i % R % N]):
                     self._ndt(i % R)
                 with torch.cuda.stream(self.s_fwds[i % R % F]):
                     self._fwd(i % R)
@@ -221,7 +234,7 @@ class PipelinedSegmentation:
         self.g_ndt, self.g_fwd, self.out = [], [], []
         for j in range(R):
             g = torch.cuda.CUDAGraph()
-            with torch.no_grad(), torch.cuda.graph(g, stream=self.s_ndt):
+            with torch.no_grad(), torch.cuda.graph(g, stream=self.s_ndts[j % N]):
                 self._ndt(j)
             self.g_ndt.append(g)
             g = torch.cuda.CUDAGraph()
@@ -229,15 +242,15 @@ class PipelinedSegmentation:
                 self.out.append(self._fwd(j))
             self.g_fwd.append(g)
         torch.cuda.synchronize(dev)
-        self._pinned = _Pinned(model, [self.plan])
+        self._pinned = _Pinned(model, self.plans)
         self.i = 0
 
     def _ndt(self, j: int) -> None:
-        """The NDT stage of ring slot j on the current stream."""
-        rows = self.rows[j]
-        self.plan.run(self.inputs[j], None, rows[0], None)
+        """The NDT stage of ring slot j on the current stream, with plan j % N."""
+        rows, plan = self.rows[j], self.plans[j % self.N]
+        plan.run(self.inputs[j], None, rows[0], None)
         for k, blk in zip(self.levels[1:] if self.levels else (), rows[1:]):
-            self.plan.prune(k, blk)
+            plan.prune(k, blk)
 
     def _fwd(self, j: int):
         """The forward stage of ring slot j: the rows of slot j - 1, in
@@ -256,25 +269,27 @@ class PipelinedSegmentation:
             self.g_fwd[j].replay()
         self.fwd_done[j].record(s_fwd)
         # rows j: last read by the forward of step i - R + 1
-        self.s_ndt.wait_event(self.fwd_done[(j + 1) % R])
-        self.s_ndt.wait_event(self.copied[j])               # no-op unless a streamed copy targets input j
-        with torch.cuda.stream(self.s_ndt):
+        s_ndt = self.s_ndts[j % self.N]
+        s_ndt.wait_event(self.fwd_done[(j + 1) % R])
+        s_ndt.wait_event(self.copied[j])                    # no-op unless a streamed copy targets input j
+        with torch.cuda.stream(s_ndt):
             self.g_ndt[j].replay()
-        self.ndt_done[j].record(self.s_ndt)
+        self.ndt_done[j].record(s_ndt)
         self.i += 1
         return j
 
     def _fork(self) -> None:
         cur = torch.cuda.current_stream(self.device)
-        for st in [self.s_ndt] + self.s_fwds:
+        for st in self.s_ndts + self.s_fwds:
             st.wait_stream(cur)
 
     def _join(self, j: int) -> None:
-        """The caller's stream waits for the last step's NDT and the last F forwards."""
+        """The caller's stream waits for the last N NDT stages and the last F forwards."""
         cur = torch.cuda.current_stream(self.device)
         for t in range(self.F):
             cur.wait_event(self.fwd_done[(j - t) % self.R])
-        cur.wait_event(self.ndt_done[j])
+        for t in range(self.N):
+            cur.wait_event(self.ndt_done[(j - t) % self.R])
 
     @property
     def points(self) -> torch.Tensor:

@@ -106,11 +106,12 @@ def test_pipelined_steps_equal_sequential_batches():
         assert torch.equal(outs[i + 1], expect[i]), f"batch {i}"
 
 
-@pytest.mark.parametrize("fwd_streams", [1, 2])
-def test_pipelined_free_running_steps_equal_sequential_batches(fwd_streams):
+@pytest.mark.parametrize("fwd_streams,ndt_streams", [(1, 1), (2, 1), (3, 2)])
+def test_pipelined_free_running_steps_equal_sequential_batches(fwd_streams, ndt_streams):
     """replay_steps: the stage streams ordered by events only (the NDT stream
-    up to a step ahead, no per-step join; with 2 forward streams consecutive
-    forwards overlap in separate workspace slots) give every step the forward
+    up to a step ahead, no per-step join; with several forward streams
+    consecutive forwards overlap in separate workspace slots, with 2 NDT
+    streams consecutive NDT stages on separate plans) give every step the forward
     of the batch before it, bit-equal to the one-graph-per-step path;
     single-step replays before it keep the ring position."""
     import torch
@@ -120,9 +121,9 @@ def test_pipelined_free_running_steps_equal_sequential_batches(fwd_streams):
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     m = NDTNetSegmentation(3, 28, 768).to(dev).eval()
-    pipe = PipelinedSegmentation(m, 400, 4, 20_000, device=dev, fwd_streams=fwd_streams)
+    pipe = PipelinedSegmentation(m, 400, 4, 20_000, device=dev, fwd_streams=fwd_streams, ndt_streams=ndt_streams)
     R = pipe.R
-    assert R == fwd_streams + 2
+    assert R >= fwd_streams + ndt_streams + 1 and R % fwd_streams == 0 and R % ndt_streams == 0
     batches = [torch.from_numpy(make_batch("L", 4, 20_000, seed0=10 * i + 1)).to(dev) for i in range(R)]
     ref = GraphedSegmentation(m, 400, 4, 20_000, device=dev)
     expect = [ref(b).clone() for b in batches]
