@@ -2787,7 +2787,7 @@ int ndnet_ndt_set_cu_share(void* plan, int front_share, int welford_share) {
   const bool on_front = P->front != 0;  // path 2 in use (not forced to path 1)
   if (front_config(P, front_share) != hipSuccess) return NDNET_ERR_HIP;
   if (!P->front_ok) {  // k_front does not fit this share: keep the previous one
-    front_config(P, prev);
+    (void)front_config(P, prev);  // the previous share fitted when it was set
     return NDNET_ERR_ARG;
   }
   P->front = on_front ? 1 : 0;
