@@ -43,10 +43,17 @@ def lr_for_epoch(base_lr: float, epoch: int) -> float:
 
 
 class Trainer:
-    """One model + Adam (+ DDP when a process group is active)."""
+    """One model + Adam (+ DDP when a process group is active).
+
+    ``graphs=True`` (one GPU, no DDP): ``step`` replays the whole training step
+    -- labelled NDT, train forward, loss, backward, Adam -- as one HIP graph per
+    input shape (``GraphedTrainStep``).  The optimizer is then Adam's fused,
+    capturable form with the learning rate in a device tensor, so
+    ``set_epoch`` still takes effect inside the graph."""
 
     def __init__(self, model: torch.nn.Module, lr: float, num_nds: int, num_classes: int,
-                 device: torch.device, ddp: Optional[bool] = None, bucket_cap_mb: float = 4.0) -> None:
+                 device: torch.device, ddp: Optional[bool] = None, bucket_cap_mb: float = 4.0,
+                 graphs: bool = False) -> None:
         import torch.distributed as dist
         self.model = model.to(device)
         self.device = device
@@ -54,6 +61,10 @@ class Trainer:
         self.base_lr = float(lr)
         if ddp is None:
             ddp = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        if graphs and (ddp or device.type != "cuda"):
+            raise ValueError("graphs=True needs one GPU and no DDP (the gradient all-reduce is not captured)")
+        self.graphs = bool(graphs)
+        self._graphed: dict = {}
         if ddp:
             from torch.nn.parallel import DistributedDataParallel as DDP
             ids = [device.index if device.index is not None else torch.cuda.current_device()] \
@@ -61,11 +72,18 @@ class Trainer:
             self.net = DDP(self.model, device_ids=ids, bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True)
         else:
             self.net = self.model
-        self.opt = torch.optim.Adam(self.model.parameters(), lr=self.base_lr)
+        if self.graphs:
+            self.opt = torch.optim.Adam(self.model.parameters(), lr=torch.tensor(self.base_lr, device=device),
+                                        capturable=True, fused=True)
+        else:
+            self.opt = torch.optim.Adam(self.model.parameters(), lr=self.base_lr)
 
     def set_epoch(self, epoch: int) -> None:
         for g in self.opt.param_groups:
-            g["lr"] = lr_for_epoch(self.base_lr, epoch)
+            if torch.is_tensor(g["lr"]):
+                g["lr"].fill_(lr_for_epoch(self.base_lr, epoch))  # the captured step reads it
+            else:
+                g["lr"] = lr_for_epoch(self.base_lr, epoch)
 
     def step_on_nds(self, pcl: torch.Tensor, covs: torch.Tensor, gt: torch.Tensor,
                     train: bool = True) -> Tuple[float, float]:
@@ -87,8 +105,95 @@ class Trainer:
 
     def step(self, points: torch.Tensor, gt_points: torch.Tensor, train: bool = True) -> Tuple[float, float]:
         """One batch of raw clouds: ``points`` [B,n,3], one-hot ``gt_points``
-        [B,n,C+1] -> the labelled NDT path on the GPU -> step_on_nds."""
+        [B,n,C+1] -> the labelled NDT path on the GPU -> step_on_nds (or, with
+        ``graphs``, a replay of the captured step)."""
+        if train and self.graphs:
+            loss, acc = self.step_graphed(points, gt_points)
+            return loss.item(), acc.item()
         from .preprocessing.ndtnet_preprocessing import ndt_preprocessing
         pcl, covs, gt = ndt_preprocessing(self.num_nds, points.to(self.device), gt_points.to(self.device),
                                           self.num_classes)
         return self.step_on_nds(pcl, covs, gt, train)
+
+    def step_graphed(self, points: torch.Tensor, gt_points: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """A training step as a graph replay; returns (loss, accuracy) as device
+        scalars, without synchronising."""
+        key = (tuple(points.shape), tuple(gt_points.shape))
+        g = self._graphed.get(key)
+        if g is None:
+            g = self._graphed[key] = GraphedTrainStep(self, points.shape, gt_points.shape[-1])
+        return g(points, gt_points)
+
+
+class GraphedTrainStep:
+    """tools/train.py:67-81 for one input shape, captured once and replayed:
+    ndt_preprocessing with labels (HIP) -> train-mode forward -> NLL loss ->
+    backward -> fused Adam, with the inputs copied into static buffers.
+
+    Capture needs the step's lazy state to exist (cuBLAS-style handles,
+    MIOpen's algorithm choices, the gradients and Adam's moments), so a few
+    steps run eagerly on a side stream first; the parameters, buffers and
+    optimizer state are snapshotted before them and restored after the
+    capture, so the first replay is the trainer's first step."""
+
+    def __init__(self, trainer: Trainer, points_shape, gt_width: int, warmup: int = 3) -> None:
+        tr = self.tr = trainer
+        dev = tr.device
+        self.s_points = torch.zeros(tuple(points_shape), dtype=torch.float32, device=dev)
+        self.s_gt = torch.zeros(tuple(points_shape[:2]) + (int(gt_width),), dtype=torch.float32, device=dev)
+        # a non-degenerate cloud for the warm-up steps (zeros would be one voxel)
+        gen = torch.Generator(device=dev).manual_seed(0)
+        self.s_points.copy_(torch.rand(self.s_points.shape, device=dev, generator=gen) * 20 - 10)
+        self.s_gt[..., 0] = 1.0
+        model, opt = tr.model, tr.opt
+        with torch.no_grad():
+            params = [p.detach().clone() for p in model.parameters()]
+            bufs = [b.detach().clone() for b in model.buffers()]
+            saved = {p: {k: v.clone() for k, v in st.items() if torch.is_tensor(v)} for p, st in opt.state.items()}
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(max(1, int(warmup))):
+                opt.zero_grad(set_to_none=True)
+                self._body()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        opt.zero_grad(set_to_none=True)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.loss, self.acc = self._body()
+        with torch.no_grad():
+            for p, s in zip(model.parameters(), params):
+                p.copy_(s)
+            for b, s in zip(model.buffers(), bufs):
+                b.copy_(s)
+            for p, st in opt.state.items():
+                before = saved.get(p, {})
+                for k, v in st.items():
+                    if torch.is_tensor(v):
+                        if k in before:
+                            v.copy_(before[k])
+                        else:
+                            v.zero_()  # a fresh moment / step count
+        torch.cuda.synchronize(dev)
+
+    def _body(self):
+        from .preprocessing.ndtnet_preprocessing import ndt_preprocessing
+        tr = self.tr
+        pcl, covs, gt = ndt_preprocessing(tr.num_nds, self.s_points, self.s_gt, tr.num_classes)
+        tr.model.train()
+        pred = tr.net(pcl, covs)
+        loss = segmentation_loss(pred, gt)
+        loss.backward()
+        tr.opt.step()
+        acc = (pred.detach().argmax(dim=-1) == gt.argmax(dim=-1)).float().mean()
+        return loss.detach(), acc
+
+    def __call__(self, points: torch.Tensor, gt_points: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        # the replay does not run Python: flip the mode here, so an eval forward
+        # after it re-folds the updated weights (NDTNetSegmentation.train)
+        self.tr.model.train()
+        self.s_points.copy_(points, non_blocking=True)
+        self.s_gt.copy_(gt_points, non_blocking=True)
+        self.graph.replay()
+        return self.loss, self.acc

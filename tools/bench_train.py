@@ -35,12 +35,33 @@ def main() -> None:
     ap.add_argument("--nds", type=int, default=1000)
     ap.add_argument("--classes", type=int, default=28)
     ap.add_argument("--feature-dim", type=int, default=768)
+    ap.add_argument("--graph", action="store_true",
+                    help="time Trainer(graphs=True): the whole step as one HIP graph replay")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     pts, gt = make_labelled_batch(a.batch, a.points, a.classes, seed0=0)
     pts, gt = torch.from_numpy(pts).to(dev), torch.from_numpy(gt).to(dev)
     model = NDTNetSegmentation(3, a.classes, a.feature_dim)
+    if a.graph:
+        tr = Trainer(model, 1e-3, a.nds, a.classes, dev, ddp=False, graphs=True)
+        for _ in range(a.warmup):
+            loss, _ = tr.step_graphed(pts, gt)
+        torch.cuda.synchronize()
+        st = torch.cuda.current_stream(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(a.steps):
+            loss, acc = tr.step_graphed(pts, gt)
+        e1.record(st)
+        torch.cuda.synchronize()
+        step = e0.elapsed_time(e1) / a.steps
+        print(json.dumps({"what": "training step (tools/train.py:67-81) as one HIP graph: HIP labelled NDT + "
+                                  "torch train forward/backward + fused capturable Adam", "batch": a.batch,
+                          "points": a.points, "nds": a.nds, "classes": a.classes, "F": a.feature_dim,
+                          "steps": a.steps, "step_ms": round(step, 4),
+                          "clouds_per_s": round(a.batch / step * 1e3, 1), "loss": round(loss.item(), 5)}))
+        return
     tr = Trainer(model, 1e-3, a.nds, a.classes, dev, ddp=False)
     names = ("ndt_labelled", "forward_train", "loss", "backward", "adam", "forward_eval_hip")
     tot = {n: 0.0 for n in names}
