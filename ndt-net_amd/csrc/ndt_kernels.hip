@@ -817,7 +817,7 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_scatter(const T* __restrict
 // register blocks of kWqU samples (one block in flight while the other is
 // folded).  A quad that meets a coordinate outside that range (non-finite
 // float, or a double outside [2^-300, 2^300]) refolds its ND with IEEE
-// divisions and the reference's NaN -> 0 step.  Labelled runs: lane 0 of the
+// divisions and the reference's NaN -> 0 step.  Labelled runs: the whole
 // quad builds the class histogram in LDS (first index of the max,
 // normal_distributions.c:107-121).
 constexpr int kWqThreads = 256;              // 4 waves x 16 quads
@@ -1301,12 +1301,48 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
       for (int q = 0; q < 9; q++) CA.cov_post[9 * o + q] = S[q];
     }
   }
-  if (live && j == 0) {
+  const uint32_t nbins = (uint32_t)ncls + 1u;
+  const bool hist_lds = (size_t)kWqNDs * nbins * sizeof(uint32_t) <= (size_t)kWqHistMax;
+  if (live && nd_lbl && hist_lds) {
+    // the whole quad counts: lane j takes the 8-label runs j, j + 4, ... of
+    // each 128-label round (the quad reads 256 contiguous bytes per round, 32
+    // loads in flight per lane) and adds into the ND's LDS histogram with
+    // return-less LDS atomics, so no increment waits on the previous one.
+    // One lane counting alone waited on a load and an LDS read-modify-write
+    // per label: L's 1675-label ND took ~100 us of a labelled run.
+    uint32_t* hist = wq_hist + (threadIdx.x >> 2) * nbins;
+    for (uint32_t k = j; k < nbins; k += 4) hist[k] = 0;
+    __builtin_amdgcn_wave_barrier();
+    const uint16_t* l = nd_lbl + (uint64_t)b * n + beg;
+    uint32_t s0 = 0;
+    for (; s0 + 128 <= cnt; s0 += 128) {
+      uint16_t v[32];
+#pragma unroll
+      for (int g = 0; g < 4; g++)
+#pragma unroll
+        for (int t = 0; t < 8; t++) v[8 * g + t] = l[s0 + 32 * g + 8 * j + t];
+#pragma unroll
+      for (int k = 0; k < 32; k++)
+        if (v[k] < nbins) atomicAdd(&hist[v[k]], 1u);
+    }
+    for (uint32_t s = s0 + j; s < cnt; s += 4)
+      if (l[s] < nbins) atomicAdd(&hist[l[s]], 1u);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS atomics are done
+    if (j == 0) {
+      uint32_t best = 0;
+      uint16_t cls = 0;
+      for (uint32_t k = 0; k < nbins; k++) {
+        const uint32_t h = hist[k];
+        if (h > best) { best = h; cls = (uint16_t)k; }
+      }
+      nd_cls[o] = cls;
+    }
+  } else if (live && j == 0) {
     uint16_t cls = 0;
-    if (nd_lbl) {
-      const uint32_t nb = (uint32_t)ncls + 1u;
-      const bool lds = (size_t)kWqNDs * nb * sizeof(uint32_t) <= (size_t)kWqHistMax;
-      uint32_t* hist = lds ? wq_hist + (threadIdx.x >> 2) * nb : hist_all + o * nb;
+    if (nd_lbl) {  // histograms too large for LDS: one lane, in global memory
+      const uint32_t nb = nbins;
+      uint32_t* hist = hist_all + o * nb;
       for (uint32_t k = 0; k < nb; k++) hist[k] = 0;
       const uint16_t* l = nd_lbl + (uint64_t)b * n + beg;
       uint32_t s2 = 0;

@@ -535,7 +535,7 @@ def test_run_parts_equal_whole_run():
     assert res[0][1] == res[1][1]
 
 
-@pytest.mark.parametrize("num_classes", [28, 300])
+@pytest.mark.parametrize("num_classes", [28, 300, 3])
 def test_full_size_labelled(num_classes):
     """SURVEY 8(f)2 at the bench's size: 16 x 100k labelled L clouds -> 1000
     NDs, every cloud's rows and one-hot classes against the oracle
@@ -545,7 +545,9 @@ def test_full_size_labelled(num_classes):
     reference driver's path, ndtnet_preprocessing.py:34).  300 classes: 301
     bins x 64 NDs per k_welford_q workgroup exceed the LDS histogram budget
     (kWqHistMax, 64 KB), so the per-ND histograms live in global memory; labels
-    uniform over all 301 values, so the first-max tie rule decides many NDs."""
+    uniform over all 301 values, so the first-max tie rule decides many NDs.
+    3 classes, uniform labels: the LDS histograms the whole quad adds into,
+    with near-ties in every ND (4 bins, ~100 labels each)."""
     import torch
     import oracle as O
     from ndnet.preprocessing.ndtnet_preprocessing import ndt_preprocessing, last_stats
@@ -575,6 +577,8 @@ def test_full_size_labelled(num_classes):
         assert np.array_equal(g[b], onehot_ref), f"cloud {b} classes"
     if num_classes == 300:  # the tie rule and the wide histogram are exercised
         assert len(np.unique(g.argmax(axis=2))) > 100
+    if num_classes == 3:
+        assert len(np.unique(g.argmax(axis=2))) == 4
 
 
 @pytest.mark.parametrize("share,k", [(2, 1000), (2, 2000)])
