@@ -397,10 +397,34 @@ def main() -> None:
     _lib.lib().ndnet_ndt_set_timing(plan.handle, 0)
     stage_ms /= reps
     fwd_ms /= reps
-    chain_ms = np.zeros(4)
+    chain_in_fwd_ms = np.zeros(4)
     for i, e0, e1 in pointnet_hip.chain_timing:
-        chain_ms[i] += e0.elapsed_time(e1) / reps
+        chain_in_fwd_ms[i] += e0.elapsed_time(e1) / reps
     pointnet_hip.chain_timing = None
+    # each chain alone, R launches back to back between two events on the
+    # launch stream: the per-launch duration rocprofv3's kernel statistics
+    # report (the events around each chain inside a forward add that launch's
+    # dispatch latency).  The inputs and the workspace are the last forward's;
+    # chain D re-arms the max-pool buffer last, as a forward does.
+    chain_ms = chain_in_fwd_ms.copy()
+    if pointnet_hip.available():
+        ws = pointnet_hip._folded(model)["ws"].get((B, k, dev, 0))
+        if ws is not None:
+            blk = p.as_strided((B, k, 12), (k * 12, 12, 1))
+            out_d = torch.empty((B, k, C + 1), device=dev)
+            R = 20
+            with torch.no_grad():
+                for i in range(4):
+                    o = out_d if i == 3 else None
+                    ws.chain(i, blk, out=o)  # warm
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    torch.cuda._sleep(sleep_cycles)
+                    e0.record()
+                    for _ in range(R):
+                        ws.chain(i, blk, out=o)
+                    e1.record()
+                    e1.synchronize()
+                    chain_ms[i] = e0.elapsed_time(e1) / R
     ndt_ms = float(stage_ms.sum())
     hip_fwd = pointnet_hip.available()
     flops = pointnet_flops_per_cloud(k, F, C) * B
@@ -415,7 +439,9 @@ def main() -> None:
                                          for f, t in zip(cflops, chain_ms)],
                    "frac_of_issued_peak": [round(float(i / (t * 1e-3)), 4) if t > 0 else None
                                            for i, t in zip(cideal, chain_ms)],
-                   "forward_other_ms": round(fwd_ms - float(chain_ms.sum()), 4),
+                   "in_forward_ms": [round(float(v), 4) for v in chain_in_fwd_ms],
+                   "in_forward_basis": "events around each chain launch inside a forward (adds its dispatch latency)",
+                   "forward_other_ms": round(fwd_ms - float(chain_in_fwd_ms.sum()), 4),
                    "forward_other": "per-cloud FC heads, weight folds and launch boundaries of the forward"}
     # the NDT front (k_reset + k_front: limits, every bisection pass, dense ids
     # and binning in ONE launch) reads the f32 points once into registers and
@@ -452,7 +478,9 @@ def main() -> None:
                                    f"points; 2 K N per point per layer at unpadded sizes)",
                     "peak_basis": "the issued-instruction peak: split-bf16 (x6) layers at BF16 2500 TF / 6 products, "
                                   "f32 layers at 157.3 TF, weighted by each layer's FLOPs",
-                    "ms": round(ms, 4), "ms_basis": "sum of the 4 chain launches (event-timed on the launch stream)",
+                    "ms": round(ms, 4), "ms_basis": "sum over chains A-D of the per-launch time of 20 back-to-back "
+                                                          "launches of that chain between two events on its stream "
+                                                          "(rocprofv3's per-launch duration)",
                     "all_chains": chains_info}
         rows = [pmc.get(f"k_pn_chain {c}") for c in "ABCD"]
         if all(r and "hbm_bytes" in r for r in rows):
