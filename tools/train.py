@@ -48,6 +48,8 @@ def main() -> None:
     ap.add_argument("--steps-per-epoch", type=int, default=8, help="synthetic batches per epoch and rank")
     ap.add_argument("--val-steps", type=int, default=2)
     ap.add_argument("--no-save", action="store_true")
+    ap.add_argument("--graphs", action="store_true",
+                    help="one GPU: replay each training step from a captured HIP graph (Trainer(graphs=True))")
     args = ap.parse_args()
     if args.task != "segmentation":
         raise NotImplementedError("only the segmentation task is on the hot path (train.py:122-123)")
@@ -58,7 +60,9 @@ def main() -> None:
     D.init("nccl", dev)
     torch.manual_seed(0)  # identical initial weights on every rank (DDP also broadcasts rank 0's)
     model = NDTNetSegmentation(3, args.n_classes, args.feature_dim)
-    tr = Trainer(model, args.learning_rate, args.n_desired_nds, args.n_classes, dev)
+    if args.graphs and world > 1:
+        raise SystemExit("--graphs runs on one GPU (the DDP all-reduce is not captured)")
+    tr = Trainer(model, args.learning_rate, args.n_desired_nds, args.n_classes, dev, graphs=args.graphs)
     path = os.path.join(args.out_path, datetime.datetime.now().strftime("%Y%m%d_%H%M%S"))
 
     loaders = {}
