@@ -1,0 +1,84 @@
+/*
+ * ndnet_train.h -- C ABI of the train-mode point-MLP kernels of
+ * libndnet_amd.so (ndt-net_amd/csrc/train_kernels.hip): the forward and
+ * backward of the reference's per-point Conv1d(k=1) + BatchNorm1d (batch
+ * statistics) [+ ReLU] blocks on gfx950, for the training step of
+ * tools/train.py:67-81.
+ *
+ * Replaces, in train mode:
+ *   ndnet/models/ndtnet.py:48-50   TNet conv1..3 + bn1..3 + ReLU
+ *   ndnet/models/ndtnet.py:148-152 NDTNet conv1 + bn1 (no ReLU), conv2/conv3 + bn2/bn3
+ *   ndnet/models/ndtnet.py:233-239 seg head conv1..3 + bn1..3 + ReLU, conv4
+ * and the autograd backward torch runs through them.  Host side:
+ * ndt-net_amd/ndnet/models/train_hip.py (the autograd Functions).
+ *
+ * Layouts are torch's Conv1d NCL: activations [B][C][N] fp32 (N points
+ * contiguous), weights [Cout][Cin] row-major.  Every entry point launches on
+ * `stream` (a hipStream_t; NULL = default stream), allocates nothing and does
+ * not synchronise (graph-capturable).  Returns 0, NDNET_ERR_ARG (-20) for an
+ * inconsistent argument or NDNET_ERR_HIP (-21) on a launch failure.
+ */
+#ifndef NDNET_TRAIN_H_
+#define NDNET_TRAIN_H_
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* C[z] (M x N) = sum over the part's clouds of A[c] (M x K) . B[c] (K x N)
+ * (+ bias[c * sbias + m]) on the fp32 MFMA (v_mfma_f32_16x16x4_f32: exact fp32
+ * products, fp32 sums in four interleaved accumulator sets; 64 x 64 tiles).
+ * Element addressing (floats):
+ *   A(m, k) = A[m * lda + k] if a_kmajor else A[k * lda + m]
+ *   B(k, n) = B[n * ldb + k] if b_kmajor else B[k * ldb + n]
+ *   C(m, n) = C[m * ldc + n]
+ * Grid z covers ceil(batch / clouds_per_part) * nchunks: z = zg * nchunks + zc
+ * sums clouds c in [zg * clouds_per_part, min(batch, (zg + 1) * clouds_per_part))
+ * (A + c * sAz, B + c * sBz) over k in [zc * kchunk, min(K, (zc + 1) * kchunk))
+ * and writes C + z * sCz.  More than one part is split-K into partial
+ * products, summed by ndnet_tr_sum_parts.  Conv1d forward: A = W (a_kmajor),
+ * B = x[b]; input gradient: A = W^T (not a_kmajor), B = dy[b]; weight gradient:
+ * A = dy[b] (a_kmajor), B = x[b]^T (b_kmajor), parts over (cloud groups,
+ * point chunks).  sbias = 0: one bias vector; sbias = M: a bias per cloud (the
+ * segmentation head's global-feature term, ndtnet.py:230-233, folded into a
+ * per-cloud bias); a bias needs one cloud per part and one chunk. */
+int ndnet_tr_gemm(const float *A, const float *B, float *C, const float *bias, int64_t sbias, int M, int N, int K,
+                  int64_t lda, int64_t ldb, int64_t ldc, int64_t sAz, int64_t sBz, int64_t sCz,
+                  int batch, int clouds_per_part, int a_kmajor, int b_kmajor, int nchunks, int kchunk,
+                  void *stream);
+
+/* out[i] = sum_{p < nparts} part[p * count + i], in p order (deterministic). */
+int ndnet_tr_sum_parts(const float *part, float *out, int64_t count, int nparts, void *stream);
+
+/* BatchNorm1d forward with batch statistics (torch's training mode) over
+ * y [B][C][N], one workgroup per channel: mean and biased variance over the
+ * B * N values (summed in double, two passes), invstd = 1 / sqrt(var + eps),
+ * z = (y - mean) * invstd * gamma + beta, then ReLU if `relu`.  Saves mean /
+ * invstd [C] for the backward and updates running_mean / running_var (may be
+ * NULL) with `momentum` and the unbiased variance, as torch does. */
+int ndnet_tr_bn_fwd(const float *y, float *z, float *mean, float *invstd, float *running_mean,
+                    float *running_var, const float *gamma, const float *beta, int B, int C, int N,
+                    float eps, float momentum, int relu, void *stream);
+
+/* Its backward, one workgroup per channel: g = dz, masked by ReLU where the
+ * forward's output (recomputed from y, mean, invstd, gamma, beta with the
+ * forward's exact roundings) was not > 0; xhat = (y - mean) * invstd,
+ * dgamma = sum g xhat, dbeta = sum g,
+ * dy = gamma invstd (g - dbeta / M - xhat dgamma / M), dbias = sum dy (the
+ * gradient of the convolution's bias).  dgamma / dbeta / dbias may be NULL. */
+int ndnet_tr_bn_bwd(const float *dz, const float *y, const float *mean, const float *invstd, const float *gamma,
+                    const float *beta, float *dy, float *dgamma, float *dbeta, float *dbias, int B, int C, int N,
+                    int relu, void *stream);
+
+/* out[c] = sum over b, n of x[b][c][n] (a bias gradient), one workgroup per channel. */
+int ndnet_tr_chan_sum(const float *x, float *out, int B, int C, int N, void *stream);
+
+/* out[r] = sum over n of x[r][n] for `rows` rows of N contiguous values (per-cloud bias gradients). */
+int ndnet_tr_row_sum(const float *x, float *out, int64_t rows, int N, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NDNET_TRAIN_H_ */

@@ -1,0 +1,454 @@
+// Train-mode point-MLP kernels for gfx950 (include/ndnet_train.h).
+//
+// The reference trains NDTNetSegmentation with torch autograd
+// (tools/train.py:67-81): every per-point block is Conv1d(k=1) -> BatchNorm1d
+// with batch statistics -> ReLU (ndnet/models/ndtnet.py:48-50, 148-152,
+// 233-239), and the backward runs the same ops in reverse.  Here each block is
+// two kernels each way, on torch's NCL layout ([B][C][N], points contiguous):
+//   forward:  k_tr_gemm (y = W x + b, fp32 MFMA)  ->  k_tr_bn_fwd (statistics,
+//             normalise, affine, ReLU; running-stat update)
+//   backward: k_tr_bn_bwd (ReLU mask, BN backward, bias gradient)  ->
+//             k_tr_gemm twice (dx = W^T dy; dW = sum dy x^T as split-K
+//             partials) -> k_tr_sum_parts
+// The GEMM reads either operand in whichever orientation torch stores it, so
+// no transpose kernels run (the MIOpen path of the same step spends a large
+// share of its time in NCHW <-> NHWC transposes around the 1x1 convolutions,
+// profiles/r03_train_graph_kernel_stats.csv).
+//
+// GEMM tiling: 64 x 64 output tile per workgroup of 4 waves, each wave 32 x 32
+// (2 x 2 blocks of v_mfma_f32_16x16x4_f32, four accumulator sets, exact fp32 products and sums as
+// torch's fp32 GEMM), k-steps of 16 through a double-buffered LDS tile with
+// the next step's global loads in flight during the current step's MFMAs.
+// Loads are bounds-checked (zero fill), so ragged sizes (K = 3 or 12 input
+// channels, 29 output classes, 1000 points) need no padding.
+//
+// BatchNorm statistics: one workgroup per channel holds the channel's B * N
+// values in registers (up to 16384), sums in double, two passes (mean, then
+// the squared deviations), so the variance has no E[x^2] - E[x]^2
+// cancellation.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "../../include/ndnet_train.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kTM = 64, kTN = 64, kTK = 16;
+constexpr int kPitch = 64 + 16;  // LDS row pitch (floats): the 4 lane quads of an A/B read hit disjoint banks
+constexpr int kGemmThreads = 256;
+
+constexpr int kBnThreads = 512;
+constexpr int kBnCache = 32;  // values per thread held in registers: B * N <= 16384 reads the channel once
+
+// global -> registers: this thread's 4 elements of the (k0 .. k0 + 16) x 64 tile.
+// A contiguous along k (a_kmajor): lanes walk k (16 per row), else along m.
+template <bool KMAJOR>
+__device__ __forceinline__ void tile_load(const float* __restrict__ P, int64_t ld, int r0, int k0, int R, int kend,
+                                          float (&v)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int kk = KMAJOR ? (t & 15) : (t >> 6) + 4 * i;
+    const int rr = KMAJOR ? (t >> 4) + 16 * i : (t & 63);
+    const int gr = r0 + rr, gk = k0 + kk;
+    v[i] = (gr < R && gk < kend) ? (KMAJOR ? P[(int64_t)gr * ld + gk] : P[(int64_t)gk * ld + gr]) : 0.0f;
+  }
+}
+
+// registers -> LDS tile [k][row] (row contiguous: one MFMA operand read per lane)
+template <bool KMAJOR>
+__device__ __forceinline__ void tile_store(float* __restrict__ s, const float (&v)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int kk = KMAJOR ? (t & 15) : (t >> 6) + 4 * i;
+    const int rr = KMAJOR ? (t >> 4) + 16 * i : (t & 63);
+    s[kk * kPitch + rr] = v[i];
+  }
+}
+
+template <bool AK, bool BK>
+__global__ __launch_bounds__(kGemmThreads) void k_tr_gemm(const float* __restrict__ A, const float* __restrict__ B,
+                                                          float* __restrict__ C, const float* __restrict__ bias,
+                                                          int64_t sbias, int M, int N, int K, int64_t lda,
+                                                          int64_t ldb, int64_t ldc, int64_t sAz, int64_t sBz,
+                                                          int64_t sCz, int batch, int cpz, int nchunks, int kchunk) {
+  __shared__ float sA[2][kTK * kPitch];
+  __shared__ float sB[2][kTK * kPitch];
+  const int z = blockIdx.z, zg = z / nchunks, zc = z - zg * nchunks;
+  const int cl0 = zg * cpz, ncl = min(cpz, batch - cl0);  // this part's clouds
+  C += z * sCz;
+  if (bias) bias += cl0 * sbias;
+  const int kbeg = zc * kchunk;
+  const int kend = min(K, kbeg + kchunk);
+  const int m0 = blockIdx.y * kTM, n0 = blockIdx.x * kTN;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  const int r16 = lane & 15, q = lane >> 4;
+
+  // one accumulator set per k-quad of the 16-wide step: four shorter fp32 sums
+  // (summed pairwise at the end) instead of one chain over all of K, and 16
+  // independent MFMA chains per wave
+  f32x4 acc[kTK / 4][2][2];
+#pragma unroll
+  for (int ks = 0; ks < kTK / 4; ks++)
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+      for (int j = 0; j < 2; j++) acc[ks][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // steps t = cloud * nst + s: the part's clouds one after another (split-K over clouds)
+  const int nst = kend > kbeg ? (kend - kbeg + kTK - 1) / kTK : 0;
+  const int total = ncl > 0 ? ncl * nst : 0;
+  float ra[4], rb[4];
+  auto load = [&](int t) {
+    const int cl = t / nst, st = t - cl * nst;
+    const int64_t c = cl0 + cl;
+    tile_load<AK>(A + c * sAz, lda, m0, kbeg + st * kTK, M, kend, ra);
+    tile_load<BK>(B + c * sBz, ldb, n0, kbeg + st * kTK, N, kend, rb);
+  };
+  if (total > 0) {
+    load(0);
+    tile_store<AK>(sA[0], ra);
+    tile_store<BK>(sB[0], rb);
+  }
+  __syncthreads();
+  for (int t = 0; t < total; t++) {
+    const int cur = t & 1;
+    const bool more = t + 1 < total;
+    if (more) load(t + 1);  // the next k-step's loads fly under this step's MFMAs
+    const float* a = sA[cur];
+    const float* b = sB[cur];
+#pragma unroll
+    for (int ks = 0; ks < kTK / 4; ks++) {
+      const int row = (ks * 4 + q) * kPitch;
+      const float a0 = a[row + wm + r16], a1 = a[row + wm + 16 + r16];
+      const float b0 = b[row + wn + r16], b1 = b[row + wn + 16 + r16];
+      acc[ks][0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[ks][0][0], 0, 0, 0);
+      acc[ks][0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[ks][0][1], 0, 0, 0);
+      acc[ks][1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[ks][1][0], 0, 0, 0);
+      acc[ks][1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[ks][1][1], 0, 0, 0);
+    }
+    if (more) {  // the other buffer was last read before the previous barrier
+      tile_store<AK>(sA[cur ^ 1], ra);
+      tile_store<BK>(sB[cur ^ 1], rb);
+    }
+    __syncthreads();
+  }
+  // lane (q, r16) of block (i, j): rows 4 q + r, column r16
+#pragma unroll
+  for (int i = 0; i < 2; i++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int gm = m0 + wm + 16 * i + 4 * q + r;
+      if (gm >= M) continue;
+      const float bv = bias ? bias[gm] : 0.0f;
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        const int gn = n0 + wn + 16 * j + r16;
+        if (gn < N)
+          C[(int64_t)gm * ldc + gn] = ((acc[0][i][j][r] + acc[1][i][j][r]) + (acc[2][i][j][r] + acc[3][i][j][r])) + bv;
+      }
+    }
+}
+
+// out[i] = part[0][i] + part[1][i] + ... in part order; 4 elements per thread,
+// eight parts' loads issued before their sums
+__global__ __launch_bounds__(256) void k_tr_sum_parts(const float* __restrict__ part, float* __restrict__ out,
+                                                      int64_t count, int nparts) {
+  const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i0 >= count) return;
+  const int w = (int)min<int64_t>(4, count - i0);
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int p0 = 0; p0 < nparts; p0 += 8) {
+    float v[8][4];
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+#pragma unroll
+      for (int e = 0; e < 4; e++)
+        v[u][e] = (p0 + u < nparts && e < w) ? part[(int64_t)(p0 + u) * count + i0 + e] : 0.0f;
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+#pragma unroll
+      for (int e = 0; e < 4; e++)
+        if (p0 + u < nparts) s[e] = (p0 + u == 0) ? v[u][e] : s[e] + v[u][e];
+  }
+  for (int e = 0; e < w; e++) out[i0 + e] = s[e];
+}
+
+// sum over the workgroup in a fixed order (wave shuffles, then the waves in order)
+__device__ double block_sum(double v, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int wave = threadIdx.x >> 6;
+  __syncthreads();  // red may still be read by the previous call
+  if ((threadIdx.x & 63) == 0) red[wave] = v;
+  __syncthreads();
+  double t = red[0];
+  for (int w = 1; w < kBnThreads / 64; w++) t += red[w];
+  return t;
+}
+
+// this thread's elements j = tid, tid + T, ... of one channel as (cloud, point),
+// advanced without divisions
+struct ChanWalk {
+  int b, n;
+  __device__ explicit ChanWalk(int N) : b(0), n(threadIdx.x) { fold(N); }
+  __device__ void fold(int N) {
+    while (n >= N) {
+      n -= N;
+      b++;
+    }
+  }
+  __device__ void next(int N) {
+    n += kBnThreads;
+    fold(N);
+  }
+  __device__ int64_t off(int C, int N, int c) const { return ((int64_t)b * C + c) * N + n; }
+};
+
+// the normalised, affine value: one rounding per operation (no contraction), so
+// the backward's ReLU mask recomputed from y equals the forward's output sign
+__device__ __forceinline__ float bn_apply(float v, float fm, float inv, float g, float bt) {
+  return __fadd_rn(__fmul_rn(__fmul_rn(__fsub_rn(v, fm), inv), g), bt);
+}
+
+__global__ __launch_bounds__(kBnThreads) void k_tr_bn_fwd(const float* __restrict__ y, float* __restrict__ z,
+                                                          float* __restrict__ mean, float* __restrict__ invstd,
+                                                          float* __restrict__ rmean, float* __restrict__ rvar,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, int Bn, int C, int N,
+                                                          float eps, float momentum, int relu) {
+  __shared__ double red[kBnThreads / 64];
+  const int c = blockIdx.x;
+  const int64_t M = (int64_t)Bn * N;
+  const bool cached = M <= (int64_t)kBnCache * kBnThreads;
+  float v[kBnCache];
+  double s = 0.0;
+  if (cached) {
+    ChanWalk w(N);
+#pragma unroll
+    for (int i = 0; i < kBnCache; i++, w.next(N)) {
+      v[i] = w.b < Bn ? y[w.off(C, N, c)] : 0.0f;
+      s += v[i];
+    }
+  } else {
+    for (ChanWalk w(N); w.b < Bn; w.next(N)) s += y[w.off(C, N, c)];
+  }
+  const double mu = block_sum(s, red) / (double)M;
+  double s2 = 0.0;
+  if (cached) {
+    ChanWalk w(N);
+#pragma unroll
+    for (int i = 0; i < kBnCache; i++, w.next(N)) {
+      const double d = (double)v[i] - mu;
+      if (w.b < Bn) s2 += d * d;
+    }
+  } else {
+    for (ChanWalk w(N); w.b < Bn; w.next(N)) {
+      const double d = (double)y[w.off(C, N, c)] - mu;
+      s2 += d * d;
+    }
+  }
+  const double var = block_sum(s2, red) / (double)M;
+  const float inv = (float)(1.0 / sqrt(var + (double)eps));
+  if (threadIdx.x == 0) {
+    mean[c] = (float)mu;
+    invstd[c] = inv;
+    if (rmean) rmean[c] = (1.0f - momentum) * rmean[c] + momentum * (float)mu;
+    if (rvar) {
+      const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+      rvar[c] = (1.0f - momentum) * rvar[c] + momentum * (float)unb;
+    }
+  }
+  const float fm = (float)mu, g = gamma[c], bt = beta[c];
+  if (cached) {
+    ChanWalk w(N);
+#pragma unroll
+    for (int i = 0; i < kBnCache; i++, w.next(N)) {
+      if (w.b < Bn) {
+        float o = bn_apply(v[i], fm, inv, g, bt);
+        if (relu) o = fmaxf(o, 0.0f);
+        z[w.off(C, N, c)] = o;
+      }
+    }
+  } else {
+    for (ChanWalk w(N); w.b < Bn; w.next(N)) {
+      const int64_t off = w.off(C, N, c);
+      float o = bn_apply(y[off], fm, inv, g, bt);
+      if (relu) o = fmaxf(o, 0.0f);
+      z[off] = o;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBnThreads) void k_tr_bn_bwd(const float* __restrict__ dz, const float* __restrict__ y,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float* __restrict__ dy,
+                                                          float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                          float* __restrict__ dbias, int Bn, int C, int N, int relu) {
+  __shared__ double red[kBnThreads / 64];
+  const int c = blockIdx.x;
+  const int64_t M = (int64_t)Bn * N;
+  const bool cached = M <= (int64_t)kBnCache * kBnThreads;
+  const float mu = mean[c], inv = invstd[c], gm = gamma[c], bt = beta[c];
+  float gv[kBnCache], xv[kBnCache];
+  double sg = 0.0, sgx = 0.0;
+  // g = dz where the forward's output was > 0 (ReLU), xhat = (y - mean) invstd
+  auto grad_at = [&](int64_t off, float& xh) {
+    const float yv = y[off];
+    float g = dz[off];
+    if (relu && !(bn_apply(yv, mu, inv, gm, bt) > 0.0f)) g = 0.0f;
+    xh = (yv - mu) * inv;
+    return g;
+  };
+  if (cached) {
+    ChanWalk w(N);
+#pragma unroll
+    for (int i = 0; i < kBnCache; i++, w.next(N)) {
+      float g = 0.0f, xh = 0.0f;
+      if (w.b < Bn) g = grad_at(w.off(C, N, c), xh);
+      gv[i] = g;
+      xv[i] = xh;
+      sg += g;
+      sgx += (double)g * xh;
+    }
+  } else {
+    for (ChanWalk w(N); w.b < Bn; w.next(N)) {
+      float xh;
+      const float g = grad_at(w.off(C, N, c), xh);
+      sg += g;
+      sgx += (double)g * xh;
+    }
+  }
+  sg = block_sum(sg, red);
+  sgx = block_sum(sgx, red);
+  const float k1 = (float)(sg / (double)M), k2 = (float)(sgx / (double)M);
+  const float scale = gm * inv;
+  double sdy = 0.0;
+  if (cached) {
+    ChanWalk w(N);
+#pragma unroll
+    for (int i = 0; i < kBnCache; i++, w.next(N)) {
+      if (w.b < Bn) {
+        const float d = scale * (gv[i] - k1 - xv[i] * k2);
+        dy[w.off(C, N, c)] = d;
+        sdy += d;
+      }
+    }
+  } else {
+    for (ChanWalk w(N); w.b < Bn; w.next(N)) {
+      const int64_t off = w.off(C, N, c);
+      float xh;
+      const float g = grad_at(off, xh);
+      const float d = scale * (g - k1 - xh * k2);
+      dy[off] = d;
+      sdy += d;
+    }
+  }
+  sdy = block_sum(sdy, red);
+  if (threadIdx.x == 0) {
+    if (dgamma) dgamma[c] = (float)sgx;
+    if (dbeta) dbeta[c] = (float)sg;
+    if (dbias) dbias[c] = (float)sdy;
+  }
+}
+
+__global__ __launch_bounds__(kBnThreads) void k_tr_chan_sum(const float* __restrict__ x, float* __restrict__ out,
+                                                            int Bn, int C, int N) {
+  __shared__ double red[kBnThreads / 64];
+  const int c = blockIdx.x;
+  double s = 0.0;
+  for (ChanWalk w(N); w.b < Bn; w.next(N)) s += x[w.off(C, N, c)];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) out[c] = (float)s;
+}
+
+// out[r] = sum of the N contiguous values of row r: one wave per row, fixed order
+__global__ __launch_bounds__(256) void k_tr_row_sum(const float* __restrict__ x, float* __restrict__ out, int64_t R,
+                                                   int N) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const float* row = x + r * N;
+  double s = 0.0;
+  for (int n = threadIdx.x & 63; n < N; n += 64) s += row[n];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((threadIdx.x & 63) == 0) out[r] = (float)s;
+}
+
+int launched() { return hipGetLastError() == hipSuccess ? 0 : -21; }
+
+}  // namespace
+
+extern "C" int ndnet_tr_gemm(const float* A, const float* B, float* C, const float* bias, int64_t sbias, int M,
+                             int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t sAz, int64_t sBz,
+                             int64_t sCz, int batch, int clouds_per_part, int a_kmajor, int b_kmajor, int nchunks,
+                             int kchunk, void* stream) {
+  if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || batch <= 0 || nchunks <= 0 || kchunk <= 0) return -20;
+  if (clouds_per_part <= 0 || clouds_per_part > batch) return -20;
+  if (lda <= 0 || ldb <= 0 || ldc < N || sAz < 0 || sBz < 0 || sCz < 0 || sbias < 0) return -20;
+  if ((int64_t)(nchunks - 1) * kchunk >= K) return -20;  // every chunk starts inside K
+  if ((int64_t)nchunks * kchunk < K) return -20;         // and together they cover it
+  if ((nchunks > 1 || clouds_per_part > 1) && bias) return -20;  // a bias belongs to one partial only
+  const int64_t parts = (batch + clouds_per_part - 1) / clouds_per_part;
+  const int64_t gz = parts * nchunks, gy = (M + kTM - 1) / kTM, gx = (N + kTN - 1) / kTN;
+  if (gz > 65535 || gy > 65535 || gx > (int64_t)INT32_MAX) return -20;
+  const dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)gz);
+  hipStream_t st = (hipStream_t)stream;
+#define NDNET_TR_GEMM(AKV, BKV)                                                                                \
+  k_tr_gemm<AKV, BKV><<<grid, kGemmThreads, 0, st>>>(A, B, C, bias, sbias, M, N, K, lda, ldb, ldc, sAz, sBz, sCz, \
+                                                     batch, clouds_per_part, nchunks, kchunk)
+  if (a_kmajor) {
+    if (b_kmajor) NDNET_TR_GEMM(true, true); else NDNET_TR_GEMM(true, false);
+  } else {
+    if (b_kmajor) NDNET_TR_GEMM(false, true); else NDNET_TR_GEMM(false, false);
+  }
+#undef NDNET_TR_GEMM
+  return launched();
+}
+
+extern "C" int ndnet_tr_sum_parts(const float* part, float* out, int64_t count, int nparts, void* stream) {
+  if (!part || !out || count <= 0 || nparts <= 0) return -20;
+  const int64_t blocks = (count + 1023) / 1024;
+  if (blocks > (int64_t)INT32_MAX) return -20;
+  k_tr_sum_parts<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(part, out, count, nparts);
+  return launched();
+}
+
+extern "C" int ndnet_tr_bn_fwd(const float* y, float* z, float* mean, float* invstd, float* running_mean,
+                               float* running_var, const float* gamma, const float* beta, int B, int C, int N,
+                               float eps, float momentum, int relu, void* stream) {
+  if (!y || !z || !mean || !invstd || !gamma || !beta || B <= 0 || C <= 0 || N <= 0) return -20;
+  k_tr_bn_fwd<<<C, kBnThreads, 0, (hipStream_t)stream>>>(y, z, mean, invstd, running_mean, running_var, gamma, beta,
+                                                         B, C, N, eps, momentum, relu);
+  return launched();
+}
+
+extern "C" int ndnet_tr_bn_bwd(const float* dz, const float* y, const float* mean, const float* invstd,
+                               const float* gamma, const float* beta, float* dy, float* dgamma, float* dbeta,
+                               float* dbias, int B, int C, int N, int relu, void* stream) {
+  if (!dz || !y || !mean || !invstd || !gamma || !beta || !dy || B <= 0 || C <= 0 || N <= 0) return -20;
+  k_tr_bn_bwd<<<C, kBnThreads, 0, (hipStream_t)stream>>>(dz, y, mean, invstd, gamma, beta, dy, dgamma, dbeta, dbias,
+                                                         B, C, N, relu);
+  return launched();
+}
+
+extern "C" int ndnet_tr_chan_sum(const float* x, float* out, int B, int C, int N, void* stream) {
+  if (!x || !out || B <= 0 || C <= 0 || N <= 0) return -20;
+  k_tr_chan_sum<<<C, kBnThreads, 0, (hipStream_t)stream>>>(x, out, B, C, N);
+  return launched();
+}
+
+extern "C" int ndnet_tr_row_sum(const float* x, float* out, int64_t rows, int N, void* stream) {
+  if (!x || !out || rows <= 0 || N <= 0 || (rows + 3) / 4 > (int64_t)INT32_MAX) return -20;
+  k_tr_row_sum<<<(unsigned)((rows + 3) / 4), 256, 0, (hipStream_t)stream>>>(x, out, rows, N);
+  return launched();
+}

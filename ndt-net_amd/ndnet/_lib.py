@@ -99,7 +99,7 @@ def lib() -> ctypes.CDLL:
             fn = getattr(_lib, name)
             fn.restype = res
             fn.argtypes = args
-        for name, (res, args) in POINTNET_EXPORTS.items():
+        for name, (res, args) in {**POINTNET_EXPORTS, **TRAIN_EXPORTS}.items():
             fn = getattr(_lib, name)
             fn.restype = res
             fn.argtypes = args
@@ -118,6 +118,20 @@ POINTNET_EXPORTS: dict = {
     "ndnet_pn_fc_run": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "ndnet_pn_fc_mfma_run": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "ndnet_pn_head3_run": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+}
+
+
+_I64 = ctypes.c_int64
+
+# include/ndnet_train.h
+TRAIN_EXPORTS: dict = {
+    "ndnet_tr_gemm": (_I, [_P, _P, _P, _P, _I64, _I, _I, _I, _I64, _I64, _I64, _I64, _I64, _I64, _I, _I, _I, _I, _I,
+                           _I, _P]),
+    "ndnet_tr_sum_parts": (_I, [_P, _P, _I64, _I, _P]),
+    "ndnet_tr_bn_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, ctypes.c_float, ctypes.c_float, _I, _P]),
+    "ndnet_tr_bn_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),  # dz y mean invstd g b
+    "ndnet_tr_chan_sum": (_I, [_P, _P, _I, _I, _I, _P]),
+    "ndnet_tr_row_sum": (_I, [_P, _P, _I64, _I, _P]),
 }
 
 

@@ -15,20 +15,43 @@ Two forward paths:
     lib/libndnet_amd.so (``ndnet.models.pointnet_hip``): BatchNorm folded into
     the 1x1 convolutions, MFMA GEMMs over (points x channels), global
     max-pool fused into the producing GEMM.
-  * anything else (training, eval-mode autograd, CPU) -> the PyTorch
-    composition below, which is also the fp32 reference the kernels are
-    tested against.
+  * train mode on the GPU -> every Conv1d(k=1) + BatchNorm1d (batch
+    statistics) [+ ReLU] block forward and backward on the train kernels of
+    lib/libndnet_amd.so (``ndnet.models.train_hip``, include/ndnet_train.h);
+    the max-pools, transforms, TNet FC heads and log-softmax stay torch ops.
+    ``NDNET_TRAIN_PATH=torch`` selects the torch composition instead (A/B).
+  * anything else (eval-mode autograd, CPU) -> the PyTorch composition below,
+    which is also the fp32 reference the kernels are tested against.
 """
 from __future__ import annotations
 
+import os
 from enum import Enum
 
 import torch
 from torch import nn
 
+_TRAIN_TORCH = os.environ.get("NDNET_TRAIN_PATH", "hip").lower() == "torch"
+
 
 def _conv(cin: int, cout: int) -> nn.Conv1d:
     return nn.Conv1d(cin, cout, 1)
+
+
+def _hip_train(conv: nn.Conv1d, bn, x: torch.Tensor) -> bool:
+    return x.is_cuda and conv.training and (bn is None or bn.training) and not _TRAIN_TORCH
+
+
+def _block(conv: nn.Conv1d, bn, x: torch.Tensor, relu: bool) -> torch.Tensor:
+    """``relu(bn(conv(x)))`` (bn / relu optional): on the HIP train kernels in
+    train mode on the GPU (ndnet.models.train_hip), else torch ops."""
+    if _hip_train(conv, bn, x):
+        from . import train_hip
+        return train_hip.conv_bn_act(conv, bn, x, relu)
+    x = conv(x)
+    if bn is not None:
+        x = bn(x)
+    return torch.relu(x) if relu else x
 
 
 class TNet(nn.Module):
@@ -46,7 +69,7 @@ class TNet(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         # pointwise MLP with BN+ReLU, max over points, FC head, + identity
         for conv, bn in ((self.conv1, self.bn1), (self.conv2, self.bn2), (self.conv3, self.bn3)):
-            x = self.relu(bn(conv(x)))
+            x = _block(conv, bn, x, True)
         g = x.amax(dim=2)
         g = self.relu(self.bn4(self.fc1(g)))
         g = self.relu(self.bn5(self.fc2(g)))
@@ -89,12 +112,12 @@ class NDTNet(nn.Module):
         xyz = torch.bmm(t, xyz)                           # t . p
         cov = torch.matmul(t.unsqueeze(1), extra.reshape(B, N, d, d)).reshape(B, N, d * d)  # t . C (left only)
         x = torch.cat((xyz.transpose(1, 2), cov), dim=2).transpose(1, 2)  # [B,12,N]
-        x = self.bn1(self.conv1(x))                       # no ReLU (reference ndtnet.py:149)
+        x = _block(self.conv1, self.bn1, x, False)        # no ReLU (reference ndtnet.py:149)
         t2 = self.t2(x)                                   # [B,64,64]
         x = torch.bmm(x.transpose(1, 2), t2).transpose(1, 2)  # x^T t2
         x_t2 = x
-        x = self.bn2(self.conv2(x))
-        x = self.bn3(self.conv3(x))
+        x = _block(self.conv2, self.bn2, x, False)
+        x = _block(self.conv3, self.bn3, x, False)
         return x, x_t2
 
 
@@ -131,11 +154,23 @@ class NDTNetSegmentation(nn.Module):
 
     def forward_torch(self, points: torch.Tensor, covariances: torch.Tensor) -> torch.Tensor:
         x, x_t2 = self.feature_extractor(points, covariances)
-        g = x.amax(dim=2, keepdim=True).expand(-1, -1, x_t2.shape[2])
-        x = torch.cat((x_t2, g), dim=1)
-        for conv, bn in ((self.conv1, self.bn1), (self.conv2, self.bn2), (self.conv3, self.bn3)):
-            x = torch.relu(bn(conv(x)))
-        x = torch.nn.functional.log_softmax(self.conv4(x), dim=1)
+        blocks = ((self.conv1, self.bn1), (self.conv2, self.bn2), (self.conv3, self.bn3))
+        if _hip_train(self.conv1, self.bn1, x_t2):
+            # conv1 over cat(x_t2, g broadcast over the points) (ndtnet.py:230-234) as a 64-channel
+            # conv with the global feature's term a per-cloud bias: W[:, 64:] g + b -- 1/13 of the
+            # layer's FLOPs forward and backward; the gradient reaches g through the bias
+            from . import train_hip
+            c = x_t2.shape[1]
+            w = self.conv1.weight
+            cb = torch.addmm(self.conv1.bias, x.amax(dim=2), w[:, c:, 0].t())
+            x = train_hip.conv_bn_act(self.conv1, self.bn1, x_t2, True, weight=w[:, :c], cloud_bias=cb)
+            blocks = blocks[1:]
+        else:
+            g = x.amax(dim=2, keepdim=True).expand(-1, -1, x_t2.shape[2])
+            x = torch.cat((x_t2, g), dim=1)
+        for conv, bn in blocks:
+            x = _block(conv, bn, x, True)
+        x = torch.nn.functional.log_softmax(_block(self.conv4, None, x, False), dim=1)
         return x.transpose(2, 1)
 
     def _needs_autograd(self, points: torch.Tensor, covariances: torch.Tensor) -> bool:

@@ -1,0 +1,219 @@
+"""Train-mode Conv1d(k=1) + BatchNorm1d [+ ReLU] blocks on the HIP kernels of
+include/ndnet_train.h (csrc/train_kernels.hip), as torch autograd Functions.
+
+The reference's training step (tools/train.py:67-81) runs every per-point
+block of NDTNetSegmentation -- ndnet/models/ndtnet.py:48-50 (TNet convs),
+:148-152 (NDTNet convs), :233-239 (segmentation head) -- as torch
+Conv1d -> BatchNorm1d (batch statistics) -> ReLU, and autograd runs their
+backward.  ``conv_bn_act`` is that block with the same arguments, results
+(fp32, within summation order) and side effects (running statistics updated
+with the module's momentum and the unbiased variance, ``num_batches_tracked``
+incremented), computed by:
+
+  forward   ndnet_tr_gemm (y = W x + b)  ->  ndnet_tr_bn_fwd
+  backward  ndnet_tr_bn_bwd (ReLU mask, BN backward, conv bias gradient)
+            -> ndnet_tr_gemm (dx = W^T dy)  +  ndnet_tr_gemm (split-K partials
+            of dW = sum dy x^T)  ->  ndnet_tr_sum_parts
+
+Everything launches on torch's current stream and allocates through torch,
+so a training step that uses these blocks is capturable as one HIP graph
+(ndnet.training.GraphedTrainStep).  No fallback: the library must load.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .. import _lib
+
+# split-K of the weight gradient: aim for this many workgroups per launch, with
+# at most this many partial products (the partials are written, then re-read
+# by ndnet_tr_sum_parts: round 3 measured 1024 / 256+ parts at 130 MB a step)
+_DW_TARGET_WGS = 256
+_DW_MAX_PARTS = 32
+_KSTEP = 16  # the GEMM's k-step
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _check_f32(*ts: torch.Tensor) -> None:
+    for t in ts:
+        if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous():
+            raise ValueError("train kernels take contiguous float32 cuda tensors")
+
+
+def gemm(A, B, C, bias, M, N, K, lda, ldb, ldc, sAz, sBz, sCz, batch, a_kmajor, b_kmajor,
+         nchunks: int = 1, kchunk: Optional[int] = None, sbias: int = 0, clouds_per_part: int = 1) -> None:
+    """ndnet_tr_gemm (include/ndnet_train.h): C[z] = sum over the part's clouds
+    of A[c] B[c] (+ bias)."""
+    rc = _lib.lib().ndnet_tr_gemm(_ptr(A), _ptr(B), _ptr(C), _ptr(bias), sbias, M, N, K, lda, ldb, ldc, sAz, sBz, sCz,
+                                  batch, clouds_per_part, int(a_kmajor), int(b_kmajor), nchunks,
+                                  K if kchunk is None else kchunk, _stream())
+    _lib.check(rc, "ndnet_tr_gemm")
+
+
+def conv_forward(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor],
+                 per_cloud_bias: bool = False) -> torch.Tensor:
+    """y[b] = W x[b] + bias (bias [Cout], or [B,Cout] per cloud): x [B,Cin,N],
+    W [Cout,Cin] -> [B,Cout,N]."""
+    Bn, Cin, N = x.shape
+    Cout = w.shape[0]
+    y = torch.empty(Bn, Cout, N, device=x.device, dtype=torch.float32)
+    gemm(w, x, y, b, Cout, N, Cin, Cin, N, N, 0, Cin * N, Cout * N, Bn, True, False,
+         sbias=Cout if per_cloud_bias else 0)
+    return y
+
+
+def conv_input_grad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """dx[b] = W^T dy[b]: dy [B,Cout,N] -> [B,Cin,N]."""
+    Bn, Cout, N = dy.shape
+    Cin = w.shape[1]
+    dx = torch.empty(Bn, Cin, N, device=dy.device, dtype=torch.float32)
+    gemm(w, dy, dx, None, Cin, N, Cout, Cin, N, N, 0, Cout * N, Cin * N, Bn, False, False)
+    return dx
+
+
+def dw_split(Bn: int, Cout: int, Cin: int, N: int):
+    """(clouds_per_part, nchunks, kchunk) of the weight gradient's split-K:
+    about _DW_TARGET_WGS workgroups but at most _DW_MAX_PARTS partial
+    products (each part then sums >= 1/32 of the batch's points) -- several
+    clouds per part when the output has many tiles, several point chunks per
+    cloud when it has few."""
+    tiles = -(-Cout // 64) * -(-Cin // 64)
+    parts = max(1, min(_DW_MAX_PARTS, -(-_DW_TARGET_WGS // tiles), Bn * -(-N // 64)))
+    if parts <= Bn:
+        return -(-Bn // parts), 1, N
+    want = -(-parts // Bn)
+    kchunk = -(-N // want)
+    kchunk = -(-kchunk // _KSTEP) * _KSTEP
+    return 1, -(-N // kchunk), kchunk
+
+
+def conv_weight_grad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """dW = sum over clouds and points of dy x^T: [Cout,Cin]."""
+    Bn, Cout, N = dy.shape
+    Cin = x.shape[1]
+    cpz, nch, kchunk = dw_split(Bn, Cout, Cin, N)
+    parts = -(-Bn // cpz) * nch
+    dw = torch.empty(Cout, Cin, device=dy.device, dtype=torch.float32)
+    out = dw if parts == 1 else torch.empty(parts, Cout, Cin, device=dy.device, dtype=torch.float32)
+    gemm(dy, x, out, None, Cout, Cin, N, N, N, Cin, Cout * N, Cin * N, Cout * Cin, Bn, True, True, nch, kchunk,
+         clouds_per_part=cpz)
+    if parts > 1:
+        _lib.check(_lib.lib().ndnet_tr_sum_parts(out.data_ptr(), dw.data_ptr(), Cout * Cin, parts, _stream()),
+                   "ndnet_tr_sum_parts")
+    return dw
+
+
+def row_sum(x: torch.Tensor) -> torch.Tensor:
+    """[B,C,N] -> [B,C]: the sum over points (a per-cloud bias gradient)."""
+    Bn, C, N = x.shape
+    out = torch.empty(Bn, C, device=x.device, dtype=torch.float32)
+    _lib.check(_lib.lib().ndnet_tr_row_sum(x.data_ptr(), out.data_ptr(), Bn * C, N, _stream()), "ndnet_tr_row_sum")
+    return out
+
+
+def chan_sum(x: torch.Tensor) -> torch.Tensor:
+    Bn, C, N = x.shape
+    out = torch.empty(C, device=x.device, dtype=torch.float32)
+    _lib.check(_lib.lib().ndnet_tr_chan_sum(x.data_ptr(), out.data_ptr(), Bn, C, N, _stream()), "ndnet_tr_chan_sum")
+    return out
+
+
+class _ConvBNAct(torch.autograd.Function):
+    """Conv1d(k=1) [-> BatchNorm1d (batch statistics)] [-> ReLU]; the bias is
+    either the conv's ``b`` [Cout] or a per-cloud ``cb`` [B,Cout]."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, cb, gamma, beta, run_mean, run_var, eps, momentum, relu):
+        x = x.contiguous()
+        w2 = w.detach().reshape(w.shape[0], -1).contiguous()
+        _check_f32(x, w2)
+        Bn, Cin, N = x.shape
+        if w2.shape[1] != Cin:
+            raise ValueError(f"conv expects {w2.shape[1]} input channels, got {Cin}")
+        if cb is not None:
+            if b is not None or tuple(cb.shape) != (Bn, w2.shape[0]):
+                raise ValueError("a per-cloud bias [B,Cout] replaces the conv bias")
+            bias = cb.detach().contiguous()
+        else:
+            bias = None if b is None else b.detach().contiguous()
+        y = conv_forward(x, w2, bias, per_cloud_bias=cb is not None)
+        ctx.w_shape, ctx.has_bias, ctx.bn, ctx.relu = w.shape, b is not None, gamma is not None, bool(relu)
+        ctx.has_cb = cb is not None
+        if gamma is None:
+            if relu:
+                raise ValueError("ReLU without BatchNorm is not a block of this model")
+            ctx.save_for_backward(x, w2)
+            return y
+        C = y.shape[1]
+        z = torch.empty_like(y)
+        mean = torch.empty(C, device=y.device, dtype=torch.float32)
+        invstd = torch.empty_like(mean)
+        g, bt = gamma.detach().contiguous(), beta.detach().contiguous()
+        rc = _lib.lib().ndnet_tr_bn_fwd(y.data_ptr(), z.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                                        _ptr(run_mean), _ptr(run_var), g.data_ptr(), bt.data_ptr(), Bn, C, N,
+                                        float(eps), float(momentum), int(relu), _stream())
+        _lib.check(rc, "ndnet_tr_bn_fwd")
+        ctx.save_for_backward(x, w2, y, mean, invstd, g, bt)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        dz = dz.contiguous()
+        need = ctx.needs_input_grad
+        dgamma = dbeta = None
+        if ctx.bn:
+            x, w2, y, mean, invstd, g, bt = ctx.saved_tensors
+            Bn, C, N = y.shape
+            dy = torch.empty_like(y)
+            dgamma = torch.empty(C, device=y.device, dtype=torch.float32)
+            dbeta = torch.empty_like(dgamma)
+            dbias = torch.empty_like(dgamma)
+            rc = _lib.lib().ndnet_tr_bn_bwd(dz.data_ptr(), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                                            g.data_ptr(), bt.data_ptr(), dy.data_ptr(), dgamma.data_ptr(),
+                                            dbeta.data_ptr(), dbias.data_ptr(), Bn, C, N, int(ctx.relu), _stream())
+            _lib.check(rc, "ndnet_tr_bn_bwd")
+        else:
+            x, w2 = ctx.saved_tensors
+            dy = dz
+            dbias = chan_sum(dy) if ctx.has_bias and need[2] else None
+        if ctx.bn and not ctx.has_bias:
+            dbias = None
+        dx = conv_input_grad(dy, w2) if need[0] else None
+        dw = conv_weight_grad(dy, x).view(ctx.w_shape) if need[1] else None
+        dcb = row_sum(dy) if ctx.has_cb and need[3] else None
+        return (dx, dw, dbias if ctx.has_bias and need[2] else None, dcb,
+                dgamma if need[4] else None, dbeta if need[5] else None, None, None, None, None, None)
+
+
+def conv_bn_act(conv: torch.nn.Conv1d, bn: Optional[torch.nn.BatchNorm1d], x: torch.Tensor,
+                relu: bool, weight: Optional[torch.Tensor] = None,
+                cloud_bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``relu(bn(conv(x)))`` (or without relu / bn) in training mode on the HIP
+    kernels; x [B,Cin,N] float32 on the GPU.  ``weight`` (a view of
+    conv.weight, e.g. its first Cin input channels) and ``cloud_bias`` [B,Cout]
+    (replacing conv.bias) run the block on part of a concatenated input whose
+    rest is constant over the points (the segmentation head)."""
+    if conv.kernel_size != (1,) or conv.groups != 1 or conv.stride != (1,) or conv.padding != (0,):
+        raise ValueError("only pointwise Conv1d(k=1) blocks run on the train kernels")
+    w = conv.weight if weight is None else weight
+    b = conv.bias if cloud_bias is None else None
+    if bn is None:
+        return _ConvBNAct.apply(x, w, b, cloud_bias, None, None, None, None, 0.0, 0.0, False)
+    if not bn.affine or bn.momentum is None:
+        raise ValueError("the train kernels take affine BatchNorm1d with a fixed momentum (the model's defaults)")
+    track = bn.track_running_stats and bn.running_mean is not None
+    out = _ConvBNAct.apply(x, w, b, cloud_bias, bn.weight, bn.bias,
+                           bn.running_mean if track else None, bn.running_var if track else None,
+                           bn.eps, bn.momentum, relu)
+    if track:
+        bn.num_batches_tracked.add_(1)
+    return out

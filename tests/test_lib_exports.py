@@ -27,7 +27,7 @@ def test_library_exports_header():
 
 def test_python_bindings_cover_header():
     from ndnet import _lib
-    assert set(declared_symbols()) <= set(_lib.EXPORTS) | set(_lib.POINTNET_EXPORTS)
+    assert set(declared_symbols()) <= set(_lib.EXPORTS) | set(_lib.POINTNET_EXPORTS) | set(_lib.TRAIN_EXPORTS)
 
 
 def test_code_object_targets_gfx950():

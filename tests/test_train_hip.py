@@ -1,0 +1,232 @@
+"""Train-mode kernels (include/ndnet_train.h) against torch fp32.
+
+The reference trains with torch autograd through Conv1d(k=1) + BatchNorm1d
+(batch statistics) + ReLU blocks (ndnet/models/ndtnet.py:48-50, 148-152,
+233-239; tools/train.py:67-81).  These tests compare the HIP GEMM in each of
+its operand layouts with a float64 product, each block's forward, running
+statistics and backward with the torch modules, and the whole
+NDTNetSegmentation train forward + backward with the torch composition
+(forward within 1e-4, as the round-2 verdict asked)."""
+import copy
+import math
+
+import pytest
+import torch
+
+from conftest import gpu_available
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _need_gpu():
+    if not gpu_available():
+        pytest.skip("no GPU")
+
+
+def _close(a, b, rel, what=""):  # relative Frobenius error
+    a, b = a.double(), b.double()
+    err = (a - b).norm().item()
+    ref = b.norm().item()
+    assert err <= rel * max(ref, 1e-30), f"{what}: |err| {err:.3e} vs |ref| {ref:.3e}"
+
+
+@pytest.mark.parametrize("case", [
+    # (batch, M, N, K, a_kmajor, b_kmajor, nchunks, kchunk, clouds per part)
+    (3, 64, 1000, 12, True, False, 1, None, 1),     # conv forward, K = 12
+    (2, 64, 1000, 3, True, False, 1, None, 1),      # conv forward, K = 3
+    (2, 29, 1000, 128, True, False, 1, None, 1),    # 29 classes
+    (2, 1024, 130, 128, True, False, 1, None, 1),
+    (2, 128, 1000, 1024, False, False, 1, None, 1),  # input gradient
+    (4, 64, 12, 1000, True, True, 4, 256, 1),       # weight gradient, split-K over points
+    (2, 1024, 128, 1000, True, True, 2, 512, 1),
+    (5, 1024, 128, 1000, True, True, 1, 1000, 2),   # split-K over cloud groups (2 + 2 + 1)
+    (6, 96, 40, 300, True, True, 3, 112, 3),        # both
+])
+def test_gemm_layouts(case):
+    from ndnet.models import train_hip
+    Bn, M, N, K, ak, bk, nch, kchunk, cpz = case
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(M * 7 + N + K)
+    A = torch.randn(Bn, M, K, device=dev, generator=g)   # logical A[z] (M x K)
+    B = torch.randn(Bn, K, N, device=dev, generator=g)   # logical B[z] (K x N)
+    bias = torch.randn(M, device=dev, generator=g) if nch == 1 and cpz == 1 else None
+    As = A.contiguous() if ak else A.transpose(1, 2).contiguous()
+    Bs = B.transpose(1, 2).contiguous() if bk else B.contiguous()
+    lda = K if ak else M
+    ldb = K if bk else N
+    groups = -(-Bn // cpz)
+    C = torch.full((groups * nch, M, N), float("nan"), device=dev)
+    train_hip.gemm(As, Bs, C, bias, M, N, K, lda, ldb, N, M * K, K * N, M * N, Bn, ak, bk, nch, kchunk,
+                   clouds_per_part=cpz)
+    torch.cuda.synchronize()
+    ref = torch.bmm(A.double(), B.double())
+    if bias is not None:
+        ref = ref + bias.double()[None, :, None]
+    if cpz > 1:  # part zg holds the sum over its clouds
+        ref = torch.stack([ref[i * cpz:(i + 1) * cpz].sum(0) for i in range(groups)])
+    got = C.view(groups, nch, M, N).double().sum(1)
+    if nch > 1 or cpz > 1:  # and ndnet_tr_sum_parts sums the parts in order
+        tot = torch.empty(M, N, device=dev)
+        from ndnet import _lib
+        _lib.check(_lib.lib().ndnet_tr_sum_parts(C.data_ptr(), tot.data_ptr(), M * N, groups * nch,
+                                                 torch.cuda.current_stream().cuda_stream), "sum_parts")
+        torch.cuda.synchronize()
+        _close(tot, ref.sum(0), 2e-6, "sum_parts")
+    assert torch.isfinite(got).all()
+    _close(got, ref, 2e-6, "gemm")
+
+
+def _pair(cin, cout, bn, seed):
+    torch.manual_seed(seed)
+    conv = torch.nn.Conv1d(cin, cout, 1).cuda()
+    norm = None
+    if bn:
+        norm = torch.nn.BatchNorm1d(cout).cuda()
+        with torch.no_grad():
+            norm.weight.uniform_(0.5, 1.5)
+            norm.bias.uniform_(-0.3, 0.3)
+            norm.running_mean.uniform_(-1, 1)
+            norm.running_var.uniform_(0.5, 2)
+    return conv, norm
+
+
+@pytest.mark.parametrize("cin,cout,bn,relu,B,N", [
+    (12, 64, True, False, 4, 1000),    # NDTNet conv1 + bn1 (no ReLU)
+    (3, 64, True, True, 4, 1000),      # TNet(3) conv1
+    (128, 1024, True, True, 16, 1000),  # TNet conv3, the bench's batch (16000 values per channel)
+    (64, 128, True, False, 20, 1000),  # 20000 values per channel: the uncached BN path
+    (128, 29, False, False, 4, 1000),  # seg conv4 (no BN)
+    (832, 512, True, True, 2, 500),
+])
+def test_block_matches_torch(cin, cout, bn, relu, B, N):
+    from ndnet.models import train_hip
+    conv, norm = _pair(cin, cout, bn, cin + cout)
+    conv2, norm2 = copy.deepcopy(conv), copy.deepcopy(norm)
+    x = (torch.randn(B, cin, N, device="cuda") * 2 + 0.5).requires_grad_(True)
+    x2 = x.detach().clone().requires_grad_(True)
+    out = train_hip.conv_bn_act(conv, norm, x, relu)
+    ref = conv2(x2)
+    if norm2 is not None:
+        ref = norm2(ref)
+    if relu:
+        ref = torch.relu(ref)
+    torch.testing.assert_close(out, ref, rtol=0, atol=1e-4)
+    if norm is not None:
+        torch.testing.assert_close(norm.running_mean, norm2.running_mean, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(norm.running_var, norm2.running_var, rtol=1e-5, atol=1e-5)
+        assert int(norm.num_batches_tracked) == int(norm2.num_batches_tracked) == 1
+    up = torch.randn_like(ref)
+    out.backward(up)
+    ref.backward(up)
+    _close(x.grad, x2.grad, 1e-4, "dx")
+    _close(conv.weight.grad, conv2.weight.grad, 1e-4, "dW")
+    if norm is not None:
+        _close(norm.weight.grad, norm2.weight.grad, 1e-4, "dgamma")
+        _close(norm.bias.grad, norm2.bias.grad, 1e-4, "dbeta")
+        # the conv bias gradient is sum(dy) ~ 0 under BN: absolute check
+        assert (conv.bias.grad - conv2.bias.grad).abs().max().item() <= 1e-3
+    else:
+        _close(conv.bias.grad, conv2.bias.grad, 1e-4, "db")
+
+
+def test_block_input_without_grad_skips_dx():
+    from ndnet.models import train_hip
+    conv, norm = _pair(3, 64, True, 5)
+    x = torch.randn(2, 3, 700, device="cuda")
+    out = train_hip.conv_bn_act(conv, norm, x, True)
+    out.sum().backward()
+    assert x.grad is None and conv.weight.grad is not None
+
+
+def _nds(B, k, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    pts = torch.randn(B, k, 3, device="cuda", generator=g) * 5
+    a = torch.randn(B, k, 3, 3, device="cuda", generator=g) * 0.3
+    cov = (a @ a.transpose(-1, -2)).reshape(B, k, 9)
+    return pts, cov
+
+
+def test_segmentation_train_forward_backward_matches_torch(monkeypatch):
+    """The whole train-mode forward (every conv block on the HIP kernels) vs
+    the torch composition: log-probs within 1e-4, running statistics, and
+    every parameter gradient of one backward."""
+    from ndnet.models import ndtnet, train_hip
+    torch.manual_seed(3)
+    model = ndtnet.NDTNetSegmentation(num_classes=28, feature_dim=768).cuda().train()
+    ref_model = copy.deepcopy(model)
+    pts, cov = _nds(4, 1000, 11)
+    calls = []
+    real = train_hip.conv_bn_act
+
+    def spy(*a, **k):
+        calls.append(1)
+        return real(*a, **k)
+
+    monkeypatch.setattr(train_hip, "conv_bn_act", spy)
+    out = model(pts, cov)
+    assert len(calls) == 13  # 3 + 3 TNet blocks, 3 NDTNet, 3 seg head + conv4
+    monkeypatch.setattr(ndtnet, "_TRAIN_TORCH", True)
+    f64_model = copy.deepcopy(ref_model).double()
+    ref = ref_model(pts, cov)
+    assert len(calls) == 13
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4)
+    # and as close to a float64 evaluation as torch's own fp32 forward is
+    f64 = f64_model(pts.double(), cov.double())
+    e_hip = (out.double() - f64).abs().max().item()
+    e_torch = (ref.double() - f64).abs().max().item()
+    print(f"max |log-prob error| vs float64: HIP {e_hip:.3e}, torch fp32 {e_torch:.3e}")
+    assert e_hip <= 2 * e_torch + 1e-6, (e_hip, e_torch)
+    for (n, b1), b2 in zip(model.named_buffers(), ref_model.buffers()):
+        if b1.dtype.is_floating_point:
+            torch.testing.assert_close(b1, b2, rtol=1e-4, atol=1e-5, msg=n)
+        else:
+            assert torch.equal(b1, b2), n
+    gt = torch.nn.functional.one_hot(torch.randint(0, 29, (4, 1000), device="cuda"), 29).float()
+    from ndnet.training import segmentation_loss
+    segmentation_loss(out, gt).backward()
+    segmentation_loss(ref, gt).backward()
+    segmentation_loss(f64, gt.double()).backward()
+    # gradients against the float64 backward: the HIP path's error next to torch fp32's own
+    # (random init + batch-statistics BN make the deep gradients ill-conditioned in fp32 for
+    # both, so the bound is relative to torch's error, not an absolute tolerance)
+    worst = 0.0
+    for (n, p1), p2, p3 in zip(model.named_parameters(), ref_model.parameters(), f64_model.parameters()):
+        assert p1.grad is not None, n
+        ref_norm = p3.grad.norm().item()
+        e_h = (p1.grad.double() - p3.grad).norm().item() / max(ref_norm, 1e-30)
+        e_t = (p2.grad.double() - p3.grad).norm().item() / max(ref_norm, 1e-30)
+        print(f"{n:45s} rel err vs float64: HIP {e_h:.2e} torch fp32 {e_t:.2e}")
+        # conv biases ahead of a BatchNorm have gradient sum(dy) ~ 0: rounding only
+        if n.endswith("bias") and "conv" in n and not n.startswith("conv4"):
+            continue
+        assert e_h <= max(3 * e_t, 1e-4), (n, e_h, e_t)
+        worst = max(worst, e_h)
+    print(f"worst relative gradient error (HIP vs float64): {worst:.2e}")
+    assert math.isfinite(out.sum().item())
+
+
+def test_block_with_cloud_bias_matches_concat():
+    """The segmentation head's conv1 over cat(x_t2, g broadcast) (ndtnet.py:230-234)
+    as a 64-channel block plus the per-cloud bias W[:, 64:] g + b."""
+    from ndnet.models import train_hip
+    conv, norm = _pair(832, 512, True, 9)
+    conv2, norm2 = copy.deepcopy(conv), copy.deepcopy(norm)
+    B, N = 3, 900
+    xt = torch.randn(B, 64, N, device="cuda").requires_grad_(True)
+    g = (torch.randn(B, 768, device="cuda") + 1).requires_grad_(True)
+    xt2, g2 = xt.detach().clone().requires_grad_(True), g.detach().clone().requires_grad_(True)
+    w = conv.weight
+    cb = torch.addmm(conv.bias, g, w[:, 64:, 0].t())
+    out = train_hip.conv_bn_act(conv, norm, xt, True, weight=w[:, :64], cloud_bias=cb)
+    ref = torch.relu(norm2(conv2(torch.cat((xt2, g2[:, :, None].expand(-1, -1, N)), dim=1))))
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4)
+    up = torch.randn_like(ref)
+    out.backward(up)
+    ref.backward(up)
+    _close(xt.grad, xt2.grad, 1e-4, "dx_t2")
+    _close(g.grad, g2.grad, 1e-4, "dg")
+    _close(conv.weight.grad, conv2.weight.grad, 1e-4, "dW")
+    _close(norm.weight.grad, norm2.weight.grad, 1e-4, "dgamma")
+    _close(norm.bias.grad, norm2.bias.grad, 1e-4, "dbeta")
+    assert (conv.bias.grad - conv2.bias.grad).abs().max().item() <= 1e-3
