@@ -56,20 +56,27 @@ int ndnet_tr_sum_parts(const float *part, float *out, int64_t count, int nparts,
  * B * N values (summed in double, two passes), invstd = 1 / sqrt(var + eps),
  * z = (y - mean) * invstd * gamma + beta, then ReLU if `relu`.  Saves mean /
  * invstd [C] for the backward and updates running_mean / running_var (may be
- * NULL) with `momentum` and the unbiased variance, as torch does. */
+ * NULL) with `momentum` and the unbiased variance, as torch does.
+ * Pool mode (pool != NULL, B <= 64): z is not written; instead pool[b][c] =
+ * max over the points of cloud b of z, pool_idx[b][c] = its first point --
+ * the block followed by ``amax(dim=2)`` (TNet conv3, ndtnet.py:50-51; NDTNet
+ * conv3 into the segmentation head's global feature, :152, :231), without the
+ * [B][C][N] activation. */
 int ndnet_tr_bn_fwd(const float *y, float *z, float *mean, float *invstd, float *running_mean,
                     float *running_var, const float *gamma, const float *beta, int B, int C, int N,
-                    float eps, float momentum, int relu, void *stream);
+                    float eps, float momentum, int relu, float *pool, int32_t *pool_idx, void *stream);
 
 /* Its backward, one workgroup per channel: g = dz, masked by ReLU where the
  * forward's output (recomputed from y, mean, invstd, gamma, beta with the
  * forward's exact roundings) was not > 0; xhat = (y - mean) * invstd,
  * dgamma = sum g xhat, dbeta = sum g,
  * dy = gamma invstd (g - dbeta / M - xhat dgamma / M), dbias = sum dy (the
- * gradient of the convolution's bias).  dgamma / dbeta / dbias may be NULL. */
+ * gradient of the convolution's bias).  dgamma / dbeta / dbias may be NULL.
+ * Pool mode (pool_idx != NULL): dz is [B][C], the gradient of the pooled
+ * output, which reaches only point pool_idx[b][c] of each cloud. */
 int ndnet_tr_bn_bwd(const float *dz, const float *y, const float *mean, const float *invstd, const float *gamma,
                     const float *beta, float *dy, float *dgamma, float *dbeta, float *dbias, int B, int C, int N,
-                    int relu, void *stream);
+                    int relu, const int32_t *pool_idx, void *stream);
 
 /* out[c] = sum over b, n of x[b][c][n] (a bias gradient), one workgroup per channel. */
 int ndnet_tr_chan_sum(const float *x, float *out, int B, int C, int N, void *stream);

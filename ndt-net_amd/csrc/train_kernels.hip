@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -39,66 +40,72 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kTM = 64, kTN = 64, kTK = 16;
-constexpr int kPitch = 64 + 16;  // LDS row pitch (floats): the 4 lane quads of an A/B read hit disjoint banks
-constexpr int kGemmThreads = 256;
 
 constexpr int kBnThreads = 512;
-constexpr int kBnCache = 32;  // values per thread held in registers: B * N <= 16384 reads the channel once
+constexpr int kBnCache = 32;
+constexpr int kPoolMaxB = 64;  // pool mode: clouds per launch  // values per thread held in registers: B * N <= 16384 reads the channel once
 
-// global -> registers: this thread's 4 elements of the (k0 .. k0 + 16) x 64 tile.
-// A contiguous along k (a_kmajor): lanes walk k (16 per row), else along m.
-template <bool KMAJOR>
+// global -> registers: this thread's 4 elements of the (k0 .. k0 + 16) x TM tile
+// (TM * 4 threads).  P contiguous along k (KMAJOR): lanes walk k (16 per row),
+// else along the row index.
+template <int TM, bool KMAJOR>
 __device__ __forceinline__ void tile_load(const float* __restrict__ P, int64_t ld, int r0, int k0, int R, int kend,
                                           float (&v)[4]) {
   const int t = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < 4; i++) {
-    const int kk = KMAJOR ? (t & 15) : (t >> 6) + 4 * i;
-    const int rr = KMAJOR ? (t >> 4) + 16 * i : (t & 63);
+    const int kk = KMAJOR ? (t & 15) : t / TM + 4 * i;
+    const int rr = KMAJOR ? (t >> 4) + (TM / 4) * i : t % TM;
     const int gr = r0 + rr, gk = k0 + kk;
     v[i] = (gr < R && gk < kend) ? (KMAJOR ? P[(int64_t)gr * ld + gk] : P[(int64_t)gk * ld + gr]) : 0.0f;
   }
 }
 
 // registers -> LDS tile [k][row] (row contiguous: one MFMA operand read per lane)
-template <bool KMAJOR>
+template <int TM, bool KMAJOR>
 __device__ __forceinline__ void tile_store(float* __restrict__ s, const float (&v)[4]) {
   const int t = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < 4; i++) {
-    const int kk = KMAJOR ? (t & 15) : (t >> 6) + 4 * i;
-    const int rr = KMAJOR ? (t >> 4) + 16 * i : (t & 63);
-    s[kk * kPitch + rr] = v[i];
+    const int kk = KMAJOR ? (t & 15) : t / TM + 4 * i;
+    const int rr = KMAJOR ? (t >> 4) + (TM / 4) * i : t % TM;
+    s[kk * (TM + 16) + rr] = v[i];
   }
 }
 
-template <bool AK, bool BK>
-__global__ __launch_bounds__(kGemmThreads) void k_tr_gemm(const float* __restrict__ A, const float* __restrict__ B,
-                                                          float* __restrict__ C, const float* __restrict__ bias,
-                                                          int64_t sbias, int M, int N, int K, int64_t lda,
-                                                          int64_t ldb, int64_t ldc, int64_t sAz, int64_t sBz,
-                                                          int64_t sCz, int batch, int cpz, int nchunks, int kchunk) {
-  __shared__ float sA[2][kTK * kPitch];
-  __shared__ float sB[2][kTK * kPitch];
+// TM x TM output tile per workgroup of TM / 8 waves: TM = 64 -> 2 x 2 waves of
+// 32 x 32 (four accumulator sets), TM = 128 -> 2 x 4 waves of 64 x 32 (two sets,
+// twice the MFMAs per LDS operand read; for the wide layers)
+template <int TM, bool AK, bool BK>
+__global__ __launch_bounds__(TM * 4) void k_tr_gemm(const float* __restrict__ A, const float* __restrict__ B,
+                                                    float* __restrict__ C, const float* __restrict__ bias,
+                                                    int64_t sbias, int M, int N, int K, int64_t lda, int64_t ldb,
+                                                    int64_t ldc, int64_t sAz, int64_t sBz, int64_t sCz, int batch,
+                                                    int cpz, int nchunks, int kchunk) {
+  constexpr int P = TM + 16;              // LDS row pitch: the 4 lane quads of an operand read hit disjoint banks
+  constexpr int WN = 2 * (TM / 64);       // waves along N
+  constexpr int IM = TM / 32;             // 16-row blocks per wave (wave tile TM / 2 rows x 32 columns)
+  constexpr int KS = TM == 64 ? 4 : 2;    // accumulator sets (k-quad ks uses set ks % KS)
+  __shared__ float sA[2][kTK * P];
+  __shared__ float sB[2][kTK * P];
   const int z = blockIdx.z, zg = z / nchunks, zc = z - zg * nchunks;
   const int cl0 = zg * cpz, ncl = min(cpz, batch - cl0);  // this part's clouds
   C += z * sCz;
   if (bias) bias += cl0 * sbias;
   const int kbeg = zc * kchunk;
   const int kend = min(K, kbeg + kchunk);
-  const int m0 = blockIdx.y * kTM, n0 = blockIdx.x * kTN;
+  const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TM;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  const int wm = (wave / WN) * (TM / 2), wn = (wave % WN) * 32;
   const int r16 = lane & 15, q = lane >> 4;
 
-  // one accumulator set per k-quad of the 16-wide step: four shorter fp32 sums
-  // (summed pairwise at the end) instead of one chain over all of K, and 16
-  // independent MFMA chains per wave
-  f32x4 acc[kTK / 4][2][2];
+  // several accumulator sets: shorter fp32 sums (added pairwise at the end)
+  // than one chain over all of K, and independent MFMA chains
+  f32x4 acc[KS][IM][2];
 #pragma unroll
-  for (int ks = 0; ks < kTK / 4; ks++)
+  for (int ks = 0; ks < KS; ks++)
 #pragma unroll
-    for (int i = 0; i < 2; i++)
+    for (int i = 0; i < IM; i++)
 #pragma unroll
       for (int j = 0; j < 2; j++) acc[ks][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -109,13 +116,13 @@ __global__ __launch_bounds__(kGemmThreads) void k_tr_gemm(const float* __restric
   auto load = [&](int t) {
     const int cl = t / nst, st = t - cl * nst;
     const int64_t c = cl0 + cl;
-    tile_load<AK>(A + c * sAz, lda, m0, kbeg + st * kTK, M, kend, ra);
-    tile_load<BK>(B + c * sBz, ldb, n0, kbeg + st * kTK, N, kend, rb);
+    tile_load<TM, AK>(A + c * sAz, lda, m0, kbeg + st * kTK, M, kend, ra);
+    tile_load<TM, BK>(B + c * sBz, ldb, n0, kbeg + st * kTK, N, kend, rb);
   };
   if (total > 0) {
     load(0);
-    tile_store<AK>(sA[0], ra);
-    tile_store<BK>(sB[0], rb);
+    tile_store<TM, AK>(sA[0], ra);
+    tile_store<TM, BK>(sB[0], rb);
   }
   __syncthreads();
   for (int t = 0; t < total; t++) {
@@ -126,23 +133,26 @@ __global__ __launch_bounds__(kGemmThreads) void k_tr_gemm(const float* __restric
     const float* b = sB[cur];
 #pragma unroll
     for (int ks = 0; ks < kTK / 4; ks++) {
-      const int row = (ks * 4 + q) * kPitch;
-      const float a0 = a[row + wm + r16], a1 = a[row + wm + 16 + r16];
+      const int row = (ks * 4 + q) * P;
+      float av[IM];
+#pragma unroll
+      for (int i = 0; i < IM; i++) av[i] = a[row + wm + 16 * i + r16];
       const float b0 = b[row + wn + r16], b1 = b[row + wn + 16 + r16];
-      acc[ks][0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[ks][0][0], 0, 0, 0);
-      acc[ks][0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[ks][0][1], 0, 0, 0);
-      acc[ks][1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[ks][1][0], 0, 0, 0);
-      acc[ks][1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[ks][1][1], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < IM; i++) {
+        acc[ks % KS][i][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], b0, acc[ks % KS][i][0], 0, 0, 0);
+        acc[ks % KS][i][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], b1, acc[ks % KS][i][1], 0, 0, 0);
+      }
     }
     if (more) {  // the other buffer was last read before the previous barrier
-      tile_store<AK>(sA[cur ^ 1], ra);
-      tile_store<BK>(sB[cur ^ 1], rb);
+      tile_store<TM, AK>(sA[cur ^ 1], ra);
+      tile_store<TM, BK>(sB[cur ^ 1], rb);
     }
     __syncthreads();
   }
   // lane (q, r16) of block (i, j): rows 4 q + r, column r16
 #pragma unroll
-  for (int i = 0; i < 2; i++)
+  for (int i = 0; i < IM; i++)
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int gm = m0 + wm + 16 * i + 4 * q + r;
@@ -151,8 +161,13 @@ __global__ __launch_bounds__(kGemmThreads) void k_tr_gemm(const float* __restric
 #pragma unroll
       for (int j = 0; j < 2; j++) {
         const int gn = n0 + wn + 16 * j + r16;
-        if (gn < N)
-          C[(int64_t)gm * ldc + gn] = ((acc[0][i][j][r] + acc[1][i][j][r]) + (acc[2][i][j][r] + acc[3][i][j][r])) + bv;
+        if (gn >= N) continue;
+        float v;
+        if (KS == 4)
+          v = (acc[0][i][j][r] + acc[1 % KS][i][j][r]) + (acc[2 % KS][i][j][r] + acc[3 % KS][i][j][r]);
+        else
+          v = acc[0][i][j][r] + acc[1 % KS][i][j][r];
+        C[(int64_t)gm * ldc + gn] = v + bv;
       }
     }
 }
@@ -223,11 +238,14 @@ __global__ __launch_bounds__(kBnThreads) void k_tr_bn_fwd(const float* __restric
                                                           float* __restrict__ rmean, float* __restrict__ rvar,
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, int Bn, int C, int N,
-                                                          float eps, float momentum, int relu) {
+                                                          float eps, float momentum, int relu,
+                                                          float* __restrict__ pool, int* __restrict__ pool_idx) {
   __shared__ double red[kBnThreads / 64];
+  __shared__ unsigned long long pk[kPoolMaxB];  // per cloud: (ordered value bits, ~point) -- max = first max
   const int c = blockIdx.x;
   const int64_t M = (int64_t)Bn * N;
   const bool cached = M <= (int64_t)kBnCache * kBnThreads;
+  if (pool && threadIdx.x < Bn) pk[threadIdx.x] = 0ull;  // ordered before use by block_sum's barriers
   float v[kBnCache];
   double s = 0.0;
   if (cached) {
@@ -267,6 +285,25 @@ __global__ __launch_bounds__(kBnThreads) void k_tr_bn_fwd(const float* __restric
     }
   }
   const float fm = (float)mu, g = gamma[c], bt = beta[c];
+  // pool mode: no z; this thread's running max per cloud (its elements visit the
+  // clouds in order), merged into pk when the cloud changes
+  unsigned long long best = 0ull;
+  int cur = -1;
+  auto emit = [&](const ChanWalk& w, float o) {
+    if (!pool) {
+      z[w.off(C, N, c)] = o;
+      return;
+    }
+    if (w.b != cur) {
+      if (cur >= 0) atomicMax(&pk[cur], best);
+      cur = w.b;
+      best = 0ull;
+    }
+    const unsigned u = __float_as_uint(o);
+    const unsigned key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    const unsigned long long k = ((unsigned long long)key << 32) | (0xFFFFFFFFu - (unsigned)w.n);
+    best = k > best ? k : best;
+  };
   if (cached) {
     ChanWalk w(N);
 #pragma unroll
@@ -274,16 +311,25 @@ __global__ __launch_bounds__(kBnThreads) void k_tr_bn_fwd(const float* __restric
       if (w.b < Bn) {
         float o = bn_apply(v[i], fm, inv, g, bt);
         if (relu) o = fmaxf(o, 0.0f);
-        z[w.off(C, N, c)] = o;
+        emit(w, o);
       }
     }
   } else {
     for (ChanWalk w(N); w.b < Bn; w.next(N)) {
-      const int64_t off = w.off(C, N, c);
-      float o = bn_apply(y[off], fm, inv, g, bt);
+      float o = bn_apply(y[w.off(C, N, c)], fm, inv, g, bt);
       if (relu) o = fmaxf(o, 0.0f);
-      z[off] = o;
+      emit(w, o);
     }
+  }
+  if (!pool) return;
+  if (cur >= 0) atomicMax(&pk[cur], best);
+  __syncthreads();
+  if (threadIdx.x < Bn) {
+    const unsigned long long k = pk[threadIdx.x];
+    const unsigned key = (unsigned)(k >> 32);
+    const unsigned u = (key & 0x80000000u) ? (key & 0x7FFFFFFFu) : ~key;
+    pool[(int64_t)threadIdx.x * C + c] = __uint_as_float(u);
+    pool_idx[(int64_t)threadIdx.x * C + c] = (int)(0xFFFFFFFFu - (unsigned)(k & 0xFFFFFFFFu));
   }
 }
 
@@ -293,7 +339,8 @@ __global__ __launch_bounds__(kBnThreads) void k_tr_bn_bwd(const float* __restric
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float* __restrict__ dy,
                                                           float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                          float* __restrict__ dbias, int Bn, int C, int N, int relu) {
+                                                          float* __restrict__ dbias, int Bn, int C, int N, int relu,
+                                                          const int* __restrict__ pool_idx) {
   __shared__ double red[kBnThreads / 64];
   const int c = blockIdx.x;
   const int64_t M = (int64_t)Bn * N;
@@ -301,10 +348,19 @@ __global__ __launch_bounds__(kBnThreads) void k_tr_bn_bwd(const float* __restric
   const float mu = mean[c], inv = invstd[c], gm = gamma[c], bt = beta[c];
   float gv[kBnCache], xv[kBnCache];
   double sg = 0.0, sgx = 0.0;
-  // g = dz where the forward's output was > 0 (ReLU), xhat = (y - mean) invstd
-  auto grad_at = [&](int64_t off, float& xh) {
+  // g = dz where the forward's output was > 0 (ReLU), xhat = (y - mean) invstd;
+  // pool mode: dz is [B][C], the gradient of the max over points, all of it at
+  // the forward's first maximum
+  auto grad_at = [&](const ChanWalk& w, float& xh) {
+    const int64_t off = w.off(C, N, c);
     const float yv = y[off];
-    float g = dz[off];
+    float g;
+    if (pool_idx) {
+      const int64_t bc = (int64_t)w.b * C + c;
+      g = w.n == pool_idx[bc] ? dz[bc] : 0.0f;
+    } else {
+      g = dz[off];
+    }
     if (relu && !(bn_apply(yv, mu, inv, gm, bt) > 0.0f)) g = 0.0f;
     xh = (yv - mu) * inv;
     return g;
@@ -314,7 +370,7 @@ __global__ __launch_bounds__(kBnThreads) void k_tr_bn_bwd(const float* __restric
 #pragma unroll
     for (int i = 0; i < kBnCache; i++, w.next(N)) {
       float g = 0.0f, xh = 0.0f;
-      if (w.b < Bn) g = grad_at(w.off(C, N, c), xh);
+      if (w.b < Bn) g = grad_at(w, xh);
       gv[i] = g;
       xv[i] = xh;
       sg += g;
@@ -323,7 +379,7 @@ __global__ __launch_bounds__(kBnThreads) void k_tr_bn_bwd(const float* __restric
   } else {
     for (ChanWalk w(N); w.b < Bn; w.next(N)) {
       float xh;
-      const float g = grad_at(w.off(C, N, c), xh);
+      const float g = grad_at(w, xh);
       sg += g;
       sgx += (double)g * xh;
     }
@@ -347,7 +403,7 @@ __global__ __launch_bounds__(kBnThreads) void k_tr_bn_bwd(const float* __restric
     for (ChanWalk w(N); w.b < Bn; w.next(N)) {
       const int64_t off = w.off(C, N, c);
       float xh;
-      const float g = grad_at(off, xh);
+      const float g = grad_at(w, xh);
       const float d = scale * (g - k1 - xh * k2);
       dy[off] = d;
       sdy += d;
@@ -386,6 +442,12 @@ __global__ __launch_bounds__(256) void k_tr_row_sum(const float* __restrict__ x,
 
 int launched() { return hipGetLastError() == hipSuccess ? 0 : -21; }
 
+// A/B switch read once (NDNET_TR_GEMM64=1: 64 x 64 tiles only)
+bool getenv_flag(const char* name) {
+  const char* v = getenv(name);
+  return v && v[0] == '1';
+}
+
 }  // namespace
 
 extern "C" int ndnet_tr_gemm(const float* A, const float* B, float* C, const float* bias, int64_t sbias, int M,
@@ -401,11 +463,21 @@ extern "C" int ndnet_tr_gemm(const float* A, const float* B, float* C, const flo
   const int64_t parts = (batch + clouds_per_part - 1) / clouds_per_part;
   const int64_t gz = parts * nchunks, gy = (M + kTM - 1) / kTM, gx = (N + kTN - 1) / kTN;
   if (gz > 65535 || gy > 65535 || gx > (int64_t)INT32_MAX) return -20;
-  const dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)gz);
+  // 128 x 128 tiles where they still give the chip >= 512 workgroups
+  const int64_t big = ((M + 127) / 128) * ((N + 127) / 128) * gz;
+  const bool wide = M >= 128 && N >= 128 && big >= 512 && !getenv_flag("NDNET_TR_GEMM64");
+  const dim3 grid(wide ? (unsigned)((N + 127) / 128) : (unsigned)gx, wide ? (unsigned)((M + 127) / 128) : (unsigned)gy,
+                  (unsigned)gz);
   hipStream_t st = (hipStream_t)stream;
-#define NDNET_TR_GEMM(AKV, BKV)                                                                                \
-  k_tr_gemm<AKV, BKV><<<grid, kGemmThreads, 0, st>>>(A, B, C, bias, sbias, M, N, K, lda, ldb, ldc, sAz, sBz, sCz, \
-                                                     batch, clouds_per_part, nchunks, kchunk)
+#define NDNET_TR_GEMM(AKV, BKV)                                                                                    \
+  do {                                                                                                             \
+    if (wide)                                                                                                      \
+      k_tr_gemm<128, AKV, BKV><<<grid, 512, 0, st>>>(A, B, C, bias, sbias, M, N, K, lda, ldb, ldc, sAz, sBz, sCz,    \
+                                                     batch, clouds_per_part, nchunks, kchunk);                     \
+    else                                                                                                           \
+      k_tr_gemm<64, AKV, BKV><<<grid, 256, 0, st>>>(A, B, C, bias, sbias, M, N, K, lda, ldb, ldc, sAz, sBz, sCz,     \
+                                                    batch, clouds_per_part, nchunks, kchunk);                      \
+  } while (0)
   if (a_kmajor) {
     if (b_kmajor) NDNET_TR_GEMM(true, true); else NDNET_TR_GEMM(true, false);
   } else {
@@ -425,19 +497,20 @@ extern "C" int ndnet_tr_sum_parts(const float* part, float* out, int64_t count, 
 
 extern "C" int ndnet_tr_bn_fwd(const float* y, float* z, float* mean, float* invstd, float* running_mean,
                                float* running_var, const float* gamma, const float* beta, int B, int C, int N,
-                               float eps, float momentum, int relu, void* stream) {
-  if (!y || !z || !mean || !invstd || !gamma || !beta || B <= 0 || C <= 0 || N <= 0) return -20;
+                               float eps, float momentum, int relu, float* pool, int32_t* pool_idx, void* stream) {
+  if (!y || !mean || !invstd || !gamma || !beta || B <= 0 || C <= 0 || N <= 0) return -20;
+  if (pool ? (!pool_idx || B > kPoolMaxB) : !z) return -20;
   k_tr_bn_fwd<<<C, kBnThreads, 0, (hipStream_t)stream>>>(y, z, mean, invstd, running_mean, running_var, gamma, beta,
-                                                         B, C, N, eps, momentum, relu);
+                                                         B, C, N, eps, momentum, relu, pool, pool_idx);
   return launched();
 }
 
 extern "C" int ndnet_tr_bn_bwd(const float* dz, const float* y, const float* mean, const float* invstd,
                                const float* gamma, const float* beta, float* dy, float* dgamma, float* dbeta,
-                               float* dbias, int B, int C, int N, int relu, void* stream) {
+                               float* dbias, int B, int C, int N, int relu, const int32_t* pool_idx, void* stream) {
   if (!dz || !y || !mean || !invstd || !gamma || !beta || !dy || B <= 0 || C <= 0 || N <= 0) return -20;
   k_tr_bn_bwd<<<C, kBnThreads, 0, (hipStream_t)stream>>>(dz, y, mean, invstd, gamma, beta, dy, dgamma, dbeta, dbias,
-                                                         B, C, N, relu);
+                                                         B, C, N, relu, pool_idx);
   return launched();
 }
 

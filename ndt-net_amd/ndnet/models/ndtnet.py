@@ -42,6 +42,15 @@ def _hip_train(conv: nn.Conv1d, bn, x: torch.Tensor) -> bool:
     return x.is_cuda and conv.training and (bn is None or bn.training) and not _TRAIN_TORCH
 
 
+def _block_pool(conv: nn.Conv1d, bn, x: torch.Tensor, relu: bool) -> torch.Tensor:
+    """``_block(...).amax(dim=2)``: on the HIP train path one fused block that
+    never materialises the [B,C,N] activation (train_hip.conv_bn_act_pool)."""
+    if _hip_train(conv, bn, x) and x.shape[0] <= 64:
+        from . import train_hip
+        return train_hip.conv_bn_act_pool(conv, bn, x, relu)
+    return _block(conv, bn, x, relu).amax(dim=2)
+
+
 def _block(conv: nn.Conv1d, bn, x: torch.Tensor, relu: bool) -> torch.Tensor:
     """``relu(bn(conv(x)))`` (bn / relu optional): on the HIP train kernels in
     train mode on the GPU (ndnet.models.train_hip), else torch ops."""
@@ -68,9 +77,9 @@ class TNet(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         # pointwise MLP with BN+ReLU, max over points, FC head, + identity
-        for conv, bn in ((self.conv1, self.bn1), (self.conv2, self.bn2), (self.conv3, self.bn3)):
-            x = _block(conv, bn, x, True)
-        g = x.amax(dim=2)
+        x = _block(self.conv1, self.bn1, x, True)
+        x = _block(self.conv2, self.bn2, x, True)
+        g = _block_pool(self.conv3, self.bn3, x, True)
         g = self.relu(self.bn4(self.fc1(g)))
         g = self.relu(self.bn5(self.fc2(g)))
         t = self.fc3(g) + torch.eye(self.in_dim, device=g.device, dtype=g.dtype).reshape(1, -1)
@@ -103,8 +112,9 @@ class NDTNet(nn.Module):
         self.t1 = TNet(in_dim=point_dim)
         self.t2 = TNet(in_dim=64)
 
-    def forward(self, points: torch.Tensor, extra: torch.Tensor):
-        """points [B,N,3], extra [B,N,9] -> (features [B,F,N], x_t2 [B,64,N])."""
+    def forward(self, points: torch.Tensor, extra: torch.Tensor, pooled: bool = False):
+        """points [B,N,3], extra [B,N,9] -> (features [B,F,N], x_t2 [B,64,N]);
+        ``pooled``: (features.amax(dim=2) [B,F], x_t2) -- what the heads use."""
         B, N, _ = points.shape
         d = self.point_dim
         xyz = points.transpose(1, 2)                      # [B,3,N]
@@ -117,6 +127,8 @@ class NDTNet(nn.Module):
         x = torch.bmm(x.transpose(1, 2), t2).transpose(1, 2)  # x^T t2
         x_t2 = x
         x = _block(self.conv2, self.bn2, x, False)
+        if pooled:
+            return _block_pool(self.conv3, self.bn3, x, False), x_t2
         x = _block(self.conv3, self.bn3, x, False)
         return x, x_t2
 
@@ -153,16 +165,17 @@ class NDTNetSegmentation(nn.Module):
         self._hip = None  # folded-weight cache of the HIP path
 
     def forward_torch(self, points: torch.Tensor, covariances: torch.Tensor) -> torch.Tensor:
-        x, x_t2 = self.feature_extractor(points, covariances)
+        hip = _hip_train(self.conv1, self.bn1, points)
+        x, x_t2 = self.feature_extractor(points, covariances, pooled=hip)
         blocks = ((self.conv1, self.bn1), (self.conv2, self.bn2), (self.conv3, self.bn3))
-        if _hip_train(self.conv1, self.bn1, x_t2):
+        if hip:
             # conv1 over cat(x_t2, g broadcast over the points) (ndtnet.py:230-234) as a 64-channel
             # conv with the global feature's term a per-cloud bias: W[:, 64:] g + b -- 1/13 of the
             # layer's FLOPs forward and backward; the gradient reaches g through the bias
             from . import train_hip
             c = x_t2.shape[1]
             w = self.conv1.weight
-            cb = torch.addmm(self.conv1.bias, x.amax(dim=2), w[:, c:, 0].t())
+            cb = torch.addmm(self.conv1.bias, x, w[:, c:, 0].t())  # x: the pooled global feature [B,F]
             x = train_hip.conv_bn_act(self.conv1, self.bn1, x_t2, True, weight=w[:, :c], cloud_bias=cb)
             blocks = blocks[1:]
         else:

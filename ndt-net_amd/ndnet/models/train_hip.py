@@ -30,7 +30,7 @@ from .. import _lib
 # split-K of the weight gradient: aim for this many workgroups per launch, with
 # at most this many partial products (the partials are written, then re-read
 # by ndnet_tr_sum_parts: round 3 measured 1024 / 256+ parts at 130 MB a step)
-_DW_TARGET_WGS = 256
+_DW_TARGET_WGS = 1024
 _DW_MAX_PARTS = 32
 _KSTEP = 16  # the GEMM's k-step
 
@@ -160,7 +160,7 @@ class _ConvBNAct(torch.autograd.Function):
         g, bt = gamma.detach().contiguous(), beta.detach().contiguous()
         rc = _lib.lib().ndnet_tr_bn_fwd(y.data_ptr(), z.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
                                         _ptr(run_mean), _ptr(run_var), g.data_ptr(), bt.data_ptr(), Bn, C, N,
-                                        float(eps), float(momentum), int(relu), _stream())
+                                        float(eps), float(momentum), int(relu), None, None, _stream())
         _lib.check(rc, "ndnet_tr_bn_fwd")
         ctx.save_for_backward(x, w2, y, mean, invstd, g, bt)
         return z
@@ -179,7 +179,8 @@ class _ConvBNAct(torch.autograd.Function):
             dbias = torch.empty_like(dgamma)
             rc = _lib.lib().ndnet_tr_bn_bwd(dz.data_ptr(), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
                                             g.data_ptr(), bt.data_ptr(), dy.data_ptr(), dgamma.data_ptr(),
-                                            dbeta.data_ptr(), dbias.data_ptr(), Bn, C, N, int(ctx.relu), _stream())
+                                            dbeta.data_ptr(), dbias.data_ptr(), Bn, C, N, int(ctx.relu), None,
+                                            _stream())
             _lib.check(rc, "ndnet_tr_bn_bwd")
         else:
             x, w2 = ctx.saved_tensors
@@ -214,6 +215,75 @@ def conv_bn_act(conv: torch.nn.Conv1d, bn: Optional[torch.nn.BatchNorm1d], x: to
     out = _ConvBNAct.apply(x, w, b, cloud_bias, bn.weight, bn.bias,
                            bn.running_mean if track else None, bn.running_var if track else None,
                            bn.eps, bn.momentum, relu)
+    if track:
+        bn.num_batches_tracked.add_(1)
+    return out
+
+
+class _ConvBNPool(torch.autograd.Function):
+    """``amax(relu(bn(conv(x))), dim=2)`` -> [B,C] without the [B,C,N]
+    activation: the BatchNorm kernel's pool mode keeps each cloud's first
+    maximum and its point; the backward sends the pooled gradient to that
+    point only.  (torch's amax backward splits a tie evenly; ties have
+    identical rows, so every parameter gradient is the same.)"""
+
+    @staticmethod
+    def forward(ctx, x, w, b, gamma, beta, run_mean, run_var, eps, momentum, relu):
+        x = x.contiguous()
+        w2 = w.detach().reshape(w.shape[0], -1).contiguous()
+        _check_f32(x, w2)
+        Bn, Cin, N = x.shape
+        if w2.shape[1] != Cin:
+            raise ValueError(f"conv expects {w2.shape[1]} input channels, got {Cin}")
+        y = conv_forward(x, w2, b.detach().contiguous())
+        C = y.shape[1]
+        pool = torch.empty(Bn, C, device=y.device, dtype=torch.float32)
+        idx = torch.empty(Bn, C, device=y.device, dtype=torch.int32)
+        mean = torch.empty(C, device=y.device, dtype=torch.float32)
+        invstd = torch.empty_like(mean)
+        g, bt = gamma.detach().contiguous(), beta.detach().contiguous()
+        rc = _lib.lib().ndnet_tr_bn_fwd(y.data_ptr(), None, mean.data_ptr(), invstd.data_ptr(),
+                                        _ptr(run_mean), _ptr(run_var), g.data_ptr(), bt.data_ptr(), Bn, C, N,
+                                        float(eps), float(momentum), int(relu), pool.data_ptr(), idx.data_ptr(),
+                                        _stream())
+        _lib.check(rc, "ndnet_tr_bn_fwd (pool)")
+        ctx.relu, ctx.w_shape = bool(relu), w.shape
+        ctx.save_for_backward(x, w2, y, mean, invstd, g, bt, idx)
+        return pool
+
+    @staticmethod
+    def backward(ctx, dpool):
+        dpool = dpool.contiguous()
+        need = ctx.needs_input_grad
+        x, w2, y, mean, invstd, g, bt, idx = ctx.saved_tensors
+        Bn, C, N = y.shape
+        dy = torch.empty_like(y)
+        dgamma = torch.empty(C, device=y.device, dtype=torch.float32)
+        dbeta = torch.empty_like(dgamma)
+        dbias = torch.empty_like(dgamma)
+        rc = _lib.lib().ndnet_tr_bn_bwd(dpool.data_ptr(), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                                        g.data_ptr(), bt.data_ptr(), dy.data_ptr(), dgamma.data_ptr(),
+                                        dbeta.data_ptr(), dbias.data_ptr(), Bn, C, N, int(ctx.relu), idx.data_ptr(),
+                                        _stream())
+        _lib.check(rc, "ndnet_tr_bn_bwd (pool)")
+        dx = conv_input_grad(dy, w2) if need[0] else None
+        dw = conv_weight_grad(dy, x).view(ctx.w_shape) if need[1] else None
+        return (dx, dw, dbias if need[2] else None, dgamma if need[3] else None, dbeta if need[4] else None,
+                None, None, None, None, None)
+
+
+def conv_bn_act_pool(conv: torch.nn.Conv1d, bn: torch.nn.BatchNorm1d, x: torch.Tensor,
+                     relu: bool) -> torch.Tensor:
+    """``relu(bn(conv(x))).amax(dim=2)`` in training mode on the HIP kernels:
+    x [B,Cin,N] -> [B,Cout] (B <= 64 clouds)."""
+    if conv.kernel_size != (1,) or conv.groups != 1 or conv.stride != (1,) or conv.padding != (0,):
+        raise ValueError("only pointwise Conv1d(k=1) blocks run on the train kernels")
+    if conv.bias is None or not bn.affine or bn.momentum is None:
+        raise ValueError("the pooled block takes a biased conv and affine BatchNorm1d with a fixed momentum")
+    track = bn.track_running_stats and bn.running_mean is not None
+    out = _ConvBNPool.apply(x, conv.weight, conv.bias, bn.weight, bn.bias,
+                            bn.running_mean if track else None, bn.running_var if track else None,
+                            bn.eps, bn.momentum, relu)
     if track:
         bn.num_batches_tracked.add_(1)
     return out

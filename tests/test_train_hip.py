@@ -157,15 +157,21 @@ def test_segmentation_train_forward_backward_matches_torch(monkeypatch):
     ref_model = copy.deepcopy(model)
     pts, cov = _nds(4, 1000, 11)
     calls = []
-    real = train_hip.conv_bn_act
+    real, real_pool = train_hip.conv_bn_act, train_hip.conv_bn_act_pool
 
     def spy(*a, **k):
         calls.append(1)
         return real(*a, **k)
 
+    def spy_pool(*a, **k):
+        calls.append(2)
+        return real_pool(*a, **k)
+
     monkeypatch.setattr(train_hip, "conv_bn_act", spy)
+    monkeypatch.setattr(train_hip, "conv_bn_act_pool", spy_pool)
     out = model(pts, cov)
-    assert len(calls) == 13  # 3 + 3 TNet blocks, 3 NDTNet, 3 seg head + conv4
+    # 3 + 3 TNet blocks (the last of each pooled), 3 NDTNet (conv3 pooled), 3 seg head + conv4
+    assert len(calls) == 13 and calls.count(2) == 3
     monkeypatch.setattr(ndtnet, "_TRAIN_TORCH", True)
     f64_model = copy.deepcopy(ref_model).double()
     ref = ref_model(pts, cov)
@@ -226,6 +232,39 @@ def test_block_with_cloud_bias_matches_concat():
     ref.backward(up)
     _close(xt.grad, xt2.grad, 1e-4, "dx_t2")
     _close(g.grad, g2.grad, 1e-4, "dg")
+    _close(conv.weight.grad, conv2.weight.grad, 1e-4, "dW")
+    _close(norm.weight.grad, norm2.weight.grad, 1e-4, "dgamma")
+    _close(norm.bias.grad, norm2.bias.grad, 1e-4, "dbeta")
+    assert (conv.bias.grad - conv2.bias.grad).abs().max().item() <= 1e-3
+
+
+@pytest.mark.parametrize("cin,cout,relu,B,N", [
+    (128, 1024, True, 16, 1000),   # TNet conv3 -> amax (ndtnet.py:50-51)
+    (128, 768, False, 4, 1000),    # NDTNet conv3 -> the seg head's global max (:152, :231)
+    (64, 128, True, 20, 700),      # uncached BatchNorm path
+])
+def test_pooled_block_matches_amax(cin, cout, relu, B, N):
+    """conv_bn_act_pool == relu(bn(conv(x))).amax(dim=2): pooled values, running
+    statistics and every gradient (the pooled gradient reaches the first max only)."""
+    from ndnet.models import train_hip
+    conv, norm = _pair(cin, cout, True, cin * 3 + cout)
+    with torch.no_grad():  # both signs of gamma: a decreasing channel pools its minimum of y
+        norm.weight[::3].neg_()
+    conv2, norm2 = copy.deepcopy(conv), copy.deepcopy(norm)
+    x = (torch.randn(B, cin, N, device="cuda") + 0.3).requires_grad_(True)
+    x2 = x.detach().clone().requires_grad_(True)
+    out = train_hip.conv_bn_act_pool(conv, norm, x, relu)
+    z = norm2(conv2(x2))
+    ref = (torch.relu(z) if relu else z).amax(dim=2)
+    assert out.shape == (B, cout)
+    torch.testing.assert_close(out, ref, rtol=0, atol=1e-4)
+    torch.testing.assert_close(norm.running_mean, norm2.running_mean, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(norm.running_var, norm2.running_var, rtol=1e-5, atol=1e-5)
+    assert int(norm.num_batches_tracked) == 1
+    up = torch.randn_like(ref)
+    out.backward(up)
+    ref.backward(up)
+    _close(x.grad, x2.grad, 1e-4, "dx")
     _close(conv.weight.grad, conv2.weight.grad, 1e-4, "dW")
     _close(norm.weight.grad, norm2.weight.grad, 1e-4, "dgamma")
     _close(norm.bias.grad, norm2.bias.grad, 1e-4, "dbeta")
