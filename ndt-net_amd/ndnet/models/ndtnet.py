@@ -119,9 +119,18 @@ class NDTNet(nn.Module):
         d = self.point_dim
         xyz = points.transpose(1, 2)                      # [B,3,N]
         t = self.t1(xyz)                                  # [B,3,3]
-        xyz = torch.bmm(t, xyz)                           # t . p
-        cov = torch.matmul(t.unsqueeze(1), extra.reshape(B, N, d, d)).reshape(B, N, d * d)  # t . C (left only)
-        x = torch.cat((xyz.transpose(1, 2), cov), dim=2).transpose(1, 2)  # [B,12,N]
+        if extra.shape[-1] == d * d and _hip_train(self.conv1, self.bn1, points):
+            # (HIP train path; the torch composition below stays the reference's op for op)
+            # t . p and t . C (left only, ndtnet.py:141-147) as ONE bmm per cloud: each point
+            # contributes 4 columns (p, C[:, 0], C[:, 1], C[:, 2]) of a [3, 4N] matrix -- torch's
+            # batched matmul of 16000 3x3 products costs ~85 us each way on this GPU
+            X = torch.cat((points.unsqueeze(-1), extra.reshape(B, N, d, d)), dim=3)  # [B,N,j,4]
+            Y = torch.bmm(t, X.permute(0, 2, 1, 3).reshape(B, d, N * (d + 1))).reshape(B, d, N, d + 1)
+            x = torch.cat((Y[..., 0], Y[..., 1:].permute(0, 1, 3, 2).reshape(B, d * d, N)), dim=1)  # [B,12,N]
+        else:
+            xyz = torch.bmm(t, xyz)                           # t . p
+            cov = torch.matmul(t.unsqueeze(1), extra.reshape(B, N, d, d)).reshape(B, N, d * d)  # t . C (left only)
+            x = torch.cat((xyz.transpose(1, 2), cov), dim=2).transpose(1, 2)  # [B,12,N]
         x = _block(self.conv1, self.bn1, x, False)        # no ReLU (reference ndtnet.py:149)
         t2 = self.t2(x)                                   # [B,64,64]
         x = torch.bmm(x.transpose(1, 2), t2).transpose(1, 2)  # x^T t2
