@@ -84,6 +84,12 @@ int ndnet_tr_chan_sum(const float *x, float *out, int B, int C, int N, void *str
 /* out[r] = sum over n of x[r][n] for `rows` rows of N contiguous values (per-cloud bias gradients). */
 int ndnet_tr_row_sum(const float *x, float *out, int64_t rows, int N, void *stream);
 
+/* count[0] += the number of the `rows` rows (of `cols` floats) whose first
+ * argmax in pred equals that in gt, NaN counting as a maximum as in
+ * torch.argmax: the training step's accuracy (tools/train.py:84-87) without a
+ * host sync; the caller zeroes count. */
+int ndnet_tr_argmax_match(const float *pred, const float *gt, int64_t rows, int cols, uint32_t *count, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

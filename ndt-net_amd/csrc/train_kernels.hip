@@ -440,6 +440,31 @@ __global__ __launch_bounds__(256) void k_tr_row_sum(const float* __restrict__ x,
   if ((threadIdx.x & 63) == 0) out[r] = (float)s;
 }
 
+// first index of the row's maximum, NaN counting as the maximum (torch.argmax)
+__device__ __forceinline__ int row_argmax(const float* __restrict__ r, int cols) {
+  int bi = 0;
+  float bv = r[0];
+  for (int j = 1; j < cols; j++) {
+    const float v = r[j];
+    if (!(bv != bv) && (v > bv || v != v)) {
+      bv = v;
+      bi = j;
+    }
+  }
+  return bi;
+}
+
+// count[0] += rows whose argmax agrees (tools/train.py:84-87): a thread per row,
+// a wave sum per wave, one integer atomic per wave (exact, so order-free)
+__global__ __launch_bounds__(256) void k_tr_argmax_match(const float* __restrict__ pred, const float* __restrict__ gt,
+                                                         int64_t rows, int cols, unsigned* __restrict__ count) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  unsigned n = r < rows ? (row_argmax(pred + r * cols, cols) == row_argmax(gt + r * cols, cols)) : 0u;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
+  if ((threadIdx.x & 63) == 0 && n) atomicAdd(count, n);
+}
+
 int launched() { return hipGetLastError() == hipSuccess ? 0 : -21; }
 
 // A/B switch read once (NDNET_TR_GEMM64=1: 64 x 64 tiles only)
@@ -523,5 +548,12 @@ extern "C" int ndnet_tr_chan_sum(const float* x, float* out, int B, int C, int N
 extern "C" int ndnet_tr_row_sum(const float* x, float* out, int64_t rows, int N, void* stream) {
   if (!x || !out || rows <= 0 || N <= 0 || (rows + 3) / 4 > (int64_t)INT32_MAX) return -20;
   k_tr_row_sum<<<(unsigned)((rows + 3) / 4), 256, 0, (hipStream_t)stream>>>(x, out, rows, N);
+  return launched();
+}
+
+extern "C" int ndnet_tr_argmax_match(const float* pred, const float* gt, int64_t rows, int cols, uint32_t* count,
+                                     void* stream) {
+  if (!pred || !gt || !count || rows <= 0 || cols <= 0 || (rows + 255) / 256 > (int64_t)INT32_MAX) return -20;
+  k_tr_argmax_match<<<(unsigned)((rows + 255) / 256), 256, 0, (hipStream_t)stream>>>(pred, gt, rows, cols, count);
   return launched();
 }

@@ -287,3 +287,4 @@ def conv_bn_act_pool(conv: torch.nn.Conv1d, bn: torch.nn.BatchNorm1d, x: torch.T
     if track:
         bn.num_batches_tracked.add_(1)
     return out
+

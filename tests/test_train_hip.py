@@ -269,3 +269,17 @@ def test_pooled_block_matches_amax(cin, cout, relu, B, N):
     _close(norm.weight.grad, norm2.weight.grad, 1e-4, "dgamma")
     _close(norm.bias.grad, norm2.bias.grad, 1e-4, "dbeta")
     assert (conv.bias.grad - conv2.bias.grad).abs().max().item() <= 1e-3
+
+
+def test_accuracy_kernel_matches_torch_argmax():
+    from ndnet.training import accuracy_tensor
+    g = torch.Generator(device="cuda").manual_seed(5)
+    pred = torch.randn(16, 1000, 29, device="cuda", generator=g)
+    gt = torch.nn.functional.one_hot(torch.randint(0, 29, (16, 1000), device="cuda", generator=g), 29).float()
+    gt[0, :500] = torch.nn.functional.one_hot(pred[0, :500].argmax(-1), 29).float()  # some matches
+    pred[1, 3, 7] = pred[1, 3].max()          # an exact tie: the first index wins
+    pred[2, 5, 4] = float("nan")              # NaN counts as the maximum
+    ref = (pred.argmax(dim=-1) == gt.argmax(dim=-1)).float().mean()
+    got = accuracy_tensor(pred, gt)
+    assert abs(got.item() - ref.item()) <= 1e-7
+
