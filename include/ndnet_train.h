@@ -90,6 +90,11 @@ int ndnet_tr_row_sum(const float *x, float *out, int64_t rows, int N, void *stre
  * host sync; the caller zeroes count. */
 int ndnet_tr_argmax_match(const float *pred, const float *gt, int64_t rows, int cols, uint32_t *count, void *stream);
 
+/* out[r] = the first argmax of row r of x [rows][cols] (NaN counting as a
+ * maximum, as torch.argmax): the labelled NDT path's class of each point from
+ * its one-hot label (ndtnet_preprocessing.py:34), batched over the clouds. */
+int ndnet_row_argmax(const float *x, int64_t rows, int cols, int32_t *out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -465,6 +465,13 @@ __global__ __launch_bounds__(256) void k_tr_argmax_match(const float* __restrict
   if ((threadIdx.x & 63) == 0 && n) atomicAdd(count, n);
 }
 
+// out[r] = first argmax of row r (NaN as the maximum): a thread per row
+__global__ __launch_bounds__(256) void k_row_argmax(const float* __restrict__ x, int64_t rows, int cols,
+                                                    int* __restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r < rows) out[r] = row_argmax(x + r * cols, cols);
+}
+
 int launched() { return hipGetLastError() == hipSuccess ? 0 : -21; }
 
 // A/B switch read once (NDNET_TR_GEMM64=1: 64 x 64 tiles only)
@@ -555,5 +562,11 @@ extern "C" int ndnet_tr_argmax_match(const float* pred, const float* gt, int64_t
                                      void* stream) {
   if (!pred || !gt || !count || rows <= 0 || cols <= 0 || (rows + 255) / 256 > (int64_t)INT32_MAX) return -20;
   k_tr_argmax_match<<<(unsigned)((rows + 255) / 256), 256, 0, (hipStream_t)stream>>>(pred, gt, rows, cols, count);
+  return launched();
+}
+
+extern "C" int ndnet_row_argmax(const float* x, int64_t rows, int cols, int32_t* out, void* stream) {
+  if (!x || !out || rows <= 0 || cols <= 0 || (rows + 255) / 256 > (int64_t)INT32_MAX) return -20;
+  k_row_argmax<<<(unsigned)((rows + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, rows, cols, out);
   return launched();
 }

@@ -134,6 +134,7 @@ TRAIN_EXPORTS: dict = {
     "ndnet_tr_chan_sum": (_I, [_P, _P, _I, _I, _I, _P]),
     "ndnet_tr_row_sum": (_I, [_P, _P, _I64, _I, _P]),
     "ndnet_tr_argmax_match": (_I, [_P, _P, _I64, _I, _P, _P]),
+    "ndnet_row_argmax": (_I, [_P, _I64, _I, _P, _P]),
 }
 
 

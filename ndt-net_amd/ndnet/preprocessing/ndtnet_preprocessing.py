@@ -186,7 +186,15 @@ def ndt_preprocessing(num_nds: int, points: torch.Tensor, classes: torch.Tensor 
     labels = None
     if labelled:
         # argmax of the one-hot labels, as ndtnet_preprocessing.py:34 does per cloud
-        labels = torch.argmax(classes.to(dev), dim=2).to(torch.int32).contiguous()
+        oh = classes.to(dev)
+        if oh.dtype == torch.float32:  # one HIP pass (torch's argmax + int cast: ~160 us at 16 x 100k x 29)
+            oh = oh.contiguous()
+            labels = torch.empty(oh.shape[:2], dtype=torch.int32, device=dev)
+            _lib.check(_lib.lib().ndnet_row_argmax(oh.data_ptr(), oh.shape[0] * oh.shape[1], oh.shape[2],
+                                                   labels.data_ptr(), torch.cuda.current_stream(dev).cuda_stream),
+                       "ndnet_row_argmax")
+        else:
+            labels = torch.argmax(oh, dim=2).to(torch.int32).contiguous()
         out_cls = torch.empty((B, num_nds, ncls + 1), dtype=torch.float32, device=dev)
     plan.run(pts, labels, out, out_cls)
     ndt_preprocessing.last_plan = plan

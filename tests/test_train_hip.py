@@ -283,3 +283,17 @@ def test_accuracy_kernel_matches_torch_argmax():
     got = accuracy_tensor(pred, gt)
     assert abs(got.item() - ref.item()) <= 1e-7
 
+
+
+def test_row_argmax_matches_torch():
+    """ndnet_row_argmax: the labelled path's point classes (ndtnet_preprocessing.py:34)."""
+    from ndnet import _lib
+    g = torch.Generator(device="cuda").manual_seed(8)
+    x = torch.randn(3, 5000, 29, device="cuda", generator=g)
+    x[0, 1, 5] = x[0, 1].max()      # tie: first index
+    x[1, 2, 9] = float("nan")       # NaN is the maximum
+    x[2, 3] = 0.0                   # all equal: index 0
+    out = torch.empty(3, 5000, dtype=torch.int32, device="cuda")
+    _lib.check(_lib.lib().ndnet_row_argmax(x.data_ptr(), 15000, 29, out.data_ptr(),
+                                           torch.cuda.current_stream().cuda_stream), "row_argmax")
+    assert torch.equal(out.long(), torch.argmax(x, dim=2))
