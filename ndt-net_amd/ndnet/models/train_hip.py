@@ -90,7 +90,7 @@ def dw_split(Bn: int, Cout: int, Cin: int, N: int):
     parts = max(1, min(_DW_MAX_PARTS, -(-_DW_TARGET_WGS // tiles), Bn * -(-N // 64)))
     if parts <= Bn:
         return -(-Bn // parts), 1, N
-    want = -(-parts // Bn)
+    want = max(1, parts // Bn)  # point chunks per cloud: B * want <= parts
     kchunk = -(-N // want)
     kchunk = -(-kchunk // _KSTEP) * _KSTEP
     return 1, -(-N // kchunk), kchunk

@@ -280,3 +280,19 @@ def test_adam_step_on_hip_nds_equals_oracle_nds():
     assert abs(l_hip - l_orc) <= 1e-5 * max(1.0, abs(l_orc))
     for (name, a), b in zip(m_hip.named_parameters(), m_orc.parameters()):
         assert (a - b).abs().max().item() <= 1e-5, name
+
+
+def test_weight_gradient_split_covers_every_point():
+    """Host logic of the train GEMM's split-K (ndnet.models.train_hip.dw_split):
+    the parts tile the (cloud, point) range exactly once, within the caps the
+    ABI enforces (ndnet_tr_gemm: chunks start inside K and cover it)."""
+    from ndnet.models.train_hip import _DW_MAX_PARTS, dw_split
+    for B in (1, 2, 5, 16, 20, 64):
+        for cout, cin in ((64, 3), (64, 12), (128, 64), (1024, 128), (768, 128), (512, 64), (256, 512), (29, 128)):
+            for N in (1, 17, 500, 1000, 4097):
+                cpz, nch, kchunk = dw_split(B, cout, cin, N)
+                assert 1 <= cpz <= B and nch >= 1 and kchunk >= 1
+                assert (nch - 1) * kchunk < N <= nch * kchunk
+                assert nch == 1 or kchunk % 16 == 0
+                parts = -(-B // cpz) * nch
+                assert parts <= max(_DW_MAX_PARTS, 1)
