@@ -40,6 +40,13 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kTM = 64, kTN = 64, kTK = 16;
+// LDS row pitch TM + kPad floats.  17: a k-major tile store (lanes = 16 k rows x 4
+// columns) and an operand read (4 lane quads = 4 k rows x 16 columns) each touch
+// (nearly) distinct banks; with + 16 the k-major store was 4-way conflicted
+#ifndef NDNET_TR_PAD
+#define NDNET_TR_PAD 17
+#endif
+constexpr int kPad = NDNET_TR_PAD;
 
 constexpr int kBnThreads = 512;
 constexpr int kBnCache = 32;
@@ -69,7 +76,7 @@ __device__ __forceinline__ void tile_store(float* __restrict__ s, const float (&
   for (int i = 0; i < 4; i++) {
     const int kk = KMAJOR ? (t & 15) : t / TM + 4 * i;
     const int rr = KMAJOR ? (t >> 4) + (TM / 4) * i : t % TM;
-    s[kk * (TM + 16) + rr] = v[i];
+    s[kk * (TM + kPad) + rr] = v[i];
   }
 }
 
@@ -82,7 +89,7 @@ __global__ __launch_bounds__(TM * 4) void k_tr_gemm(const float* __restrict__ A,
                                                     int64_t sbias, int M, int N, int K, int64_t lda, int64_t ldb,
                                                     int64_t ldc, int64_t sAz, int64_t sBz, int64_t sCz, int batch,
                                                     int cpz, int nchunks, int kchunk) {
-  constexpr int P = TM + 16;              // LDS row pitch: the 4 lane quads of an operand read hit disjoint banks
+  constexpr int P = TM + kPad;            // LDS row pitch (kPad)
   constexpr int WN = 2 * (TM / 64);       // waves along N
   constexpr int IM = TM / 32;             // 16-row blocks per wave (wave tile TM / 2 rows x 32 columns)
   constexpr int KS = TM == 64 ? 4 : 2;    // accumulator sets (k-quad ks uses set ks % KS)
