@@ -2,9 +2,11 @@
 """The training step of tools/train.py:67-81, timed by stage
 on one GPU: labelled NDT on HIP (16 x 100k points -> 1000 NDs, 28 classes,
 one-hot) -> NDTNetSegmentation train-mode forward (BatchNorm batch
-statistics) -> NLL loss -> backward -> Adam.  The forward / backward are
-torch autograd (hipBLASLt / MIOpen kernels); the eval forward of the same
-batch on the HIP chains is timed beside them for the gap.
+statistics) -> NLL loss -> backward -> Adam.  The conv blocks' forward and
+backward run on the HIP train kernels (include/ndnet_train.h, autograd
+Functions of ndnet.models.train_hip); NDNET_TRAIN_PATH=torch runs the torch
+composition (MIOpen / hipBLASLt) instead, for the A/B.  The eval forward of
+the same batch on the HIP chains is timed beside them.
 
     python tools/bench_train.py [--steps 20] [--warmup 5] [--batch 16]
 
@@ -24,6 +26,9 @@ from ndnet.models.ndtnet import NDTNetSegmentation  # noqa: E402
 from ndnet.preprocessing.ndtnet_preprocessing import ndt_preprocessing  # noqa: E402
 from ndnet.synthetic import make_labelled_batch  # noqa: E402
 from ndnet.training import Trainer, segmentation_loss  # noqa: E402
+
+# which train-mode blocks run: the HIP kernels (default) or the torch composition
+TRAIN_PATH = "torch" if os.environ.get("NDNET_TRAIN_PATH", "hip").lower() == "torch" else "hip"
 
 
 def main() -> None:
@@ -57,7 +62,8 @@ def main() -> None:
         torch.cuda.synchronize()
         step = e0.elapsed_time(e1) / a.steps
         print(json.dumps({"what": "training step (tools/train.py:67-81) as one HIP graph: HIP labelled NDT + "
-                                  "torch train forward/backward + fused capturable Adam", "batch": a.batch,
+                                  "train forward/backward + fused capturable Adam", "train_path": TRAIN_PATH,
+                          "batch": a.batch,
                           "points": a.points, "nds": a.nds, "classes": a.classes, "F": a.feature_dim,
                           "steps": a.steps, "step_ms": round(step, 4),
                           "clouds_per_s": round(a.batch / step * 1e3, 1), "loss": round(loss.item(), 5)}))
@@ -91,8 +97,9 @@ def main() -> None:
                 tot[n] += ev[i].elapsed_time(ev[i + 1])
     ms = {n: round(v / a.steps, 4) for n, v in tot.items()}
     step = sum(v for n, v in ms.items() if n != "forward_eval_hip")
-    print(json.dumps({"what": "training step (tools/train.py:67-81): HIP labelled NDT + torch train "
-                              "forward/backward + Adam", "batch": a.batch, "points": a.points, "nds": a.nds,
+    print(json.dumps({"what": "training step (tools/train.py:67-81): HIP labelled NDT + train "
+                              "forward/backward + Adam", "train_path": TRAIN_PATH, "batch": a.batch,
+                      "points": a.points, "nds": a.nds,
                       "classes": a.classes, "F": a.feature_dim, "steps": a.steps, "ms": ms,
                       "step_ms": round(step, 4), "clouds_per_s": round(a.batch / step * 1e3, 1),
                       "train_forward_vs_hip_eval": round(ms["forward_train"] / ms["forward_eval_hip"], 2)}))
