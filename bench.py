@@ -226,9 +226,16 @@ def main() -> None:
         return out
 
     def run_plan():
-        """The NDT plan the timed steps ran (the pipeline's own, else the cached one)."""
+        """The NDT plan the timed steps ran (the pipeline's first, else the cached one)."""
         g = None if args.eager else graphed
         return g.plan if g is not None and hasattr(g, "plan") else get_plan(B, n, k, -1, dev)
+
+    def all_run_stats():
+        """host_stats() of every plan the timed steps ran (the pipeline's NDT
+        streams each have a plan of their own)."""
+        g = None if args.eager else graphed
+        plans = getattr(g, "plans", None) or [run_plan()]
+        return [st for pl in plans for st in pl.host_stats()]
 
     with torch.no_grad():
         # settle: replay the step for --settle-ms before the W warmup steps, so
@@ -275,8 +282,8 @@ def main() -> None:
             torch.cuda.synchronize()
             D.barrier()
             t_o = D.max_over_ranks(time.perf_counter() - t0)
+        assert all(st.rc == 0 for st in all_run_stats()), [st.rc for st in all_run_stats()]
         ost = run_plan().host_stats()
-        assert all(st.rc == 0 for st in ost), [st.rc for st in ost]
         other = {"kind": okind, "value": round(total_clouds / t_o, 2), "unit": "clouds/s",
                  "ms_per_step": round(1e3 * t_o / args.steps, 4),
                  "pruned_per_cloud": round(float(np.mean([st.num_nds - k for st in ost])), 1)}
@@ -324,7 +331,7 @@ def main() -> None:
             pcie["overlapped"] = {"value": round(total_clouds / t_ov, 2),
                                   "ms_per_step": round(1e3 * t_ov / args.steps, 4),
                                   "how": "PipelinedSegmentation.replay_streamed: ring of input buffers, copy stream"}
-    stats = run_plan().host_stats()
+    stats = all_run_stats()
     assert all(s.rc == 0 for s in stats), [s.rc for s in stats]
     assert all(torch.isfinite(o).all() for o in (out if isinstance(out, list) else [out]))
 

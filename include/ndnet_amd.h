@@ -156,6 +156,14 @@ int ndnet_ndt_set_exact_counts(void *plan, int on);
  * float input with the plan's shapes in LDS only (otherwise direct). */
 int ndnet_ndt_set_front_staged(void *plan, int on);
 
+/* k_welford_q computes the moments of an ND with at least min_samples points
+ * on a whole wave (the mean recurrence alone on three lanes, the per-sample
+ * products on all 64, the ordered sums on six), every other ND on a lane
+ * quad of a 16-ND wave.  Identical results either way (the same IEEE
+ * operations in the reference's order, normal_distributions.c:75-103); the
+ * threshold only moves work.  Default 256; min_samples >= 1. */
+int ndnet_ndt_set_heavy_threshold(void *plan, uint32_t min_samples);
+
 /* Split ndnet_ndt_run in two stream-ordered calls (a caller that overlaps the
  * run with other work on another stream, e.g. ndnet.pipeline): part 1 runs the
  * front only (k_front: limits, bisection, dense ids, binning), part 2 the rest
@@ -235,6 +243,16 @@ int ndnet_ndt_debug_front_marks(void *plan, unsigned long long *marks);
 /* Start / end stamps (s_memrealtime) of every k_front workgroup of the last
  * run at timing level 2: marks[B][G][2]; *G = workgroups per cloud. */
 int ndnet_ndt_debug_front_wg_marks(void *plan, unsigned long long *marks, int *G);
+
+/* k_welford_q per-item stamps of the last run at timing level 2: *items =
+ * capacity B * (ndcap + ceil(ndcap / 16)) (items past the run's count keep
+ * old values); marks[item * 8 + i]: 0 s_memrealtime at the item's start
+ * (100 MHz), 1..3 s_memtime (shader clock) at its start, after the moments,
+ * at its end; 4 = heavy << 63 | samples of its longest ND << 32 | wave id;
+ * 5..7 (heavy items) shader cycles in the whole-wave path's phases 0 + 2
+ * (loads, per-sample products), 1 (mean recurrence), 3 (ordered sums).
+ * Heavy items come first.  marks must hold 8 * capacity values; synchronises. */
+int ndnet_ndt_debug_wq_marks(void *plan, unsigned long long *marks, uint32_t *items);
 
 /* Library identification (no GPU needed). */
 const char *ndnet_amd_version(void);

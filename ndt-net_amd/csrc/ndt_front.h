@@ -69,6 +69,8 @@ struct FrontArgs {
   uint32_t* vox;                // [B][ndcap]
   uint32_t* nd_n;               // [B][ndcap]
   uint32_t* nd_base;            // [B][ndcap]
+  uint32_t* heavy;              // [B][ndcap] NDs with >= heavy_t points (CloudCtl::heavy_n)
+  uint32_t heavy_t;
   void* nd_pts;                 // [B * n + slack][3] T
   uint16_t* nd_lbl;             // [B][n] or null
   unsigned long long* lims;     // [B][G][6]
@@ -263,6 +265,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
   __shared__ FrontState s;
   __shared__ uint32_t scratch[32];
   __shared__ unsigned long long scratch64[16];
+  __shared__ uint32_t s_heavy;  // workgroup 0: heavy NDs listed so far
   __shared__ uint32_t s_bad[kWorkers];
   // Workgroup -> (cloud, g).  Blocks are dealt round-robin over the 8 XCDs
   // (MI355X_MICROARCH.md, speed only: the barriers below hold whatever the
@@ -824,6 +827,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
       st_sc1(wg + (uint64_t)g * ndcap + d, run);
     }
     FRONT_MARK(23);
+    if (t == 0) s_heavy = 0;
     if (!cloud_sync(s, bar, G)) goto fail;
     FRONT_MARK(24);
     // ND bases (scan of the per-ND totals over NDs) + earlier workgroups'
@@ -883,11 +887,14 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
         if (g == 0) {
           A.nd_n[(uint64_t)b * ndcap + d] = tot_d;
           A.nd_base[(uint64_t)b * ndcap + d] = start;
+          // k_welford_q gives these a wave each; their order does not matter
+          if (tot_d >= A.heavy_t) A.heavy[(uint64_t)b * ndcap + atomicAdd(&s_heavy, 1u)] = d;
         }
         addv[d] = start + pre;  // a point's destination: addv[d] + hist[r][d] + its rank
       }
     }
     __syncthreads();
+    if (g == 0 && t == 0) c.heavy_n = s_heavy;
     FRONT_MARK(25);
     // ---- scatter: every point to its ND's run, in index order ----
     T* out = (T*)A.nd_pts + (uint64_t)b * n * 3;

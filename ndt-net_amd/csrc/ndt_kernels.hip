@@ -50,6 +50,13 @@ constexpr int kChunk = 256;          // slots per chunk of the chip-wide event s
 constexpr int kMergeLdsChunks = 34;  // k_kl_merge stages score + NaN keys in LDS up to this many chunks (136 KB)
 constexpr int kMergeScoreChunks = 72; // ... and the score runs alone up to this many (144 KB; k <= 2440)
 constexpr int kMaxChunks = 6 * 16384 / kChunk;  // ndcap <= 16384
+// NDs with at least this many samples get a whole wave each in k_welford_q
+// (wq_heavy): k_front / k_bin_offsets list them per cloud.  The plan's
+// default (ndnet_ndt_set_heavy_threshold).
+#ifndef NDNET_WQ_HEAVY
+#define NDNET_WQ_HEAVY 256
+#endif
+constexpr uint32_t kWqHeavy = NDNET_WQ_HEAVY;
 
 enum State : uint32_t { kSearching = 0, kAccepted = 1, kFailed = 2 };
 
@@ -88,6 +95,8 @@ struct CloudCtl {
   uint32_t flag_count;   // events of a deferred cloud, counted by k_kl_rank_chunks (zeroed per run)
   uint32_t list_off;     // physical index of the retained list's first entry (the prunes' pending
                          // left shifts, ndt.c:69-72; always 0 on the global-memory prune path)
+  uint32_t heavy_n;      // NDs of the accepted grid with >= kWqHeavy samples, listed in Plan::heavy
+                         // (written by the binning of every run that accepts a grid)
 };
 
 struct Plan {
@@ -106,6 +115,7 @@ struct Plan {
   int ev_created;
   hipEvent_t ev[8];
   unsigned long long* kl_marks;  // [B][16] s_memrealtime stamps (timing level 2)
+  unsigned long long* wq_marks;  // [wq_items][kWqMarkW] k_welford_q per-item stamps (timing level 2)
   // device buffers
   CloudCtl* ctl;
   uint32_t* stamps;    // [B][vcap]
@@ -174,6 +184,9 @@ struct Plan {
   int lists_built;            // the deferred lists of the last run are built (no further build launches)
   int front_staged;           // k_front's scatter through LDS records (ndnet_ndt_set_front_staged; default 1)
   int run_part;               // ndnet_ndt_set_run_part: 0 whole run, 1 front only, 2 from k_welford_q on
+  uint32_t* heavy;            // [B][ndcap] the heavy NDs of each cloud (CloudCtl::heavy_n of them)
+  double* rtab;               // [n + 1][2] (rc, rl) per count for wq_heavy's divisions
+  uint32_t heavy_t;           // NDs with >= heavy_t samples take wq_heavy (ndnet_ndt_set_heavy_threshold)
 };
 
 // ------------------------------------------------------------------ helpers
@@ -681,12 +694,16 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_count(const CloudCtl* ctl, 
   for (uint32_t d = threadIdx.x; d < nd; d += blockDim.x) row[d] = hist[d];
 }
 
-__global__ void __launch_bounds__(1024) k_bin_offsets(const CloudCtl* ctl, uint32_t* counts_all, uint32_t* nd_n,
-                                                      uint32_t* nd_base, uint32_t ndcap, uint32_t nbins) {
+__global__ void __launch_bounds__(1024) k_bin_offsets(CloudCtl* ctl, uint32_t* counts_all, uint32_t* nd_n,
+                                                      uint32_t* nd_base, uint32_t* heavy, uint32_t heavy_t,
+                                                      uint32_t ndcap, uint32_t nbins) {
   const int b = blockIdx.x;
-  const CloudCtl& c = ctl[b];
+  CloudCtl& c = ctl[b];
   if (c.state != kAccepted) return;
   __shared__ uint32_t scratch[16];
+  __shared__ uint32_t s_heavy;
+  if (threadIdx.x == 0) s_heavy = 0;
+  __syncthreads();
   const uint32_t nd = c.num_nds;
   uint32_t* cnt = counts_all + (uint64_t)b * nbins * ndcap;
   uint32_t carry = 0;
@@ -709,6 +726,7 @@ __global__ void __launch_bounds__(1024) k_bin_offsets(const CloudCtl* ctl, uint3
     if (d < nd) {
       nd_n[(uint64_t)b * ndcap + d] = tot_d;
       nd_base[(uint64_t)b * ndcap + d] = start;
+      if (tot_d >= heavy_t) heavy[(uint64_t)b * ndcap + atomicAdd(&s_heavy, 1u)] = d;  // a wave each in k_welford_q
       uint32_t run = start;
       uint32_t ch = 0;
       for (; ch + 8 <= nbins; ch += 8) {
@@ -729,6 +747,8 @@ __global__ void __launch_bounds__(1024) k_bin_offsets(const CloudCtl* ctl, uint3
     }
     carry += tot;
   }
+  __syncthreads();
+  if (threadIdx.x == 0) c.heavy_n = s_heavy;
 }
 
 template <typename T>
@@ -820,6 +840,8 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_scatter(const T* __restrict
 // divisions and the reference's NaN -> 0 step.  Labelled runs: the whole
 // quad builds the class histogram in LDS (first index of the max,
 // normal_distributions.c:107-121).
+constexpr int kWqMarkW = 8;  // per item at timing level 2: realtime start, memtime start / moments done / end, meta,
+                             // heavy items: cycles in phases 0 + 2, 1, 3
 constexpr int kWqThreads = 256;              // 4 waves x 16 quads
 constexpr int kWqNDs = kWqThreads / 4;
 constexpr int kWqU = 16;                     // samples per prefetch block
@@ -906,6 +928,224 @@ __device__ inline uint32_t qslot_of_dir(uint32_t d) {  // q-slot of the neighbou
   return (0x0b1a29u >> (4 * d)) & 0xfu;  // {d0: 9, d1: 2, d2: 10, d3: 1, d4: 11, d5: 0}
 }
 
+// ---- one long ND's moments on a whole wave (wq_heavy) ----
+//
+// The lane-quad fold issues ~18 wave instructions per sample for the 16 NDs
+// of a wave, so a wave lasts as long as its longest ND: on L clouds (heaviest
+// ND 1675 samples) that one quad set the whole kernel's time.  Only the mean
+// is a true recurrence:
+//   t_i = x_i - mean_{i-1};  mean_i = mean_{i-1} + t_i / n_i
+// Everything else of a sample -- u_i = x_i - mean_i, t_i u_i, the
+// off-diagonal u_a t_b and its division by n_i -- depends only on that
+// sequence and the sample, and only the sums m2 += t u and cov_ab += u_a t_b / n
+// must run in sample order.  So per 64-sample block:
+//   0. every lane loads one sample (record + its (rc, rl) entry);
+//   1. lanes 0..2 (one axis each) run the mean recurrence alone: 4 dependent
+//      FP64 operations per sample, the means to LDS;
+//   2. every lane computes its own sample's six addends from the means;
+//   3. lanes 0..5 add them in sample order (one accumulator each).
+// The same IEEE operations on the same operands in the same order as the
+// reference (normal_distributions.c:75-103), so the same bits; ~7 wave
+// instructions per sample instead of ~18, on one ND.
+//
+// The division t / n is RN(t rc + RN(t rl)) with rc ~ 1/n (within an ulp) and
+// rl = RN((1 - n rc) / n) (1 - n rc is exact): t rc + RN(t rl) is within
+// 2^-104 |t/n| of t/n, while t/n (t a double, n < 2^32 an integer) is never a
+// rounding midpoint and never within 2^-86 |t/n| of one, so the fused add
+// rounds to RN(t / n) -- two dependent operations instead of three
+// (div_fast).  Range: every operand here is normal (|t| >= 2^-353 or 0 for
+// the coordinates the fast path admits); a zero t may give a zero of the
+// other sign, which no sum can see (they start at +0 and never become -0).
+// tests/test_oracle.py::test_rtab_division_is_ieee checks the rule against
+// the division on 10^7 operands.
+constexpr int kHvXS = 65;  // LDS row strides (doubles) of the heavy stage: distinct banks for lanes 0..5
+constexpr int kHvMS = 67;
+constexpr int kHvVS = 65;
+constexpr int kHvLds = 3 * kHvXS + 3 * kHvMS + 6 * kHvVS;  // 786 doubles = 6288 B per wave
+
+template <typename T>
+struct HvRec {
+  T x, y, z;
+  double2 r;  // (rc, rl) of n = this sample's count
+};
+
+template <typename T>
+__device__ inline void hv_load(HvRec<T>& h, const T* __restrict__ rec, const double2* __restrict__ rtab,
+                               uint32_t q0, uint32_t lane, uint32_t cnt) {
+  const uint32_t q0l = q0 + lane, q = q0l < cnt ? q0l : cnt - 1;
+  const T* p = rec + 3u * q;
+  h.x = p[0];
+  h.y = p[1];
+  h.z = p[2];
+  h.r = rtab[q + 1];
+}
+
+// Phase 1 over one group of 8 samples (lanes 0..2): x and (rc, rl) already
+// in registers (loaded a group ahead, so no LDS latency is waited out).
+template <bool kChk>  // kChk: the block's last group may be partial (nb wave-uniform)
+__device__ inline void hv_chain8(double& m, const double (&x)[8], const double2 (&r)[8], double* __restrict__ ma,
+                                 uint32_t i0, uint32_t nb) {
+#pragma unroll
+  for (int u = 0; u < 8; u++) {
+    if (!kChk || i0 + u < nb) {
+      const double t = x[u] - m;
+      m = m + fma(t, r[u].x, t * r[u].y);
+      ma[i0 + u] = m;
+    }
+  }
+}
+__device__ inline void hv_load8(double (&x)[8], double2 (&r)[8], const double* __restrict__ xa,
+                                const double2* __restrict__ R, uint32_t i0) {
+#pragma unroll
+  for (int u = 0; u < 8; u++) {
+    x[u] = xa[i0 + u];
+    r[u] = R[i0 + u];
+  }
+}
+
+template <typename T, bool kStamp = false>  // kStamp: phase cycle totals to ph[0..2] (timing level 2)
+__device__ inline void wq_heavy(const T* __restrict__ rec, uint32_t cnt, const double2* __restrict__ rtab,
+                                double* __restrict__ lds, uint32_t lane, double& mean, double& m2, double& off,
+                                bool& bad, unsigned long long* ph = nullptr) {
+  unsigned long long ts = 0, c02 = 0, c1 = 0, c3 = 0;
+  auto stamp = [&](unsigned long long& acc) __attribute__((always_inline)) {
+    if constexpr (kStamp) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      acc += t - ts;
+      ts = t;
+    }
+  };
+  if constexpr (kStamp) ts = __builtin_amdgcn_s_memtime();
+  double* X = lds;                    // [3][kHvXS] the block's coordinates
+  double* M = lds + 3 * kHvXS;        // [3][kHvMS] [0] the mean before the block, [1 + i] after sample i
+  double* V = M + 3 * kHvMS;          // [6][kHvVS] per-sample addends: t u (3 axes), u_a t_b / n (3 pairs)
+  double2* R = reinterpret_cast<double2*>(V);  // [64] (rc, rl) of the block's samples (phases 0-1; V from 2 on)
+  const uint32_t a = lane < 3 ? lane : 0;
+  double m = 0.0, acc = 0.0;
+  bool out = false;
+  HvRec<T> h0, h1, h2;  // blocks q0, q0 + 64, q0 + 128 in flight
+  hv_load(h0, rec, rtab, 0, lane, cnt);
+  hv_load(h1, rec, rtab, 64, lane, cnt);
+  hv_load(h2, rec, rtab, 128, lane, cnt);
+  for (uint32_t q0 = 0; q0 < cnt; q0 += 64) {
+    const HvRec<T> h = h0;
+    h0 = h1;
+    h1 = h2;
+    hv_load(h2, rec, rtab, q0 + 192, lane, cnt);
+    const uint32_t nb = cnt - q0 < 64u ? cnt - q0 : 64u;  // samples of this block (wave-uniform)
+    const double x0 = (double)h.x, x1 = (double)h.y, x2 = (double)h.z;
+    if constexpr (!std::is_same<T, float>::value)
+      out |= lane < nb && !(wq_in_range(h.x) && wq_in_range(h.y) && wq_in_range(h.z));
+    // 0. the block to LDS; the running mean as M[.][0]
+    X[lane] = x0;
+    X[kHvXS + lane] = x1;
+    X[2 * kHvXS + lane] = x2;
+    R[lane] = h.r;
+    if (lane < 3) M[a * kHvMS] = m;
+    asm volatile("" ::: "memory");  // one wave's LDS operations complete in order
+    stamp(c02);
+    // 1. the mean recurrence, lanes 0..2, 8 samples per group, the next
+    //    group's operands loaded before this group's chain
+    if (lane < 3) {
+      const double* xa = X + a * kHvXS;
+      double* ma = M + a * kHvMS + 1;
+      double xA[8], xB[8];
+      double2 rA[8], rB[8];
+      hv_load8(xA, rA, xa, R, 0);
+      if (nb == 64) {
+        for (uint32_t i0 = 0; i0 < 64; i0 += 16) {
+          hv_load8(xB, rB, xa, R, i0 + 8);
+          hv_chain8<false>(m, xA, rA, ma, i0, 64);
+          if (i0 + 16 < 64) hv_load8(xA, rA, xa, R, i0 + 16);
+          hv_chain8<false>(m, xB, rB, ma, i0 + 8, 64);
+        }
+      } else {
+        for (uint32_t i0 = 0; i0 < nb; i0 += 16) {
+          if (i0 + 8 < nb) hv_load8(xB, rB, xa, R, i0 + 8);
+          hv_chain8<true>(m, xA, rA, ma, i0, nb);
+          if (i0 + 8 >= nb) break;
+          if (i0 + 16 < nb) hv_load8(xA, rA, xa, R, i0 + 16);
+          hv_chain8<true>(m, xB, rB, ma, i0 + 8, nb);
+        }
+      }
+    }
+    asm volatile("" ::: "memory");
+    stamp(c1);
+    // 2. every lane: its sample's addends
+    {
+      const double t0 = x0 - M[lane], u0 = x0 - M[lane + 1];
+      const double t1 = x1 - M[kHvMS + lane], u1 = x1 - M[kHvMS + lane + 1];
+      const double t2 = x2 - M[2 * kHvMS + lane], u2 = x2 - M[2 * kHvMS + lane + 1];
+      const double p01 = u0 * t1, p12 = u1 * t2, p02 = u0 * t2;
+      asm volatile("" ::: "memory");  // R (under V) is read by phase 1 only
+      V[lane] = t0 * u0;
+      V[kHvVS + lane] = t1 * u1;
+      V[2 * kHvVS + lane] = t2 * u2;
+      V[3 * kHvVS + lane] = fma(p01, h.r.x, p01 * h.r.y);
+      V[4 * kHvVS + lane] = fma(p12, h.r.x, p12 * h.r.y);
+      V[5 * kHvVS + lane] = fma(p02, h.r.x, p02 * h.r.y);
+    }
+    asm volatile("" ::: "memory");
+    stamp(c02);
+    // 3. the ordered sums, lanes 0..5: m2_0..2, cov_01, cov_12, cov_02;
+    //    16 addends per group, the next group loaded ahead
+    if (lane < 6) {
+      const double* v = V + lane * kHvVS;
+      double vA[16], vB[16];
+#pragma unroll
+      for (int u = 0; u < 16; u++) vA[u] = v[u];
+      if (nb == 64) {
+        for (uint32_t i0 = 0; i0 < 64; i0 += 32) {
+#pragma unroll
+          for (int u = 0; u < 16; u++) vB[u] = v[i0 + 16 + u];
+#pragma unroll
+          for (int u = 0; u < 16; u++) acc = acc + vA[u];
+          if (i0 + 32 < 64) {
+#pragma unroll
+            for (int u = 0; u < 16; u++) vA[u] = v[i0 + 32 + u];
+          }
+#pragma unroll
+          for (int u = 0; u < 16; u++) acc = acc + vB[u];
+        }
+      } else
+      for (uint32_t i0 = 0; i0 < nb; i0 += 32) {
+        if (i0 + 16 < nb) {
+#pragma unroll
+          for (int u = 0; u < 16; u++) vB[u] = v[i0 + 16 + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 16; u++)
+          if (i0 + u < nb) acc = acc + vA[u];
+        if (i0 + 16 >= nb) break;
+        if (i0 + 32 < nb) {
+#pragma unroll
+          for (int u = 0; u < 16; u++) vA[u] = v[i0 + 32 + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 16; u++)
+          if (i0 + 16 + u < nb) acc = acc + vB[u];
+      }
+    }
+    asm volatile("" ::: "memory");
+    stamp(c3);
+  }
+  if constexpr (kStamp) {
+    ph[0] = c02;
+    ph[1] = c1;
+    ph[2] = c3;
+  }
+  // lane j < 3: mean_j, m2_j and the pair the quad layout gives lane j
+  // ((0,1), (1,2), (0,2): the accumulator of lane j + 3)
+  const double o3 = __shfl_down(acc, 3, 64);
+  const bool anyout = __any(out);
+  if (lane < 3) {
+    mean = m;
+    m2 = acc;
+    off = o3;
+    bad = anyout;
+  }
+}
+
 // What k_welford_q writes for the KL stage after an ND's moments (the LU
 // chains, formerly their own kernel): neighbours, chain masks, the chain's
 // in-place LU states and the final (post-KL) covariance.
@@ -934,26 +1174,40 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
                                                           const uint32_t* __restrict__ nd_base, double* nd_mean,
                                                           double* nd_cov, uint16_t* nd_cls, uint32_t* hist_all,
                                                           int ncls, uint64_t n, uint32_t ndcap, uint32_t* wq_ctr,
-                                                          WqChainArgs CA) {
+                                                          const uint32_t* __restrict__ heavy, uint32_t heavy_t,
+                                                          const double2* __restrict__ rtab,
+                                                          unsigned long long* __restrict__ wq_marks, WqChainArgs CA) {
   extern __shared__ __attribute__((aligned(16))) unsigned char wq_smem[];
-  __shared__ __attribute__((aligned(16))) float wq_stage[std::is_same<T, float>::value && NDNET_WQ_VLOAD ? kWqNDs : 1]
-                                                        [kWqStageQ];
+  // the quads' record transposes; a heavy item's wave uses its 16 rows (6400 B) as its wq_heavy stage
+  __shared__ __attribute__((aligned(16))) float wq_stage[kWqNDs][kWqStageQ];
+  static_assert(kHvLds * sizeof(double) <= 16 * kWqStageQ * sizeof(float), "heavy stage fits a wave's rows");
   double* lrt = (double*)wq_smem;                                // [kWqRt] refined reciprocals of 1..kWqRt
-  uint32_t* pre = (uint32_t*)(wq_smem + kWqRt * sizeof(double));  // [B + 1] first item of each cloud
-  uint32_t* wq_hist = pre + ((B + 1 + 3) & ~3);                   // labelled runs: [kWqNDs][ncls + 1]
+  const uint32_t bw = (uint32_t)((B + 1 + 3) & ~3);
+  uint32_t* pre = (uint32_t*)(wq_smem + kWqRt * sizeof(double));  // [B + 1] first light item of each cloud
+  uint32_t* hpre = pre + bw;                                      // [B + 1] first heavy item of each cloud
+  uint32_t* wq_hist = hpre + bw;                                  // labelled runs: [kWqNDs][ncls + 1]
   for (uint32_t i = threadIdx.x; i < (uint32_t)kWqRt; i += kWqThreads) lrt[i] = recip_refined((double)(i + 1));
-  // items = (cloud, group of 16 NDs) of this run, in cloud order: one per wave
-  // of a persistent grid (one workgroup per CU, one wave per SIMD), so no
-  // SIMD holds two ND groups while another idles
-  for (int i = threadIdx.x; i < B; i += kWqThreads)
-    pre[i + 1] = ctl[i].state == kAccepted ? (ctl[i].num_nds + 15u) / 16u : 0u;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    pre[0] = 0;
-    for (int i = 0; i < B; i++) pre[i + 1] += pre[i];
+  // items: first the heavy NDs (>= kWqHeavy samples, listed by k_front /
+  // k_bin_offsets), one per wave, so the longest work starts at once; then
+  // (cloud, group of 16 NDs), in cloud order, whose heavy NDs are skipped.
+  // One item per wave of a persistent grid (one workgroup per CU, one wave
+  // per SIMD), so no SIMD holds two ND groups while another idles.
+  for (int i = threadIdx.x; i < B; i += kWqThreads) {
+    const bool acc = ctl[i].state == kAccepted;
+    pre[i + 1] = acc ? (ctl[i].num_nds + 15u) / 16u : 0u;
+    hpre[i + 1] = acc ? ctl[i].heavy_n : 0u;
   }
   __syncthreads();
-  const uint32_t total = pre[B];
+  if (threadIdx.x == 0) {
+    pre[0] = hpre[0] = 0;
+    for (int i = 0; i < B; i++) {
+      pre[i + 1] += pre[i];
+      hpre[i + 1] += hpre[i];
+    }
+  }
+  __syncthreads();
+  const uint32_t H = hpre[B];
+  const uint32_t total = H + pre[B];
   const uint32_t lane = threadIdx.x & 63, j = lane & 3;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // first round static (one item per wave), then a shared counter: a wave
@@ -983,20 +1237,31 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
     return __builtin_amdgcn_readfirstlane(v);
   };
   for (uint32_t item = blockIdx.x * (kWqThreads / 64) + wave; item < total; item = next_item()) {
+  const bool hv = item < H;  // a heavy ND (wave-uniform)
+  unsigned long long mk_rt = 0, mk_t0 = 0, mk_t1 = 0;
+  if (wq_marks) {
+    mk_rt = __builtin_amdgcn_s_memrealtime();
+    mk_t0 = __builtin_amdgcn_s_memtime();
+  }
+  const uint32_t li = hv ? item : item - H;
+  const uint32_t* const ip = hv ? hpre : pre;
   int lo = 0, hi = B - 1;  // the cloud whose items hold `item`
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    if (pre[mid] <= item) lo = mid;
+    if (ip[mid] <= li) lo = mid;
     else hi = mid - 1;
   }
   const int b = lo;
   const uint32_t nd = ctl[b].num_nds;
-  const uint32_t wd0 = (item - pre[b]) * 16u;  // first ND of my wave
-  const uint32_t d = wd0 + (lane >> 2);
-  const bool live = d < nd;
-  const uint64_t o = (uint64_t)b * ndcap + (live ? d : wd0);
+  // heavy: quad 0 holds the ND, the other quads idle; light: 16 NDs
+  const uint32_t wd0 = hv ? heavy[(uint64_t)b * ndcap + (li - hpre[b])] : (li - pre[b]) * 16u;
+  const uint32_t d = hv ? wd0 : wd0 + (lane >> 2);
+  const uint64_t o = (uint64_t)b * ndcap + (d < nd ? d : wd0);
   const uint32_t beg = nd_base[o];
-  const uint32_t cnt = live ? nd_n[o] : 0u;
+  const uint32_t c0 = nd_n[o];
+  // a light group's heavy NDs are done by their own items
+  const bool live = hv ? lane < 4 : (d < nd && c0 < heavy_t);
+  const uint32_t cnt = live ? c0 : 0u;
   const uint32_t last = cnt ? cnt - 1u : 0u;
   const uint32_t jj = j < 3 ? j : 0u;
   const T* src = nd_pts + ((uint64_t)b * n + beg) * 3 + jj;
@@ -1220,7 +1485,16 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
       load(r3, q0 + 7 * kU);
     }
   };
-  run(mx, true, std::false_type{});
+  unsigned long long ph[3] = {0, 0, 0};
+  if (hv) {
+    const T* rec = nd_pts + ((uint64_t)b * n + __builtin_amdgcn_readfirstlane(beg)) * 3;
+    const uint32_t hc = __builtin_amdgcn_readfirstlane(c0);  // c0, beg: the same in every lane here
+    double* hl = reinterpret_cast<double*>(&wq_stage[wave * 16][0]);
+    if (wq_marks) wq_heavy<T, true>(rec, hc, rtab, hl, lane, mean, m2, off, bad, ph);
+    else wq_heavy<T>(rec, hc, rtab, hl, lane, mean, m2, off, bad);
+  } else
+    run(mx, true, std::false_type{});
+  if (wq_marks) mk_t1 = __builtin_amdgcn_s_memtime();
   // float input: every finite coordinate is in div_fast's exact range, and a
   // non-finite one makes the running mean non-finite from then on (x - mean
   // and mean + ... stay inf / NaN), so the final state flags it
@@ -1248,10 +1522,9 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
     nd_cov[9 * o + 3 * ib + ia] = off;
   }
   // The ND's KL chain: eligible directions (a neighbour, and
-  // more than one sample on both sides), the chain mask, and every in-place
-  // LU state of the chain, stored step-major ([t][j][ND], coalesced across
-  // the wave's quads); lane 0 of the quad runs it on the covariance gathered
-  // from lanes 0..2.
+  // more than one sample on both sides) and the chain mask.  The in-place LU
+  // states of the chain are k_lu_chains' (one ND per lane: here only one
+  // lane of a quad would run it, 3 of 4 idle, at the end of every item).
   {
     uint32_t el = 0;
 #pragma unroll
@@ -1262,44 +1535,7 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
     }
     el |= (uint32_t)__builtin_amdgcn_mov_dpp((int)el, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
     el |= (uint32_t)__builtin_amdgcn_mov_dpp((int)el, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-    double S[9];
-    S[0] = dpp_d<0x00>(vd);
-    S[4] = dpp_d<0x55>(vd);
-    S[8] = dpp_d<0xAA>(vd);
-    S[1] = S[3] = dpp_d<0x00>(off);
-    S[5] = S[7] = dpp_d<0x55>(off);
-    S[2] = S[6] = dpp_d<0xAA>(off);
-    if (live && j == 0) {
-      const uint32_t mask = chain_mask(el);
-      const int nT = __popc(mask);
-      CA.nkeys[o] = mask;
-      const uint64_t ob = (uint64_t)b * ndcap, u = o - ob;
-      double* chain = CA.chain + ob * 108 + u;
-      uint32_t* ps = CA.chain_ps + ob * 12 + u;
-      const bool flags_only = CA.lazy_k && nd <= CA.lazy_k;  // a deferred cloud (wave-uniform)
-      uint32_t okb = 0;
-#ifdef NDNET_WQ_NOCHAIN  // timing experiment only (wrong results): no LU chain
-      for (int t = 0; t < 0; t++) {
-#else
-      for (int t = 0; t < nT; t++) {
-#endif
-        uint32_t perm;
-        int sg;
-        lu3(S, perm, sg);
-        if (flags_only) {  // what kl_event's flag reads of the state (kullback_leibler.c:57-70)
-          okb |= (lu3_det(S, sg) != 0 && lu3_sgndet(S, sg) != 0 ? 1u : 0u) << t;
-          continue;
-        }
-#ifndef NDNET_WQ_NOCHAINSTORE  // timing experiment only (wrong results): LU chain without its stores
-#pragma unroll
-        for (int q = 0; q < 9; q++) chain[(uint64_t)(9 * t + q) * ndcap] = S[q];
-        ps[(uint64_t)t * ndcap] = perm | (sg < 0 ? 0x100u : 0u);
-#endif
-      }
-      if (flags_only) CA.chain_ok[o] = okb;
-#pragma unroll
-      for (int q = 0; q < 9; q++) CA.cov_post[9 * o + q] = S[q];
-    }
+    if (live && j == 0) CA.nkeys[o] = chain_mask(el);
   }
   const uint32_t nbins = (uint32_t)ncls + 1u;
   const bool hist_lds = (size_t)kWqNDs * nbins * sizeof(uint32_t) <= (size_t)kWqHistMax;
@@ -1361,6 +1597,21 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
         if (hist[k] > best) { best = hist[k]; cls = (uint16_t)k; }
     }
     nd_cls[o] = cls;
+  }
+  if (wq_marks) {
+    const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+    const uint32_t mxc = hv ? c0 : mx;
+    if (lane == 0) {
+      unsigned long long* w = wq_marks + (uint64_t)item * kWqMarkW;
+      w[0] = mk_rt;
+      w[1] = mk_t0;
+      w[2] = mk_t1;
+      w[3] = t2;
+      w[4] = ((unsigned long long)hv << 63) | ((unsigned long long)mxc << 32) | (blockIdx.x * 4u + wave);
+      w[5] = ph[0];
+      w[6] = ph[1];
+      w[7] = ph[2];
+    }
   }
   }  // item
 }
@@ -2375,13 +2626,15 @@ static void plan_free(Plan* P) {
   if (P->ev_created)
     for (int i = 0; i < 7; i++) (void)hipEventDestroy(P->ev[i]);
   if (P->kl_marks) (void)hipFree(P->kl_marks);
+  if (P->wq_marks) (void)hipFree(P->wq_marks);
   if (P->fmarks) (void)hipFree(P->fmarks);
   void* bufs[] = {P->flims, P->frec, P->fwgcnt, P->fbar, P->ctl, P->stamps, P->dense_of, P->vox, P->gbits, P->pkeys, P->did, P->bin_cnt, P->nd_base,
                   P->nd_pts, P->nd_lbl, P->nd_n,
                   P->nd_mean, P->nd_cov, P->nd_cov_post, P->nd_cls, P->hist, P->nb, P->keys, P->nkeys,
                   P->chain, P->chain_ps, P->chain_ok, P->slot_val, P->slot_flag, P->ev_val, P->ev_p, P->ev_q, P->ev_min,
                   P->sort_key, P->sort_idx, P->nan_list, P->nan_key, P->nan_slot, P->chunk_nanbase, P->ord_val, P->ord_p, P->ord_q,
-                  P->first_occ, P->tmp_u32, P->alive, P->d_stats, P->chunk_cnt, P->chunk_min, P->wq_ctr};
+                  P->first_occ, P->tmp_u32, P->alive, P->d_stats, P->chunk_cnt, P->chunk_min, P->wq_ctr,
+                  P->heavy, P->rtab};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete P;
@@ -2481,6 +2734,49 @@ __global__ void __launch_bounds__(256) k_kl_chains(KLArgs A) {
   }
 }
 
+// Every ND's in-place LU chain after the moments (the GSL calls
+// of kullback_leibler.c:57-63 per event, in the order chain_mask gives), one
+// ND per lane: each state stored step-major ([t][q][ND], coalesced), the
+// last as the post-KL covariance.  A cloud whose list is deferred (lazy run,
+// num_nds <= lazy_k) keeps only which states have det != 0 and sgndet != 0
+// (chain_ok: all its event flags read); k_kl_chains stores its states if the
+// list is ever built.
+__global__ void __launch_bounds__(256) k_lu_chains(const CloudCtl* __restrict__ ctl, const double* __restrict__ nd_cov,
+                                                   const uint32_t* __restrict__ nkeys, double* chain,
+                                                   uint32_t* chain_ps, uint32_t* chain_ok, double* cov_post,
+                                                   uint32_t ndcap, uint64_t lazy_k) {
+  const int b = blockIdx.y;
+  const CloudCtl& c = ctl[b];
+  if (c.state != kAccepted) return;
+  const uint32_t nd = c.num_nds;
+  const uint32_t u = blockIdx.x * 256 + threadIdx.x;
+  if (u >= nd) return;
+  const uint64_t ob = (uint64_t)b * ndcap;
+  double S[9];
+#pragma unroll
+  for (int q = 0; q < 9; q++) S[q] = nd_cov[9 * (ob + u) + q];
+  const int nT = __popc(nkeys[ob + u]);
+  const bool flags_only = lazy_k && nd <= lazy_k;  // a deferred cloud (uniform over the cloud)
+  double* ch = chain + ob * 108 + u;
+  uint32_t* ps = chain_ps + ob * 12 + u;
+  uint32_t okb = 0;
+  for (int t = 0; t < nT; t++) {
+    uint32_t perm;
+    int sg;
+    lu3(S, perm, sg);
+    if (flags_only) {  // what kl_event's flag reads of the state (kullback_leibler.c:57-70)
+      okb |= (lu3_det(S, sg) != 0 && lu3_sgndet(S, sg) != 0 ? 1u : 0u) << t;
+      continue;
+    }
+#pragma unroll
+    for (int q = 0; q < 9; q++) ch[(uint64_t)(9 * t + q) * ndcap] = S[q];
+    ps[(uint64_t)t * ndcap] = perm | (sg < 0 ? 0x100u : 0u);
+  }
+  if (flags_only) chain_ok[ob + u] = okb;
+#pragma unroll
+  for (int q = 0; q < 9; q++) cov_post[9 * (ob + u) + q] = S[q];
+}
+
 static void launch_list_sort(Plan* P, const KLArgs& A, hipStream_t st) {
   const int B = P->B;
   k_kl_rank_chunks<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
@@ -2538,6 +2834,8 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
     F.vox = P->vox;
     F.nd_n = P->nd_n;
     F.nd_base = P->nd_base;
+    F.heavy = P->heavy;
+    F.heavy_t = P->heavy_t;
     F.nd_pts = P->nd_pts;
     F.nd_lbl = lbl ? P->nd_lbl : nullptr;
     F.lims = P->flims;
@@ -2580,7 +2878,8 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
   if (P->timing) HIPCHK(hipEventRecord(P->ev[3], st));
   k_bin_count<<<dim3(P->nbins, B), kBinThreads, P->ndcap * sizeof(uint32_t), st>>>(
       P->ctl, P->pkeys, P->dense_of, P->did, P->bin_cnt, n, P->vcap, P->ndcap, P->nbins);
-  k_bin_offsets<<<B, 1024, 0, st>>>(P->ctl, P->bin_cnt, P->nd_n, P->nd_base, P->ndcap, P->nbins);
+  k_bin_offsets<<<B, 1024, 0, st>>>(P->ctl, P->bin_cnt, P->nd_n, P->nd_base, P->heavy, P->heavy_t, P->ndcap,
+                                     P->nbins);
   k_bin_scatter<T><<<dim3(P->nbins, B), kBinThreads, 0, st>>>(pts, lbl, P->ctl, P->did, P->bin_cnt,
                                                                (T*)P->nd_pts, lbl ? P->nd_lbl : nullptr, n,
                                                                P->ndcap, P->nbins);
@@ -2592,12 +2891,16 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
   }
 welford:
   P->lists_built = 0;
-  k_welford_q<T><<<P->wq_grid, kWqThreads, kWqRt * sizeof(double) + 4 * ((B + 1 + 3) & ~3) + (lbl ? P->wq_lds : 0),
+  k_welford_q<T><<<P->wq_grid, kWqThreads, kWqRt * sizeof(double) + 8 * ((B + 1 + 3) & ~3) + (lbl ? P->wq_lds : 0),
                     st>>>(
       P->ctl, B, (const T*)P->nd_pts, lbl ? P->nd_lbl : nullptr, P->nd_n, P->nd_base, P->nd_mean, P->nd_cov,
-      P->nd_cls, P->hist, P->ncls, n, P->ndcap, P->wq_ctr,
+      P->nd_cls, P->hist, P->ncls, n, P->ndcap, P->wq_ctr, P->heavy, P->heavy_t, (const double2*)P->rtab,
+      P->timing >= 2 ? P->wq_marks : nullptr,
       WqChainArgs{P->vox, P->dense_of, P->nb, P->nkeys, P->chain, P->chain_ps, P->nd_cov_post, P->vcap,
                   P->eager_list ? 0ull : (uint64_t)P->k, P->chain_ok});
+  k_lu_chains<<<dim3((P->ndcap + 255) / 256, B), 256, 0, st>>>(P->ctl, P->nd_cov, P->nkeys, P->chain, P->chain_ps,
+                                                              P->chain_ok, P->nd_cov_post, P->ndcap,
+                                                              P->eager_list ? 0ull : (uint64_t)P->k);
   if (P->timing) HIPCHK(hipEventRecord(P->ev[5], st));
   KLArgs A = kl_args(P, P->k, out, out_cls, pc64, cov64, cls16);
   A.stats_out = stats_dst;
@@ -2680,6 +2983,7 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   P->vcap = voxel_capacity ? voxel_capacity : (1ull << 22);
   P->front_sync_ticks = 200000000ull;  // 2 s at the 100 MHz constant clock
   P->front_staged = 1;
+  P->heavy_t = kWqHeavy;
   const double upper = (double)num_desired * (1 + 0.2);
   P->ndcap = (uint32_t)upper + 1;
   P->ecap = 6 * P->ndcap;
@@ -2743,6 +3047,8 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   A_(chunk_min, B * P->nchunk);
   A_(d_stats, B);
   A_(wq_ctr, 128);
+  A_(heavy, B * nd);
+  A_(rtab, 2 * (n + 1));
   // k_front: G workgroups per cloud, all resident together (G * B <= CUs);
   // each owns bpw bins, whose per-ND counts and ranks live in its LDS.  The
   // per-workgroup buffers are sized for the largest G (CU share 1).
@@ -2765,6 +3071,16 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   if (e == hipSuccess) e = hipMemset(P->stamps, 0, B * P->vcap * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(P->d_stats, 0, B * sizeof(ndnet_ndt_stats));
   if (e == hipSuccess) e = hipMemset(P->wq_ctr, 0, 128 * sizeof(uint32_t));
+  if (e == hipSuccess) {
+    // wq_heavy's division table: rc = RN(1/c), rl = RN((1 - c rc) / c), 1 - c rc exact (one fma)
+    std::vector<double> rt(2 * (n + 1), 0.0);
+    for (size_t c = 1; c <= n; c++) {
+      const double dc = (double)c, rc = 1.0 / dc;
+      rt[2 * c] = rc;
+      rt[2 * c + 1] = fma(-dc, rc, 1.0) / dc;
+    }
+    e = hipMemcpy(P->rtab, rt.data(), rt.size() * sizeof(double), hipMemcpyHostToDevice);
+  }
   {
     const size_t hb = (size_t)kWqNDs * (size_t)nb * sizeof(uint32_t);
     P->wq_lds = num_classes >= 0 && hb <= (size_t)kWqHistMax ? hb : 0;
@@ -2781,10 +3097,10 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   }
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_welford_q<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(kWqRt * sizeof(double) + 4 * ((batch + 1 + 3) & ~3) + kWqHistMax));
+                            (int)(kWqRt * sizeof(double) + 8 * ((batch + 1 + 3) & ~3) + kWqHistMax));
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_welford_q<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(kWqRt * sizeof(double) + 4 * ((batch + 1 + 3) & ~3) + kWqHistMax));
+                            (int)(kWqRt * sizeof(double) + 8 * ((batch + 1 + 3) & ~3) + kWqHistMax));
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_kl_merge<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(2 * kMergeLdsChunks * kChunk * sizeof(unsigned long long)));
@@ -2845,6 +3161,13 @@ int ndnet_ndt_set_front_staged(void* plan, int on) {
   return NDNET_OK;
 }
 
+int ndnet_ndt_set_heavy_threshold(void* plan, uint32_t min_samples) {
+  Plan* P = (Plan*)plan;
+  if (!P || min_samples == 0) return NDNET_ERR_ARG;
+  P->heavy_t = min_samples;
+  return NDNET_OK;
+}
+
 int ndnet_ndt_set_run_part(void* plan, int part) {
   Plan* P = (Plan*)plan;
   if (!P || part < 0 || part > 2) return NDNET_ERR_ARG;
@@ -2876,6 +3199,11 @@ int ndnet_ndt_set_timing(void* plan, int enable) {
   if (enable >= 2 && !P->fmarks) {
     HIPCHK(hipMalloc(&P->fmarks, (size_t)P->B * kFrontMarkStride * sizeof(unsigned long long)));
     HIPCHK(hipMemset(P->fmarks, 0, (size_t)P->B * kFrontMarkStride * sizeof(unsigned long long)));
+  }
+  if (enable >= 2 && !P->wq_marks) {
+    const size_t items = (size_t)P->B * (P->ndcap + (P->ndcap + 15) / 16);
+    HIPCHK(hipMalloc(&P->wq_marks, items * kWqMarkW * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(P->wq_marks, 0, items * kWqMarkW * sizeof(unsigned long long)));
   }
   if (enable >= 2 && !P->kl_marks) {
     HIPCHK(hipMalloc(&P->kl_marks, (size_t)P->B * 16 * sizeof(unsigned long long)));
@@ -2934,6 +3262,16 @@ int ndnet_ndt_debug_kl_marks(void* plan, unsigned long long* marks) {
   if (!P || !marks || !P->kl_marks) return NDNET_ERR_ARG;
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(marks, P->kl_marks, (size_t)P->B * 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return NDNET_OK;
+}
+
+int ndnet_ndt_debug_wq_marks(void* plan, unsigned long long* marks, uint32_t* items) {
+  Plan* P = (Plan*)plan;
+  if (!P || !marks || !items || !P->wq_marks) return NDNET_ERR_ARG;
+  HIPCHK(hipDeviceSynchronize());
+  const size_t cap = (size_t)P->B * (P->ndcap + (P->ndcap + 15) / 16);
+  *items = (uint32_t)cap;
+  HIPCHK(hipMemcpy(marks, P->wq_marks, cap * kWqMarkW * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return NDNET_OK;
 }
 

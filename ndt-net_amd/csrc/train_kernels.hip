@@ -481,10 +481,17 @@ __global__ __launch_bounds__(256) void k_row_argmax(const float* __restrict__ x,
 
 int launched() { return hipGetLastError() == hipSuccess ? 0 : -21; }
 
-// A/B switch read once (NDNET_TR_GEMM64=1: 64 x 64 tiles only)
 bool getenv_flag(const char* name) {
   const char* v = getenv(name);
   return v && v[0] == '1';
+}
+// A/B switch NDNET_TR_GEMM64=1 (64 x 64 tiles only), read once: the
+// process's tile choice is fixed at the first launch: a graph captured
+// before the variable changed and an eager step after it use the same
+// summation order
+bool gemm64_only() {
+  static const bool v = getenv_flag("NDNET_TR_GEMM64");
+  return v;
 }
 
 }  // namespace
@@ -504,7 +511,7 @@ extern "C" int ndnet_tr_gemm(const float* A, const float* B, float* C, const flo
   if (gz > 65535 || gy > 65535 || gx > (int64_t)INT32_MAX) return -20;
   // 128 x 128 tiles where they still give the chip >= 512 workgroups
   const int64_t big = ((M + 127) / 128) * ((N + 127) / 128) * gz;
-  const bool wide = M >= 128 && N >= 128 && big >= 512 && !getenv_flag("NDNET_TR_GEMM64");
+  const bool wide = M >= 128 && N >= 128 && big >= 512 && !gemm64_only();
   const dim3 grid(wide ? (unsigned)((N + 127) / 128) : (unsigned)gx, wide ? (unsigned)((M + 127) / 128) : (unsigned)gy,
                   (unsigned)gz);
   hipStream_t st = (hipStream_t)stream;

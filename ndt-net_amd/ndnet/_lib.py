@@ -72,6 +72,7 @@ EXPORTS = {
     "ndnet_ndt_set_front_staged": (_I, [_P, _I]),
     "ndnet_ndt_set_run_part": (_I, [_P, _I]),
     "ndnet_ndt_set_lazy_list": (_I, [_P, _I]),
+    "ndnet_ndt_set_heavy_threshold": (_I, [_P, ctypes.c_uint32]),
     "ndnet_ndt_debug_set_sync_timeout": (_I, [_P, ctypes.c_uint64]),
     "ndnet_ndt_run": (_I, [_P, _P, _P, _P, _P, _P, _P]),
     "ndnet_ndt_run_f64": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),
@@ -80,6 +81,7 @@ EXPORTS = {
     "ndnet_ndt_debug_set_epoch": (_I, [_P, ctypes.c_uint32]),
     "ndnet_ndt_debug_kl_marks": (_I, [_P, _P]),
     "ndnet_ndt_debug_front_marks": (_I, [_P, _P]),
+    "ndnet_ndt_debug_wq_marks": (_I, [_P, _P, ctypes.POINTER(ctypes.c_uint32)]),
     "ndnet_ndt_debug_front_wg_marks": (_I, [_P, _P, ctypes.POINTER(_I)]),
     "ndnet_ndt_set_timing": (_I, [_P, _I]),
     "ndnet_ndt_stage_ms": (_I, [_P, _P]),

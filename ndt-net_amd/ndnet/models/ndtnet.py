@@ -39,7 +39,12 @@ def _conv(cin: int, cout: int) -> nn.Conv1d:
 
 
 def _hip_train(conv: nn.Conv1d, bn, x: torch.Tensor) -> bool:
-    return x.is_cuda and conv.training and (bn is None or bn.training) and not _TRAIN_TORCH
+    """The HIP train kernels compute in fp32: any other input or weight dtype,
+    or an autocast region (which would have torch's convs run narrower), takes
+    the torch composition."""
+    return (x.is_cuda and conv.training and (bn is None or bn.training) and not _TRAIN_TORCH
+            and x.dtype == torch.float32 and conv.weight.dtype == torch.float32
+            and not torch.is_autocast_enabled("cuda"))
 
 
 def _block_pool(conv: nn.Conv1d, bn, x: torch.Tensor, relu: bool) -> torch.Tensor:

@@ -224,8 +224,11 @@ class _ConvBNPool(torch.autograd.Function):
     """``amax(relu(bn(conv(x))), dim=2)`` -> [B,C] without the [B,C,N]
     activation: the BatchNorm kernel's pool mode keeps each cloud's first
     maximum and its point; the backward sends the pooled gradient to that
-    point only.  (torch's amax backward splits a tie evenly; ties have
-    identical rows, so every parameter gradient is the same.)"""
+    point only.  That is the index routing of the reference's
+    ``torch.max(x, 2)`` (ndtnet.py:50, :224), not the even split of this
+    package's torch composition (``amax``): distinct points whose activations
+    round to the same fp32 maximum get different weight gradients from the
+    two (identical points give the same gradients either way)."""
 
     @staticmethod
     def forward(ctx, x, w, b, gamma, beta, run_mean, run_var, eps, momentum, relu):

@@ -92,6 +92,13 @@ class NdtPlan:
         include/ndnet_amd.h ndnet_ndt_set_lazy_list)."""
         _lib.check(_lib.lib().ndnet_ndt_set_lazy_list(self.handle, 1 if on else 0), "ndnet_ndt_set_lazy_list")
 
+    def set_heavy_threshold(self, min_samples: int) -> None:
+        """NDs with at least ``min_samples`` points get a whole wave in
+        k_welford_q (include/ndnet_amd.h ndnet_ndt_set_heavy_threshold;
+        identical results, default 256)."""
+        _lib.check(_lib.lib().ndnet_ndt_set_heavy_threshold(self.handle, int(min_samples)),
+                   "ndnet_ndt_set_heavy_threshold")
+
     @property
     def path(self) -> int:
         return int(_lib.lib().ndnet_ndt_get_path(self.handle))

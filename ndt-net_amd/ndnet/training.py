@@ -36,7 +36,9 @@ def accuracy_tensor(pred: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
     """Fraction of NDs whose argmax class matches (train.py:84-87), as a 0-d
     tensor on pred's device (no host sync).  On the GPU one HIP kernel
     (ndnet_tr_argmax_match: torch's reduction kernels took ~83 us per argmax)."""
-    if pred.is_cuda and pred.dtype == torch.float32 and gt.dtype == torch.float32:
+    if (pred.is_cuda and gt.is_cuda and pred.shape == gt.shape and pred.numel() > 0
+            and pred.dtype == torch.float32 and gt.dtype == torch.float32):
+        # the kernel indexes gt with pred's rows and columns: only for equal shapes
         from . import _lib
         p, g = pred.contiguous(), gt.contiguous()
         cnt = torch.zeros((), device=pred.device, dtype=torch.int32)

@@ -749,3 +749,39 @@ void orc_glibc_rand_points(double* out, uint64_t count, unsigned seed, int resee
   if (reseed) srand(seed);
   for (uint64_t i = 0; i < count; i++) out[i] = (double)rand() / RAND_MAX;
 }
+
+/* The division rule of the device's long-ND Welford path (k_welford_q,
+ * wq_heavy): t / n as fma(t, rc, t * rl) with rc = 1.0 / n and
+ * rl = fma(-n, rc, 1.0) / n.  Returns how many of `samples` random (t, n)
+ * pairs -- t over the operand range the fast path admits (2^-360 .. 2^302,
+ * both signs, random and few-bit mantissas), n in 1 .. n_max plus powers of
+ * two and their neighbours -- differ from the IEEE division t / n in any bit.
+ * Test infrastructure (tests/test_oracle.py). */
+static uint64_t rtab_rng(uint64_t* s) {
+  *s ^= *s << 13;
+  *s ^= *s >> 7;
+  *s ^= *s << 17;
+  return *s;
+}
+uint64_t orc_rtab_div_mismatches(uint64_t n_max, uint64_t samples, uint64_t seed) {
+  uint64_t s = seed * 0x9E3779B97F4A7C15ull + 1, bad = 0;
+  for (uint64_t i = 0; i < samples; i++) {
+    uint64_t r = rtab_rng(&s);
+    uint64_t n;
+    switch (r & 3) {
+      case 0: { const int k = (int)((r >> 2) % 32); n = (1ull << k) + ((r >> 8) % 3) - 1; if (!n) n = 1; break; }
+      default: n = 1 + (r >> 2) % n_max;
+    }
+    r = rtab_rng(&s);
+    uint64_t mant = (r >> 11) | (1ull << 52);
+    if ((r & 7) == 0) mant = ((r >> 3) & 0xffff) | 1;             /* few significant bits */
+    else if ((r & 7) == 1) mant = (1ull << 52) | ((r >> 3) & 0xf); /* near a power of two */
+    const int e = -360 + (int)(rtab_rng(&s) % 662);
+    double t = ldexp((double)mant, e - 52);
+    if (r & 8) t = -t;
+    const double dn = (double)n, rc = 1.0 / dn, rl = fma(-dn, rc, 1.0) / dn;
+    const double q = fma(t, rc, t * rl), ref = t / dn;
+    if (memcmp(&q, &ref, sizeof q) != 0 && !(q == 0.0 && ref == 0.0)) bad++;
+  }
+  return bad;
+}

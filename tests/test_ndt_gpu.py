@@ -608,3 +608,103 @@ def test_cu_share_results_identical(share, k):
             torch.cuda.synchronize()
             res.append((out.cpu().numpy(), [bytes(st) for st in plan.host_stats()]))
         assert np.array_equal(res[0][0], res[1][0]) and res[0][1] == res[1][1], kind
+
+
+def _run_thresholds(pts, k, thresholds, path=2, labels=None, num_classes=-1):
+    """One plan per heavy threshold over the same batch: rows, one-hot
+    classes, stats and every dumped intermediate (counts, means, pre- and
+    post-KL covariances, list, kept set)."""
+    import torch
+    from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
+    B, n, _ = pts.shape
+    res = []
+    for t in thresholds:
+        plan = NdtPlan(B, n, k, num_classes)
+        plan.set_path(path)
+        plan.set_lazy_list(False)
+        plan.set_heavy_threshold(t)
+        out = torch.empty((B, k, 12), dtype=torch.float32, device="cuda")
+        lbl = None if labels is None else torch.from_numpy(labels.astype(np.int32)).cuda()
+        oc = None if labels is None else torch.empty((B, k, num_classes + 1), dtype=torch.float32, device="cuda")
+        plan.run(torch.from_numpy(np.ascontiguousarray(pts, dtype=np.float32)).cuda(), lbl, out, oc)
+        torch.cuda.synchronize()
+        stats = plan.host_stats()
+        dumps = [_dump(plan, b, int(stats[b].num_nds), int(stats[b].num_events)) if stats[b].rc == 0 else None
+                 for b in range(B)]
+        res.append((out.cpu().numpy(), None if oc is None else oc.cpu().numpy(),
+                    [bytes(st) for st in stats], dumps, [int(st.num_nds) for st in stats]))
+    return res
+
+
+def _same(res):
+    o0, c0, s0, d0, _ = res[0]
+    for o, c, s, d, _ in res[1:]:
+        assert np.array_equal(o, o0)
+        assert (c is None and c0 is None) or np.array_equal(c, c0)
+        assert s == s0
+        for b in range(len(d0)):
+            if d0[b] is None:
+                assert d[b] is None
+                continue
+            for key in d0[b]:
+                assert np.array_equal(d[b][key], d0[b][key], equal_nan=True), (b, key)
+
+
+@pytest.mark.parametrize("path", [1, 2])
+def test_heavy_nds_equal_quad_path(path):
+    """k_welford_q's whole-wave path for long NDs (wq_heavy: the mean
+    recurrence on three lanes, per-sample products on 64, ordered sums on
+    six) against the lane-quad path: threshold 1 (every ND on a wave), 256
+    (the default), 2^31 (none), on clouds of few NDs (4096..20000 points -> 8..40
+    NDs: 100..2500 samples per ND, partial last blocks of every length) and
+    L clouds, with both binning paths; bit for bit, and the rows equal the
+    oracle's."""
+    import oracle as O
+    from ndnet.synthetic import make_batch
+    rng = np.random.default_rng(11)
+    few = np.stack([rng.uniform(-5, 5, (20_000, 3)).astype(np.float32),
+                    make_batch("L", 1, 20_000, seed0=3)[0],
+                    np.concatenate([rng.normal(0, 0.3, (12_000, 3)), rng.uniform(-9, 9, (8_000, 3))]).astype(np.float32)])
+    for pts, k in ((few, 8), (few, 40), (make_batch("L", 4, 50_000, seed0=40), 500)):
+        res = _run_thresholds(pts, k, (1, 256, 1 << 31), path=path)
+        _same(res)
+        for b in range(len(pts)):
+            pc, cov, r = O.downsample_f32(pts[b], k)
+            assert res[0][2][b] is not None
+            if r.rc == 0:
+                assert np.array_equal(res[0][0][b, :, :3], pc) and np.array_equal(res[0][0][b, :, 3:], cov), b
+        if k == 8:  # heavy NDs present at the default threshold
+            assert any(d is not None and d["nd_n"].max() >= 256 for d in res[0][3])
+
+
+def test_heavy_nds_labelled_and_full_size():
+    """The labelled path (class histograms of heavy NDs on their own wave) and
+    the full-size L batch (16 x 100k -> 1000: the default threshold's heavy
+    NDs, up to 1675 samples) equal the all-quad path bit for bit."""
+    from ndnet.synthetic import make_batch
+    rng = np.random.default_rng(12)
+    pts = make_batch("L", 3, 20_000, seed0=8)
+    lbl = rng.integers(0, 29, (3, 20_000))
+    _same(_run_thresholds(pts, 30, (1, 256, 1 << 31), labels=lbl, num_classes=28))
+    _same(_run_thresholds(make_batch("L", 16, 100_000), 1000, (256, 1 << 31)))
+
+
+def test_heavy_nds_float64_and_out_of_range():
+    """Double input (the legacy ABI's ndnet_ndt_run_f64) with heavy NDs: a
+    plain cloud, and one with coordinates outside the fast path's range
+    (|x| = 1e-95 < 2^-300: the wave refolds those NDs with IEEE divisions),
+    against the oracle's legacy chain."""
+    import oracle as O
+    from ndnet.preprocessing.ndt_legacy import NDT_Sampler
+    rng = np.random.default_rng(13)
+    for tiny in (False, True):
+        a = rng.uniform(-5, 5, (6000, 3))
+        if tiny:
+            a[::7, 1] = 1e-95 * np.sign(a[::7, 1])
+        s = NDT_Sampler(a)
+        pc, cov, _ = s.downsample(16)
+        ref = O.LegacyChain(a)
+        pc2, cov2 = ref.downsample(16)
+        assert np.array_equal(pc, pc2, equal_nan=True) and np.array_equal(cov, cov2, equal_nan=True), tiny
+        s.cleanup()
+        ref.cleanup()

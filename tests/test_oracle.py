@@ -200,3 +200,15 @@ def test_fullsize_fixture_pins_oracle():
                 rows[:, :3] = np.nan_to_num(pc.astype(np.float32), nan=0.0, posinf=0.0, neginf=0.0)
                 rows[:, 3:] = np.nan_to_num(cov.astype(np.float32), nan=0.0, posinf=0.0, neginf=0.0)
                 assert hashlib.sha256(rows.tobytes()).digest() == z[f"{cfg}_{kind}_sha"][b, lv].tobytes()
+
+
+def test_rtab_division_is_ieee():
+    """k_welford_q's long-ND path divides t / n as fma(t, rc, t * rl)
+    (csrc/ndt_kernels.hip, wq_heavy): bit-identical to the IEEE division on
+    10^7 random operands over the range its fast path admits, n up to 2^22
+    plus powers of two and their neighbours."""
+    import ctypes
+    L = O.lib()
+    L.orc_rtab_div_mismatches.restype = ctypes.c_uint64
+    L.orc_rtab_div_mismatches.argtypes = [ctypes.c_uint64] * 3
+    assert L.orc_rtab_div_mismatches(1 << 22, 10_000_000, 7) == 0

@@ -297,3 +297,40 @@ def test_row_argmax_matches_torch():
     _lib.check(_lib.lib().ndnet_row_argmax(x.data_ptr(), 15000, 29, out.data_ptr(),
                                            torch.cuda.current_stream().cuda_stream), "row_argmax")
     assert torch.equal(out.long(), torch.argmax(x, dim=2))
+
+
+def test_float64_train_forward_backward_takes_torch_path(monkeypatch):
+    """A float64 model in train mode on the GPU runs the torch composition
+    (the HIP train kernels are fp32 only): no train kernel is called, the
+    output is float64, and its gradients equal an explicit torch-path run."""
+    from ndnet.models import ndtnet, train_hip
+    torch.manual_seed(4)
+    model = ndtnet.NDTNetSegmentation(num_classes=5, feature_dim=64).cuda().double().train()
+    ref_model = copy.deepcopy(model)
+    pts, cov = _nds(2, 300, 12)
+    pts, cov = pts.double(), cov.double()
+
+    def boom(*a, **k):
+        raise AssertionError("HIP train kernel called for a float64 model")
+
+    monkeypatch.setattr(train_hip, "conv_bn_act", boom)
+    monkeypatch.setattr(train_hip, "conv_bn_act_pool", boom)
+    out = model(pts, cov)
+    assert out.dtype == torch.float64
+    out.sum().backward()
+    monkeypatch.setattr(ndtnet, "_TRAIN_TORCH", True)
+    ref = ref_model(pts, cov)
+    ref.sum().backward()
+    assert torch.equal(out, ref)
+    for (n, p1), p2 in zip(model.named_parameters(), ref_model.parameters()):
+        assert torch.equal(p1.grad, p2.grad), n
+
+
+def test_accuracy_shape_mismatch_does_not_take_kernel():
+    """accuracy_tensor with gt shaped unlike pred: the torch comparison (it
+    broadcasts or raises), never the kernel indexing gt with pred's rows."""
+    from ndnet.training import accuracy_tensor
+    pred = torch.randn(2, 10, 5, device="cuda")
+    gt = torch.nn.functional.one_hot(pred[0].argmax(-1), 5).float()  # [10, 5]: broadcasts
+    ref = (pred.argmax(dim=-1) == gt.argmax(dim=-1)).float().mean()
+    assert accuracy_tensor(pred, gt).item() == ref.item()

@@ -50,6 +50,179 @@ __global__ void indep(double* out, double a, double b, unsigned long long* cyc) 
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// The Welford mean chain per sample: t = x - m, then m += t / n as
+// RN(t rc + RN(t rl)) -- 4 dependent ops (sub, mul, fma, add) -- or the
+// refined-reciprocal division (sub, mul, fma, fma, add: 5), with FILL
+// independent FP64 ops per sample issued beside it (the work that could hide
+// in the chain's bubbles).
+template <int FIVE, int FILL>
+__global__ void meanchain(double* out, double a, double b, unsigned long long* cyc) {
+  double m = a + threadIdx.x * 1e-9, x = b, rc = 1.0 / 3.0, rl = 1e-17, cn = 3.0;
+  double f[FILL > 0 ? FILL : 1];
+  for (int k = 0; k < (FILL > 0 ? FILL : 1); k++) f[k] = a + k;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#pragma unroll 1
+  for (int i = 0; i < kIters; i++) {
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+      const double t = x - m;
+      double q;
+      if constexpr (FIVE) {
+        const double q0 = t * rc;
+        const double rem = fma(-cn, q0, t);
+        q = fma(rem, rc, q0);
+      } else {
+        const double p = t * rl;
+        q = fma(t, rc, p);
+      }
+      m = m + q;
+#pragma unroll
+      for (int k = 0; k < FILL; k++) f[k] = fma(f[k], b, a);
+    }
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+  double s = m;
+  for (int k = 0; k < FILL; k++) s += f[k];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+// wq_heavy's phase 1 as it runs in k_welford_q: lanes 0..2 (or all lanes,
+// EXEC3 = 0) run the mean recurrence over 64-sample blocks whose x and
+// (rc, rl) come from LDS (XR: 0 registers, 1 LDS), writing each mean to LDS
+// (MW), the next group's operands loaded a group ahead.
+template <int XR, int MW, int EXEC3, int PIN = 0>
+__global__ void phase1(double* out, double a, double b, unsigned long long* cyc) {
+  __shared__ double X[3][65];
+  __shared__ double M[3][67];
+  __shared__ double2 R[64];
+  const int lane = threadIdx.x;
+  for (int i = lane; i < 3 * 65; i += 64) (&X[0][0])[i] = a + i * 1e-3;
+  R[lane] = make_double2(1.0 / (lane + 1), 1e-17 * (lane + 1));
+  __syncthreads();
+  double m = b;
+  const int ax = lane < 3 ? lane : 0;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  if (!EXEC3 || lane < 3) {
+    const double* xa = &X[ax][0];
+    double* ma = &M[ax][1];
+#pragma unroll 1
+    for (int it = 0; it < kIters / 8; it++) {
+      double xA[8], xB[8];
+      double2 rA[8], rB[8];
+      auto ld = [&](double (&x)[8], double2 (&r)[8], int i0) {
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          if (XR) { x[u] = xa[i0 + u]; r[u] = R[i0 + u]; }
+          else { x[u] = a + u; r[u] = make_double2(0.25 + u, 1e-17); }
+        }
+      };
+      auto ch = [&](const double (&x)[8], const double2 (&r)[8], int i0) {
+        double mm[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const double t = x[u] - m;
+          m = m + fma(t, r[u].x, t * r[u].y);
+          mm[u] = m;
+          if (MW == 1) ma[i0 + u] = m;
+        }
+        if (MW == 2) {
+#pragma unroll
+          for (int u = 0; u < 8; u++) ma[i0 + u] = mm[u];
+        }
+      };
+      ld(xA, rA, 0);
+      for (int i0 = 0; i0 < 64; i0 += 16) {
+        ld(xB, rB, i0 + 8);
+        if (PIN) asm volatile("" ::: "memory");  // the loads stay ahead of the chain they do not feed
+        ch(xA, rA, i0);
+        if (i0 + 16 < 64) ld(xA, rA, i0 + 16);
+        if (PIN) asm volatile("" ::: "memory");
+        ch(xB, rB, i0 + 8);
+      }
+      asm volatile("" ::: "memory");
+    }
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+  out[blockIdx.x * blockDim.x + threadIdx.x] = m + M[ax][5];
+}
+
+// Phase 1 without LDS reads: lanes 0..2 load their own coordinate from global
+// memory (a dword per sample, immediate offsets), (rc, rl) arrive in SGPRs
+// (scalar loads of a uniform table), the mean goes out per sample
+// (MW: 0 none, 1 ds_write_b64, 2 global_store_dwordx2).
+template <int MW>
+__global__ void phase1g(double* out, const float* __restrict__ pts, const double2* __restrict__ rt,
+                        double* mout, unsigned long long* cyc) {
+  __shared__ double M[3][67];
+  const int lane = threadIdx.x;
+  const int ax = lane < 3 ? lane : 0;
+  double m = 0.5;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  if (lane < 3) {
+    double* ma = &M[ax][1];
+#pragma unroll 1
+    for (int it = 0; it < kIters / 8; it++) {
+      const float* p = pts + 3 * 64 * (it & 15) + ax;
+      const double2* r = rt + 64 * (it & 15);
+      double* mg = mout + 3 * 64 * (it & 15) + ax * 64;
+      float xA[8], xB[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) xA[u] = p[3 * u];
+      for (int i0 = 0; i0 < 64; i0 += 16) {
+#pragma unroll
+        for (int u = 0; u < 8; u++) xB[u] = p[3 * (i0 + 8 + u)];
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const double2 q = r[i0 + u];
+          const double t = (double)xA[u] - m;
+          m = m + fma(t, q.x, t * q.y);
+          if (MW == 1) ma[i0 + u] = m;
+          if (MW == 2) mg[i0 + u] = m;
+        }
+        if (i0 + 16 < 64) {
+#pragma unroll
+          for (int u = 0; u < 8; u++) xA[u] = p[3 * (i0 + 16 + u)];
+        }
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const double2 q = r[i0 + 8 + u];
+          const double t = (double)xB[u] - m;
+          m = m + fma(t, q.x, t * q.y);
+          if (MW == 1) ma[i0 + 8 + u] = m;
+          if (MW == 2) mg[i0 + 8 + u] = m;
+        }
+      }
+    }
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+  out[blockIdx.x * blockDim.x + threadIdx.x] = m + M[ax][5];
+}
+
+template <int MW>
+static void rung(const char* name) {
+  double *out, *mout;
+  float* pts;
+  double2* rt;
+  unsigned long long* cyc;
+  hipMalloc(&out, 64 * sizeof(double));
+  hipMalloc(&mout, 3 * 64 * 16 * sizeof(double));
+  hipMalloc(&pts, 3 * 64 * 16 * sizeof(float));
+  hipMalloc(&rt, 64 * 16 * sizeof(double2));
+  hipMemset(pts, 0, 3 * 64 * 16 * sizeof(float));
+  hipMemset(rt, 0, 64 * 16 * sizeof(double2));
+  hipMalloc(&cyc, sizeof(unsigned long long));
+  for (int r = 0; r < 2; r++) hipLaunchKernelGGL(phase1g<MW>, dim3(1), dim3(64), 0, 0, out, pts, rt, mout, cyc);
+  hipDeviceSynchronize();
+  unsigned long long c;
+  hipMemcpy(&c, cyc, sizeof(c), hipMemcpyDeviceToHost);
+  printf("%-44s: %.2f cycles per sample\n", name, (double)c / ((double)(kIters / 8) * 64));
+}
+
 template <typename K>
 static void run(const char* name, K kern, int blocks, int threads, int ops_per_iter) {
   double* out;
@@ -78,5 +251,27 @@ int main() {
   run("independent v_fma_f64 x8", indep<8>, 1, 64, 64);
   run("independent v_fma_f64 x8, 4 waves (1 per SIMD)", indep<8>, 1, 256, 64);
   run("independent v_fma_f64 x8, 8 waves (2 per SIMD)", indep<8>, 1, 512, 64);
+  // cycles per sample (ops_per_iter = 8 samples)
+  run("mean chain 4-op, per sample", meanchain<0, 0>, 1, 64, 8);
+  run("mean chain 5-op, per sample", meanchain<1, 0>, 1, 64, 8);
+  run("mean chain 4-op + 2 fill, per sample", meanchain<0, 2>, 1, 64, 8);
+  run("mean chain 4-op + 4 fill, per sample", meanchain<0, 4>, 1, 64, 8);
+  run("mean chain 4-op + 8 fill, per sample", meanchain<0, 8>, 1, 64, 8);
+  run("mean chain 4-op, 2 waves/SIMD, per sample", meanchain<0, 0>, 1, 512, 8);
+  run("mean chain 4-op + 4 fill, 2 waves/SIMD", meanchain<0, 4>, 1, 512, 8);
+  run("mean chain 5-op + 8 fill, per sample", meanchain<1, 8>, 1, 64, 8);
+  // cycles per sample (64 samples per iteration, kIters / 8 iterations)
+  run("phase1: chain only, 3 lanes", phase1<0, 0, 1>, 1, 64, 8);
+  run("phase1: + LDS x, R reads, 3 lanes", phase1<1, 0, 1>, 1, 64, 8);
+  run("phase1: + LDS M writes, 3 lanes", phase1<1, 1, 1>, 1, 64, 8);
+  run("phase1: chain + M writes (no reads), 3 lanes", phase1<0, 1, 1>, 1, 64, 8);
+  run("phase1: LDS reads + writes, 64 lanes", phase1<1, 1, 0>, 1, 64, 8);
+  run("phase1: pinned LDS reads, 3 lanes", phase1<1, 0, 1, 1>, 1, 64, 8);
+  run("phase1: pinned LDS reads + writes, 3 lanes", phase1<1, 1, 1, 1>, 1, 64, 8);
+  run("phase1: pinned reads + group-end writes", phase1<1, 2, 1, 1>, 1, 64, 8);
+  run("phase1: group-end writes only", phase1<0, 2, 1, 1>, 1, 64, 8);
+  rung<0>("phase1g: global x, SGPR rc/rl, no M out");
+  rung<1>("phase1g: + ds_write_b64 per sample");
+  rung<2>("phase1g: + global_store_dwordx2 per sample");
   return 0;
 }
