@@ -265,7 +265,7 @@ def main() -> None:
 
     # ---- the other synthetic distribution on the same graph (SURVEY §8d "also
     # report L"): the L clouds exercise the prune (~128 of ~1128 NDs removed) ----
-    other = None
+    other, other_pts = None, None
     if not args.eager and not levels and not args.no_other:
         okind = "L" if args.kind == "U" else "U"
         opts = torch.from_numpy(make_batch(okind, B, n, seed0=shard0)).to(dev)
@@ -284,6 +284,7 @@ def main() -> None:
             t_o = D.max_over_ranks(time.perf_counter() - t0)
         assert all(st.rc == 0 for st in all_run_stats()), [st.rc for st in all_run_stats()]
         ost = run_plan().host_stats()
+        other_pts = opts
         other = {"kind": okind, "value": round(total_clouds / t_o, 2), "unit": "clouds/s",
                  "ms_per_step": round(1e3 * t_o / args.steps, 4),
                  "pruned_per_cloud": round(float(np.mean([st.num_nds - k for st in ost])), 1)}
@@ -374,26 +375,64 @@ def main() -> None:
                                 "workload": f"batch {B} x {k} x 12-D NDs, NDTNetSegmentation F={F} C={C} eval forward alone"},
         }
 
+        # ---- config C5 (BASELINE configs[4], tools/train_multiscale.py): the
+        # multiscale step -- downsample to 2000, prune to 1000 and 500, a
+        # forward per level -- through the same stream pipeline ----
+        c5 = (2000, 1000, 500)
+        from ndnet.pipeline import PipelinedSegmentation
+        p5 = PipelinedSegmentation(model, c5[0], B, n, device=dev, levels=c5)
+        p5.load_resident(pts)
+        with torch.no_grad():
+            t5 = time.perf_counter()
+            while (time.perf_counter() - t5) * 1e3 < min(args.settle_ms, 200.0):
+                p5.replay_steps(12)
+                torch.cuda.synchronize()
+            p5.replay_steps(max(2, args.warmup))
+            torch.cuda.synchronize()
+            D.barrier()
+            t5 = time.perf_counter()
+            p5.replay_steps(args.steps)
+            torch.cuda.synchronize()
+            D.barrier()
+            t5 = D.max_over_ranks(time.perf_counter() - t5)
+        assert all(st.rc == 0 for pl in p5.plans for st in pl.host_stats())
+        config_lines["C5_multiscale"] = {
+            "value": round(total_clouds / t5, 2), "unit": "clouds/s", "ms_per_step": round(1e3 * t5 / args.steps, 4),
+            "workload": f"batch {B} x {n} pts ({args.kind}) -> downsample {c5[0]} -> prune {c5[1]} -> prune {c5[2]}, "
+                        f"NDTNetSegmentation F={F} C={C} eval per level (3 forwards per step), stream pipeline"}
+        del p5
+
     # ---- stage timing (HIP events on the stream the kernels run on) ----
     # Each timed region starts behind a ~2 ms device-side sleep on the same
     # stream, so the host has queued every launch of the region before its
     # first event fires: the events bracket kernel time, not Python launch gaps.
     plan = get_plan(B, n, k, -1, dev)
-    _lib.lib().ndnet_ndt_set_timing(plan.handle, 1)
     stage_names = ["reset+limits", "bisection (15 launches)", "dense ids", "binning", "welford + LU chains",
                    "kl (scores, order, prune, rows)"]
-    stage_ms = np.zeros(6)
-    fwd_ms = 0.0
     reps = max(3, min(args.steps, 10))
     sleep_cycles = int(5e6)
+
+    def ndt_stage_ms(points):
+        """Per-stage ms of ndt_preprocessing on ``points`` (the plan's events)."""
+        _lib.lib().ndnet_ndt_set_timing(plan.handle, 1)
+        acc = np.zeros(6)
+        with torch.no_grad():
+            for _ in range(reps):
+                torch.cuda._sleep(sleep_cycles)
+                ndt_preprocessing(k, points)
+                ms = np.zeros(6, np.float32)
+                _lib.lib().ndnet_ndt_stage_ms(plan.handle, ms.ctypes.data)
+                acc += ms
+        _lib.lib().ndnet_ndt_set_timing(plan.handle, 0)
+        return acc / reps
+
+    stage_ms = ndt_stage_ms(pts)
+    other_stage_ms = ndt_stage_ms(other_pts) if other_pts is not None else None
+    fwd_ms = 0.0
     pointnet_hip.chain_timing = []
     with torch.no_grad():
+        p, c, _ = ndt_preprocessing(k, pts)
         for _ in range(reps):
-            torch.cuda._sleep(sleep_cycles)
-            p, c, _ = ndt_preprocessing(k, pts)
-            ms = np.zeros(6, np.float32)
-            _lib.lib().ndnet_ndt_stage_ms(plan.handle, ms.ctypes.data)
-            stage_ms += ms
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda._sleep(sleep_cycles)
             e0.record()
@@ -401,8 +440,6 @@ def main() -> None:
             e1.record()
             e1.synchronize()
             fwd_ms += e0.elapsed_time(e1)
-    _lib.lib().ndnet_ndt_set_timing(plan.handle, 0)
-    stage_ms /= reps
     fwd_ms /= reps
     chain_in_fwd_ms = np.zeros(4)
     for i, e0, e1 in pointnet_hip.chain_timing:
@@ -459,6 +496,11 @@ def main() -> None:
         stage_names = ["k_front (limits, bisection, dense ids, binning)", "welford + LU chains",
                        "kl (scores, order, prune, rows)"]
         stage_ms = np.array([stage_ms[0], stage_ms[4], stage_ms[5]])
+        if other_stage_ms is not None:
+            other_stage_ms = np.array([other_stage_ms[0], other_stage_ms[4], other_stage_ms[5]])
+    if other is not None and other_stage_ms is not None:
+        other["stages_ms"] = {nm: round(float(v), 4) for nm, v in zip(stage_names, other_stage_ms)}
+        other["stages_basis"] = "per-stage HIP events around ndt_preprocessing on the other distribution's batch"
     ndt_single = {  # stage index -> (kernel, algorithmic bytes per launch, what)
         0: ("k_front", 24.0 * n * B, "f32 xyz read once + written once grouped by ND (12 N + 12 N per cloud)")
            if front else ("k_limits", 12.0 * n * B, "f32 xyz read once (12 N per cloud)"),

@@ -186,6 +186,7 @@ struct Plan {
   int run_part;               // ndnet_ndt_set_run_part: 0 whole run, 1 front only, 2 from k_welford_q on
   uint32_t* heavy;            // [B][ndcap] the heavy NDs of each cloud (CloudCtl::heavy_n of them)
   double* rtab;               // [n + 1][2] (rc, rl) per count for wq_heavy's divisions
+  uint32_t* lu_done;          // [B][ceil(ndcap / 64)] k_welford_q's per-group completion counters (re-armed to 0)
   uint32_t heavy_t;           // NDs with >= heavy_t samples take wq_heavy (ndnet_ndt_set_heavy_threshold)
 };
 
@@ -939,14 +940,19 @@ __device__ inline uint32_t qslot_of_dir(uint32_t d) {  // q-slot of the neighbou
 // off-diagonal u_a t_b and its division by n_i -- depends only on that
 // sequence and the sample, and only the sums m2 += t u and cov_ab += u_a t_b / n
 // must run in sample order.  So per 64-sample block:
-//   0. every lane loads one sample (record + its (rc, rl) entry);
-//   1. lanes 0..2 (one axis each) run the mean recurrence alone: 4 dependent
-//      FP64 operations per sample, the means to LDS;
-//   2. every lane computes its own sample's six addends from the means;
-//   3. lanes 0..5 add them in sample order (one accumulator each).
+//   0. every lane loads one sample (its record and (rc, rl)), the block's
+//      coordinates go to LDS;
+//   1. lanes 0..2 (one axis each) run the mean recurrence, 4 dependent FP64
+//      operations per sample, (rc, rl) from scalar loads, the means to LDS;
+//      in the same loop lanes 3..8 add the PREVIOUS block's addends in sample
+//      order (one accumulator each: m2 of the three axes, cov_01, cov_12,
+//      cov_02): one add per sample beside the recurrence, its latency hidden;
+//   2. every lane computes its own sample's six addends from the means.
 // The same IEEE operations on the same operands in the same order as the
-// reference (normal_distributions.c:75-103), so the same bits; ~7 wave
-// instructions per sample instead of ~18, on one ND.
+// reference (normal_distributions.c:75-103), so the same bits.  LDS traffic
+// of the loop is one 16-byte read and one 16-byte write per lane per two
+// samples (the loop's operands are loaded a group ahead; a lone wave pays
+// ~15-30 cycles per LDS instruction: tools/ubench/fp64_latency.hip).
 //
 // The division t / n is RN(t rc + RN(t rl)) with rc ~ 1/n (within an ulp) and
 // rl = RN((1 - n rc) / n) (1 - n rc is exact): t rc + RN(t rl) is within
@@ -957,11 +963,10 @@ __device__ inline uint32_t qslot_of_dir(uint32_t d) {  // q-slot of the neighbou
 // the coordinates the fast path admits); a zero t may give a zero of the
 // other sign, which no sum can see (they start at +0 and never become -0).
 // tests/test_oracle.py::test_rtab_division_is_ieee checks the rule against
-// the division on 10^7 operands.
-constexpr int kHvXS = 65;  // LDS row strides (doubles) of the heavy stage: distinct banks for lanes 0..5
-constexpr int kHvMS = 67;
-constexpr int kHvVS = 65;
-constexpr int kHvLds = 3 * kHvXS + 3 * kHvMS + 6 * kHvVS;  // 786 doubles = 6288 B per wave
+// the division on 10^7 operands.  rtab[0] = (0, 0): a step with it is an
+// exact no-op (t + 0), which pads the last block's recurrence to 64 steps.
+constexpr int kHvS = 66;  // LDS row stride (doubles): 16-byte rows on distinct banks for lanes 0..8
+constexpr int kHvLds = 12 * kHvS;  // X[3], M[3], V[6] rows: 792 doubles = 6336 B per wave
 
 template <typename T>
 struct HvRec {
@@ -980,34 +985,159 @@ __device__ inline void hv_load(HvRec<T>& h, const T* __restrict__ rec, const dou
   h.r = rtab[q + 1];
 }
 
-// Phase 1 over one group of 8 samples (lanes 0..2): x and (rc, rl) already
-// in registers (loaded a group ahead, so no LDS latency is waited out).
-template <bool kChk>  // kChk: the block's last group may be partial (nb wave-uniform)
-__device__ inline void hv_chain8(double& m, const double (&x)[8], const double2 (&r)[8], double* __restrict__ ma,
-                                 uint32_t i0, uint32_t nb) {
+// 8 steps of the fused loop: lanes 0..2 the recurrence (m), lanes 3..8 the
+// ordered sums (acc); xv = the lane's coordinate or addend, r = (rc, rl) in
+// scalar registers; the means (garbage in lanes 3..8) kept for the write.
+__device__ inline void hv_steps8(double& m, double& acc, const double (&xv)[8], const double2 (&r)[8],
+                                 double (&mo)[8]) {
 #pragma unroll
   for (int u = 0; u < 8; u++) {
-    if (!kChk || i0 + u < nb) {
-      const double t = x[u] - m;
-      m = m + fma(t, r[u].x, t * r[u].y);
-      ma[i0 + u] = m;
-    }
+    const double t = xv[u] - m;
+    m = m + fma(t, r[u].x, t * r[u].y);
+    acc = acc + xv[u];
+    mo[u] = m;
   }
 }
-__device__ inline void hv_load8(double (&x)[8], double2 (&r)[8], const double* __restrict__ xa,
-                                const double2* __restrict__ R, uint32_t i0) {
+
+template <bool kTail>  // kTail: the last block, steps past nb use rtab[0] (no-ops)
+__device__ inline void hv_ops8(double (&xv)[8], double2 (&r)[8], const double* __restrict__ rd,
+                               const double2* __restrict__ rtab, uint32_t q0, uint32_t i0, uint32_t nb) {
+#pragma unroll
+  for (int u = 0; u < 8; u += 2) {
+    const double2 v = *reinterpret_cast<const double2*>(rd + i0 + u);
+    xv[u] = v.x;
+    xv[u + 1] = v.y;
+  }
+#pragma unroll
+  for (int u = 0; u < 8; u++) r[u] = rtab[kTail ? (i0 + u < nb ? q0 + i0 + u + 1 : 0u) : q0 + i0 + u + 1];
+}
+
+__device__ inline void hv_write8(double* __restrict__ wr, const double (&mo)[8], uint32_t i0) {
+#pragma unroll
+  for (int u = 0; u < 8; u += 2) *reinterpret_cast<double2*>(wr + i0 + u) = make_double2(mo[u], mo[u + 1]);
+}
+
+// the fused loop over one block: 64 steps, operands a group of 8 ahead, each
+// group's means written while the next group runs
+template <bool kTail>
+__device__ inline void hv_block(double& m, double& acc, const double* __restrict__ rd, double* __restrict__ wr,
+                                const double2* __restrict__ rtab, uint32_t q0, uint32_t nb) {
+  double xA[8], xB[8], mA[8], mB[8];
+  double2 rA[8], rB[8];
+  hv_ops8<kTail>(xA, rA, rd, rtab, q0, 0, nb);
+  hv_ops8<kTail>(xB, rB, rd, rtab, q0, 8, nb);
+  asm volatile("" ::: "memory");
+  hv_steps8(m, acc, xA, rA, mA);
+#pragma unroll
+  for (uint32_t i0 = 8; i0 < 64; i0 += 16) {
+    hv_write8(wr, mA, i0 - 8);
+    if (i0 + 8 < 64) hv_ops8<kTail>(xA, rA, rd, rtab, q0, i0 + 8, nb);
+    asm volatile("" ::: "memory");
+    hv_steps8(m, acc, xB, rB, mB);
+    hv_write8(wr, mB, i0);
+    if (i0 + 16 < 64) hv_ops8<kTail>(xB, rB, rd, rtab, q0, i0 + 16, nb);
+    asm volatile("" ::: "memory");
+    if (i0 + 8 < 64) hv_steps8(m, acc, xA, rA, mA);
+  }
+}
+
+// The full-block loop with its memory operations as inline asm, so that
+// their order and waits are exactly this: per group G of 8 steps, one
+// s_waitcnt lgkmcnt(0) covers its operands (issued a group earlier: four
+// ds_read_b128 of the lane's row, two s_load_dwordx16 of the (rc, rl) table)
+// and the mean writes of group G - 2; then the means of group G - 1 are
+// written and group G + 1's operands issued before group G's steps.  (With
+// compiler-placed loads the scalar loads, which return out of order, made
+// every wait an lgkmcnt(0) right at the use.)  The wait's in-out operands
+// keep every use of the loaded registers behind it.
+typedef unsigned int hv_u16 __attribute__((ext_vector_type(16)));
+typedef double hv_d2 __attribute__((ext_vector_type(2)));  // native vector (HIP's double2 is a struct)
+
+struct HvOps {
+  hv_d2 x[4];  // 8 steps' coordinates (lanes 0..2) or addends (lanes 3..8)
+  hv_u16 r0, r1;  // (rc, rl) of the 8 steps, in scalar registers
+};
+
+template <int G>
+__device__ inline void hv_issue(HvOps& o, uint32_t rda, const double2* rtq) {
+  hv_d2 x0, x1, x2, x3;
+  hv_u16 r0, r1;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(x0) : "v"(rda), "n"(64 * G));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(x1) : "v"(rda), "n"(64 * G + 16));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(x2) : "v"(rda), "n"(64 * G + 32));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(x3) : "v"(rda), "n"(64 * G + 48));
+  asm volatile("s_load_dwordx16 %0, %1, %2" : "=s"(r0) : "s"(rtq), "n"(128 * G));
+  asm volatile("s_load_dwordx16 %0, %1, %2" : "=s"(r1) : "s"(rtq), "n"(128 * G + 64));
+  o.x[0] = x0;
+  o.x[1] = x1;
+  o.x[2] = x2;
+  o.x[3] = x3;
+  o.r0 = r0;
+  o.r1 = r1;
+}
+__device__ inline void hv_wait(HvOps& o) {
+  hv_d2 x0 = o.x[0], x1 = o.x[1], x2 = o.x[2], x3 = o.x[3];
+  hv_u16 r0 = o.r0, r1 = o.r1;
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+s"(r0), "+s"(r1));
+  o.x[0] = x0;
+  o.x[1] = x1;
+  o.x[2] = x2;
+  o.x[3] = x3;
+  o.r0 = r0;
+  o.r1 = r1;
+}
+template <int G>
+__device__ inline void hv_put(uint32_t wra, const double (&mo)[8]) {
+  const hv_d2 a = {mo[0], mo[1]}, b = {mo[2], mo[3]}, c = {mo[4], mo[5]}, d = {mo[6], mo[7]};
+  asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(wra), "v"(a), "n"(64 * G));
+  asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(wra), "v"(b), "n"(64 * G + 16));
+  asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(wra), "v"(c), "n"(64 * G + 32));
+  asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(wra), "v"(d), "n"(64 * G + 48));
+}
+__device__ inline double hv_sd(const hv_u16& v, int k) {
+  return __builtin_bit_cast(double, (unsigned long long)v[2 * k] | ((unsigned long long)v[2 * k + 1] << 32));
+}
+__device__ inline void hv_steps(double& m, double& acc, const HvOps& o, double (&mo)[8]) {
 #pragma unroll
   for (int u = 0; u < 8; u++) {
-    x[u] = xa[i0 + u];
-    r[u] = R[i0 + u];
+    const double xv = o.x[u >> 1][u & 1];
+    const hv_u16& r = u < 4 ? o.r0 : o.r1;
+    const double rc = hv_sd(r, 2 * (u & 3)), rl = hv_sd(r, 2 * (u & 3) + 1);
+    const double t = xv - m;
+    m = m + fma(t, rc, t * rl);
+    acc = acc + xv;
+    mo[u] = m;
   }
+}
+template <int G>  // group G of a full block: wait for its operands, write G - 1's means, issue G + 1's operands, step
+__device__ inline void hv_group(double& m, double& acc, HvOps& cur, HvOps& nxt, double (&mcur)[8],
+                                double (&mprev)[8], uint32_t rda, uint32_t wra, const double2* rtq) {
+  hv_wait(cur);
+  if constexpr (G > 0) hv_put<G - 1>(wra, mprev);
+  if constexpr (G < 7) hv_issue<G + 1>(nxt, rda, rtq);
+  hv_steps(m, acc, cur, mcur);
+}
+__device__ inline void hv_block_asm(double& m, double& acc, uint32_t rda, uint32_t wra, const double2* rtq) {
+  HvOps A, B;
+  double mA[8], mB[8];
+  hv_issue<0>(A, rda, rtq);
+  hv_group<0>(m, acc, A, B, mA, mB, rda, wra, rtq);
+  hv_group<1>(m, acc, B, A, mB, mA, rda, wra, rtq);
+  hv_group<2>(m, acc, A, B, mA, mB, rda, wra, rtq);
+  hv_group<3>(m, acc, B, A, mB, mA, rda, wra, rtq);
+  hv_group<4>(m, acc, A, B, mA, mB, rda, wra, rtq);
+  hv_group<5>(m, acc, B, A, mB, mA, rda, wra, rtq);
+  hv_group<6>(m, acc, A, B, mA, mB, rda, wra, rtq);
+  hv_group<7>(m, acc, B, A, mB, mA, rda, wra, rtq);
+  hv_put<7>(wra, mB);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the block's means are in LDS for phase 2
 }
 
 template <typename T, bool kStamp = false>  // kStamp: phase cycle totals to ph[0..2] (timing level 2)
 __device__ inline void wq_heavy(const T* __restrict__ rec, uint32_t cnt, const double2* __restrict__ rtab,
                                 double* __restrict__ lds, uint32_t lane, double& mean, double& m2, double& off,
                                 bool& bad, unsigned long long* ph = nullptr) {
-  unsigned long long ts = 0, c02 = 0, c1 = 0, c3 = 0;
+  unsigned long long ts = 0, c0 = 0, c1 = 0, c2 = 0;
   auto stamp = [&](unsigned long long& acc) __attribute__((always_inline)) {
     if constexpr (kStamp) {
       const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -1016,132 +1146,85 @@ __device__ inline void wq_heavy(const T* __restrict__ rec, uint32_t cnt, const d
     }
   };
   if constexpr (kStamp) ts = __builtin_amdgcn_s_memtime();
-  double* X = lds;                    // [3][kHvXS] the block's coordinates
-  double* M = lds + 3 * kHvXS;        // [3][kHvMS] [0] the mean before the block, [1 + i] after sample i
-  double* V = M + 3 * kHvMS;          // [6][kHvVS] per-sample addends: t u (3 axes), u_a t_b / n (3 pairs)
-  double2* R = reinterpret_cast<double2*>(V);  // [64] (rc, rl) of the block's samples (phases 0-1; V from 2 on)
+  double* X = lds;              // [3][kHvS] the block's coordinates
+  double* M = lds + 3 * kHvS;   // [3][kHvS] [1] the mean before the block, [2 + i] after sample i
+  double* V = lds + 6 * kHvS;   // [6][kHvS] the previous block's addends: t u (3 axes), u_a t_b / n (3 pairs)
   const uint32_t a = lane < 3 ? lane : 0;
+  // the fused loop's rows: lanes 0..2 read X[a] and write M[a][2..]; lanes
+  // 3..8 read V[lane - 3] and write their (unused) means back over what they
+  // have read
+  const double* rd = lane < 3 ? X + a * kHvS : V + (lane < 9 ? lane - 3 : 0) * kHvS;
+  double* wr = lane < 3 ? M + a * kHvS + 2 : V + (lane < 9 ? lane - 3 : 0) * kHvS;
   double m = 0.0, acc = 0.0;
   bool out = false;
+#pragma unroll
+  for (int p = 0; p < 6; p++) V[p * kHvS + lane] = 0.0;  // block 0 has no previous addends
   HvRec<T> h0, h1, h2;  // blocks q0, q0 + 64, q0 + 128 in flight
   hv_load(h0, rec, rtab, 0, lane, cnt);
   hv_load(h1, rec, rtab, 64, lane, cnt);
   hv_load(h2, rec, rtab, 128, lane, cnt);
+  uint32_t nb = 64;
   for (uint32_t q0 = 0; q0 < cnt; q0 += 64) {
     const HvRec<T> h = h0;
     h0 = h1;
     h1 = h2;
     hv_load(h2, rec, rtab, q0 + 192, lane, cnt);
-    const uint32_t nb = cnt - q0 < 64u ? cnt - q0 : 64u;  // samples of this block (wave-uniform)
+    nb = cnt - q0 < 64u ? cnt - q0 : 64u;  // samples of this block (wave-uniform)
     const double x0 = (double)h.x, x1 = (double)h.y, x2 = (double)h.z;
     if constexpr (!std::is_same<T, float>::value)
       out |= lane < nb && !(wq_in_range(h.x) && wq_in_range(h.y) && wq_in_range(h.z));
-    // 0. the block to LDS; the running mean as M[.][0]
+    // 0. the block to LDS; the running mean as M[.][1]
     X[lane] = x0;
-    X[kHvXS + lane] = x1;
-    X[2 * kHvXS + lane] = x2;
-    R[lane] = h.r;
-    if (lane < 3) M[a * kHvMS] = m;
+    X[kHvS + lane] = x1;
+    X[2 * kHvS + lane] = x2;
+    if (lane < 3) M[a * kHvS + 1] = m;
     asm volatile("" ::: "memory");  // one wave's LDS operations complete in order
-    stamp(c02);
-    // 1. the mean recurrence, lanes 0..2, 8 samples per group, the next
-    //    group's operands loaded before this group's chain
-    if (lane < 3) {
-      const double* xa = X + a * kHvXS;
-      double* ma = M + a * kHvMS + 1;
-      double xA[8], xB[8];
-      double2 rA[8], rB[8];
-      hv_load8(xA, rA, xa, R, 0);
-      if (nb == 64) {
-        for (uint32_t i0 = 0; i0 < 64; i0 += 16) {
-          hv_load8(xB, rB, xa, R, i0 + 8);
-          hv_chain8<false>(m, xA, rA, ma, i0, 64);
-          if (i0 + 16 < 64) hv_load8(xA, rA, xa, R, i0 + 16);
-          hv_chain8<false>(m, xB, rB, ma, i0 + 8, 64);
-        }
-      } else {
-        for (uint32_t i0 = 0; i0 < nb; i0 += 16) {
-          if (i0 + 8 < nb) hv_load8(xB, rB, xa, R, i0 + 8);
-          hv_chain8<true>(m, xA, rA, ma, i0, nb);
-          if (i0 + 8 >= nb) break;
-          if (i0 + 16 < nb) hv_load8(xA, rA, xa, R, i0 + 16);
-          hv_chain8<true>(m, xB, rB, ma, i0 + 8, nb);
-        }
-      }
+    stamp(c0);
+    // 1. the recurrence (lanes 0..2) + the previous block's ordered sums (lanes 3..8)
+    if (lane < 9) {
+      if (nb == 64)
+        hv_block_asm(m, acc, (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const double*)rd,
+                     (uint32_t)(uintptr_t)(__attribute__((address_space(3))) double*)wr, rtab + q0 + 1);
+      else
+        hv_block<true>(m, acc, rd, wr, rtab, q0, nb);
     }
     asm volatile("" ::: "memory");
     stamp(c1);
-    // 2. every lane: its sample's addends
+    // 2. every lane: its sample's addends (lanes past nb: unused)
     {
-      const double t0 = x0 - M[lane], u0 = x0 - M[lane + 1];
-      const double t1 = x1 - M[kHvMS + lane], u1 = x1 - M[kHvMS + lane + 1];
-      const double t2 = x2 - M[2 * kHvMS + lane], u2 = x2 - M[2 * kHvMS + lane + 1];
+      const double t0 = x0 - M[lane + 1], u0 = x0 - M[lane + 2];
+      const double t1 = x1 - M[kHvS + lane + 1], u1 = x1 - M[kHvS + lane + 2];
+      const double t2 = x2 - M[2 * kHvS + lane + 1], u2 = x2 - M[2 * kHvS + lane + 2];
       const double p01 = u0 * t1, p12 = u1 * t2, p02 = u0 * t2;
-      asm volatile("" ::: "memory");  // R (under V) is read by phase 1 only
       V[lane] = t0 * u0;
-      V[kHvVS + lane] = t1 * u1;
-      V[2 * kHvVS + lane] = t2 * u2;
-      V[3 * kHvVS + lane] = fma(p01, h.r.x, p01 * h.r.y);
-      V[4 * kHvVS + lane] = fma(p12, h.r.x, p12 * h.r.y);
-      V[5 * kHvVS + lane] = fma(p02, h.r.x, p02 * h.r.y);
+      V[kHvS + lane] = t1 * u1;
+      V[2 * kHvS + lane] = t2 * u2;
+      V[3 * kHvS + lane] = fma(p01, h.r.x, p01 * h.r.y);
+      V[4 * kHvS + lane] = fma(p12, h.r.x, p12 * h.r.y);
+      V[5 * kHvS + lane] = fma(p02, h.r.x, p02 * h.r.y);
     }
     asm volatile("" ::: "memory");
-    stamp(c02);
-    // 3. the ordered sums, lanes 0..5: m2_0..2, cov_01, cov_12, cov_02;
-    //    16 addends per group, the next group loaded ahead
-    if (lane < 6) {
-      const double* v = V + lane * kHvVS;
-      double vA[16], vB[16];
-#pragma unroll
-      for (int u = 0; u < 16; u++) vA[u] = v[u];
-      if (nb == 64) {
-        for (uint32_t i0 = 0; i0 < 64; i0 += 32) {
-#pragma unroll
-          for (int u = 0; u < 16; u++) vB[u] = v[i0 + 16 + u];
-#pragma unroll
-          for (int u = 0; u < 16; u++) acc = acc + vA[u];
-          if (i0 + 32 < 64) {
-#pragma unroll
-            for (int u = 0; u < 16; u++) vA[u] = v[i0 + 32 + u];
-          }
-#pragma unroll
-          for (int u = 0; u < 16; u++) acc = acc + vB[u];
-        }
-      } else
-      for (uint32_t i0 = 0; i0 < nb; i0 += 32) {
-        if (i0 + 16 < nb) {
-#pragma unroll
-          for (int u = 0; u < 16; u++) vB[u] = v[i0 + 16 + u];
-        }
-#pragma unroll
-        for (int u = 0; u < 16; u++)
-          if (i0 + u < nb) acc = acc + vA[u];
-        if (i0 + 16 >= nb) break;
-        if (i0 + 32 < nb) {
-#pragma unroll
-          for (int u = 0; u < 16; u++) vA[u] = v[i0 + 32 + u];
-        }
-#pragma unroll
-        for (int u = 0; u < 16; u++)
-          if (i0 + 16 + u < nb) acc = acc + vB[u];
-      }
-    }
-    asm volatile("" ::: "memory");
-    stamp(c3);
+    stamp(c2);
   }
+  // the last block's ordered sums
+  if (lane >= 3 && lane < 9) {
+    const double* v = V + (lane - 3) * kHvS;
+    for (uint32_t i = 0; i < nb; i++) acc = acc + v[i];
+  }
+  stamp(c1);
   if constexpr (kStamp) {
-    ph[0] = c02;
+    ph[0] = c0 + c2;
     ph[1] = c1;
-    ph[2] = c3;
+    ph[2] = 0;
   }
-  // lane j < 3: mean_j, m2_j and the pair the quad layout gives lane j
-  // ((0,1), (1,2), (0,2): the accumulator of lane j + 3)
-  const double o3 = __shfl_down(acc, 3, 64);
+  // lane j < 3: mean_j, m2_j (lane 3 + j) and the pair the quad layout gives
+  // lane j ((0,1), (1,2), (0,2): lane 6 + j)
+  const double s3 = __shfl_down(acc, 3, 64), s6 = __shfl_down(acc, 6, 64);
   const bool anyout = __any(out);
   if (lane < 3) {
     mean = m;
-    m2 = acc;
-    off = o3;
+    m2 = s3;
+    off = s6;
     bad = anyout;
   }
 }
@@ -1154,6 +1237,7 @@ struct WqChainArgs {
   const uint32_t* dense;   // [B][vcap] dense id of each voxel (kInvalid: empty)
   int32_t* nb;             // [B][ndcap][6]
   uint32_t* nkeys;         // [B][ndcap] chain masks
+  const double* cov_pre;   // [B][ndcap][9] the moments' covariances (k_welford_q's nd_cov)
   double* chain;           // [B][108][ndcap] step-major LU states
   uint32_t* chain_ps;      // [B][12][ndcap]
   double* cov_post;        // [B][ndcap][9]
@@ -1165,7 +1249,53 @@ struct WqChainArgs {
   // 0: every cloud stores its states.
   uint64_t lazy_k;
   uint32_t* chain_ok;      // [B][ndcap]
+  uint32_t* lu_done;       // [B][ceil(ndcap / 64)] NDs of each 64-ND group whose moments are stored (re-armed to 0)
 };
+
+__device__ inline void st_sc1_f64(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline double ld_sc1_f64(const double* p) {
+  return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// The in-place LU chain of ND u (the GSL calls of
+// kullback_leibler.c:57-63 per event, in chain_mask's order), one ND per
+// lane, by the wave that completed u's 64-ND group: the covariances and masks
+// other waves stored (sc1) are read with sc1 loads.  Each state is stored
+// step-major ([t][q][ND], coalesced), the last as the post-KL covariance.  A
+// cloud whose list is deferred (lazy run, num_nds <= lazy_k) keeps only
+// which states have det != 0 and sgndet != 0 (chain_ok: all its event flags
+// read); k_kl_chains stores its states if the list is ever built.
+__device__ inline void wq_lu_group(const WqChainArgs& CA, int b, uint32_t u, uint32_t nd, uint32_t ndcap) {
+  if (u >= nd) return;
+  const uint64_t ob = (uint64_t)b * ndcap;
+  double S[9];
+#pragma unroll
+  for (int q = 0; q < 9; q++) S[q] = ld_sc1_f64(&CA.cov_pre[9 * (ob + u) + q]);
+  const int nT = __popc(__hip_atomic_load(&CA.nkeys[ob + u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const bool flags_only = CA.lazy_k && nd <= CA.lazy_k;  // a deferred cloud
+  double* ch = CA.chain + ob * 108 + u;
+  uint32_t* ps = CA.chain_ps + ob * 12 + u;
+  uint32_t okb = 0;
+  for (int t = 0; t < nT; t++) {
+    uint32_t perm;
+    int sg;
+    lu3(S, perm, sg);
+    if (flags_only) {  // what kl_event's flag reads of the state (kullback_leibler.c:57-70)
+      okb |= (lu3_det(S, sg) != 0 && lu3_sgndet(S, sg) != 0 ? 1u : 0u) << t;
+      continue;
+    }
+#pragma unroll
+    for (int q = 0; q < 9; q++) ch[(uint64_t)(9 * t + q) * ndcap] = S[q];
+    ps[(uint64_t)t * ndcap] = perm | (sg < 0 ? 0x100u : 0u);
+  }
+  if (flags_only) CA.chain_ok[ob + u] = okb;
+#pragma unroll
+  for (int q = 0; q < 9; q++) CA.cov_post[9 * (ob + u) + q] = S[q];
+}
 
 template <typename T>
 __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, int B, const T* __restrict__ nd_pts,
@@ -1181,6 +1311,7 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
   // the quads' record transposes; a heavy item's wave uses its 16 rows (6400 B) as its wq_heavy stage
   __shared__ __attribute__((aligned(16))) float wq_stage[kWqNDs][kWqStageQ];
   static_assert(kHvLds * sizeof(double) <= 16 * kWqStageQ * sizeof(float), "heavy stage fits a wave's rows");
+  static_assert((16 * kWqStageQ * sizeof(float)) % 16 == 0, "16-byte aligned heavy stage");
   double* lrt = (double*)wq_smem;                                // [kWqRt] refined reciprocals of 1..kWqRt
   const uint32_t bw = (uint32_t)((B + 1 + 3) & ~3);
   uint32_t* pre = (uint32_t*)(wq_smem + kWqRt * sizeof(double));  // [B + 1] first light item of each cloud
@@ -1515,16 +1646,19 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
   const double vraw = m2 / (double)cnt;
   const double vd = (vraw != vraw) ? 0.0 : vraw;
   if (live && j < 3) {
+    // the covariance and (below) the chain mask are handed to the wave that
+    // completes this ND's 64-ND group (wq_lu_group): write-through (sc1)
+    // stores, drained before the group counter (MI355X_MICROARCH.md,
+    // inter-workgroup visibility)
     nd_mean[3 * o + j] = mean;
-    nd_cov[9 * o + 4 * j] = vd;
+    st_sc1_f64(&nd_cov[9 * o + 4 * j], vd);
     const uint32_t ia = j == 2 ? 0u : j, ib = j == 2 ? 2u : j + 1u;
-    nd_cov[9 * o + 3 * ia + ib] = off;
-    nd_cov[9 * o + 3 * ib + ia] = off;
+    st_sc1_f64(&nd_cov[9 * o + 3 * ia + ib], off);
+    st_sc1_f64(&nd_cov[9 * o + 3 * ib + ia], off);
   }
   // The ND's KL chain: eligible directions (a neighbour, and
   // more than one sample on both sides) and the chain mask.  The in-place LU
-  // states of the chain are k_lu_chains' (one ND per lane: here only one
-  // lane of a quad would run it, 3 of 4 idle, at the end of every item).
+  // states of the chain: wq_lu_group, one ND per lane.
   {
     uint32_t el = 0;
 #pragma unroll
@@ -1535,7 +1669,7 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
     }
     el |= (uint32_t)__builtin_amdgcn_mov_dpp((int)el, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
     el |= (uint32_t)__builtin_amdgcn_mov_dpp((int)el, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-    if (live && j == 0) CA.nkeys[o] = chain_mask(el);
+    if (live && j == 0) __hip_atomic_store(&CA.nkeys[o], chain_mask(el), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   const uint32_t nbins = (uint32_t)ncls + 1u;
   const bool hist_lds = (size_t)kWqNDs * nbins * sizeof(uint32_t) <= (size_t)kWqHistMax;
@@ -1597,6 +1731,24 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
         if (hist[k] > best) { best = hist[k]; cls = (uint16_t)k; }
     }
     nd_cls[o] = cls;
+  }
+  // count this item's NDs into their 64-ND group; the wave that completes a
+  // group runs its LU chains, one ND per lane
+  {
+    const uint32_t nlive = hv ? 1u : (uint32_t)__popcll(__ballot(live && j == 0));
+    if (nlive) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores are done
+      const uint32_t g = wd0 / 64u, gcap = (ndcap + 63u) / 64u;
+      const uint32_t total = nd - 64u * g < 64u ? nd - 64u * g : 64u;
+      uint32_t* gc = CA.lu_done + (uint64_t)b * gcap + g;
+      uint32_t old = 0;
+      if (lane == 0) old = __hip_atomic_fetch_add(gc, nlive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      old = __builtin_amdgcn_readfirstlane(old);
+      if (old + nlive == total) {
+        if (lane == 0) __hip_atomic_store(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+        wq_lu_group(CA, b, 64u * g + lane, nd, ndcap);
+      }
+    }
   }
   if (wq_marks) {
     const unsigned long long t2 = __builtin_amdgcn_s_memtime();
@@ -2634,7 +2786,7 @@ static void plan_free(Plan* P) {
                   P->chain, P->chain_ps, P->chain_ok, P->slot_val, P->slot_flag, P->ev_val, P->ev_p, P->ev_q, P->ev_min,
                   P->sort_key, P->sort_idx, P->nan_list, P->nan_key, P->nan_slot, P->chunk_nanbase, P->ord_val, P->ord_p, P->ord_q,
                   P->first_occ, P->tmp_u32, P->alive, P->d_stats, P->chunk_cnt, P->chunk_min, P->wq_ctr,
-                  P->heavy, P->rtab};
+                  P->heavy, P->rtab, P->lu_done};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete P;
@@ -2732,49 +2884,6 @@ __global__ void __launch_bounds__(256) k_kl_chains(KLArgs A) {
     for (int q = 0; q < 9; q++) chain[(uint64_t)(9 * t + q) * A.ndcap] = S[q];
     ps[(uint64_t)t * A.ndcap] = perm | (sg < 0 ? 0x100u : 0u);
   }
-}
-
-// Every ND's in-place LU chain after the moments (the GSL calls
-// of kullback_leibler.c:57-63 per event, in the order chain_mask gives), one
-// ND per lane: each state stored step-major ([t][q][ND], coalesced), the
-// last as the post-KL covariance.  A cloud whose list is deferred (lazy run,
-// num_nds <= lazy_k) keeps only which states have det != 0 and sgndet != 0
-// (chain_ok: all its event flags read); k_kl_chains stores its states if the
-// list is ever built.
-__global__ void __launch_bounds__(256) k_lu_chains(const CloudCtl* __restrict__ ctl, const double* __restrict__ nd_cov,
-                                                   const uint32_t* __restrict__ nkeys, double* chain,
-                                                   uint32_t* chain_ps, uint32_t* chain_ok, double* cov_post,
-                                                   uint32_t ndcap, uint64_t lazy_k) {
-  const int b = blockIdx.y;
-  const CloudCtl& c = ctl[b];
-  if (c.state != kAccepted) return;
-  const uint32_t nd = c.num_nds;
-  const uint32_t u = blockIdx.x * 256 + threadIdx.x;
-  if (u >= nd) return;
-  const uint64_t ob = (uint64_t)b * ndcap;
-  double S[9];
-#pragma unroll
-  for (int q = 0; q < 9; q++) S[q] = nd_cov[9 * (ob + u) + q];
-  const int nT = __popc(nkeys[ob + u]);
-  const bool flags_only = lazy_k && nd <= lazy_k;  // a deferred cloud (uniform over the cloud)
-  double* ch = chain + ob * 108 + u;
-  uint32_t* ps = chain_ps + ob * 12 + u;
-  uint32_t okb = 0;
-  for (int t = 0; t < nT; t++) {
-    uint32_t perm;
-    int sg;
-    lu3(S, perm, sg);
-    if (flags_only) {  // what kl_event's flag reads of the state (kullback_leibler.c:57-70)
-      okb |= (lu3_det(S, sg) != 0 && lu3_sgndet(S, sg) != 0 ? 1u : 0u) << t;
-      continue;
-    }
-#pragma unroll
-    for (int q = 0; q < 9; q++) ch[(uint64_t)(9 * t + q) * ndcap] = S[q];
-    ps[(uint64_t)t * ndcap] = perm | (sg < 0 ? 0x100u : 0u);
-  }
-  if (flags_only) chain_ok[ob + u] = okb;
-#pragma unroll
-  for (int q = 0; q < 9; q++) cov_post[9 * (ob + u) + q] = S[q];
 }
 
 static void launch_list_sort(Plan* P, const KLArgs& A, hipStream_t st) {
@@ -2896,11 +3005,8 @@ welford:
       P->ctl, B, (const T*)P->nd_pts, lbl ? P->nd_lbl : nullptr, P->nd_n, P->nd_base, P->nd_mean, P->nd_cov,
       P->nd_cls, P->hist, P->ncls, n, P->ndcap, P->wq_ctr, P->heavy, P->heavy_t, (const double2*)P->rtab,
       P->timing >= 2 ? P->wq_marks : nullptr,
-      WqChainArgs{P->vox, P->dense_of, P->nb, P->nkeys, P->chain, P->chain_ps, P->nd_cov_post, P->vcap,
-                  P->eager_list ? 0ull : (uint64_t)P->k, P->chain_ok});
-  k_lu_chains<<<dim3((P->ndcap + 255) / 256, B), 256, 0, st>>>(P->ctl, P->nd_cov, P->nkeys, P->chain, P->chain_ps,
-                                                              P->chain_ok, P->nd_cov_post, P->ndcap,
-                                                              P->eager_list ? 0ull : (uint64_t)P->k);
+      WqChainArgs{P->vox, P->dense_of, P->nb, P->nkeys, P->nd_cov, P->chain, P->chain_ps, P->nd_cov_post, P->vcap,
+                  P->eager_list ? 0ull : (uint64_t)P->k, P->chain_ok, P->lu_done});
   if (P->timing) HIPCHK(hipEventRecord(P->ev[5], st));
   KLArgs A = kl_args(P, P->k, out, out_cls, pc64, cov64, cls16);
   A.stats_out = stats_dst;
@@ -3049,6 +3155,7 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   A_(wq_ctr, 128);
   A_(heavy, B * nd);
   A_(rtab, 2 * (n + 1));
+  A_(lu_done, B * ((nd + 63) / 64));
   // k_front: G workgroups per cloud, all resident together (G * B <= CUs);
   // each owns bpw bins, whose per-ND counts and ranks live in its LDS.  The
   // per-workgroup buffers are sized for the largest G (CU share 1).
@@ -3071,6 +3178,7 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   if (e == hipSuccess) e = hipMemset(P->stamps, 0, B * P->vcap * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(P->d_stats, 0, B * sizeof(ndnet_ndt_stats));
   if (e == hipSuccess) e = hipMemset(P->wq_ctr, 0, 128 * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemset(P->lu_done, 0, B * ((nd + 63) / 64) * sizeof(uint32_t));
   if (e == hipSuccess) {
     // wq_heavy's division table: rc = RN(1/c), rl = RN((1 - c rc) / c), 1 - c rc exact (one fma)
     std::vector<double> rt(2 * (n + 1), 0.0);

@@ -223,6 +223,110 @@ static void rung(const char* name) {
   printf("%-44s: %.2f cycles per sample\n", name, (double)c / ((double)(kIters / 8) * 64));
 }
 
+// ---- k_welford_q's heavy-ND loop (copied from csrc/ndt_kernels.hip) alone on one wave ----
+typedef unsigned int hv_u16 __attribute__((ext_vector_type(16)));
+typedef double hv_d2 __attribute__((ext_vector_type(2)));  // native vector (HIP's double2 is a struct)
+
+struct HvOps {
+  hv_d2 x[4];  // 8 steps' coordinates (lanes 0..2) or addends (lanes 3..8)
+  hv_u16 r0, r1;  // (rc, rl) of the 8 steps, in scalar registers
+};
+
+template <int G>
+__device__ inline void hv_issue(HvOps& o, uint32_t rda, const double2* rtq) {
+  hv_d2 x0, x1, x2, x3;
+  hv_u16 r0, r1;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(x0) : "v"(rda), "n"(64 * G));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(x1) : "v"(rda), "n"(64 * G + 16));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(x2) : "v"(rda), "n"(64 * G + 32));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(x3) : "v"(rda), "n"(64 * G + 48));
+  asm volatile("s_load_dwordx16 %0, %1, %2" : "=s"(r0) : "s"(rtq), "n"(128 * G));
+  asm volatile("s_load_dwordx16 %0, %1, %2" : "=s"(r1) : "s"(rtq), "n"(128 * G + 64));
+  o.x[0] = x0;
+  o.x[1] = x1;
+  o.x[2] = x2;
+  o.x[3] = x3;
+  o.r0 = r0;
+  o.r1 = r1;
+}
+__device__ inline void hv_wait(HvOps& o) {
+  hv_d2 x0 = o.x[0], x1 = o.x[1], x2 = o.x[2], x3 = o.x[3];
+  hv_u16 r0 = o.r0, r1 = o.r1;
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+s"(r0), "+s"(r1));
+  o.x[0] = x0;
+  o.x[1] = x1;
+  o.x[2] = x2;
+  o.x[3] = x3;
+  o.r0 = r0;
+  o.r1 = r1;
+}
+template <int G>
+__device__ inline void hv_put(uint32_t wra, const double (&mo)[8]) {
+  const hv_d2 a = {mo[0], mo[1]}, b = {mo[2], mo[3]}, c = {mo[4], mo[5]}, d = {mo[6], mo[7]};
+  asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(wra), "v"(a), "n"(64 * G));
+  asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(wra), "v"(b), "n"(64 * G + 16));
+  asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(wra), "v"(c), "n"(64 * G + 32));
+  asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(wra), "v"(d), "n"(64 * G + 48));
+}
+__device__ inline double hv_sd(const hv_u16& v, int k) {
+  return __builtin_bit_cast(double, (unsigned long long)v[2 * k] | ((unsigned long long)v[2 * k + 1] << 32));
+}
+__device__ inline void hv_steps(double& m, double& acc, const HvOps& o, double (&mo)[8]) {
+#pragma unroll
+  for (int u = 0; u < 8; u++) {
+    const double xv = o.x[u >> 1][u & 1];
+    const hv_u16& r = u < 4 ? o.r0 : o.r1;
+    const double rc = hv_sd(r, 2 * (u & 3)), rl = hv_sd(r, 2 * (u & 3) + 1);
+    const double t = xv - m;
+    m = m + fma(t, rc, t * rl);
+    acc = acc + xv;
+    mo[u] = m;
+  }
+}
+template <int G>  // group G of a full block: wait for its operands, write G - 1's means, issue G + 1's operands, step
+__device__ inline void hv_group(double& m, double& acc, HvOps& cur, HvOps& nxt, double (&mcur)[8],
+                                double (&mprev)[8], uint32_t rda, uint32_t wra, const double2* rtq) {
+  hv_wait(cur);
+  if constexpr (G > 0) hv_put<G - 1>(wra, mprev);
+  if constexpr (G < 7) hv_issue<G + 1>(nxt, rda, rtq);
+  hv_steps(m, acc, cur, mcur);
+}
+__device__ inline void hv_block_asm(double& m, double& acc, uint32_t rda, uint32_t wra, const double2* rtq) {
+  HvOps A, B;
+  double mA[8], mB[8];
+  hv_issue<0>(A, rda, rtq);
+  hv_group<0>(m, acc, A, B, mA, mB, rda, wra, rtq);
+  hv_group<1>(m, acc, B, A, mB, mA, rda, wra, rtq);
+  hv_group<2>(m, acc, A, B, mA, mB, rda, wra, rtq);
+  hv_group<3>(m, acc, B, A, mB, mA, rda, wra, rtq);
+  hv_group<4>(m, acc, A, B, mA, mB, rda, wra, rtq);
+  hv_group<5>(m, acc, B, A, mB, mA, rda, wra, rtq);
+  hv_group<6>(m, acc, A, B, mA, mB, rda, wra, rtq);
+  hv_group<7>(m, acc, B, A, mB, mA, rda, wra, rtq);
+  hv_put<7>(wra, mB);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the block's means are in LDS for phase 2
+}
+
+
+__global__ void hv_loop(double* out, const double2* __restrict__ rtab, unsigned long long* cyc, int blocks) {
+  __shared__ __attribute__((aligned(16))) double lds[12 * 66];
+  const int lane = threadIdx.x;
+  for (int i = lane; i < 12 * 66; i += 64) lds[i] = 1.0 + i * 1e-3;
+  __syncthreads();
+  const double* rd = lane < 3 ? lds + lane * 66 : lds + (6 + (lane < 9 ? lane - 3 : 0)) * 66;
+  double* wr = lane < 3 ? lds + (3 + lane) * 66 + 2 : lds + (6 + (lane < 9 ? lane - 3 : 0)) * 66;
+  double m = 0.5, acc = 0.0;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  if (lane < 9) {
+    for (int k = 0; k < blocks; k++)
+      hv_block_asm(m, acc, (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const double*)rd,
+                   (uint32_t)(uintptr_t)(__attribute__((address_space(3))) double*)wr, rtab + 64 * (k & 7) + 1);
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+  out[blockIdx.x * blockDim.x + threadIdx.x] = m + acc;
+}
+
 template <typename K>
 static void run(const char* name, K kern, int blocks, int threads, int ops_per_iter) {
   double* out;
@@ -270,6 +374,20 @@ int main() {
   run("phase1: pinned LDS reads + writes, 3 lanes", phase1<1, 1, 1, 1>, 1, 64, 8);
   run("phase1: pinned reads + group-end writes", phase1<1, 2, 1, 1>, 1, 64, 8);
   run("phase1: group-end writes only", phase1<0, 2, 1, 1>, 1, 64, 8);
+  {
+    double* out;
+    double2* rt;
+    unsigned long long* cyc;
+    hipMalloc(&out, 64 * sizeof(double));
+    hipMalloc(&rt, 600 * sizeof(double2));
+    hipMemset(rt, 0, 600 * sizeof(double2));
+    hipMalloc(&cyc, sizeof(unsigned long long));
+    for (int r = 0; r < 2; r++) hipLaunchKernelGGL(hv_loop, dim3(1), dim3(64), 0, 0, out, rt, cyc, 256);
+    hipDeviceSynchronize();
+    unsigned long long c;
+    hipMemcpy(&c, cyc, sizeof(c), hipMemcpyDeviceToHost);
+    printf("%-44s: %.2f cycles per sample\n", "hv_block_asm alone (one wave)", (double)c / (256.0 * 64));
+  }
   rung<0>("phase1g: global x, SGPR rc/rl, no M out");
   rung<1>("phase1g: + ds_write_b64 per sample");
   rung<2>("phase1g: + global_store_dwordx2 per sample");

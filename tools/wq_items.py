@@ -81,7 +81,7 @@ print(f"cycles per sample, heavy items: {q(per_sample_h)}")
 print(f"cycles per sample (of the group's longest ND), light items: {q(per_sample_l)}")
 if phases and len(np.concatenate(phases)):
     P = np.concatenate(phases)
-    print("heavy items, cycles per sample by phase (median): 0+2 loads/products %.1f, 1 mean recurrence %.1f, "
-          "3 ordered sums %.1f" % tuple(np.median(P, axis=0)))
+    print("heavy items, cycles per sample by phase (median): 0+2 loads/products %.1f, 1 mean recurrence + "
+          "ordered sums %.1f" % tuple(np.median(P, axis=0))[:2])
 print(f"epilogue cycles, heavy: {q(epi_h)}; light: {q(epi_l)}")
 print(f"span us over reps: {[round(s, 1) for s in spans]}")
