@@ -254,6 +254,16 @@ int ndnet_ndt_debug_front_wg_marks(void *plan, unsigned long long *marks, int *G
  * Heavy items come first.  marks must hold 8 * capacity values; synchronises. */
 int ndnet_ndt_debug_wq_marks(void *plan, unsigned long long *marks, uint32_t *items);
 
+/* The device's in-place LU chain (the GSL 2.7.1 LU_decomp restatement the
+ * KL stage applies once per event, kullback_leibler.c:57-63) on n row-major
+ * 3x3 matrices d_A [n][9]: `steps` (1..12) successive decompositions of each,
+ * every state to d_states [n][steps][9], its permutation (p0 | p1 << 2 |
+ * p2 << 4) | (signum < 0) << 8 to d_ps [n][steps], and d_flags [n][steps] =
+ * det != 0 && sgndet != 0 (the event flag, kullback_leibler.c:57-70).  For
+ * the parity tests; stream-ordered on `stream`. */
+int ndnet_debug_lu_chain(const double *d_A, uint32_t n, int steps, double *d_states, uint32_t *d_ps,
+                         uint32_t *d_flags, void *stream);
+
 /* Library identification (no GPU needed). */
 const char *ndnet_amd_version(void);
 

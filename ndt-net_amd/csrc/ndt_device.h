@@ -202,68 +202,89 @@ NDNET_FN void welford_update(Welford& w, const double* x) {
 // per column, first max |a| as pivot (cblas idamax), full row swap, scale the
 // sub-column by 1/a_jj (divide when |a_jj| < DBL_MIN), rank-1 update
 // a_ic += a_jc * (-a_ij).  perm/signum from the pivot sequence.
+// c ? a : b as two v_cndmask_b32 on a lane mask: a plain select of two
+// elements of the caller's matrix can be folded into a select of their
+// addresses, which turns the register-resident matrix into scratch memory.
+NDNET_FN double lu_sel(bool c, double a, double b) {
+  const unsigned long long lanes = __ballot(c);
+  const unsigned long long ua = __builtin_bit_cast(unsigned long long, a);
+  const unsigned long long ub = __builtin_bit_cast(unsigned long long, b);
+  uint32_t lo, hi;
+  asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(lo) : "v"((uint32_t)ub), "v"((uint32_t)ua), "s"(lanes));
+  asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(hi) : "v"((uint32_t)(ub >> 32)), "v"((uint32_t)(ua >> 32)), "s"(lanes));
+  return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32));
+}
+
 NDNET_FN void lu3(double* A, uint32_t& perm_packed, int& signum) {
-  // Every array index below is a compile-time constant (pivot rows are
-  // applied with selects), so A stays in registers: a dynamically indexed
-  // private array would live in scratch or LDS.
-  int ipiv0 = 0, ipiv1 = 1;
+  // Written out per column with selects, no loops over rows: every index is
+  // a compile-time constant (A stays in registers) and no pivot decision
+  // becomes a branch (the generic loop form compiled to ~300 instructions
+  // per decomposition with 14 exec-masked branches, tools/ubench/lu_chain.hip).
+  // Column 0: first max |a| over rows 0..2 (cblas idamax: a > max, max from 0).
+  const double a00 = fabs(A[0]), a10 = fabs(A[3]), a20 = fabs(A[6]);
+  const double m0 = a00 > 0.0 ? a00 : 0.0;
+  const bool b1 = a10 > m0;
+  const double m1 = b1 ? a10 : m0;
+  const bool b2 = a20 > m1;
+  const bool s1 = b1 && !b2;  // pivot row 1
+  double r0[3], r1[3], r2[3];  // the rows after swapping row 0 with the pivot row
 #pragma unroll
-  for (int j = 0; j < 3; j++) {
-    double mx = 0.0;
-    int jp = j;
-#pragma unroll
-    for (int i = j; i < 3; i++) {
-      const double a = fabs(A[i * 3 + j]);
-      if (a > mx) { mx = a; jp = i; }
+  for (int c = 0; c < 3; c++) {
+    r0[c] = lu_sel(b2, A[6 + c], lu_sel(b1, A[3 + c], A[c]));
+    r1[c] = lu_sel(s1, A[c], A[3 + c]);
+    r2[c] = lu_sel(b2, A[c], A[6 + c]);
+  }
+  {
+    const double ajj = r0[0];
+    if (fabs(ajj) >= kDblMin) {
+      const double s = 1.0 / ajj;
+      r1[0] = s * r1[0];
+      r2[0] = s * r2[0];
+    } else {
+      r1[0] = r1[0] / ajj;
+      r2[0] = r2[0] / ajj;
     }
-    if (j == 0) ipiv0 = jp;
-    if (j == 1) ipiv1 = jp;
+    const double t1 = -1.0 * r1[0], t2 = -1.0 * r2[0];
+    r1[1] = r1[1] + r0[1] * t1;
+    r1[2] = r1[2] + r0[2] * t1;
+    r2[1] = r2[1] + r0[1] * t2;
+    r2[2] = r2[2] + r0[2] * t2;
+  }
+  // Column 1: pivot between rows 1 and 2 (full-row swap)
+  const double a11 = fabs(r1[1]), a21 = fabs(r2[1]);
+  const bool bb = a21 > (a11 > 0.0 ? a11 : 0.0);
+  double n1[3], n2[3];
 #pragma unroll
-    for (int i = j + 1; i < 3; i++) {
-      const bool sw = jp == i;
-#pragma unroll
-      for (int c = 0; c < 3; c++) {
-        const double t = A[j * 3 + c];
-        A[j * 3 + c] = sw ? A[i * 3 + c] : t;
-        A[i * 3 + c] = sw ? t : A[i * 3 + c];
-      }
+  for (int c = 0; c < 3; c++) {
+    n1[c] = lu_sel(bb, r2[c], r1[c]);
+    n2[c] = lu_sel(bb, r1[c], r2[c]);
+  }
+  {
+    const double ajj = n1[1];
+    if (fabs(ajj) >= kDblMin) {
+      const double s = 1.0 / ajj;
+      n2[1] = s * n2[1];
+    } else {
+      n2[1] = n2[1] / ajj;
     }
-    if (j < 2) {
-      const double ajj = A[j * 3 + j];
-      if (fabs(ajj) >= kDblMin) {
-        const double s = 1.0 / ajj;
+    const double t = -1.0 * n2[1];
+    n2[2] = n2[2] + n1[2] * t;
+  }
 #pragma unroll
-        for (int i = j + 1; i < 3; i++) A[i * 3 + j] = s * A[i * 3 + j];
-      } else {
-#pragma unroll
-        for (int i = j + 1; i < 3; i++) A[i * 3 + j] = A[i * 3 + j] / ajj;
-      }
-#pragma unroll
-      for (int i = j + 1; i < 3; i++) {
-        const double t = -1.0 * A[i * 3 + j];
-#pragma unroll
-        for (int c = j + 1; c < 3; c++) A[i * 3 + c] = A[i * 3 + c] + A[j * 3 + c] * t;
-      }
-    }
+  for (int c = 0; c < 3; c++) {
+    A[c] = r0[c];
+    A[3 + c] = n1[c];
+    A[6 + c] = n2[c];
   }
   // permutation from the pivots (gsl_permutation_swap per step; a swap of
-  // two distinct positions flips the sign, ipiv[2] == 2 always)
-  int p0 = 0, p1 = 1, p2 = 2, s = 1;
-  if (ipiv0 != 0) {
-    const int t = p0;
-    p0 = ipiv0 == 1 ? p1 : p2;
-    if (ipiv0 == 1) p1 = t;
-    else p2 = t;
-    s = -s;
-  }
-  if (ipiv1 != 1) {  // ipiv1 == 2
-    const int t = p1;
-    p1 = p2;
-    p2 = t;
-    s = -s;
-  }
-  perm_packed = (uint32_t)p0 | ((uint32_t)p1 << 2) | ((uint32_t)p2 << 4);
-  signum = s;
+  // two distinct positions flips the sign; column 2 never swaps):
+  // pivot row 1 -> (1, 0, 2), row 2 -> (2, 1, 0); then rows 1, 2 swapped by bb
+  const uint32_t q0 = b2 ? 2u : (s1 ? 1u : 0u);
+  const uint32_t q1 = s1 ? 0u : 1u;
+  const uint32_t q2 = b2 ? 0u : 2u;
+  const uint32_t p1 = bb ? q2 : q1, p2 = bb ? q1 : q2;
+  perm_packed = q0 | (p1 << 2) | (p2 << 4);
+  signum = ((b1 || b2) != bb) ? -1 : 1;
 }
 
 NDNET_FN double lu3_det(const double* LU, int signum) {

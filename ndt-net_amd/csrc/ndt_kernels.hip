@@ -1297,6 +1297,27 @@ __device__ inline void wq_lu_group(const WqChainArgs& CA, int b, uint32_t u, uin
   for (int q = 0; q < 9; q++) CA.cov_post[9 * (ob + u) + q] = S[q];
 }
 
+// ndnet_debug_lu_chain: the device LU chain (lu3 + the event flags, as
+// wq_lu_group runs them) on n given matrices, every state recorded.
+__global__ void __launch_bounds__(64) k_debug_lu_chain(const double* A, uint32_t n, int steps, double* states,
+                                                        uint32_t* ps, uint32_t* flags) {
+  const uint32_t m = blockIdx.x * 64 + threadIdx.x;
+  if (m >= n) return;
+  double S[9];
+#pragma unroll
+  for (int q = 0; q < 9; q++) S[q] = A[9 * (uint64_t)m + q];
+  for (int t = 0; t < steps; t++) {
+    uint32_t perm;
+    int sg;
+    lu3(S, perm, sg);
+    const uint64_t r = (uint64_t)m * steps + t;
+#pragma unroll
+    for (int q = 0; q < 9; q++) states[9 * r + q] = S[q];
+    ps[r] = perm | (sg < 0 ? 0x100u : 0u);
+    flags[r] = lu3_det(S, sg) != 0 && lu3_sgndet(S, sg) != 0 ? 1u : 0u;
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, int B, const T* __restrict__ nd_pts,
                                                           const uint16_t* __restrict__ nd_lbl,
@@ -1444,8 +1465,12 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
 #pragma unroll
       for (int i = 0; i < kU / 4; i++) {
         const uint32_t q = q0 + (uint32_t)(kU / 4) * j + (uint32_t)i;
+#ifdef NDNET_WQ_NOLOAD  // timing experiment only: no point loads (wrong results)
+        r.v[i] = make_float3(1.0f + 0.001f * (float)(q & 7), 2.0f, 3.0f);
+#else
         const float* pq = rec + 3u * (q < last ? q : last);
         r.v[i] = make_float3(pq[0], pq[1], pq[2]);
+#endif
       }
     } else {
 #pragma unroll
@@ -1507,7 +1532,13 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
       for (int u = 0; u < kU; u++) r[u] = rb.v[u];
     }
     double cr[kU];
+#ifdef NDNET_WQ_NORECIP  // timing experiment only (wrong results): reciprocals without their LDS reads
+    if constexpr (!kExact)
+#pragma unroll
+      for (int u = 0; u < kU; u++) cr[u] = 1.0 / 3.0 + u;
+#else
     if constexpr (!kExact) recips(cr, q0);
+#endif
     double pt = 0.0, pu = 0.0, pcn = 1.0, prc = 1.0;       // the previous sample's head results
     unsigned long long plane = 0;
     if constexpr (kExact) {
@@ -3370,6 +3401,15 @@ int ndnet_ndt_debug_kl_marks(void* plan, unsigned long long* marks) {
   if (!P || !marks || !P->kl_marks) return NDNET_ERR_ARG;
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(marks, P->kl_marks, (size_t)P->B * 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return NDNET_OK;
+}
+
+int ndnet_debug_lu_chain(const double* d_A, uint32_t n, int steps, double* d_states, uint32_t* d_ps,
+                         uint32_t* d_flags, void* stream) {
+  if (!d_A || !d_states || !d_ps || !d_flags || steps <= 0 || steps > 12) return NDNET_ERR_ARG;
+  if (n == 0) return NDNET_OK;
+  k_debug_lu_chain<<<(n + 63) / 64, 64, 0, (hipStream_t)stream>>>(d_A, n, steps, d_states, d_ps, d_flags);
+  HIPCHK(hipGetLastError());
   return NDNET_OK;
 }
 

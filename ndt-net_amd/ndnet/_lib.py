@@ -82,6 +82,7 @@ EXPORTS = {
     "ndnet_ndt_debug_kl_marks": (_I, [_P, _P]),
     "ndnet_ndt_debug_front_marks": (_I, [_P, _P]),
     "ndnet_ndt_debug_wq_marks": (_I, [_P, _P, ctypes.POINTER(ctypes.c_uint32)]),
+    "ndnet_debug_lu_chain": (_I, [_P, ctypes.c_uint32, _I, _P, _P, _P, _P]),
     "ndnet_ndt_debug_front_wg_marks": (_I, [_P, _P, ctypes.POINTER(_I)]),
     "ndnet_ndt_set_timing": (_I, [_P, _I]),
     "ndnet_ndt_stage_ms": (_I, [_P, _P]),

@@ -785,3 +785,22 @@ uint64_t orc_rtab_div_mismatches(uint64_t n_max, uint64_t samples, uint64_t seed
   }
   return bad;
 }
+
+/* The in-place LU chain of one ND: `steps` successive
+ * gsl_linalg_LU_decomp calls on the same matrix, recording every state
+ * (9 doubles), its permutation | (signum < 0) << 8 packed as the device packs
+ * it (p0 | p1 << 2 | p2 << 4), and the event flag kl_divergence reads of it
+ * (det != 0 and sgndet != 0, kullback_leibler.c:57-70).  n matrices. */
+void orc_lu_chain(const double* A, uint64_t n, int steps, double* states, uint32_t* ps, uint32_t* flags) {
+  for (uint64_t m = 0; m < n; m++) {
+    double S[9];
+    memcpy(S, A + 9 * m, sizeof S);
+    for (int t = 0; t < steps; t++) {
+      int perm[3], sg;
+      orc_lu_decomp(S, perm, &sg);
+      memcpy(states + (m * steps + t) * 9, S, sizeof S);
+      ps[m * steps + t] = (uint32_t)perm[0] | ((uint32_t)perm[1] << 2) | ((uint32_t)perm[2] << 4) | (sg < 0 ? 0x100u : 0u);
+      flags[m * steps + t] = (orc_lu_det(S, sg) != 0 && orc_lu_sgndet(S, sg) != 0) ? 1u : 0u;
+    }
+  }
+}

@@ -708,3 +708,64 @@ def test_heavy_nds_float64_and_out_of_range():
         assert np.array_equal(pc, pc2, equal_nan=True) and np.array_equal(cov, cov2, equal_nan=True), tiny
         s.cleanup()
         ref.cleanup()
+
+
+def _lu_cases(seed):
+    """3x3 matrices for the LU chain: random covariances (SPD and rank-1),
+    random general matrices, ties between pivot candidates, zero / negative-zero
+    columns, pivots below DBL_MIN, huge and tiny entries, NaN and inf."""
+    rng = np.random.default_rng(seed)
+    mats = []
+    for _ in range(2000):
+        a = rng.normal(size=(3, 3))
+        mats.append(a @ a.T)
+    for _ in range(500):
+        v = rng.normal(size=3)
+        mats.append(np.outer(v, v))
+    mats += list(rng.normal(size=(1500, 3, 3)))
+    mats += list(rng.integers(-2, 3, size=(1500, 3, 3)).astype(np.float64))  # ties and exact zeros
+    for _ in range(300):
+        a = rng.normal(size=(3, 3))
+        a[:, rng.integers(0, 3)] = 0.0
+        a[rng.integers(0, 3), rng.integers(0, 3)] = -0.0
+        mats.append(a)
+    for scale in (1e-310, 1e-300, 1e300, 3e307):
+        mats += list(rng.normal(size=(100, 3, 3)) * scale)
+    a = rng.normal(size=(50, 3, 3))
+    a[:, 0, 0] = np.nan
+    mats += list(a)
+    a = rng.normal(size=(50, 3, 3))
+    a[:, 1, 2] = np.inf
+    mats += list(a)
+    return np.ascontiguousarray(np.array(mats, dtype=np.float64).reshape(-1, 9))
+
+
+def test_lu_chain_matches_oracle():
+    """The device LU chain (lu3 + event flags, run by k_welford_q's group
+    hand-off for every ND) against the oracle's GSL 2.7.1 LU_decomp
+    restatement: every state, permutation, sign and flag of 12 chained
+    decompositions, bit for bit, on ~6000 matrices with ties, zeros,
+    sub-DBL_MIN pivots, huge / tiny entries, NaN and inf."""
+    import torch
+    import oracle as O
+    from ndnet import _lib
+    A = _lu_cases(21)
+    n, steps = len(A), 12
+    st_h = np.zeros((n, steps, 9))
+    ps_h = np.zeros((n, steps), np.uint32)
+    fl_h = np.zeros((n, steps), np.uint32)
+    O.lib().orc_lu_chain(O._ptr(A), ctypes.c_uint64(n), ctypes.c_int(steps), O._ptr(st_h), O._ptr(ps_h),
+                         O._ptr(fl_h))
+    dA = torch.from_numpy(A).cuda()
+    st = torch.empty((n, steps, 9), dtype=torch.float64, device="cuda")
+    ps = torch.empty((n, steps), dtype=torch.int32, device="cuda")
+    fl = torch.empty((n, steps), dtype=torch.int32, device="cuda")
+    _lib.check(_lib.lib().ndnet_debug_lu_chain(dA.data_ptr(), n, steps, st.data_ptr(), ps.data_ptr(), fl.data_ptr(),
+                                               torch.cuda.current_stream().cuda_stream), "debug_lu_chain")
+    torch.cuda.synchronize()
+    got = st.cpu().numpy()
+    nan = np.isnan(st_h)  # NaN payloads may differ; every other value bit for bit (signed zeros too)
+    assert np.array_equal(np.isnan(got), nan)
+    assert np.array_equal(got.view(np.uint64)[~nan], st_h.view(np.uint64)[~nan])
+    assert np.array_equal(ps.cpu().numpy().astype(np.uint32), ps_h)
+    assert np.array_equal(fl.cpu().numpy().astype(np.uint32), fl_h)

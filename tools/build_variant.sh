@@ -13,5 +13,5 @@ C="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -Wno-un
 /opt/rocm/bin/hipcc $C $FLAGS -c -o $P/build/v_$NAME/pointnet_kernels.o $P/csrc/pointnet_kernels.hip &
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $P/lib/variants/libndnet_amd_$NAME.so \
-  $P/build/v_$NAME/ndt_kernels.o $P/build/ndt_legacy_abi.o $P/build/v_$NAME/pointnet_kernels.o $P/build/pointnet_chain_t32.o $P/build/ply_ingest.o -lpthread
+  $P/build/v_$NAME/ndt_kernels.o $P/build/ndt_legacy_abi.o $P/build/v_$NAME/pointnet_kernels.o $P/build/pointnet_chain_t32.o $P/build/ply_ingest.o $P/build/train_kernels.o -lpthread
 echo "built $P/lib/variants/libndnet_amd_$NAME.so"

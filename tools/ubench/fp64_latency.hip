@@ -291,6 +291,86 @@ __device__ inline void hv_group(double& m, double& acc, HvOps& cur, HvOps& nxt, 
   if constexpr (G < 7) hv_issue<G + 1>(nxt, rda, rtq);
   hv_steps(m, acc, cur, mcur);
 }
+// The same loop with (rc, rl) from an LDS row R[64] (written with the
+// block) instead of scalar loads: every memory operation of the loop is then
+// LDS, which completes in order, so the waits count (lgkmcnt(N)) and the
+// operands are issued two groups ahead.  Per group: 4 ds_read_b128 of the
+// lane's row, 8 broadcast ds_read_b128 of R, 4 ds_write_b128 of the means.
+struct HvOps2 {
+  hv_d2 x[4];
+  hv_d2 r[8];  // (rc, rl) of the 8 steps
+};
+template <int G>
+__device__ inline void hv_issue2(HvOps2& o, uint32_t rda, uint32_t ra) {
+  hv_d2 x0, x1, x2, x3, r0, r1, r2, r3, r4, r5, r6, r7;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(x0) : "v"(rda), "n"(64 * G));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(x1) : "v"(rda), "n"(64 * G + 16));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(x2) : "v"(rda), "n"(64 * G + 32));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(x3) : "v"(rda), "n"(64 * G + 48));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r0) : "v"(ra), "n"(128 * G));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r1) : "v"(ra), "n"(128 * G + 16));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r2) : "v"(ra), "n"(128 * G + 32));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r3) : "v"(ra), "n"(128 * G + 48));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r4) : "v"(ra), "n"(128 * G + 64));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r5) : "v"(ra), "n"(128 * G + 80));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r6) : "v"(ra), "n"(128 * G + 96));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r7) : "v"(ra), "n"(128 * G + 112));
+  o.x[0] = x0; o.x[1] = x1; o.x[2] = x2; o.x[3] = x3;
+  o.r[0] = r0; o.r[1] = r1; o.r[2] = r2; o.r[3] = r3; o.r[4] = r4; o.r[5] = r5; o.r[6] = r6; o.r[7] = r7;
+}
+template <int N>  // all but the N youngest LDS operations done; the group's registers held behind it
+__device__ inline void hv_wait2(HvOps2& o) {
+  hv_d2 x0 = o.x[0], x1 = o.x[1], x2 = o.x[2], x3 = o.x[3];
+  hv_d2 r0 = o.r[0], r1 = o.r[1], r2 = o.r[2], r3 = o.r[3], r4 = o.r[4], r5 = o.r[5], r6 = o.r[6], r7 = o.r[7];
+  asm volatile("s_waitcnt lgkmcnt(%12)"
+               : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5),
+                 "+v"(r6), "+v"(r7)
+               : "n"(N));
+  o.x[0] = x0; o.x[1] = x1; o.x[2] = x2; o.x[3] = x3;
+  o.r[0] = r0; o.r[1] = r1; o.r[2] = r2; o.r[3] = r3; o.r[4] = r4; o.r[5] = r5; o.r[6] = r6; o.r[7] = r7;
+}
+__device__ inline void hv_steps2(double& m, double& acc, const HvOps2& o, double (&mo)[8]) {
+#pragma unroll
+  for (int u = 0; u < 8; u++) {
+    const double xv = o.x[u >> 1][u & 1];
+    const double t = xv - m;
+    m = m + fma(t, o.r[u][0], t * o.r[u][1]);
+    acc = acc + xv;
+    mo[u] = m;
+  }
+}
+// group G: wait for its operands R(G), write G - 1's means W(G - 1), issue
+// R(G + 2), step.  R(G + 2) and W(G - 1) go out at the top of group G, so
+// the operations younger than R(G) at its wait are: G = 0, 1: R(G + 1) (12);
+// G = 2..6: W(G - 2) and R(G + 1) (16: lgkmcnt(15), the field's maximum, waits
+// for one more); G = 7: W(5) (4).
+template <int G>
+__device__ inline void hv_group2(double& m, double& acc, HvOps2 (&ops)[3], double (&mcur)[8], double (&mprev)[8],
+                                 uint32_t rda, uint32_t wra, uint32_t ra) {
+  if constexpr (G < 2) hv_wait2<12>(ops[G % 3]);
+  else if constexpr (G < 7) hv_wait2<15>(ops[G % 3]);
+  else hv_wait2<4>(ops[G % 3]);
+  if constexpr (G > 0) hv_put<G - 1>(wra, mprev);
+  if constexpr (G + 2 < 8) hv_issue2<G + 2>(ops[(G + 2) % 3], rda, ra);
+  hv_steps2(m, acc, ops[G % 3], mcur);
+}
+__device__ inline void hv_block_lds(double& m, double& acc, uint32_t rda, uint32_t wra, uint32_t ra) {
+  HvOps2 ops[3];
+  double mA[8], mB[8];
+  hv_issue2<0>(ops[0], rda, ra);
+  hv_issue2<1>(ops[1], rda, ra);
+  hv_group2<0>(m, acc, ops, mA, mB, rda, wra, ra);
+  hv_group2<1>(m, acc, ops, mB, mA, rda, wra, ra);
+  hv_group2<2>(m, acc, ops, mA, mB, rda, wra, ra);
+  hv_group2<3>(m, acc, ops, mB, mA, rda, wra, ra);
+  hv_group2<4>(m, acc, ops, mA, mB, rda, wra, ra);
+  hv_group2<5>(m, acc, ops, mB, mA, rda, wra, ra);
+  hv_group2<6>(m, acc, ops, mA, mB, rda, wra, ra);
+  hv_group2<7>(m, acc, ops, mB, mA, rda, wra, ra);
+  hv_put<7>(wra, mB);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the block's means are in LDS for phase 2
+}
+
 __device__ inline void hv_block_asm(double& m, double& acc, uint32_t rda, uint32_t wra, const double2* rtq) {
   HvOps A, B;
   double mA[8], mB[8];
@@ -309,18 +389,24 @@ __device__ inline void hv_block_asm(double& m, double& acc, uint32_t rda, uint32
 
 
 __global__ void hv_loop(double* out, const double2* __restrict__ rtab, unsigned long long* cyc, int blocks) {
-  __shared__ __attribute__((aligned(16))) double lds[12 * 66];
+  __shared__ __attribute__((aligned(16))) double lds[12 * 66 + 128];
   const int lane = threadIdx.x;
-  for (int i = lane; i < 12 * 66; i += 64) lds[i] = 1.0 + i * 1e-3;
+  for (int i = lane; i < 12 * 66 + 128; i += 64) lds[i] = 1.0 + i * 1e-3;
   __syncthreads();
   const double* rd = lane < 3 ? lds + lane * 66 : lds + (6 + (lane < 9 ? lane - 3 : 0)) * 66;
   double* wr = lane < 3 ? lds + (3 + lane) * 66 + 2 : lds + (6 + (lane < 9 ? lane - 3 : 0)) * 66;
   double m = 0.5, acc = 0.0;
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
   if (lane < 9) {
-    for (int k = 0; k < blocks; k++)
-      hv_block_asm(m, acc, (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const double*)rd,
-                   (uint32_t)(uintptr_t)(__attribute__((address_space(3))) double*)wr, rtab + 64 * (k & 7) + 1);
+    for (int k = 0; k < blocks; k++) {
+      if (blocks > 0)
+        hv_block_asm(m, acc, (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const double*)rd,
+                     (uint32_t)(uintptr_t)(__attribute__((address_space(3))) double*)wr, rtab + 64 * (k & 7) + 1);
+    }
+    for (int k = 0; k < -blocks; k++)
+      hv_block_lds(m, acc, (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const double*)rd,
+                   (uint32_t)(uintptr_t)(__attribute__((address_space(3))) double*)wr,
+                   (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const double*)(lds + 12 * 66));
   }
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
   if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
@@ -378,7 +464,7 @@ int main() {
     double* out;
     double2* rt;
     unsigned long long* cyc;
-    hipMalloc(&out, 64 * sizeof(double));
+    hipMalloc(&out, 1024 * 64 * sizeof(double));
     hipMalloc(&rt, 600 * sizeof(double2));
     hipMemset(rt, 0, 600 * sizeof(double2));
     hipMalloc(&cyc, sizeof(unsigned long long));
@@ -387,6 +473,19 @@ int main() {
     unsigned long long c;
     hipMemcpy(&c, cyc, sizeof(c), hipMemcpyDeviceToHost);
     printf("%-44s: %.2f cycles per sample\n", "hv_block_asm alone (one wave)", (double)c / (256.0 * 64));
+    for (int r = 0; r < 2; r++) hipLaunchKernelGGL(hv_loop, dim3(1), dim3(64), 0, 0, out, rt, cyc, -256);
+    hipDeviceSynchronize();
+    hipMemcpy(&c, cyc, sizeof(c), hipMemcpyDeviceToHost);
+    printf("%-44s: %.2f cycles per sample\n", "hv_block_lds alone (one wave)", (double)c / (256.0 * 64));
+    // one wave per SIMD on every CU: the LDS loop beside three others
+    for (int r = 0; r < 2; r++) hipLaunchKernelGGL(hv_loop, dim3(1024), dim3(64), 0, 0, out, rt, cyc, -256);
+    hipDeviceSynchronize();
+    hipMemcpy(&c, cyc, sizeof(c), hipMemcpyDeviceToHost);
+    printf("%-44s: %.2f cycles per sample\n", "hv_block_lds, 1024 waves", (double)c / (256.0 * 64));
+    for (int r = 0; r < 2; r++) hipLaunchKernelGGL(hv_loop, dim3(1024), dim3(64), 0, 0, out, rt, cyc, 256);
+    hipDeviceSynchronize();
+    hipMemcpy(&c, cyc, sizeof(c), hipMemcpyDeviceToHost);
+    printf("%-44s: %.2f cycles per sample\n", "hv_block_asm, 1024 waves", (double)c / (256.0 * 64));
   }
   rung<0>("phase1g: global x, SGPR rc/rl, no M out");
   rung<1>("phase1g: + ds_write_b64 per sample");
