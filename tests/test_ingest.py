@@ -79,3 +79,30 @@ def test_reader_errors(tmp_path):
         read_ply(str(p), 28)
     with pytest.raises(FileNotFoundError):
         read_ply(str(tmp_path / "missing.ply"), 28)
+
+
+def test_carla_seg_matches_reference_run_fixture(tmp_path):
+    """ndnet.datasets.CARLA_Seg and the restatement in oracle/ingest_oracle.py
+    against the reference's own CARLA_Seg.get_data_pcl, run in the build
+    container (tests/golden/make_ingest_golden.py -> ingest_carla_seg.npz):
+    identical float32 points and one-hot classes for the same scans and
+    np.random seeds, including n_samples == the scan's size (a permutation)."""
+    import ingest_oracle as O
+    from conftest import golden
+    from ndnet.datasets import CARLA_Seg
+    z = golden("ingest_carla_seg.npz")
+    nc = int(z["n_classes"])
+    for i, (n, seed, ns, rs) in enumerate(z["scans"]):
+        d = tmp_path / f"s{i}"
+        d.mkdir()
+        _write_scan(d / "0000.ply", int(n), nc, int(seed))
+        ds = CARLA_Seg(nc, int(ns), str(d))
+        np.random.seed(int(rs))
+        pts, gt = ds[0]
+        assert np.array_equal(pts.numpy(), z[f"points_{i}"])
+        g = gt.numpy()
+        assert g.shape == (int(ns), nc + 1) and (g.sum(axis=1) == 1).all()
+        assert np.array_equal(g.argmax(axis=1), z[f"classes_{i}"])
+        np.random.seed(int(rs))
+        rp, rg = O.get_data_pcl(str(d / "0000.ply"), nc, int(ns))
+        assert np.array_equal(rp, z[f"points_{i}"]) and np.array_equal(rg.argmax(axis=1), z[f"classes_{i}"])
