@@ -126,6 +126,54 @@ int ndnet_pn_fc_run(const float *in, int ld_in, const float *W, const float *bia
  * workgroups, each summing its waves' K-slices in a fixed order. */
 int ndnet_pn_fc_mfma_run(const float *in, int ld_in, const float *Wf, const float *bias, float *out, int ld_out,
                          int batch, int K, int N, int relu, void *stream);
+/* BatchNorm fold of the eval forward's weights, re-run in place after a
+ * weight update (the host-side first fold: pointnet_hip._Folded; the folds
+ * it restates: ndtnet.py's Conv1d / Linear + BatchNorm1d pairs, :45-60,
+ * :148-161, :218-241, with running statistics).  One job writes one output
+ * tensor from one layer's parameters; the folded weight of layer row n and
+ * input column k is
+ *   fw(n, k) = w[n * ld + k0 + k] * (gamma[n] / sqrt(var[n] + eps))
+ * (no BatchNorm: gamma == NULL, fw = w), every operation a separately
+ * rounded fp32 operation as torch computes the fold.  Kinds:
+ *   NDNET_FOLD_WT     out[k][n] (Kp x Np floats) = fw(n, k), zero padded
+ *   NDNET_FOLD_FRAG   the same W^T fragment-major (ndnet_pn_layer.w, prec 0)
+ *   NDNET_FOLD_FRAG6  the same W^T split-bf16 (ndnet_pn_layer.w, prec 1;
+ *                     bf16 rounding to nearest even, residuals exact)
+ *   NDNET_FOLD_ROWS   out[n][k] (N x K floats) = fw(n, k)
+ *   NDNET_FOLD_BASIS  TNet(3)'s t1 basis of conv1 (K == 12):
+ *                     out[3a + c][r][n] = E_ac^T fw^T with E_ac the 0/1
+ *                     matrix of p -> t1 p, C -> t1 C (pointnet_hip._Folded)
+ *   NDNET_FOLD_BIAS   out[n] (Np floats) = (bias[n] - mean[n]) * s[n] + beta[n]
+ *                     (no BatchNorm: bias[n]), + 1 on the diagonal of an
+ *                     eye x eye matrix when eye > 0, zero padded
+ * ndnet_pn_fold_prepare validates a host copy of the job list and fills each
+ * job's block0 (its first workgroup), returning the grid size in
+ * *num_blocks; ndnet_pn_fold_run then runs the list from DEVICE memory in
+ * one launch (graph-capturable, no allocation).  NDNET_ERR_ARG (-20) on an
+ * invalid job. */
+#define NDNET_FOLD_WT 0
+#define NDNET_FOLD_FRAG 1
+#define NDNET_FOLD_FRAG6 2
+#define NDNET_FOLD_ROWS 3
+#define NDNET_FOLD_BASIS 4
+#define NDNET_FOLD_BIAS 5
+typedef struct ndnet_pn_fold_job {
+  const float *w;                          /* layer weight, rows of ld floats (not read by BIAS) */
+  const float *bias;                       /* layer bias [N] (BIAS only) */
+  const float *gamma, *beta, *mean, *var;  /* BatchNorm1d weight, bias, running mean / var; NULL: none */
+  void *out;                               /* the output tensor (bf16 for FRAG6, else fp32), 16-byte aligned */
+  int32_t kind;
+  int32_t N, K;                            /* layer rows (outputs) and the input columns used */
+  int32_t ld, k0;                          /* row stride of w and the first column used */
+  int32_t Kp, Np;                          /* padded sizes (WT / FRAG / FRAG6: Kp x Np; BIAS: Np) */
+  int32_t eye;
+  float eps;
+  int32_t reserved;
+  int64_t block0;                          /* filled by ndnet_pn_fold_prepare */
+} ndnet_pn_fold_job;
+int ndnet_pn_fold_prepare(ndnet_pn_fold_job *host_jobs, int num_jobs, int64_t *num_blocks);
+int ndnet_pn_fold_run(const ndnet_pn_fold_job *device_jobs, int num_jobs, int64_t num_blocks, void *stream);
+
 int ndnet_pn_head3_run(const float *h2, int ld_h, const float *W3, const float *b3, const float *basis,
                        float *t1, float *w1f, int batch, int K, int kin, int nout, void *stream);
 

@@ -1298,6 +1298,118 @@ __global__ void __launch_bounds__(256) k_pn_head3(const float* __restrict__ h2, 
   }
 }
 
+#if NDNET_PN_TILE == 64
+// ---- the BatchNorm fold, in place (ndnet_pn_fold_run, include/ndnet_pointnet.h) ----
+// HBM-bound copy work (~14 MB read, ~40 MB written for the F = 1024 model):
+// each thread writes one unit (4 fp32 of a fragment, 8 bf16 of each split
+// plane, else one float), so every output row is written with full-width,
+// contiguous stores; the strided weight reads hit L2.
+constexpr int kFoldThreads = 256;
+
+__device__ inline uint16_t fold_bf16(float x) {  // torch's float -> bfloat16: round to nearest even
+  uint32_t u = __float_as_uint(x);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+__device__ inline float fold_w(const ndnet_pn_fold_job& J, int n, int k) {
+#pragma clang fp contract(off)
+  if (n >= J.N || k >= J.K) return 0.0f;
+  const float w = J.w[(int64_t)n * J.ld + J.k0 + k];
+  if (!J.gamma) return w;
+  return w * (J.gamma[n] / sqrtf(J.var[n] + J.eps));  // pointnet_hip._bn_fold, operation by operation
+}
+
+__host__ __device__ inline int64_t fold_units(const ndnet_pn_fold_job& J) {
+  switch (J.kind) {
+    case NDNET_FOLD_WT: return (int64_t)J.Kp * J.Np;
+    case NDNET_FOLD_FRAG: return (int64_t)J.Kp * J.Np / 4;
+    case NDNET_FOLD_FRAG6: return (int64_t)J.Kp * J.Np / 8;
+    case NDNET_FOLD_ROWS: return (int64_t)J.N * J.K;
+    case NDNET_FOLD_BASIS: return (int64_t)9 * J.K * J.N;
+    default: return J.Np;
+  }
+}
+
+__global__ void __launch_bounds__(kFoldThreads) k_pn_fold(const ndnet_pn_fold_job* __restrict__ jobs, int num_jobs) {
+#pragma clang fp contract(off)
+  int j = 0;  // this workgroup's job: the last one starting at or before it (block0 ascends)
+  for (int i = 1; i < num_jobs; i++)
+    if (jobs[i].block0 <= (int64_t)blockIdx.x) j = i;
+  const ndnet_pn_fold_job J = jobs[j];
+  const int64_t u = ((int64_t)blockIdx.x - J.block0) * kFoldThreads + threadIdx.x;
+  if (u >= fold_units(J)) return;
+  switch (J.kind) {
+    case NDNET_FOLD_WT: {
+      const int n = (int)(u % J.Np), k = (int)(u / J.Np);
+      static_cast<float*>(J.out)[u] = fold_w(J, n, k);
+      break;
+    }
+    case NDNET_FOLD_FRAG: {  // [cb][kg][kq][cl][s]: k = 16 kg + 4 kq + s, n = 16 cb + cl
+      const int kgs = J.Kp / 16;
+      const int cl = (int)(u % 16), kq = (int)(u / 16 % 4), kg = (int)(u / 64 % kgs), cb = (int)(u / (64 * kgs));
+      const int k = 16 * kg + 4 * kq, n = 16 * cb + cl;
+      f32x4 v = {fold_w(J, n, k), fold_w(J, n, k + 1), fold_w(J, n, k + 2), fold_w(J, n, k + 3)};
+      reinterpret_cast<f32x4*>(J.out)[u] = v;
+      break;
+    }
+    case NDNET_FOLD_FRAG6: {  // [cb][kg][plane][kq][cl][j]: k = 32 kg + 8 kq + j, n = 16 cb + cl
+      const int kgs = J.Kp / 32;
+      const int cl = (int)(u % 16), kq = (int)(u / 16 % 4), kg = (int)(u / 64 % kgs), cb = (int)(u / (64 * kgs));
+      const int k = 32 * kg + 8 * kq, n = 16 * cb + cl;
+      uint32_t p[3][4];
+#pragma unroll
+      for (int t = 0; t < 8; t += 2) {
+        uint16_t hv[2], mv[2], lv[2];
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+          const float w = fold_w(J, n, k + t + e);
+          hv[e] = fold_bf16(w);
+          const float r = w - __uint_as_float((uint32_t)hv[e] << 16);
+          mv[e] = fold_bf16(r);
+          lv[e] = fold_bf16(r - __uint_as_float((uint32_t)mv[e] << 16));
+        }
+        p[0][t / 2] = hv[0] | ((uint32_t)hv[1] << 16);
+        p[1][t / 2] = mv[0] | ((uint32_t)mv[1] << 16);
+        p[2][t / 2] = lv[0] | ((uint32_t)lv[1] << 16);
+      }
+      const int64_t unit = u % 64 + (u / 64) * 192;  // 64 units per (cb, kg), three planes of them
+      uint4* o = reinterpret_cast<uint4*>(J.out);
+#pragma unroll
+      for (int pl = 0; pl < 3; pl++) o[unit + 64 * pl] = make_uint4(p[pl][0], p[pl][1], p[pl][2], p[pl][3]);
+      break;
+    }
+    case NDNET_FOLD_ROWS: {
+      const int n = (int)(u / J.K), k = (int)(u % J.K);
+      static_cast<float*>(J.out)[u] = fold_w(J, n, k);
+      break;
+    }
+    case NDNET_FOLD_BASIS: {  // out[3a + c][r][n]: r < 3 the point (t1 p), else the covariance rows (t1 C)
+      const int n = (int)(u % J.N), r = (int)(u / J.N % J.K), ac = (int)(u / ((int64_t)J.N * J.K));
+      const int a = ac / 3, c = ac % 3;
+      float v = 0.0f;
+      if (r < 3) {
+        if (r == c) v = fold_w(J, n, a);
+      } else if ((r - 3) / 3 == c) {
+        v = fold_w(J, n, 3 + 3 * a + (r - 3) % 3);
+      }
+      static_cast<float*>(J.out)[u] = v;
+      break;
+    }
+    default: {  // NDNET_FOLD_BIAS
+      const int n = (int)u;
+      float v = 0.0f;
+      if (n < J.N) {
+        v = J.bias[n];
+        if (J.gamma) v = (v - J.mean[n]) * (J.gamma[n] / sqrtf(J.var[n] + J.eps)) + J.beta[n];
+        if (J.eye > 0) v = v + (n / J.eye == n % J.eye ? 1.0f : 0.0f);
+      }
+      static_cast<float*>(J.out)[u] = v;
+    }
+  }
+}
+#endif
+
 }  // namespace
 
 extern "C" {
@@ -1333,6 +1445,38 @@ int ndnet_pn_head3_run(const float* h2, int ld_h, const float* W3, const float* 
       nout % 16)
     return -20;
   k_pn_head3<<<batch, 256, 0, (hipStream_t)stream>>>(h2, ld_h, W3, b3, basis, t1, w1f, K, kin, nout);
+  return hipGetLastError() == hipSuccess ? 0 : -21;
+}
+
+int ndnet_pn_fold_prepare(ndnet_pn_fold_job* jobs, int num_jobs, int64_t* num_blocks) {
+  if (!jobs || num_jobs <= 0 || !num_blocks) return -20;
+  int64_t blocks = 0;
+  for (int i = 0; i < num_jobs; i++) {
+    ndnet_pn_fold_job& J = jobs[i];
+    const bool bn = J.gamma != nullptr;
+    if (!J.out || (uintptr_t)J.out % 16 || J.kind < NDNET_FOLD_WT || J.kind > NDNET_FOLD_BIAS || J.N <= 0 ||
+        (bn && (!J.beta || !J.mean || !J.var || !(J.eps >= 0.0f))) || (!bn && (J.beta || J.mean || J.var)))
+      return -20;
+    if (J.kind == NDNET_FOLD_BIAS) {
+      if (!J.bias || J.Np < J.N || J.eye < 0 || (J.eye > 0 && J.eye * J.eye != J.N)) return -20;
+    } else {
+      if (!J.w || J.K <= 0 || J.k0 < 0 || J.ld < J.k0 + J.K) return -20;
+      if (J.kind == NDNET_FOLD_WT && (J.Kp < J.K || J.Np < J.N)) return -20;
+      if (J.kind == NDNET_FOLD_FRAG && (J.Kp < J.K || J.Np < J.N || J.Kp % 16 || J.Np % 16)) return -20;
+      if (J.kind == NDNET_FOLD_FRAG6 && (J.Kp < J.K || J.Np < J.N || J.Kp % 32 || J.Np % 16)) return -20;
+      if (J.kind == NDNET_FOLD_BASIS && J.K != 12) return -20;
+    }
+    J.block0 = blocks;
+    blocks += (fold_units(J) + kFoldThreads - 1) / kFoldThreads;
+  }
+  if (blocks <= 0 || blocks > 0x7fffffff) return -20;
+  *num_blocks = blocks;
+  return 0;
+}
+
+int ndnet_pn_fold_run(const ndnet_pn_fold_job* jobs, int num_jobs, int64_t num_blocks, void* stream) {
+  if (!jobs || num_jobs <= 0 || num_blocks <= 0 || num_blocks > 0x7fffffff) return -20;
+  k_pn_fold<<<(unsigned)num_blocks, kFoldThreads, 0, (hipStream_t)stream>>>(jobs, num_jobs);
   return hipGetLastError() == hipSuccess ? 0 : -21;
 }
 

@@ -218,9 +218,10 @@ class NDTNetSegmentation(nn.Module):
         return self.forward_torch(points, covariances)
 
     def train(self, mode: bool = True):
-        # entering training: weights will change, drop the folded copy (a
-        # captured graph keeps its own reference, ndnet.pipeline); a redundant
-        # eval() keeps it
-        if bool(mode) != self.training:
-            self._hip = None
+        # a mode change: weights may change (also inside a replayed training
+        # graph, which bumps no tensor versions), so the next eval forward
+        # re-folds -- in place, one ndnet_pn_fold_run launch
+        # (pointnet_hip._folded); a redundant eval() keeps the fold
+        if bool(mode) != self.training and self._hip is not None:
+            self._hip["stale"] = True
         return super().train(mode)

@@ -93,6 +93,14 @@ class _Chain(ctypes.Structure):
                 ("fold_out_b", ctypes.c_void_p)]
 
 
+class _FoldJob(ctypes.Structure):  # ndnet_pn_fold_job (include/ndnet_pointnet.h)
+    _fields_ = [("w", ctypes.c_void_p), ("bias", ctypes.c_void_p), ("gamma", ctypes.c_void_p),
+                ("beta", ctypes.c_void_p), ("mean", ctypes.c_void_p), ("var", ctypes.c_void_p),
+                ("out", ctypes.c_void_p), ("kind", ctypes.c_int32), ("N", ctypes.c_int32), ("K", ctypes.c_int32),
+                ("ld", ctypes.c_int32), ("k0", ctypes.c_int32), ("Kp", ctypes.c_int32), ("Np", ctypes.c_int32),
+                ("eye", ctypes.c_int32), ("eps", ctypes.c_float), ("reserved", ctypes.c_int32),
+                ("block0", ctypes.c_int64)]
+
 
 
 def available() -> bool:
@@ -231,6 +239,114 @@ class _Folded:
             # the identity the TNet heads add (ndtnet.py:59), folded into fc3's bias
             self.t1["c3"] = self.t1["c3"] + torch.eye(3, device=dev).reshape(-1)
             self.t2["c3"] = self.t2["c3"] + torch.eye(64, device=dev).reshape(-1)
+        self.tensors = _tensors(m)
+        self.prec = (SPLIT_BF16, X6_NARROW)
+        self.jobs = self._fold_jobs(m)
+        self._dev_jobs, self._blocks = None, 0
+
+    def _fold_jobs(self, m) -> list:
+        """The recipe of every tensor above as ndnet_pn_fold_job fields (kind,
+        out, layer, BatchNorm, k0, K, Kp, Np, eye): what ``refold`` re-runs in
+        place.  Aliases of parameters (fc3 / conv4 weights, conv4 bias) need
+        none.  Only for fp32, contiguous parameters (else None: a re-fold
+        rebuilds)."""
+        if not all(t.dtype == torch.float32 and t.is_contiguous() for t in m.parameters()):
+            return None
+        fe = m.feature_extractor
+        jobs, src = [], {}
+
+        def add(kind, out, layer, bn, k0=0, K=None, Kp=0, Np=0, eye=0):
+            ld = layer.weight.shape[1]
+            K = ld - k0 if K is None else K
+            jobs.append((kind, out, layer, bn, k0, K, Kp, Np, eye))
+            src[id(out)] = (layer, bn, k0, K)
+
+        def rows(out, layer, bn, k0=0, K=None):
+            add(3, out, layer, bn, k0, K)
+
+        def wt(out, layer, bn, k0=0, K=None):
+            add(0, out, layer, bn, k0, K, out.shape[0], out.shape[1])
+
+        def bias(out, layer, bn, eye=0):
+            add(5, out, layer, bn, Np=out.shape[0], eye=eye)
+
+        for t, tm, d in ((self.t1, fe.t1, 3), (self.t2, fe.t2, 64)):
+            for i in (1, 2, 3):
+                conv, bn = getattr(tm, f"conv{i}"), getattr(tm, f"bn{i}")
+                rows(t[f"w{i}"], conv, bn)
+                bias(t[f"b{i}"], conv, bn)
+            rows(t["f1"], tm.fc1, tm.bn4)
+            bias(t["c1"], tm.fc1, tm.bn4)
+            rows(t["f2"], tm.fc2, tm.bn5)
+            bias(t["c2"], tm.fc2, tm.bn5)
+            bias(t["c3"], tm.fc3, None, eye=d)
+            src[id(t["f3"])] = (tm.fc3, None, 0, tm.fc3.weight.shape[1])  # the parameter itself
+        for (w, b), conv, bn in (((self.c1w, self.c1b), fe.conv1, fe.bn1), ((self.c2w, self.c2b), fe.conv2, fe.bn2),
+                                 ((self.c3w, self.c3b), fe.conv3, fe.bn3), ((self.s1w, self.s1b), m.conv1, m.bn1),
+                                 ((self.s2w, self.s2b), m.conv2, m.bn2), ((self.s3w, self.s3b), m.conv3, m.bn3)):
+            rows(w, conv, bn)
+            bias(b, conv, bn)
+        rows(self.s1a, m.conv1, m.bn1, 0, 64)
+        rows(self.s1g, m.conv1, m.bn1, 64, self.F)
+        wt(self.s1bT, m.conv1, m.bn1, 64, self.F)
+        for layers, tm in ((self.A, fe.t1), (self.B_tail, fe.t2)):
+            for i, (w, _) in enumerate(layers, 1):
+                wt(w, getattr(tm, f"conv{i}"), getattr(tm, f"bn{i}"))
+        wt(self.C_tail[0], fe.conv3, fe.bn3)
+        bias(self.C_tail[1], fe.conv3, fe.bn3)
+        wt(self.D_tail[0][0], m.conv2, m.bn2)
+        wt(self.D_tail[1][0], m.conv3, m.bn3)
+        wt(self.D_tail[2][0], m.conv4, None)
+        bias(self.D_tail[2][1], m.conv4, None)
+        wt(self.c1wT, fe.conv1, fe.bn1)
+        wt(self.C_mid[0], fe.conv2, fe.bn2)
+        wt(self.s1aT, m.conv1, m.bn1, 0, 64)
+        add(4, self.t1_basis, fe.conv1, fe.bn1)
+        wts = {id(w): w for w, _ in self.A + self.B_tail + [self.C_mid, self.C_tail, (self.s1aT, None)] + self.D_tail}
+        for key, out in self.frag.items():
+            layer, bn, k0, K = src[key]
+            add(1, out, layer, bn, k0, K, *wts[key].shape)
+        for w in self.wide:
+            layer, bn, k0, K = src[id(w)]
+            add(2, self.frag6[id(w)], layer, bn, k0, K, *w.shape)
+        fcs = (self.t1["f1"], self.t1["f2"], self.t2["f1"], self.t2["f2"], self.t2["f3"], self.s1g)
+        for w in fcs:
+            layer, bn, k0, K = src[id(w)]
+            add(1, self.fcf[id(w)], layer, bn, k0, K, w.shape[1], w.shape[0])
+        return jobs
+
+    def can_refold(self, tensors) -> bool:
+        """In place: the same parameter / buffer tensors, on a GPU, at the same precision."""
+        return (self.jobs is not None and self.prec == (SPLIT_BF16, X6_NARROW) and self.c1wT.is_cuda
+                and len(tensors) == len(self.tensors) and all(a is b for a, b in zip(tensors, self.tensors))
+                and all(t.is_contiguous() and t.dtype == torch.float32 for t in tensors if t.is_floating_point()))
+
+    def refold(self) -> None:
+        """Every fold above again, from the current weights and running
+        statistics, into the same tensors: one ``ndnet_pn_fold_run`` launch on
+        the current stream (the workspaces and prebuilt chain argument blocks
+        that point at these tensors stay valid)."""
+        dev = self.c1wT.device
+        if self._dev_jobs is None:
+            arr = (_FoldJob * len(self.jobs))()
+            for J, (kind, out, layer, bn, k0, K, Kp, Np, eye) in zip(arr, self.jobs):
+                J.kind, J.out, J.N, J.K, J.ld, J.k0 = kind, out.data_ptr(), layer.weight.shape[0], K, \
+                    layer.weight.shape[1], k0
+                J.Kp, J.Np, J.eye = Kp, Np, eye
+                if kind == 5:
+                    J.bias = layer.bias.data_ptr()
+                else:
+                    J.w = layer.weight.data_ptr()
+                if bn is not None:
+                    J.gamma, J.beta = bn.weight.data_ptr(), bn.bias.data_ptr()
+                    J.mean, J.var, J.eps = bn.running_mean.data_ptr(), bn.running_var.data_ptr(), bn.eps
+            blocks = ctypes.c_int64()
+            _lib.check(_lib.lib().ndnet_pn_fold_prepare(arr, len(arr), ctypes.byref(blocks)), "ndnet_pn_fold_prepare")
+            self._dev_jobs = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(dev)
+            self._blocks = blocks.value
+        rc = _lib.lib().ndnet_pn_fold_run(self._dev_jobs.data_ptr(), len(self.jobs), self._blocks,
+                                          _lib.stream_ptr(dev))
+        _lib.check(rc, "ndnet_pn_fold_run")
 
 
 def _tensors(m) -> list:
@@ -419,10 +535,19 @@ def _folded(model):
     cache = model._hip
     if cache is None:
         tensors = _tensors(model)
-        cache = model._hip = {"tensors": tensors, "sig": None}
+        cache = model._hip = {"tensors": tensors, "sig": None, "stale": False}
     sig = _signature(cache["tensors"])
-    if cache["sig"] != sig:
-        cache.update(sig=sig, W=_Folded(model), ws={})
+    if cache["sig"] != sig or cache["stale"]:
+        # stale: the model was in train mode since the last fold, where a
+        # replayed training graph updates the weights without bumping their
+        # versions (ndnet.training.GraphedTrainStep)
+        W = cache.get("W")
+        if W is not None and W.can_refold(_tensors(model)):
+            W.refold()  # one launch, in place: workspaces and argument blocks stay valid
+        else:
+            cache.update(tensors=_tensors(model), W=_Folded(model), ws={})
+            sig = _signature(cache["tensors"])
+        cache.update(sig=sig, stale=False)
     return cache
 
 

@@ -98,6 +98,103 @@ def test_hip_forward_on_ndt_rows():
     assert (out - ref).abs().max().item() < TOL
 
 
+@pytest.mark.parametrize("F,C", [(768, 28), (64, 5)])
+def test_fold_jobs_cover_every_folded_tensor(F, C):
+    """The re-fold's job list (ndnet_pn_fold_job per output, the kernel's
+    launch on the GPU): each job writes exactly its output tensor's elements,
+    and every tensor the forward reads is either re-folded or a parameter."""
+    from ndnet.models import pointnet_hip as ph
+    m = _model(F, C)
+    W = ph._Folded(m)
+    size = {0: lambda K, N, Kp, Np: Kp * Np, 1: lambda K, N, Kp, Np: Kp * Np, 2: lambda K, N, Kp, Np: 3 * Kp * Np,
+            3: lambda K, N, Kp, Np: N * K, 4: lambda K, N, Kp, Np: 9 * K * N, 5: lambda K, N, Kp, Np: Np}
+    outs = set()
+    for kind, out, layer, bn, k0, K, Kp, Np, eye in W.jobs:
+        N = layer.weight.shape[0]
+        assert out.is_contiguous() and out.numel() == size[kind](K, N, Kp, Np)
+        assert out.dtype == (torch.bfloat16 if kind == 2 else torch.float32)
+        assert k0 + K <= layer.weight.shape[1] and (bn is None or bn.num_features == N)
+        outs.add(id(out))
+    params = {id(t) for t in m.parameters()}
+    read = [w for w, _ in W.A + W.B_tail + [W.C_mid, W.C_tail] + W.D_tail] + [W.s1aT, W.t1_basis]
+    read += [b for _, b in W.A + W.B_tail + [W.C_mid, W.C_tail] + W.D_tail] + [W.c1b, W.s1b, W.s1g]
+    read += list(W.frag.values()) + list(W.frag6.values()) + list(W.fcf.values())
+    for t in (W.t1, W.t2):
+        read += [t[k] for k in ("f1", "c1", "f2", "c2", "c3")]
+    for t in read:
+        assert id(t) in outs or id(t) in params
+    assert len(outs) == len(W.jobs)
+
+
+def _perturb(m, seed, versions=True):
+    """Scales every parameter and moves every BatchNorm's running statistics;
+    ``versions=False`` writes through ``.data`` (no version bump: what a
+    replayed training graph does to the weights)."""
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    with torch.no_grad():
+        for t in list(m.parameters()) + [b for b in m.buffers() if b.is_floating_point()]:
+            d = t if versions else t.data
+            d.mul_(1.0 + 0.05 * torch.randn(t.shape, device="cuda", generator=g))
+            if t.dim() == 1:
+                d.add_(0.01 * torch.rand(t.shape, device="cuda", generator=g))  # running_var stays > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("F,C", [(768, 28), (64, 5)])
+def test_refold_in_place_equals_fresh_fold(F, C):
+    """ndnet_pn_fold_run (one launch) re-folds changed weights and running
+    statistics into the SAME tensors; every one of them equals what a fresh
+    torch fold writes, bit for bit (fp32 operations in torch's order, bf16
+    rounding to nearest even), and the forward follows the new weights."""
+    from ndnet.models import pointnet_hip as ph
+    m = _model(F, C, "cuda")
+    g = torch.Generator(device="cuda").manual_seed(F + C)
+    p = torch.rand((3, 200, 3), device="cuda", generator=g) * 20 - 10
+    c = torch.randn((3, 200, 9), device="cuda", generator=g) * 0.1
+    with torch.no_grad():
+        m(p, c)
+    cache = m._hip
+    W, ws = cache["W"], dict(cache["ws"])
+    assert W.jobs is not None and len(W.jobs) > 60
+    _perturb(m, 1)
+    with torch.no_grad():
+        out = m(p, c)
+    assert m._hip is cache and cache["W"] is W and cache["ws"] == ws, "re-fold must be in place"
+    fresh = ph._Folded(m)
+    bad = []
+    for j, f in zip(W.jobs, fresh.jobs):
+        a, b = j[1], f[1]
+        assert a.shape == b.shape and a.dtype == b.dtype and j[0] == f[0]
+        if not torch.equal(a, b):
+            bad.append((j[0], tuple(a.shape), (a.float() - b.float()).abs().max().item()))
+    assert not bad, bad
+    with torch.no_grad():
+        ref = m.forward_torch(p, c)
+    assert (out - ref).abs().max().item() < TOL
+
+
+@pytest.mark.gpu
+def test_mode_switch_refolds_weights_changed_without_versions():
+    """A replayed training graph changes weights without bumping versions:
+    the mode switch (train() -> eval()) marks the fold stale, so the next eval
+    forward re-folds; without a mode switch the fold is kept."""
+    m = _model(64, 5, "cuda")
+    p = torch.rand((2, 100, 3), device="cuda") * 20 - 10
+    c = torch.randn((2, 100, 9), device="cuda") * 0.1
+    with torch.no_grad():
+        first = m(p, c).clone()
+        m.train()
+        _perturb(m, 2, versions=False)
+        m.eval()
+        out = m(p, c)
+        ref = m.forward_torch(p, c)
+    assert (out - ref).abs().max().item() < TOL and (out - first).abs().max().item() > 1e-3
+    with torch.no_grad():
+        _perturb(m, 3, versions=False)
+        kept = m(p, c)   # no mode switch, no version bump: the previous fold
+    assert torch.equal(kept, out)
+
+
 def test_fragment_layout_matches_mfma_operands():
     """_frag puts W^T[k][n] where k-group kg, column block cb, lane 16 kq + cl,
     element s of the float4 with k = 16 kg + 4 kq + s, n = 16 cb + cl

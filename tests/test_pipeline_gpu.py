@@ -210,12 +210,12 @@ def test_graph_keeps_captured_fold_alive():
     g = GraphedSegmentation(m, k, B, n)
     first = g(pts).clone()
     m.eval()                       # redundant: keeps the fold
-    m.train()                      # drops the model's cache (the graph keeps its own)
+    m.train()                      # marks the fold stale
     m.eval()
     with torch.no_grad():
         from ndnet.preprocessing.ndtnet_preprocessing import ndt_preprocessing
         p, c, _ = ndt_preprocessing(k, pts)
-        eager = m(p, c).clone()   # re-folds into fresh buffers
+        eager = m(p, c).clone()   # re-folds in place: the same values into the graph's buffers
         junk = [torch.randn(1 << 20, device="cuda") for _ in range(8)]  # reuse freed blocks, if any
     again = g(pts).clone()
     torch.cuda.synchronize()

@@ -147,6 +147,31 @@ def _nds(B, k, seed):
     return pts, cov
 
 
+@pytest.mark.parametrize("name", ["ndtnet_seg_F768_C28.npz", "ndtnet_seg_F64_C5.npz"])
+def test_train_forward_matches_reference_fixture(monkeypatch, name):
+    """The HIP train-mode forward (BatchNorm batch statistics, every conv
+    block on the train kernels) against the log-probs the reference module
+    itself produced in train mode on the same weights and input
+    (tests/golden/make_golden.py, ``out_train``): within 1e-4."""
+    import numpy as np
+    from conftest import golden
+    from model_init import deterministic_state
+    from ndnet.models import ndtnet, train_hip
+    z = golden(name)
+    m = ndtnet.NDTNetSegmentation(3, int(z["num_classes"]), int(z["feature_dim"]))
+    m.load_state_dict(deterministic_state(m.state_dict()))
+    m = m.cuda().train()
+    calls = []
+    real, real_pool = train_hip.conv_bn_act, train_hip.conv_bn_act_pool
+    monkeypatch.setattr(train_hip, "conv_bn_act", lambda *a, **k: calls.append(1) or real(*a, **k))
+    monkeypatch.setattr(train_hip, "conv_bn_act_pool", lambda *a, **k: calls.append(2) or real_pool(*a, **k))
+    out = m(torch.from_numpy(z["points"]).cuda(), torch.from_numpy(z["covs"]).cuda())
+    assert len(calls) == 13, "the train forward must run on the HIP kernels"
+    err = np.abs(out.detach().cpu().numpy() - z["out_train"]).max()
+    print(f"max |log-prob - reference out_train| = {err:.3e}")
+    assert err <= 1e-4
+
+
 def test_segmentation_train_forward_backward_matches_torch(monkeypatch):
     """The whole train-mode forward (every conv block on the HIP kernels) vs
     the torch composition: log-probs within 1e-4, running statistics, and

@@ -22,6 +22,7 @@ import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "ndt-net_amd"))
+from ndnet.models import pointnet_hip  # noqa: E402
 from ndnet.models.ndtnet import NDTNetSegmentation  # noqa: E402
 from ndnet.preprocessing.ndtnet_preprocessing import ndt_preprocessing  # noqa: E402
 from ndnet.synthetic import make_labelled_batch  # noqa: E402
@@ -61,15 +62,29 @@ def main() -> None:
         e1.record(st)
         torch.cuda.synchronize()
         step = e0.elapsed_time(e1) / a.steps
+        # an eval forward right after a replayed step: re-fold (in place, one launch) + the HIP forward
+        pcl, covs, _ = ndt_preprocessing(a.nds, pts, gt, a.classes)
+        after = []
+        for _ in range(5):
+            tr.step_graphed(pts, gt)
+            model.eval()
+            e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e2.record(st)
+            with torch.no_grad():
+                model(pcl, covs)
+            e3.record(st)
+            torch.cuda.synchronize()
+            after.append(e2.elapsed_time(e3))
         print(json.dumps({"what": "training step (tools/train.py:67-81) as one HIP graph: HIP labelled NDT + "
                                   "train forward/backward + fused capturable Adam", "train_path": TRAIN_PATH,
                           "batch": a.batch,
                           "points": a.points, "nds": a.nds, "classes": a.classes, "F": a.feature_dim,
                           "steps": a.steps, "step_ms": round(step, 4),
-                          "clouds_per_s": round(a.batch / step * 1e3, 1), "loss": round(loss.item(), 5)}))
+                          "clouds_per_s": round(a.batch / step * 1e3, 1), "loss": round(loss.item(), 5),
+                          "eval_forward_after_step_ms": round(sorted(after)[len(after) // 2], 4)}))
         return
     tr = Trainer(model, 1e-3, a.nds, a.classes, dev, ddp=False)
-    names = ("ndt_labelled", "forward_train", "loss", "backward", "adam", "forward_eval_hip")
+    names = ("ndt_labelled", "forward_train", "loss", "backward", "adam", "refold", "forward_eval_hip")
     tot = {n: 0.0 for n in names}
     st = torch.cuda.current_stream(dev)
     for it in range(a.warmup + a.steps):
@@ -88,15 +103,17 @@ def main() -> None:
         tr.opt.step()
         ev[5].record(st)
         model.eval()
+        pointnet_hip._folded(model)  # the re-fold of the updated weights (ndnet_pn_fold_run), else inside the forward
+        ev[6].record(st)
         with torch.no_grad():
             model(pcl, covs)
-        ev[6].record(st)
+        ev[7].record(st)
         torch.cuda.synchronize()
         if it >= a.warmup:
             for i, n in enumerate(names):
                 tot[n] += ev[i].elapsed_time(ev[i + 1])
     ms = {n: round(v / a.steps, 4) for n, v in tot.items()}
-    step = sum(v for n, v in ms.items() if n != "forward_eval_hip")
+    step = sum(v for n, v in ms.items() if n not in ("refold", "forward_eval_hip"))
     print(json.dumps({"what": "training step (tools/train.py:67-81): HIP labelled NDT + train "
                               "forward/backward + Adam", "train_path": TRAIN_PATH, "batch": a.batch,
                       "points": a.points, "nds": a.nds,
