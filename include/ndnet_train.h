@@ -61,10 +61,12 @@ int ndnet_tr_sum_parts(const float *part, float *out, int64_t count, int nparts,
  * max over the points of cloud b of z, pool_idx[b][c] = its first point --
  * the block followed by ``amax(dim=2)`` (TNet conv3, ndtnet.py:50-51; NDTNet
  * conv3 into the segmentation head's global feature, :152, :231), without the
- * [B][C][N] activation. */
+ * [B][C][N] activation.  batches_tracked (may be NULL): the module's int64
+ * num_batches_tracked, incremented by the launch (no launch of its own). */
 int ndnet_tr_bn_fwd(const float *y, float *z, float *mean, float *invstd, float *running_mean,
                     float *running_var, const float *gamma, const float *beta, int B, int C, int N,
-                    float eps, float momentum, int relu, float *pool, int32_t *pool_idx, void *stream);
+                    float eps, float momentum, int relu, float *pool, int32_t *pool_idx,
+                    int64_t *batches_tracked, void *stream);
 
 /* Its backward, one workgroup per channel: g = dz, masked by ReLU where the
  * forward's output (recomputed from y, mean, invstd, gamma, beta with the

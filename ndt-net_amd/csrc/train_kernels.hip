@@ -40,43 +40,66 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kTM = 64, kTN = 64, kTK = 16;
-// LDS row pitch TM + kPad floats.  17: a k-major tile store (lanes = 16 k rows x 4
-// columns) and an operand read (4 lane quads = 4 k rows x 16 columns) each touch
-// (nearly) distinct banks; with + 16 the k-major store was 4-way conflicted
-#ifndef NDNET_TR_PAD
-#define NDNET_TR_PAD 17
-#endif
-constexpr int kPad = NDNET_TR_PAD;
+// LDS row pitch of a [k][row] tile, by how the operand is stored (ds_write_b32
+// / ds_read_b32 bank = dword address mod 32, two 32-lane groups per wave):
+//  * k-major operands (a thread holds 4 consecutive k of one row, stored as 4
+//    dwords): pitch = TM + 18 -- the 8 rows x 4 k-quads of a lane group land
+//    on distinct banks (4 * 18 = 8 mod 32); the MFMA operand reads (2 k rows x
+//    16 columns per group) overlap on 2 banks;
+//  * row-major operands (4 consecutive rows of one k, one ds_write_b128):
+//    pitch = TM + 16 (16-byte aligned rows; operand reads conflict-free).
+// Round 3's single pitch TM + 17 with one scalar load per element:
+// profiles/r03t6_train_pad17.txt.
+template <int TM, bool KMAJOR>
+constexpr int tile_pitch() { return TM + (KMAJOR ? 18 : 16); }
 
 constexpr int kBnThreads = 512;
-constexpr int kBnCache = 32;
+constexpr int kBnValues = 16384;  // values per channel held in registers across the workgroup (B * N <= this
+                                  // reads the channel once)
 constexpr int kPoolMaxB = 64;  // pool mode: clouds per launch  // values per thread held in registers: B * N <= 16384 reads the channel once
 
 // global -> registers: this thread's 4 elements of the (k0 .. k0 + 16) x TM tile
-// (TM * 4 threads).  P contiguous along k (KMAJOR): lanes walk k (16 per row),
-// else along the row index.
+// (TM * 4 threads), P contiguous along k (KMAJOR) or along the row index.  Each thread loads 4 consecutive elements along the contiguous axis: one
+// 16-byte load when they are in range and aligned (the common case: k-steps
+// of 16, rows of 1000 points), else element by element with zero fill.
+// KMAJOR: row t / 4, k (t % 4) * 4 .. + 3; else k t / (TM / 4), rows
+// (t % (TM / 4)) * 4 .. + 3.
 template <int TM, bool KMAJOR>
 __device__ __forceinline__ void tile_load(const float* __restrict__ P, int64_t ld, int r0, int k0, int R, int kend,
                                           float (&v)[4]) {
   const int t = threadIdx.x;
+  const int kk = KMAJOR ? (t & 3) * 4 : t / (TM / 4);
+  const int rr = KMAJOR ? t >> 2 : (t % (TM / 4)) * 4;
+  const int gr = r0 + rr, gk = k0 + kk;
+  const float* p = KMAJOR ? P + (int64_t)gr * ld + gk : P + (int64_t)gk * ld + gr;
+  const bool full = KMAJOR ? (gr < R && gk + 3 < kend) : (gk < kend && gr + 3 < R);
+  if (full && ((uintptr_t)p & 15) == 0) {
+    const f32x4 x = *reinterpret_cast<const f32x4*>(p);
+    v[0] = x[0];
+    v[1] = x[1];
+    v[2] = x[2];
+    v[3] = x[3];
+  } else {
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const int kk = KMAJOR ? (t & 15) : t / TM + 4 * i;
-    const int rr = KMAJOR ? (t >> 4) + (TM / 4) * i : t % TM;
-    const int gr = r0 + rr, gk = k0 + kk;
-    v[i] = (gr < R && gk < kend) ? (KMAJOR ? P[(int64_t)gr * ld + gk] : P[(int64_t)gk * ld + gr]) : 0.0f;
+    for (int i = 0; i < 4; i++) {
+      const bool in = KMAJOR ? (gr < R && gk + i < kend) : (gk < kend && gr + i < R);
+      v[i] = in ? p[i] : 0.0f;
+    }
   }
 }
 
 // registers -> LDS tile [k][row] (row contiguous: one MFMA operand read per lane)
 template <int TM, bool KMAJOR>
 __device__ __forceinline__ void tile_store(float* __restrict__ s, const float (&v)[4]) {
+  constexpr int P = tile_pitch<TM, KMAJOR>();
   const int t = threadIdx.x;
+  if (KMAJOR) {
+    const int kk = (t & 3) * 4, rr = t >> 2;
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const int kk = KMAJOR ? (t & 15) : t / TM + 4 * i;
-    const int rr = KMAJOR ? (t >> 4) + (TM / 4) * i : t % TM;
-    s[kk * (TM + kPad) + rr] = v[i];
+    for (int i = 0; i < 4; i++) s[(kk + i) * P + rr] = v[i];
+  } else {
+    const int kk = t / (TM / 4), rr = (t % (TM / 4)) * 4;
+    *reinterpret_cast<f32x4*>(s + kk * P + rr) = f32x4{v[0], v[1], v[2], v[3]};
   }
 }
 
@@ -89,12 +112,12 @@ __global__ __launch_bounds__(TM * 4) void k_tr_gemm(const float* __restrict__ A,
                                                     int64_t sbias, int M, int N, int K, int64_t lda, int64_t ldb,
                                                     int64_t ldc, int64_t sAz, int64_t sBz, int64_t sCz, int batch,
                                                     int cpz, int nchunks, int kchunk) {
-  constexpr int P = TM + kPad;            // LDS row pitch (kPad)
+  constexpr int PA = tile_pitch<TM, AK>(), PB = tile_pitch<TM, BK>();  // LDS row pitches
   constexpr int WN = 2 * (TM / 64);       // waves along N
   constexpr int IM = TM / 32;             // 16-row blocks per wave (wave tile TM / 2 rows x 32 columns)
   constexpr int KS = TM == 64 ? 4 : 2;    // accumulator sets (k-quad ks uses set ks % KS)
-  __shared__ float sA[2][kTK * P];
-  __shared__ float sB[2][kTK * P];
+  __shared__ __attribute__((aligned(16))) float sA[2][kTK * PA];
+  __shared__ __attribute__((aligned(16))) float sB[2][kTK * PB];
   const int z = blockIdx.z, zg = z / nchunks, zc = z - zg * nchunks;
   const int cl0 = zg * cpz, ncl = min(cpz, batch - cl0);  // this part's clouds
   C += z * sCz;
@@ -140,11 +163,11 @@ __global__ __launch_bounds__(TM * 4) void k_tr_gemm(const float* __restrict__ A,
     const float* b = sB[cur];
 #pragma unroll
     for (int ks = 0; ks < kTK / 4; ks++) {
-      const int row = (ks * 4 + q) * P;
+      const int oa = (ks * 4 + q) * PA, ob = (ks * 4 + q) * PB;
       float av[IM];
 #pragma unroll
-      for (int i = 0; i < IM; i++) av[i] = a[row + wm + 16 * i + r16];
-      const float b0 = b[row + wn + r16], b1 = b[row + wn + 16 + r16];
+      for (int i = 0; i < IM; i++) av[i] = a[oa + wm + 16 * i + r16];
+      const float b0 = b[ob + wn + r16], b1 = b[ob + wn + 16 + r16];
 #pragma unroll
       for (int i = 0; i < IM; i++) {
         acc[ks % KS][i][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], b0, acc[ks % KS][i][0], 0, 0, 0);
@@ -204,6 +227,7 @@ __global__ __launch_bounds__(256) void k_tr_sum_parts(const float* __restrict__ 
 }
 
 // sum over the workgroup in a fixed order (wave shuffles, then the waves in order)
+template <int T>
 __device__ double block_sum(double v, double* red) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -212,12 +236,13 @@ __device__ double block_sum(double v, double* red) {
   if ((threadIdx.x & 63) == 0) red[wave] = v;
   __syncthreads();
   double t = red[0];
-  for (int w = 1; w < kBnThreads / 64; w++) t += red[w];
+  for (int w = 1; w < T / 64; w++) t += red[w];
   return t;
 }
 
 // this thread's elements j = tid, tid + T, ... of one channel as (cloud, point),
 // advanced without divisions
+template <int T>
 struct ChanWalk {
   int b, n;
   __device__ explicit ChanWalk(int N) : b(0), n(threadIdx.x) { fold(N); }
@@ -228,7 +253,7 @@ struct ChanWalk {
     }
   }
   __device__ void next(int N) {
-    n += kBnThreads;
+    n += T;
     fold(N);
   }
   __device__ int64_t off(int C, int N, int c) const { return ((int64_t)b * C + c) * N + n; }
@@ -240,47 +265,52 @@ __device__ __forceinline__ float bn_apply(float v, float fm, float inv, float g,
   return __fadd_rn(__fmul_rn(__fmul_rn(__fsub_rn(v, fm), inv), g), bt);
 }
 
-__global__ __launch_bounds__(kBnThreads) void k_tr_bn_fwd(const float* __restrict__ y, float* __restrict__ z,
+template <int T>
+__global__ __launch_bounds__(T) void k_tr_bn_fwd(const float* __restrict__ y, float* __restrict__ z,
                                                           float* __restrict__ mean, float* __restrict__ invstd,
                                                           float* __restrict__ rmean, float* __restrict__ rvar,
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, int Bn, int C, int N,
                                                           float eps, float momentum, int relu,
-                                                          float* __restrict__ pool, int* __restrict__ pool_idx) {
-  __shared__ double red[kBnThreads / 64];
+                                                          float* __restrict__ pool, int* __restrict__ pool_idx,
+                                                          long long* __restrict__ batches_tracked) {
+  __shared__ double red[T / 64];
+  constexpr int kCache = kBnValues / T;
   __shared__ unsigned long long pk[kPoolMaxB];  // per cloud: (ordered value bits, ~point) -- max = first max
   const int c = blockIdx.x;
+  // BatchNorm1d's num_batches_tracked += 1 (torch does it as a launch of its own)
+  if (batches_tracked && c == 0 && threadIdx.x == 0) batches_tracked[0] += 1;
   const int64_t M = (int64_t)Bn * N;
-  const bool cached = M <= (int64_t)kBnCache * kBnThreads;
+  const bool cached = M <= (int64_t)kBnValues;
   if (pool && threadIdx.x < Bn) pk[threadIdx.x] = 0ull;  // ordered before use by block_sum's barriers
-  float v[kBnCache];
+  float v[kCache];
   double s = 0.0;
   if (cached) {
-    ChanWalk w(N);
+    ChanWalk<T> w(N);
 #pragma unroll
-    for (int i = 0; i < kBnCache; i++, w.next(N)) {
+    for (int i = 0; i < kCache; i++, w.next(N)) {
       v[i] = w.b < Bn ? y[w.off(C, N, c)] : 0.0f;
       s += v[i];
     }
   } else {
-    for (ChanWalk w(N); w.b < Bn; w.next(N)) s += y[w.off(C, N, c)];
+    for (ChanWalk<T> w(N); w.b < Bn; w.next(N)) s += y[w.off(C, N, c)];
   }
-  const double mu = block_sum(s, red) / (double)M;
+  const double mu = block_sum<T>(s, red) / (double)M;
   double s2 = 0.0;
   if (cached) {
-    ChanWalk w(N);
+    ChanWalk<T> w(N);
 #pragma unroll
-    for (int i = 0; i < kBnCache; i++, w.next(N)) {
+    for (int i = 0; i < kCache; i++, w.next(N)) {
       const double d = (double)v[i] - mu;
       if (w.b < Bn) s2 += d * d;
     }
   } else {
-    for (ChanWalk w(N); w.b < Bn; w.next(N)) {
+    for (ChanWalk<T> w(N); w.b < Bn; w.next(N)) {
       const double d = (double)y[w.off(C, N, c)] - mu;
       s2 += d * d;
     }
   }
-  const double var = block_sum(s2, red) / (double)M;
+  const double var = block_sum<T>(s2, red) / (double)M;
   const float inv = (float)(1.0 / sqrt(var + (double)eps));
   if (threadIdx.x == 0) {
     mean[c] = (float)mu;
@@ -296,7 +326,7 @@ __global__ __launch_bounds__(kBnThreads) void k_tr_bn_fwd(const float* __restric
   // clouds in order), merged into pk when the cloud changes
   unsigned long long best = 0ull;
   int cur = -1;
-  auto emit = [&](const ChanWalk& w, float o) {
+  auto emit = [&](const ChanWalk<T>& w, float o) {
     if (!pool) {
       z[w.off(C, N, c)] = o;
       return;
@@ -312,9 +342,9 @@ __global__ __launch_bounds__(kBnThreads) void k_tr_bn_fwd(const float* __restric
     best = k > best ? k : best;
   };
   if (cached) {
-    ChanWalk w(N);
+    ChanWalk<T> w(N);
 #pragma unroll
-    for (int i = 0; i < kBnCache; i++, w.next(N)) {
+    for (int i = 0; i < kCache; i++, w.next(N)) {
       if (w.b < Bn) {
         float o = bn_apply(v[i], fm, inv, g, bt);
         if (relu) o = fmaxf(o, 0.0f);
@@ -322,7 +352,7 @@ __global__ __launch_bounds__(kBnThreads) void k_tr_bn_fwd(const float* __restric
       }
     }
   } else {
-    for (ChanWalk w(N); w.b < Bn; w.next(N)) {
+    for (ChanWalk<T> w(N); w.b < Bn; w.next(N)) {
       float o = bn_apply(y[w.off(C, N, c)], fm, inv, g, bt);
       if (relu) o = fmaxf(o, 0.0f);
       emit(w, o);
@@ -340,7 +370,8 @@ __global__ __launch_bounds__(kBnThreads) void k_tr_bn_fwd(const float* __restric
   }
 }
 
-__global__ __launch_bounds__(kBnThreads) void k_tr_bn_bwd(const float* __restrict__ dz, const float* __restrict__ y,
+template <int T>
+__global__ __launch_bounds__(T) void k_tr_bn_bwd(const float* __restrict__ dz, const float* __restrict__ y,
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ invstd,
                                                           const float* __restrict__ gamma,
@@ -348,17 +379,18 @@ __global__ __launch_bounds__(kBnThreads) void k_tr_bn_bwd(const float* __restric
                                                           float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                           float* __restrict__ dbias, int Bn, int C, int N, int relu,
                                                           const int* __restrict__ pool_idx) {
-  __shared__ double red[kBnThreads / 64];
+  __shared__ double red[T / 64];
+  constexpr int kCache = kBnValues / T;
   const int c = blockIdx.x;
   const int64_t M = (int64_t)Bn * N;
-  const bool cached = M <= (int64_t)kBnCache * kBnThreads;
+  const bool cached = M <= (int64_t)kBnValues;
   const float mu = mean[c], inv = invstd[c], gm = gamma[c], bt = beta[c];
-  float gv[kBnCache], xv[kBnCache];
+  float gv[kCache], xv[kCache];
   double sg = 0.0, sgx = 0.0;
   // g = dz where the forward's output was > 0 (ReLU), xhat = (y - mean) invstd;
   // pool mode: dz is [B][C], the gradient of the max over points, all of it at
   // the forward's first maximum
-  auto grad_at = [&](const ChanWalk& w, float& xh) {
+  auto grad_at = [&](const ChanWalk<T>& w, float& xh) {
     const int64_t off = w.off(C, N, c);
     const float yv = y[off];
     float g;
@@ -373,9 +405,9 @@ __global__ __launch_bounds__(kBnThreads) void k_tr_bn_bwd(const float* __restric
     return g;
   };
   if (cached) {
-    ChanWalk w(N);
+    ChanWalk<T> w(N);
 #pragma unroll
-    for (int i = 0; i < kBnCache; i++, w.next(N)) {
+    for (int i = 0; i < kCache; i++, w.next(N)) {
       float g = 0.0f, xh = 0.0f;
       if (w.b < Bn) g = grad_at(w, xh);
       gv[i] = g;
@@ -384,22 +416,22 @@ __global__ __launch_bounds__(kBnThreads) void k_tr_bn_bwd(const float* __restric
       sgx += (double)g * xh;
     }
   } else {
-    for (ChanWalk w(N); w.b < Bn; w.next(N)) {
+    for (ChanWalk<T> w(N); w.b < Bn; w.next(N)) {
       float xh;
       const float g = grad_at(w, xh);
       sg += g;
       sgx += (double)g * xh;
     }
   }
-  sg = block_sum(sg, red);
-  sgx = block_sum(sgx, red);
+  sg = block_sum<T>(sg, red);
+  sgx = block_sum<T>(sgx, red);
   const float k1 = (float)(sg / (double)M), k2 = (float)(sgx / (double)M);
   const float scale = gm * inv;
   double sdy = 0.0;
   if (cached) {
-    ChanWalk w(N);
+    ChanWalk<T> w(N);
 #pragma unroll
-    for (int i = 0; i < kBnCache; i++, w.next(N)) {
+    for (int i = 0; i < kCache; i++, w.next(N)) {
       if (w.b < Bn) {
         const float d = scale * (gv[i] - k1 - xv[i] * k2);
         dy[w.off(C, N, c)] = d;
@@ -407,7 +439,7 @@ __global__ __launch_bounds__(kBnThreads) void k_tr_bn_bwd(const float* __restric
       }
     }
   } else {
-    for (ChanWalk w(N); w.b < Bn; w.next(N)) {
+    for (ChanWalk<T> w(N); w.b < Bn; w.next(N)) {
       const int64_t off = w.off(C, N, c);
       float xh;
       const float g = grad_at(w, xh);
@@ -416,7 +448,7 @@ __global__ __launch_bounds__(kBnThreads) void k_tr_bn_bwd(const float* __restric
       sdy += d;
     }
   }
-  sdy = block_sum(sdy, red);
+  sdy = block_sum<T>(sdy, red);
   if (threadIdx.x == 0) {
     if (dgamma) dgamma[c] = (float)sgx;
     if (dbeta) dbeta[c] = (float)sg;
@@ -429,8 +461,8 @@ __global__ __launch_bounds__(kBnThreads) void k_tr_chan_sum(const float* __restr
   __shared__ double red[kBnThreads / 64];
   const int c = blockIdx.x;
   double s = 0.0;
-  for (ChanWalk w(N); w.b < Bn; w.next(N)) s += x[w.off(C, N, c)];
-  s = block_sum(s, red);
+  for (ChanWalk<kBnThreads> w(N); w.b < Bn; w.next(N)) s += x[w.off(C, N, c)];
+  s = block_sum<kBnThreads>(s, red);
   if (threadIdx.x == 0) out[c] = (float)s;
 }
 
@@ -479,6 +511,33 @@ __global__ __launch_bounds__(256) void k_row_argmax(const float* __restrict__ x,
   if (r < rows) out[r] = row_argmax(x + r * cols, cols);
 }
 
+// The same for narrow rows (cols <= kArgmaxStagedCols), HBM-bound: a thread per
+// row reading its own row strides 4 * cols bytes between lanes, so every load
+// instruction touches 64 lines (the labelled path's [B * n][C + 1] one-hot
+// classes: 185 MB per 16 x 100k batch took 0.58 ms).  Here the workgroup's 256
+// rows -- one contiguous block -- are loaded as 16-byte vectors by consecutive
+// lanes into LDS, then each thread scans its row there (an odd row pitch is
+// bank-conflict free).
+constexpr int kArgmaxStagedCols = 48;
+__global__ __launch_bounds__(256) void k_row_argmax_staged(const float* __restrict__ x, int64_t rows, int cols,
+                                                           int* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float s[256 * kArgmaxStagedCols];
+  const int64_t r0 = (int64_t)blockIdx.x * 256;
+  const int nr = (int)min<int64_t>(256, rows - r0);
+  const int count = nr * cols;
+  const float* src = x + r0 * cols;
+  if (((uintptr_t)src & 15) == 0) {
+    const int n4 = count >> 2;
+    const f32x4* s4 = reinterpret_cast<const f32x4*>(src);
+    for (int i = threadIdx.x; i < n4; i += 256) reinterpret_cast<f32x4*>(s)[i] = __builtin_nontemporal_load(s4 + i);
+    for (int i = (n4 << 2) + threadIdx.x; i < count; i += 256) s[i] = src[i];
+  } else {
+    for (int i = threadIdx.x; i < count; i += 256) s[i] = src[i];
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < nr) out[r0 + threadIdx.x] = row_argmax(s + threadIdx.x * cols, cols);
+}
+
 int launched() { return hipGetLastError() == hipSuccess ? 0 : -21; }
 
 bool getenv_flag(const char* name) {
@@ -492,6 +551,14 @@ bool getenv_flag(const char* name) {
 bool gemm64_only() {
   static const bool v = getenv_flag("NDNET_TR_GEMM64");
   return v;
+}
+// BatchNorm kernels on 1024-thread workgroups for layers of < 512 channels
+// (one workgroup per channel: the narrow layers leave most CUs idle at 512
+// threads).  NDNET_TR_BN1024=1 (A/B, read once like NDNET_TR_GEMM64: the
+// workgroup size sets the statistics' summation order).
+bool bn_wide_groups(int C) {
+  static const bool v = getenv_flag("NDNET_TR_BN1024");
+  return v && C < 512;
 }
 
 }  // namespace
@@ -543,11 +610,17 @@ extern "C" int ndnet_tr_sum_parts(const float* part, float* out, int64_t count, 
 
 extern "C" int ndnet_tr_bn_fwd(const float* y, float* z, float* mean, float* invstd, float* running_mean,
                                float* running_var, const float* gamma, const float* beta, int B, int C, int N,
-                               float eps, float momentum, int relu, float* pool, int32_t* pool_idx, void* stream) {
+                               float eps, float momentum, int relu, float* pool, int32_t* pool_idx,
+                               int64_t* batches_tracked, void* stream) {
   if (!y || !mean || !invstd || !gamma || !beta || B <= 0 || C <= 0 || N <= 0) return -20;
   if (pool ? (!pool_idx || B > kPoolMaxB) : !z) return -20;
-  k_tr_bn_fwd<<<C, kBnThreads, 0, (hipStream_t)stream>>>(y, z, mean, invstd, running_mean, running_var, gamma, beta,
-                                                         B, C, N, eps, momentum, relu, pool, pool_idx);
+  long long* nbt = reinterpret_cast<long long*>(batches_tracked);
+  if (bn_wide_groups(C))
+    k_tr_bn_fwd<1024><<<C, 1024, 0, (hipStream_t)stream>>>(y, z, mean, invstd, running_mean, running_var, gamma, beta,
+                                                           B, C, N, eps, momentum, relu, pool, pool_idx, nbt);
+  else
+    k_tr_bn_fwd<kBnThreads><<<C, kBnThreads, 0, (hipStream_t)stream>>>(
+        y, z, mean, invstd, running_mean, running_var, gamma, beta, B, C, N, eps, momentum, relu, pool, pool_idx, nbt);
   return launched();
 }
 
@@ -555,8 +628,12 @@ extern "C" int ndnet_tr_bn_bwd(const float* dz, const float* y, const float* mea
                                const float* gamma, const float* beta, float* dy, float* dgamma, float* dbeta,
                                float* dbias, int B, int C, int N, int relu, const int32_t* pool_idx, void* stream) {
   if (!dz || !y || !mean || !invstd || !gamma || !beta || !dy || B <= 0 || C <= 0 || N <= 0) return -20;
-  k_tr_bn_bwd<<<C, kBnThreads, 0, (hipStream_t)stream>>>(dz, y, mean, invstd, gamma, beta, dy, dgamma, dbeta, dbias,
-                                                         B, C, N, relu, pool_idx);
+  if (bn_wide_groups(C))
+    k_tr_bn_bwd<1024><<<C, 1024, 0, (hipStream_t)stream>>>(dz, y, mean, invstd, gamma, beta, dy, dgamma, dbeta,
+                                                           dbias, B, C, N, relu, pool_idx);
+  else
+    k_tr_bn_bwd<kBnThreads><<<C, kBnThreads, 0, (hipStream_t)stream>>>(dz, y, mean, invstd, gamma, beta, dy, dgamma,
+                                                                       dbeta, dbias, B, C, N, relu, pool_idx);
   return launched();
 }
 
@@ -581,6 +658,9 @@ extern "C" int ndnet_tr_argmax_match(const float* pred, const float* gt, int64_t
 
 extern "C" int ndnet_row_argmax(const float* x, int64_t rows, int cols, int32_t* out, void* stream) {
   if (!x || !out || rows <= 0 || cols <= 0 || (rows + 255) / 256 > (int64_t)INT32_MAX) return -20;
-  k_row_argmax<<<(unsigned)((rows + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, rows, cols, out);
+  if (cols <= kArgmaxStagedCols)
+    k_row_argmax_staged<<<(unsigned)((rows + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, rows, cols, out);
+  else
+    k_row_argmax<<<(unsigned)((rows + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, rows, cols, out);
   return launched();
 }

@@ -134,7 +134,7 @@ TRAIN_EXPORTS: dict = {
                            _I, _P]),
     "ndnet_tr_sum_parts": (_I, [_P, _P, _I64, _I, _P]),
     "ndnet_tr_bn_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, ctypes.c_float, ctypes.c_float, _I, _P, _P,
-                             _P]),
+                             _P, _P]),
     "ndnet_tr_bn_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P]),
     "ndnet_tr_chan_sum": (_I, [_P, _P, _I, _I, _I, _P]),
     "ndnet_tr_row_sum": (_I, [_P, _P, _I64, _I, _P]),

@@ -43,6 +43,15 @@ def _stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
+def _batches_tracked(bn) -> Optional[torch.Tensor]:
+    """The module's num_batches_tracked when the BatchNorm kernel can increment
+    it in its own launch (a one-element int64 device tensor), else None."""
+    t = getattr(bn, "num_batches_tracked", None)
+    if t is not None and t.is_cuda and t.dtype == torch.int64 and t.numel() == 1 and t.is_contiguous():
+        return t
+    return None
+
+
 def _check_f32(*ts: torch.Tensor) -> None:
     for t in ts:
         if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous():
@@ -132,7 +141,7 @@ class _ConvBNAct(torch.autograd.Function):
     either the conv's ``b`` [Cout] or a per-cloud ``cb`` [B,Cout]."""
 
     @staticmethod
-    def forward(ctx, x, w, b, cb, gamma, beta, run_mean, run_var, eps, momentum, relu):
+    def forward(ctx, x, w, b, cb, gamma, beta, run_mean, run_var, eps, momentum, relu, nbt=None):
         x = x.contiguous()
         w2 = w.detach().reshape(w.shape[0], -1).contiguous()
         _check_f32(x, w2)
@@ -160,7 +169,7 @@ class _ConvBNAct(torch.autograd.Function):
         g, bt = gamma.detach().contiguous(), beta.detach().contiguous()
         rc = _lib.lib().ndnet_tr_bn_fwd(y.data_ptr(), z.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
                                         _ptr(run_mean), _ptr(run_var), g.data_ptr(), bt.data_ptr(), Bn, C, N,
-                                        float(eps), float(momentum), int(relu), None, None, _stream())
+                                        float(eps), float(momentum), int(relu), None, None, _ptr(nbt), _stream())
         _lib.check(rc, "ndnet_tr_bn_fwd")
         ctx.save_for_backward(x, w2, y, mean, invstd, g, bt)
         return z
@@ -192,7 +201,7 @@ class _ConvBNAct(torch.autograd.Function):
         dw = conv_weight_grad(dy, x).view(ctx.w_shape) if need[1] else None
         dcb = row_sum(dy) if ctx.has_cb and need[3] else None
         return (dx, dw, dbias if ctx.has_bias and need[2] else None, dcb,
-                dgamma if need[4] else None, dbeta if need[5] else None, None, None, None, None, None)
+                dgamma if need[4] else None, dbeta if need[5] else None, None, None, None, None, None, None)
 
 
 def conv_bn_act(conv: torch.nn.Conv1d, bn: Optional[torch.nn.BatchNorm1d], x: torch.Tensor,
@@ -212,10 +221,11 @@ def conv_bn_act(conv: torch.nn.Conv1d, bn: Optional[torch.nn.BatchNorm1d], x: to
     if not bn.affine or bn.momentum is None:
         raise ValueError("the train kernels take affine BatchNorm1d with a fixed momentum (the model's defaults)")
     track = bn.track_running_stats and bn.running_mean is not None
+    nbt = _batches_tracked(bn) if track else None
     out = _ConvBNAct.apply(x, w, b, cloud_bias, bn.weight, bn.bias,
                            bn.running_mean if track else None, bn.running_var if track else None,
-                           bn.eps, bn.momentum, relu)
-    if track:
+                           bn.eps, bn.momentum, relu, nbt)
+    if track and nbt is None:
         bn.num_batches_tracked.add_(1)
     return out
 
@@ -231,7 +241,7 @@ class _ConvBNPool(torch.autograd.Function):
     two (identical points give the same gradients either way)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, gamma, beta, run_mean, run_var, eps, momentum, relu):
+    def forward(ctx, x, w, b, gamma, beta, run_mean, run_var, eps, momentum, relu, nbt=None):
         x = x.contiguous()
         w2 = w.detach().reshape(w.shape[0], -1).contiguous()
         _check_f32(x, w2)
@@ -248,7 +258,7 @@ class _ConvBNPool(torch.autograd.Function):
         rc = _lib.lib().ndnet_tr_bn_fwd(y.data_ptr(), None, mean.data_ptr(), invstd.data_ptr(),
                                         _ptr(run_mean), _ptr(run_var), g.data_ptr(), bt.data_ptr(), Bn, C, N,
                                         float(eps), float(momentum), int(relu), pool.data_ptr(), idx.data_ptr(),
-                                        _stream())
+                                        _ptr(nbt), _stream())
         _lib.check(rc, "ndnet_tr_bn_fwd (pool)")
         ctx.relu, ctx.w_shape = bool(relu), w.shape
         ctx.save_for_backward(x, w2, y, mean, invstd, g, bt, idx)
@@ -272,7 +282,7 @@ class _ConvBNPool(torch.autograd.Function):
         dx = conv_input_grad(dy, w2) if need[0] else None
         dw = conv_weight_grad(dy, x).view(ctx.w_shape) if need[1] else None
         return (dx, dw, dbias if need[2] else None, dgamma if need[3] else None, dbeta if need[4] else None,
-                None, None, None, None, None)
+                None, None, None, None, None, None)
 
 
 def conv_bn_act_pool(conv: torch.nn.Conv1d, bn: torch.nn.BatchNorm1d, x: torch.Tensor,
@@ -284,10 +294,11 @@ def conv_bn_act_pool(conv: torch.nn.Conv1d, bn: torch.nn.BatchNorm1d, x: torch.T
     if conv.bias is None or not bn.affine or bn.momentum is None:
         raise ValueError("the pooled block takes a biased conv and affine BatchNorm1d with a fixed momentum")
     track = bn.track_running_stats and bn.running_mean is not None
+    nbt = _batches_tracked(bn) if track else None
     out = _ConvBNPool.apply(x, conv.weight, conv.bias, bn.weight, bn.bias,
                             bn.running_mean if track else None, bn.running_var if track else None,
-                            bn.eps, bn.momentum, relu)
-    if track:
+                            bn.eps, bn.momentum, relu, nbt)
+    if track and nbt is None:
         bn.num_batches_tracked.add_(1)
     return out
 

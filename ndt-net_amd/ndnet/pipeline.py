@@ -50,6 +50,11 @@ PIPE_FWD_STREAMS = int(os.environ.get("NDNET_PIPE_FWD_STREAMS", "3"))
 # 53.2k clouds/s, but U 83k -> 79k and C5 26.0k -> 25.7k, so 1 by default
 # (profiles/r03ah_ndt_streams.txt)
 PIPE_NDT_STREAMS = int(os.environ.get("NDNET_PIPE_NDT_STREAMS", "1"))
+# Stream priorities: "none" (default), "fwd" (the forward streams high, so the
+# TNet heads' few workgroups are dispatched ahead of k_front / chain
+# workgroups queued on the other streams) or "ndt".  A/B in
+# profiles/r04_priority_ab.txt.
+PIPE_PRIORITY = os.environ.get("NDNET_PIPE_PRIORITY", "none")
 
 
 class _Pinned:
@@ -216,9 +221,10 @@ class PipelinedSegmentation:
                     plan.set_cu_share(cu_share, PIPE_WQ_SHARE)
                 except RuntimeError:  # k_front does not fit that share for this shape
                     pass
-        # stream priorities (either way) measured 35-40% slower than none
-        self.s_ndts = [torch.cuda.Stream(device=dev) for _ in range(N)]
-        self.s_fwds = [torch.cuda.Stream(device=dev) for _ in range(F)]
+        # stream priorities (NDNET_PIPE_PRIORITY): none by default, see PIPE_PRIORITY
+        hi = torch.cuda.Stream.priority_range()[1] if PIPE_PRIORITY != "none" else 0
+        self.s_ndts = [torch.cuda.Stream(device=dev, priority=hi if PIPE_PRIORITY == "ndt" else 0) for _ in range(N)]
+        self.s_fwds = [torch.cuda.Stream(device=dev, priority=hi if PIPE_PRIORITY == "fwd" else 0) for _ in range(F)]
         self.s_copy = torch.cuda.Stream(device=dev)
         self.ndt_done = [torch.cuda.Event() for _ in range(R)]  # NDT of slot j finished (rows j, input j free)
         self.fwd_done = [torch.cuda.Event() for _ in range(R)]  # forward of slot j finished (rows j - 1 free)

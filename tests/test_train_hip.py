@@ -310,16 +310,19 @@ def test_accuracy_kernel_matches_torch_argmax():
 
 
 
-def test_row_argmax_matches_torch():
-    """ndnet_row_argmax: the labelled path's point classes (ndtnet_preprocessing.py:34)."""
+@pytest.mark.parametrize("cols,offset", [(29, 0), (29, 1), (4, 0), (48, 3), (64, 0)])
+def test_row_argmax_matches_torch(cols, offset):
+    """ndnet_row_argmax: the labelled path's point classes (ndtnet_preprocessing.py:34);
+    narrow rows staged through LDS (16-byte loads when aligned), wide rows a thread each."""
     from ndnet import _lib
-    g = torch.Generator(device="cuda").manual_seed(8)
-    x = torch.randn(3, 5000, 29, device="cuda", generator=g)
-    x[0, 1, 5] = x[0, 1].max()      # tie: first index
-    x[1, 2, 9] = float("nan")       # NaN is the maximum
-    x[2, 3] = 0.0                   # all equal: index 0
+    g = torch.Generator(device="cuda").manual_seed(8 + cols)
+    buf = torch.randn(3 * 5000 * cols + offset, device="cuda", generator=g)
+    x = buf[offset:].view(3, 5000, cols)
+    x[0, 1, cols - 1] = x[0, 1].max()  # tie: first index
+    x[1, 2, cols // 2] = float("nan")  # NaN is the maximum
+    x[2, 3] = 0.0                      # all equal: index 0
     out = torch.empty(3, 5000, dtype=torch.int32, device="cuda")
-    _lib.check(_lib.lib().ndnet_row_argmax(x.data_ptr(), 15000, 29, out.data_ptr(),
+    _lib.check(_lib.lib().ndnet_row_argmax(x.data_ptr(), 15000, cols, out.data_ptr(),
                                            torch.cuda.current_stream().cuda_stream), "row_argmax")
     assert torch.equal(out.long(), torch.argmax(x, dim=2))
 
