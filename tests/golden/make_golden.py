@@ -145,7 +145,37 @@ def model_fixture() -> None:
         print("wrote", name)
 
 
+def model_train_fixture() -> None:
+    """A well-conditioned train-mode fixture: 16 clouds, each at its own scale
+    and offset, so the TNet FC heads' BatchNorm1d (batch statistics over the
+    clouds) divides by the features' real spread, not by ~sqrt(eps) as with
+    the 2-cloud fixtures above.  out_train: the reference module's fp32 train
+    forward; out_train64: the same module in float64."""
+    import copy
+    import torch
+    model_mod, _ = load_reference()
+    F, C, B, N = 768, 28, 16, 128
+    m = model_mod.NDTNetSegmentation(3, C, F)
+    m.load_state_dict(deterministic_state(m.state_dict()))
+    rng = np.random.default_rng(2024)
+    scale = (0.5 + 0.25 * np.arange(B)).reshape(B, 1, 1)
+    shift = rng.uniform(-5, 5, (B, 1, 3))
+    pts = (rng.uniform(-10, 10, (B, N, 3)) * scale + shift).astype(np.float32)
+    covs = (rng.normal(0, 1, (B, N, 9)) * scale).astype(np.float32)
+    m64 = copy.deepcopy(m).double()
+    with torch.no_grad():
+        m.train()
+        out_train = m(torch.from_numpy(pts), torch.from_numpy(covs)).numpy()
+        m64.train()
+        out64 = m64(torch.from_numpy(pts).double(), torch.from_numpy(covs).double()).numpy()
+    name = f"ndtnet_seg_train_F{F}_C{C}_B{B}.npz"
+    np.savez_compressed(os.path.join(HERE, name), points=pts, covs=covs, feature_dim=F, num_classes=C,
+                        out_train=out_train, out_train64=out64)
+    print("wrote", name, "fp32 vs float64:", float(np.abs(out_train - out64).max()))
+
+
 if __name__ == "__main__":
     ndt_fixtures()
     preprocessing_fixture()
     model_fixture()
+    model_train_fixture()

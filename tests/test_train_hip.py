@@ -152,7 +152,19 @@ def test_train_forward_matches_reference_fixture(monkeypatch, name):
     """The HIP train-mode forward (BatchNorm batch statistics, every conv
     block on the train kernels) against the log-probs the reference module
     itself produced in train mode on the same weights and input
-    (tests/golden/make_golden.py, ``out_train``): within 1e-4."""
+    (tests/golden/make_golden.py, ``out_train``).
+
+    The fixtures hold B = 2 clouds, so the TNet FC heads' BatchNorm1d
+    normalises each feature over two samples: a feature whose two values
+    differ by less than sqrt(eps) is divided by ~sqrt(eps), which scales any
+    fp32 summation-order difference up to ~300x.  The bar is therefore 1e-4
+    OR within 3x of torch's own fp32 GPU composition of the same forward, and
+    -- against a float64 evaluation of the same module -- within 3x of the
+    larger of the reference's and torch GPU's fp32 errors (round 4 measured:
+    F768 HIP 2.4e-2 vs reference 1.3e-2; F64 HIP 1.2e-2 vs reference 1.6e-3,
+    torch GPU 7.7e-3 from out_train).  The 16-cloud fixture below is the
+    tight (1e-4) check."""
+    import copy
     import numpy as np
     from conftest import golden
     from model_init import deterministic_state
@@ -160,16 +172,55 @@ def test_train_forward_matches_reference_fixture(monkeypatch, name):
     z = golden(name)
     m = ndtnet.NDTNetSegmentation(3, int(z["num_classes"]), int(z["feature_dim"]))
     m.load_state_dict(deterministic_state(m.state_dict()))
+    m64 = copy.deepcopy(m).double().train()
+    m_t = copy.deepcopy(m).cuda().train()
+    m = m.cuda().train()
+    p, c = torch.from_numpy(z["points"]), torch.from_numpy(z["covs"])
+    calls = []
+    real, real_pool = train_hip.conv_bn_act, train_hip.conv_bn_act_pool
+    monkeypatch.setattr(train_hip, "conv_bn_act", lambda *a, **k: calls.append(1) or real(*a, **k))
+    monkeypatch.setattr(train_hip, "conv_bn_act_pool", lambda *a, **k: calls.append(2) or real_pool(*a, **k))
+    out = m(p.cuda(), c.cuda()).detach().cpu().double().numpy()
+    assert len(calls) == 13, "the train forward must run on the HIP kernels"
+    monkeypatch.setattr(ndtnet, "_TRAIN_TORCH", True)
+    out_t = m_t(p.cuda(), c.cuda()).detach().cpu().double().numpy()
+    assert len(calls) == 13
+    with torch.no_grad():
+        out64 = m64(p.double(), c.double()).numpy()
+    ref = z["out_train"].astype(np.float64)
+    e_hip, e_torch = np.abs(out - ref).max(), np.abs(out_t - ref).max()
+    x_hip, x_ref, x_torch = np.abs(out - out64).max(), np.abs(ref - out64).max(), np.abs(out_t - out64).max()
+    print(f"vs out_train: HIP {e_hip:.3e}, torch GPU fp32 {e_torch:.3e}; "
+          f"vs float64: HIP {x_hip:.3e}, reference fp32 {x_ref:.3e}, torch GPU fp32 {x_torch:.3e}")
+    assert e_hip <= max(1e-4, 3.0 * e_torch)
+    assert x_hip <= 3.0 * max(x_ref, x_torch) + 1e-6
+
+
+def test_train_forward_matches_reference_fixture_b16(monkeypatch):
+    """The same on the well-conditioned fixture (16 clouds at distinct scales,
+    make_golden.model_train_fixture; the reference's own fp32 train forward is
+    within 1.8e-5 of its float64 one there): the HIP train forward within
+    1e-4 of the reference's out_train, and no further from the float64
+    result than 2x the reference's own fp32 error."""
+    import numpy as np
+    from conftest import golden
+    from model_init import deterministic_state
+    from ndnet.models import ndtnet, train_hip
+    z = golden("ndtnet_seg_train_F768_C28_B16.npz")
+    m = ndtnet.NDTNetSegmentation(3, int(z["num_classes"]), int(z["feature_dim"]))
+    m.load_state_dict(deterministic_state(m.state_dict()))
     m = m.cuda().train()
     calls = []
     real, real_pool = train_hip.conv_bn_act, train_hip.conv_bn_act_pool
     monkeypatch.setattr(train_hip, "conv_bn_act", lambda *a, **k: calls.append(1) or real(*a, **k))
     monkeypatch.setattr(train_hip, "conv_bn_act_pool", lambda *a, **k: calls.append(2) or real_pool(*a, **k))
-    out = m(torch.from_numpy(z["points"]).cuda(), torch.from_numpy(z["covs"]).cuda())
+    out = m(torch.from_numpy(z["points"]).cuda(), torch.from_numpy(z["covs"]).cuda()).detach().cpu().double().numpy()
     assert len(calls) == 13, "the train forward must run on the HIP kernels"
-    err = np.abs(out.detach().cpu().numpy() - z["out_train"]).max()
-    print(f"max |log-prob - reference out_train| = {err:.3e}")
-    assert err <= 1e-4
+    ref, ref64 = z["out_train"].astype(np.float64), z["out_train64"]
+    e, x, x_ref = np.abs(out - ref).max(), np.abs(out - ref64).max(), np.abs(ref - ref64).max()
+    print(f"HIP vs out_train {e:.3e}; vs float64: HIP {x:.3e}, reference fp32 {x_ref:.3e}")
+    assert e <= 1e-4
+    assert x <= 2.0 * x_ref + 1e-6
 
 
 def test_segmentation_train_forward_backward_matches_torch(monkeypatch):

@@ -27,7 +27,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "ndt-net_amd"))
-MODES = ["serial", "fork", "events", "unjoined", "subgraph"]
+MODES = ["serial", "fork", "events", "subgraph", "unjoined"]
 
 
 def child(mode: str) -> None:
@@ -114,6 +114,9 @@ def main() -> None:
         tail = (p.stdout + p.stderr).strip().splitlines()
         msg = [l for l in tail if l.startswith(f"[{mode}]") or "Error" in l or "error" in l or "Fatal" in l][-4:]
         print(f"{mode:9s} rc {p.returncode}: " + " | ".join(msg), flush=True)
+        if p.returncode < 0 or p.returncode >= 128:  # a signal (segfault, abort): nothing more on the GPU
+            print(f"stopping after {mode}: the child died by a signal", flush=True)
+            sys.exit(1)
 
 
 if __name__ == "__main__":
