@@ -554,10 +554,14 @@ bool gemm64_only() {
 }
 // BatchNorm kernels on 1024-thread workgroups for layers of < 512 channels
 // (one workgroup per channel: the narrow layers leave most CUs idle at 512
-// threads).  NDNET_TR_BN1024=1 (A/B, read once like NDNET_TR_GEMM64: the
+// threads): graphed step 3.021 -> 2.968 ms (profiles/r04_train_hip.txt).
+// NDNET_TR_BN1024=0 keeps 512 threads (read once like NDNET_TR_GEMM64: the
 // workgroup size sets the statistics' summation order).
 bool bn_wide_groups(int C) {
-  static const bool v = getenv_flag("NDNET_TR_BN1024");
+  static const bool v = [] {
+    const char* e = getenv("NDNET_TR_BN1024");
+    return !(e && e[0] == '0');
+  }();
   return v && C < 512;
 }
 

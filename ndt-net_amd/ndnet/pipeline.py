@@ -52,8 +52,8 @@ PIPE_FWD_STREAMS = int(os.environ.get("NDNET_PIPE_FWD_STREAMS", "3"))
 PIPE_NDT_STREAMS = int(os.environ.get("NDNET_PIPE_NDT_STREAMS", "1"))
 # Stream priorities: "none" (default), "fwd" (the forward streams high, so the
 # TNet heads' few workgroups are dispatched ahead of k_front / chain
-# workgroups queued on the other streams) or "ndt".  A/B in
-# profiles/r04_priority_ab.txt.
+# workgroups queued on the other streams) or "ndt".  Measured
+# (profiles/r04_priority_ab.txt): none 83.6k, fwd 71.5k, ndt 79.9k clouds/s.
 PIPE_PRIORITY = os.environ.get("NDNET_PIPE_PRIORITY", "none")
 
 
@@ -170,8 +170,10 @@ class PipelinedSegmentation:
     stream at both ends (its output is ready in stream order);
     ``replay_steps(k)`` runs k steps joined only at the ends, so the NDT
     stream runs up to a step ahead of the forward stream and no per-step
-    join separates the graphs.  (One graph holding several steps crashed
-    hipStreamEndCapture on this ROCm, profiles/r03t_pipeline.txt.)
+    join separates the graphs.  (Round 3 recorded a crash capturing several
+    steps in one graph; round 4 found every such capture form working or
+    failing cleanly, profiles/r04_capture_probe.txt: a multi-step graph would
+    end in a join of every stream, which the per-stage graphs avoid.)
 
     ``points`` is the buffer the NEXT step reads (fill it, then replay);
     ``load_resident(pts)`` fills every buffer.  ``replay_streamed(host_next)``

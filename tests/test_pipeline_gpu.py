@@ -322,3 +322,64 @@ def test_two_stream_forward_capture_matches_eager():
         torch.cuda.synchronize()
         for o, e in zip(outs, eager):
             assert torch.equal(o, e)
+
+
+def test_two_unrolled_pipelined_steps_in_one_graph():
+    """Round-3 DESIGN recorded a host segfault in hipStreamEndCapture for one
+    graph holding several unrolled pipelined steps.  Round 4 re-ran that
+    capture (tools/capture_probe.py, profiles/r04_capture_probe.txt): the
+    pipeline's own pattern -- NDT and forward streams forked from the capture
+    stream by events, every cross-stream order an event recorded inside the
+    capture, every side stream joined back before the capture ends -- captures
+    and replays correctly; an unjoined stream fails cleanly
+    (hipErrorStreamCaptureUnjoined) and replaying a graph inside a capture is
+    refused by torch, neither crashes.  Two unrolled steps in one graph,
+    replayed, equal the eager steps."""
+    import torch
+    from ndnet.pipeline import PipelinedSegmentation
+    from ndnet.synthetic import make_batch
+    dev = torch.device("cuda", 0)
+    B, n, k = 4, 20000, 200
+    m = _model(F=768, C=28)
+    pipe = PipelinedSegmentation(m, k, B, n, device=dev)
+    for j in range(pipe.R):
+        pipe.inputs[j].copy_(torch.from_numpy(make_batch("U" if j % 2 else "L", B, n, seed0=10 * j)).to(dev))
+    F = pipe.F
+    with torch.no_grad():
+        for j in (0, 1, 2):
+            pipe._ndt(j)
+        ref = [pipe._fwd(j).clone() for j in (1, 2)]
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    cap = torch.cuda.Stream(device=dev)
+    cap.wait_stream(torch.cuda.current_stream(dev))
+    ev = [torch.cuda.Event() for _ in range(8)]
+    outs = []
+    s_ndt = pipe.s_ndts[0]
+    with torch.no_grad(), torch.cuda.graph(g, stream=cap):
+        ev[0].record(cap)
+        s_ndt.wait_event(ev[0])
+        for s in pipe.s_fwds:
+            s.wait_event(ev[0])
+        for i, j in enumerate((1, 2)):
+            with torch.cuda.stream(s_ndt):
+                pipe._ndt(j)
+            ev[1 + i].record(s_ndt)
+            s_f = pipe.s_fwds[j % F]
+            s_f.wait_event(ev[1 + i])
+            with torch.cuda.stream(s_f):
+                outs.append(pipe._fwd(j))
+            ev[4 + i].record(s_f)
+        for i in range(2):
+            cap.wait_event(ev[4 + i])
+        ev[7].record(s_ndt)
+        cap.wait_event(ev[7])
+        for s in pipe.s_fwds:  # streams without work in this capture join too
+            e = torch.cuda.Event()
+            e.record(s)
+            cap.wait_event(e)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    for a, b in zip(outs, ref):
+        assert torch.equal(a, b)
