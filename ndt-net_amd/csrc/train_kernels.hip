@@ -58,10 +58,11 @@ constexpr int kBnValues = 16384;  // values per channel held in registers across
                                   // reads the channel once)
 constexpr int kPoolMaxB = 64;  // pool mode: clouds per launch  // values per thread held in registers: B * N <= 16384 reads the channel once
 
-// global -> registers: this thread's 4 elements of the (k0 .. k0 + 16) x TM tile
-// (TM * 4 threads), P contiguous along k (KMAJOR) or along the row index.  Each thread loads 4 consecutive elements along the contiguous axis: one
-// 16-byte load when they are in range and aligned (the common case: k-steps
-// of 16, rows of 1000 points), else element by element with zero fill.
+// global -> registers: this thread's 4 elements of the (k0 .. k0 + 16) x TM
+// tile (TM * 4 threads), P contiguous along k (KMAJOR) or along the row
+// index.  Each thread loads 4 consecutive elements along the contiguous axis:
+// one 16-byte load when they are in range and aligned (the common case:
+// k-steps of 16, rows of 1000 points), else element by element with zero fill.
 // KMAJOR: row t / 4, k (t % 4) * 4 .. + 3; else k t / (TM / 4), rows
 // (t % (TM / 4)) * 4 .. + 3.
 template <int TM, bool KMAJOR>
@@ -202,6 +203,157 @@ __global__ __launch_bounds__(TM * 4) void k_tr_gemm(const float* __restrict__ A,
     }
 }
 
+// ---- the same GEMM on the bf16 matrix cores, fp32-accurate ("x6") ----
+// Every operand x is split x = h + m + l into three bf16 in the tile store
+// (h = bf16(x), m = bf16(x - h), l = bf16(x - h - m): 24 significant bits, each
+// residual exact in fp32), and a product keeps the six partial products of
+// weight >= 2^-16 (mm, mh, lh, hl, hm, hh, smallest first), each exact and
+// accumulated in fp32 by v_mfma_f32_16x16x32_bf16 -- the eval chains' form
+// (pointnet_kernels.hip, test_split_bf16_layers_are_fp32_accurate).  Six
+// 16-cycle MFMAs per 16x16x32 block against eight 32-cycle fp32 ones.
+// 64 x 64 tile, 4 waves of 32 x 32, k-steps of 32; LDS tiles [row][k] per
+// plane (pitch 48 bf16), double-buffered; a thread loads and splits 8
+// consecutive k of one row per operand and stores each plane with one
+// ds_write_b128.
+typedef __bf16 tr_bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int kX6K = 32, kX6P = 48, kX6Plane = 64 * kX6P;
+
+template <bool KMAJOR>
+__device__ __forceinline__ void x6_load(const float* __restrict__ P, int64_t ld, int r0, int k0, int R, int kend,
+                                        float (&v)[8]) {
+  const int t = threadIdx.x;
+  const int rr = KMAJOR ? t >> 2 : t & 63, kk = KMAJOR ? (t & 3) * 8 : (t >> 6) * 8;
+  const int gr = r0 + rr, gk = k0 + kk;
+  if (KMAJOR) {
+    const float* p = P + (int64_t)gr * ld + gk;
+    if (gr < R && gk + 7 < kend && ((uintptr_t)p & 15) == 0) {
+      const f32x4 x0 = reinterpret_cast<const f32x4*>(p)[0], x1 = reinterpret_cast<const f32x4*>(p)[1];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        v[i] = x0[i];
+        v[4 + i] = x1[i];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; i++) v[i] = (gr < R && gk + i < kend) ? p[i] : 0.0f;
+    }
+  } else {  // lanes walk the rows: each of the 8 loads is 64 consecutive floats of a wave
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] = (gr < R && gk + i < kend) ? P[(int64_t)(gk + i) * ld + gr] : 0.0f;
+  }
+}
+
+template <bool KMAJOR>
+__device__ __forceinline__ void x6_store(__bf16* __restrict__ s, const float (&v)[8]) {
+  const int t = threadIdx.x;
+  const int rr = KMAJOR ? t >> 2 : t & 63, kk = KMAJOR ? (t & 3) * 8 : (t >> 6) * 8;
+  tr_bf16x8 h, m, l;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const __bf16 hh = (__bf16)v[i];
+    const float r = v[i] - (float)hh;
+    const __bf16 mm = (__bf16)r;
+    h[i] = hh;
+    m[i] = mm;
+    l[i] = (__bf16)(r - (float)mm);
+  }
+  const int e = rr * kX6P + kk;
+  *reinterpret_cast<tr_bf16x8*>(s + e) = h;
+  *reinterpret_cast<tr_bf16x8*>(s + kX6Plane + e) = m;
+  *reinterpret_cast<tr_bf16x8*>(s + 2 * kX6Plane + e) = l;
+}
+
+template <bool AK, bool BK>
+__global__ __launch_bounds__(256) void k_tr_gemm_x6(const float* __restrict__ A, const float* __restrict__ B,
+                                                    float* __restrict__ C, const float* __restrict__ bias,
+                                                    int64_t sbias, int M, int N, int K, int64_t lda, int64_t ldb,
+                                                    int64_t ldc, int64_t sAz, int64_t sBz, int64_t sCz, int batch,
+                                                    int cpz, int nchunks, int kchunk) {
+#pragma clang fp contract(off)
+  __shared__ __attribute__((aligned(16))) __bf16 sA[2][3 * kX6Plane];
+  __shared__ __attribute__((aligned(16))) __bf16 sB[2][3 * kX6Plane];
+  const int z = blockIdx.z, zg = z / nchunks, zc = z - zg * nchunks;
+  const int cl0 = zg * cpz, ncl = min(cpz, batch - cl0);
+  C += z * sCz;
+  if (bias) bias += cl0 * sbias;
+  const int kbeg = zc * kchunk;
+  const int kend = min(K, kbeg + kchunk);
+  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  const int r16 = lane & 15, q = lane >> 4;
+  f32x4 acc[2][2][2];  // [set][row block][column block]: k-steps alternate between two sets
+#pragma unroll
+  for (int s = 0; s < 2; s++)
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+      for (int j = 0; j < 2; j++) acc[s][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nst = kend > kbeg ? (kend - kbeg + kX6K - 1) / kX6K : 0;
+  const int total = ncl > 0 ? ncl * nst : 0;
+  float ra[8], rb[8];
+  auto load = [&](int t) {
+    const int cl = t / nst, st = t - cl * nst;
+    const int64_t c = cl0 + cl;
+    x6_load<AK>(A + c * sAz, lda, m0, kbeg + st * kX6K, M, kend, ra);
+    x6_load<BK>(B + c * sBz, ldb, n0, kbeg + st * kX6K, N, kend, rb);
+  };
+  if (total > 0) {
+    load(0);
+    x6_store<AK>(sA[0], ra);
+    x6_store<BK>(sB[0], rb);
+  }
+  __syncthreads();
+  for (int t = 0; t < total; t++) {
+    const int cur = t & 1;
+    const bool more = t + 1 < total;
+    if (more) load(t + 1);
+    const __bf16* a = sA[cur] + 8 * q;
+    const __bf16* b = sB[cur] + 8 * q;
+    tr_bf16x8 af[2][3], bw[2][3];
+#pragma unroll
+    for (int p = 0; p < 3; p++)
+#pragma unroll
+      for (int i = 0; i < 2; i++) {
+        af[i][p] = *reinterpret_cast<const tr_bf16x8*>(a + p * kX6Plane + (wm + 16 * i + r16) * kX6P);
+        bw[i][p] = *reinterpret_cast<const tr_bf16x8*>(b + p * kX6Plane + (wn + 16 * i + r16) * kX6P);
+      }
+    f32x4(&ac)[2][2] = acc[t & 1];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        f32x4 x = ac[i][j];
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], bw[j][1], x, 0, 0, 0);  // m m
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], bw[j][0], x, 0, 0, 0);  // m h
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][2], bw[j][0], x, 0, 0, 0);  // l h
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bw[j][2], x, 0, 0, 0);  // h l
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bw[j][1], x, 0, 0, 0);  // h m
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bw[j][0], x, 0, 0, 0);  // h h
+        ac[i][j] = x;
+      }
+    if (more) {
+      x6_store<AK>(sA[cur ^ 1], ra);
+      x6_store<BK>(sB[cur ^ 1], rb);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; i++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int gm = m0 + wm + 16 * i + 4 * q + r;
+      if (gm >= M) continue;
+      const float bv = bias ? bias[gm] : 0.0f;
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        const int gn = n0 + wn + 16 * j + r16;
+        if (gn >= N) continue;
+        C[(int64_t)gm * ldc + gn] = (acc[0][i][j][r] + acc[1][i][j][r]) + bv;
+      }
+    }
+}
+
 // out[i] = part[0][i] + part[1][i] + ... in part order; 4 elements per thread,
 // eight parts' loads issued before their sums
 __global__ __launch_bounds__(256) void k_tr_sum_parts(const float* __restrict__ part, float* __restrict__ out,
@@ -322,44 +474,80 @@ __global__ __launch_bounds__(T) void k_tr_bn_fwd(const float* __restrict__ y, fl
     }
   }
   const float fm = (float)mu, g = gamma[c], bt = beta[c];
-  // pool mode: no z; this thread's running max per cloud (its elements visit the
-  // clouds in order), merged into pk when the cloud changes
-  unsigned long long best = 0ull;
-  int cur = -1;
-  auto emit = [&](const ChanWalk<T>& w, float o) {
-    if (!pool) {
-      z[w.off(C, N, c)] = o;
-      return;
+  if (!pool) {
+    if (cached) {
+      ChanWalk<T> w(N);
+#pragma unroll
+      for (int i = 0; i < kCache; i++, w.next(N)) {
+        if (w.b < Bn) {
+          float o = bn_apply(v[i], fm, inv, g, bt);
+          if (relu) o = fmaxf(o, 0.0f);
+          z[w.off(C, N, c)] = o;
+        }
+      }
+    } else {
+      for (ChanWalk<T> w(N); w.b < Bn; w.next(N)) {
+        float o = bn_apply(y[w.off(C, N, c)], fm, inv, g, bt);
+        if (relu) o = fmaxf(o, 0.0f);
+        z[w.off(C, N, c)] = o;
+      }
     }
-    if (w.b != cur) {
-      if (cur >= 0) atomicMax(&pk[cur], best);
-      cur = w.b;
-      best = 0ull;
-    }
+    return;
+  }
+  // Pool mode: no z; per cloud the first maximum (largest ordered value key,
+  // then smallest point).  A wave's 64 elements of one step are consecutive
+  // (cloud, point) positions, so they span few clouds (two for N >= 64), and
+  // its steps visit the clouds in order: the wave reduces each step per cloud
+  // (key maximum, then the first lane holding it) into a running maximum
+  // that lane 0 merges into pk when the cloud changes -- a few LDS atomics per
+  // wave instead of one per thread and cloud (round 3: ~24 per thread on 16
+  // addresses, the pooled launches 2x slower per byte than the plain ones).
+  const int lane = threadIdx.x & 63;
+  unsigned long long run_k = 0ull;
+  int run_c = -1;
+  auto flush = [&]() {
+    if (run_c >= 0 && lane == 0) atomicMax(&pk[run_c], run_k);
+  };
+  auto group_max = [&](bool in, unsigned key, int n) {
+    unsigned km = in ? key : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) km = max(km, (unsigned)__shfl_xor((int)km, o));
+    const unsigned long long hit = __ballot(in && key == km);
+    const int first = __ffsll((long long)hit) - 1;
+    const int nf = __shfl(n, first);
+    return ((unsigned long long)km << 32) | (0xFFFFFFFFu - (unsigned)nf);
+  };
+  auto step = [&](const ChanWalk<T>& w, float val) {
+    const bool valid = w.b < Bn;
+    float o = bn_apply(val, fm, inv, g, bt);
+    if (relu) o = fmaxf(o, 0.0f);
     const unsigned u = __float_as_uint(o);
     const unsigned key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-    const unsigned long long k = ((unsigned long long)key << 32) | (0xFFFFFFFFu - (unsigned)w.n);
-    best = k > best ? k : best;
+    // the clouds this step's lanes hold, in lane (= cloud) order: two at most
+    // for N >= 64, any number for shorter clouds
+    unsigned long long pending = __ballot(valid);
+    while (pending) {
+      const int cc = __shfl(w.b, __ffsll((long long)pending) - 1);
+      const bool in = valid && w.b == cc;
+      const unsigned long long k = group_max(in, key, w.n);
+      if (cc != run_c) {
+        flush();
+        run_c = cc;
+        run_k = k;
+      } else {
+        run_k = k > run_k ? k : run_k;
+      }
+      pending &= ~__ballot(in);
+    }
   };
   if (cached) {
     ChanWalk<T> w(N);
 #pragma unroll
-    for (int i = 0; i < kCache; i++, w.next(N)) {
-      if (w.b < Bn) {
-        float o = bn_apply(v[i], fm, inv, g, bt);
-        if (relu) o = fmaxf(o, 0.0f);
-        emit(w, o);
-      }
-    }
+    for (int i = 0; i < kCache; i++, w.next(N)) step(w, v[i]);
   } else {
-    for (ChanWalk<T> w(N); w.b < Bn; w.next(N)) {
-      float o = bn_apply(y[w.off(C, N, c)], fm, inv, g, bt);
-      if (relu) o = fmaxf(o, 0.0f);
-      emit(w, o);
-    }
+    for (ChanWalk<T> w(N); __any(w.b < Bn); w.next(N)) step(w, w.b < Bn ? y[w.off(C, N, c)] : 0.0f);
   }
-  if (!pool) return;
-  if (cur >= 0) atomicMax(&pk[cur], best);
+  flush();
   __syncthreads();
   if (threadIdx.x < Bn) {
     const unsigned long long k = pk[threadIdx.x];
@@ -552,6 +740,12 @@ bool gemm64_only() {
   static const bool v = getenv_flag("NDNET_TR_GEMM64");
   return v;
 }
+// The split-bf16 ("x6") GEMM (k_tr_gemm_x6): NDNET_TR_X6=1, read once (it
+// sets the summation order of every train GEMM in the process).
+bool gemm_x6() {
+  static const bool v = getenv_flag("NDNET_TR_X6");
+  return v;
+}
 // BatchNorm kernels on 1024-thread workgroups for layers of < 512 channels
 // (one workgroup per channel: the narrow layers leave most CUs idle at 512
 // threads): graphed step 3.021 -> 2.968 ms (profiles/r04_train_hip.txt).
@@ -595,6 +789,19 @@ extern "C" int ndnet_tr_gemm(const float* A, const float* B, float* C, const flo
       k_tr_gemm<64, AKV, BKV><<<grid, 256, 0, st>>>(A, B, C, bias, sbias, M, N, K, lda, ldb, ldc, sAz, sBz, sCz,     \
                                                     batch, clouds_per_part, nchunks, kchunk);                      \
   } while (0)
+  if (gemm_x6()) {  // 64 x 64 tiles only
+    const dim3 g6((unsigned)gx, (unsigned)gy, (unsigned)gz);
+#define NDNET_TR_GEMM6(AKV, BKV)                                                                                   \
+  k_tr_gemm_x6<AKV, BKV><<<g6, 256, 0, st>>>(A, B, C, bias, sbias, M, N, K, lda, ldb, ldc, sAz, sBz, sCz, batch,     \
+                                           clouds_per_part, nchunks, kchunk)
+    if (a_kmajor) {
+      if (b_kmajor) NDNET_TR_GEMM6(true, true); else NDNET_TR_GEMM6(true, false);
+    } else {
+      if (b_kmajor) NDNET_TR_GEMM6(false, true); else NDNET_TR_GEMM6(false, false);
+    }
+#undef NDNET_TR_GEMM6
+    return launched();
+  }
   if (a_kmajor) {
     if (b_kmajor) NDNET_TR_GEMM(true, true); else NDNET_TR_GEMM(true, false);
   } else {

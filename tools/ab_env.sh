@@ -12,7 +12,7 @@ for A in "$@"; do
   V=${A%%:*}
   ENVS=""
   [ "$V" != "$A" ] && ENVS=${A#*:}
-  env ${ENVS//,/ } timeout -k 10 150 python bench.py --no-cpu-baseline --no-other --steps 50 > $OUT/$V.log 2>&1 || { echo "$V failed"; tail -5 $OUT/$V.log; exit 1; }
+  env ${ENVS//,/ } timeout -k 10 150 python bench.py --no-cpu-baseline --no-other --steps 50 ${AB_ARGS} > $OUT/$V.log 2>&1 || { echo "$V failed"; tail -5 $OUT/$V.log; exit 1; }
   python3 - "$V" "$OUT/$V.log" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
