@@ -474,80 +474,44 @@ __global__ __launch_bounds__(T) void k_tr_bn_fwd(const float* __restrict__ y, fl
     }
   }
   const float fm = (float)mu, g = gamma[c], bt = beta[c];
-  if (!pool) {
-    if (cached) {
-      ChanWalk<T> w(N);
-#pragma unroll
-      for (int i = 0; i < kCache; i++, w.next(N)) {
-        if (w.b < Bn) {
-          float o = bn_apply(v[i], fm, inv, g, bt);
-          if (relu) o = fmaxf(o, 0.0f);
-          z[w.off(C, N, c)] = o;
-        }
-      }
-    } else {
-      for (ChanWalk<T> w(N); w.b < Bn; w.next(N)) {
-        float o = bn_apply(y[w.off(C, N, c)], fm, inv, g, bt);
-        if (relu) o = fmaxf(o, 0.0f);
-        z[w.off(C, N, c)] = o;
-      }
+  // pool mode: no z; this thread's running max per cloud (its elements visit the
+  // clouds in order), merged into pk when the cloud changes
+  unsigned long long best = 0ull;
+  int cur = -1;
+  auto emit = [&](const ChanWalk<T>& w, float o) {
+    if (!pool) {
+      z[w.off(C, N, c)] = o;
+      return;
     }
-    return;
-  }
-  // Pool mode: no z; per cloud the first maximum (largest ordered value key,
-  // then smallest point).  A wave's 64 elements of one step are consecutive
-  // (cloud, point) positions, so they span few clouds (two for N >= 64), and
-  // its steps visit the clouds in order: the wave reduces each step per cloud
-  // (key maximum, then the first lane holding it) into a running maximum
-  // that lane 0 merges into pk when the cloud changes -- a few LDS atomics per
-  // wave instead of one per thread and cloud (round 3: ~24 per thread on 16
-  // addresses, the pooled launches 2x slower per byte than the plain ones).
-  const int lane = threadIdx.x & 63;
-  unsigned long long run_k = 0ull;
-  int run_c = -1;
-  auto flush = [&]() {
-    if (run_c >= 0 && lane == 0) atomicMax(&pk[run_c], run_k);
-  };
-  auto group_max = [&](bool in, unsigned key, int n) {
-    unsigned km = in ? key : 0u;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) km = max(km, (unsigned)__shfl_xor((int)km, o));
-    const unsigned long long hit = __ballot(in && key == km);
-    const int first = __ffsll((long long)hit) - 1;
-    const int nf = __shfl(n, first);
-    return ((unsigned long long)km << 32) | (0xFFFFFFFFu - (unsigned)nf);
-  };
-  auto step = [&](const ChanWalk<T>& w, float val) {
-    const bool valid = w.b < Bn;
-    float o = bn_apply(val, fm, inv, g, bt);
-    if (relu) o = fmaxf(o, 0.0f);
+    if (w.b != cur) {
+      if (cur >= 0) atomicMax(&pk[cur], best);
+      cur = w.b;
+      best = 0ull;
+    }
     const unsigned u = __float_as_uint(o);
     const unsigned key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-    // the clouds this step's lanes hold, in lane (= cloud) order: two at most
-    // for N >= 64, any number for shorter clouds
-    unsigned long long pending = __ballot(valid);
-    while (pending) {
-      const int cc = __shfl(w.b, __ffsll((long long)pending) - 1);
-      const bool in = valid && w.b == cc;
-      const unsigned long long k = group_max(in, key, w.n);
-      if (cc != run_c) {
-        flush();
-        run_c = cc;
-        run_k = k;
-      } else {
-        run_k = k > run_k ? k : run_k;
-      }
-      pending &= ~__ballot(in);
-    }
+    const unsigned long long k = ((unsigned long long)key << 32) | (0xFFFFFFFFu - (unsigned)w.n);
+    best = k > best ? k : best;
   };
   if (cached) {
     ChanWalk<T> w(N);
 #pragma unroll
-    for (int i = 0; i < kCache; i++, w.next(N)) step(w, v[i]);
+    for (int i = 0; i < kCache; i++, w.next(N)) {
+      if (w.b < Bn) {
+        float o = bn_apply(v[i], fm, inv, g, bt);
+        if (relu) o = fmaxf(o, 0.0f);
+        emit(w, o);
+      }
+    }
   } else {
-    for (ChanWalk<T> w(N); __any(w.b < Bn); w.next(N)) step(w, w.b < Bn ? y[w.off(C, N, c)] : 0.0f);
+    for (ChanWalk<T> w(N); w.b < Bn; w.next(N)) {
+      float o = bn_apply(y[w.off(C, N, c)], fm, inv, g, bt);
+      if (relu) o = fmaxf(o, 0.0f);
+      emit(w, o);
+    }
   }
-  flush();
+  if (!pool) return;
+  if (cur >= 0) atomicMax(&pk[cur], best);
   __syncthreads();
   if (threadIdx.x < Bn) {
     const unsigned long long k = pk[threadIdx.x];
@@ -740,11 +704,20 @@ bool gemm64_only() {
   static const bool v = getenv_flag("NDNET_TR_GEMM64");
   return v;
 }
-// The split-bf16 ("x6") GEMM (k_tr_gemm_x6): NDNET_TR_X6=1, read once (it
-// sets the summation order of every train GEMM in the process).
-bool gemm_x6() {
-  static const bool v = getenv_flag("NDNET_TR_X6");
-  return v;
+// Which train GEMMs run split-bf16 (k_tr_gemm_x6), NDNET_TR_X6, read once
+// (it sets the process's summation orders): "dw" (default) the weight
+// gradients (both operands k-major: 54 vs 64 us on the 1024 x 128 layers,
+// -70 us a step), "all" every GEMM (the forward and input-gradient shapes
+// measured slower than the fp32 kernel's 128 x 128 tiles), "0" none
+// (profiles/r04_train_x6.txt).
+bool gemm_x6(bool a_kmajor, bool b_kmajor) {
+  static const int mode = [] {
+    const char* e = getenv("NDNET_TR_X6");
+    if (!e) return 1;
+    if (e[0] == '0') return 0;
+    return (e[0] == 'a' || e[0] == '1') ? 2 : 1;
+  }();
+  return mode == 2 || (mode == 1 && a_kmajor && b_kmajor);
 }
 // BatchNorm kernels on 1024-thread workgroups for layers of < 512 channels
 // (one workgroup per channel: the narrow layers leave most CUs idle at 512
@@ -789,7 +762,7 @@ extern "C" int ndnet_tr_gemm(const float* A, const float* B, float* C, const flo
       k_tr_gemm<64, AKV, BKV><<<grid, 256, 0, st>>>(A, B, C, bias, sbias, M, N, K, lda, ldb, ldc, sAz, sBz, sCz,     \
                                                     batch, clouds_per_part, nchunks, kchunk);                      \
   } while (0)
-  if (gemm_x6()) {  // 64 x 64 tiles only
+  if (gemm_x6(a_kmajor != 0, b_kmajor != 0)) {  // 64 x 64 tiles only
     const dim3 g6((unsigned)gx, (unsigned)gy, (unsigned)gz);
 #define NDNET_TR_GEMM6(AKV, BKV)                                                                                   \
   k_tr_gemm_x6<AKV, BKV><<<g6, 256, 0, st>>>(A, B, C, bias, sbias, M, N, K, lda, ldb, ldc, sAz, sBz, sCz, batch,     \
