@@ -107,7 +107,7 @@ __device__ __forceinline__ void tile_store(float* __restrict__ s, const float (&
 // TM x TM output tile per workgroup of TM / 8 waves: TM = 64 -> 2 x 2 waves of
 // 32 x 32 (four accumulator sets), TM = 128 -> 2 x 4 waves of 64 x 32 (two sets,
 // twice the MFMAs per LDS operand read; for the wide layers)
-template <int TM, bool AK, bool BK>
+template <int TM, bool AK, bool BK, int KT = kTK>  // KT: k per LDS step, 16 or 32 (two 16-deep sub-tiles)
 __global__ __launch_bounds__(TM * 4) void k_tr_gemm(const float* __restrict__ A, const float* __restrict__ B,
                                                     float* __restrict__ C, const float* __restrict__ bias,
                                                     int64_t sbias, int M, int N, int K, int64_t lda, int64_t ldb,
@@ -117,8 +117,9 @@ __global__ __launch_bounds__(TM * 4) void k_tr_gemm(const float* __restrict__ A,
   constexpr int WN = 2 * (TM / 64);       // waves along N
   constexpr int IM = TM / 32;             // 16-row blocks per wave (wave tile TM / 2 rows x 32 columns)
   constexpr int KS = TM == 64 ? 4 : 2;    // accumulator sets (k-quad ks uses set ks % KS)
-  __shared__ __attribute__((aligned(16))) float sA[2][kTK * PA];
-  __shared__ __attribute__((aligned(16))) float sB[2][kTK * PB];
+  constexpr int NS = KT / kTK;             // 16-deep sub-tiles per step
+  __shared__ __attribute__((aligned(16))) float sA[2][KT * PA];
+  __shared__ __attribute__((aligned(16))) float sB[2][KT * PB];
   const int z = blockIdx.z, zg = z / nchunks, zc = z - zg * nchunks;
   const int cl0 = zg * cpz, ncl = min(cpz, batch - cl0);  // this part's clouds
   C += z * sCz;
@@ -141,19 +142,28 @@ __global__ __launch_bounds__(TM * 4) void k_tr_gemm(const float* __restrict__ A,
       for (int j = 0; j < 2; j++) acc[ks][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // steps t = cloud * nst + s: the part's clouds one after another (split-K over clouds)
-  const int nst = kend > kbeg ? (kend - kbeg + kTK - 1) / kTK : 0;
+  const int nst = kend > kbeg ? (kend - kbeg + KT - 1) / KT : 0;
   const int total = ncl > 0 ? ncl * nst : 0;
-  float ra[4], rb[4];
+  float ra[NS][4], rb[NS][4];
   auto load = [&](int t) {
     const int cl = t / nst, st = t - cl * nst;
     const int64_t c = cl0 + cl;
-    tile_load<TM, AK>(A + c * sAz, lda, m0, kbeg + st * kTK, M, kend, ra);
-    tile_load<TM, BK>(B + c * sBz, ldb, n0, kbeg + st * kTK, N, kend, rb);
+#pragma unroll
+    for (int u = 0; u < NS; u++) {
+      tile_load<TM, AK>(A + c * sAz, lda, m0, kbeg + st * KT + kTK * u, M, kend, ra[u]);
+      tile_load<TM, BK>(B + c * sBz, ldb, n0, kbeg + st * KT + kTK * u, N, kend, rb[u]);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < NS; u++) {
+      tile_store<TM, AK>(sA[buf] + kTK * PA * u, ra[u]);
+      tile_store<TM, BK>(sB[buf] + kTK * PB * u, rb[u]);
+    }
   };
   if (total > 0) {
     load(0);
-    tile_store<TM, AK>(sA[0], ra);
-    tile_store<TM, BK>(sB[0], rb);
+    store(0);
   }
   __syncthreads();
   for (int t = 0; t < total; t++) {
@@ -163,7 +173,7 @@ __global__ __launch_bounds__(TM * 4) void k_tr_gemm(const float* __restrict__ A,
     const float* a = sA[cur];
     const float* b = sB[cur];
 #pragma unroll
-    for (int ks = 0; ks < kTK / 4; ks++) {
+    for (int ks = 0; ks < KT / 4; ks++) {  // k-quad ks of the step adds into set ks % KS (the global k-quad's)
       const int oa = (ks * 4 + q) * PA, ob = (ks * 4 + q) * PB;
       float av[IM];
 #pragma unroll
@@ -175,10 +185,7 @@ __global__ __launch_bounds__(TM * 4) void k_tr_gemm(const float* __restrict__ A,
         acc[ks % KS][i][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], b1, acc[ks % KS][i][1], 0, 0, 0);
       }
     }
-    if (more) {  // the other buffer was last read before the previous barrier
-      tile_store<TM, AK>(sA[cur ^ 1], ra);
-      tile_store<TM, BK>(sB[cur ^ 1], rb);
-    }
+    if (more) store(cur ^ 1);  // the other buffer was last read before the previous barrier
     __syncthreads();
   }
   // lane (q, r16) of block (i, j): rows 4 q + r, column r16
@@ -704,6 +711,17 @@ bool gemm64_only() {
   static const bool v = getenv_flag("NDNET_TR_GEMM64");
   return v;
 }
+// k per LDS step of the fp32 train GEMM: 32 (default; the same sums in the
+// same order as 16, half the barriers, twice the LDS: graphed step 2.893 ->
+// 2.849 ms, the 128 x 1024 layers' input gradients 61.8 -> 54.5 us,
+// profiles/r04_train_x6.txt) or NDNET_TR_KT=16
+bool gemm_k32() {
+  static const bool v = [] {
+    const char* e = getenv("NDNET_TR_KT");
+    return !(e && e[0] == '1');
+  }();
+  return v;
+}
 // Which train GEMMs run split-bf16 (k_tr_gemm_x6), NDNET_TR_X6, read once
 // (it sets the process's summation orders): "dw" (default) the weight
 // gradients (both operands k-major: 54 vs 64 us on the 1024 x 128 layers,
@@ -755,13 +773,20 @@ extern "C" int ndnet_tr_gemm(const float* A, const float* B, float* C, const flo
   hipStream_t st = (hipStream_t)stream;
 #define NDNET_TR_GEMM(AKV, BKV)                                                                                    \
   do {                                                                                                             \
-    if (wide)                                                                                                      \
+    if (wide && k32)                                                                                               \
+      k_tr_gemm<128, AKV, BKV, 32><<<grid, 512, 0, st>>>(A, B, C, bias, sbias, M, N, K, lda, ldb, ldc, sAz, sBz,     \
+                                                         sCz, batch, clouds_per_part, nchunks, kchunk);            \
+    else if (wide)                                                                                                 \
       k_tr_gemm<128, AKV, BKV><<<grid, 512, 0, st>>>(A, B, C, bias, sbias, M, N, K, lda, ldb, ldc, sAz, sBz, sCz,    \
                                                      batch, clouds_per_part, nchunks, kchunk);                     \
+    else if (k32)                                                                                                  \
+      k_tr_gemm<64, AKV, BKV, 32><<<grid, 256, 0, st>>>(A, B, C, bias, sbias, M, N, K, lda, ldb, ldc, sAz, sBz, sCz, \
+                                                        batch, clouds_per_part, nchunks, kchunk);                  \
     else                                                                                                           \
       k_tr_gemm<64, AKV, BKV><<<grid, 256, 0, st>>>(A, B, C, bias, sbias, M, N, K, lda, ldb, ldc, sAz, sBz, sCz,     \
                                                     batch, clouds_per_part, nchunks, kchunk);                      \
   } while (0)
+  const bool k32 = gemm_k32();
   if (gemm_x6(a_kmajor != 0, b_kmajor != 0)) {  // 64 x 64 tiles only
     const dim3 g6((unsigned)gx, (unsigned)gy, (unsigned)gz);
 #define NDNET_TR_GEMM6(AKV, BKV)                                                                                   \
