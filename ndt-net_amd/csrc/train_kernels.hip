@@ -711,6 +711,14 @@ bool gemm64_only() {
   static const bool v = getenv_flag("NDNET_TR_GEMM64");
   return v;
 }
+// 128 x 128 tiles when they still give this many workgroups (NDNET_TR_WIDE_MIN, A/B)
+int64_t wide_min_wgs() {
+  static const int64_t v = [] {
+    const char* e = getenv("NDNET_TR_WIDE_MIN");
+    return e ? (int64_t)atoll(e) : (int64_t)512;
+  }();
+  return v;
+}
 // k per LDS step of the fp32 train GEMM: 32 (default; the same sums in the
 // same order as 16, half the barriers, twice the LDS: graphed step 2.893 ->
 // 2.849 ms, the 128 x 1024 layers' input gradients 61.8 -> 54.5 us,
@@ -767,7 +775,7 @@ extern "C" int ndnet_tr_gemm(const float* A, const float* B, float* C, const flo
   if (gz > 65535 || gy > 65535 || gx > (int64_t)INT32_MAX) return -20;
   // 128 x 128 tiles where they still give the chip >= 512 workgroups
   const int64_t big = ((M + 127) / 128) * ((N + 127) / 128) * gz;
-  const bool wide = M >= 128 && N >= 128 && big >= 512 && !gemm64_only();
+  const bool wide = M >= 128 && N >= 128 && big >= wide_min_wgs() && !gemm64_only();
   const dim3 grid(wide ? (unsigned)((N + 127) / 128) : (unsigned)gx, wide ? (unsigned)((M + 127) / 128) : (unsigned)gy,
                   (unsigned)gz);
   hipStream_t st = (hipStream_t)stream;

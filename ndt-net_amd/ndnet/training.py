@@ -134,14 +134,25 @@ class Trainer:
                                           self.num_classes)
         return self.step_on_nds(pcl, covs, gt, train)
 
-    def step_graphed(self, points: torch.Tensor, gt_points: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-        """A training step as a graph replay; returns (loss, accuracy) as device
-        scalars, without synchronising."""
-        key = (tuple(points.shape), tuple(gt_points.shape))
+    def _graph_for(self, points_shape, gt_shape) -> "GraphedTrainStep":
+        key = (tuple(points_shape), tuple(gt_shape))
         g = self._graphed.get(key)
         if g is None:
-            g = self._graphed[key] = GraphedTrainStep(self, points.shape, gt_points.shape[-1])
-        return g(points, gt_points)
+            g = self._graphed[key] = GraphedTrainStep(self, points_shape, gt_shape[-1])
+        return g
+
+    def step_graphed(self, points: torch.Tensor, gt_points: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """A training step as a graph replay; returns (loss, accuracy) as device
+        scalars, without synchronising.  Passing the graph's own input buffers
+        (``graph_inputs``) skips the copies into them."""
+        return self._graph_for(points.shape, gt_points.shape)(points, gt_points)
+
+    def graph_inputs(self, points_shape, gt_shape) -> Tuple[torch.Tensor, torch.Tensor]:
+        """The static (points, one-hot gt) buffers the captured step of this
+        shape reads: a loader can fill them in place (e.g. a pinned-host copy)
+        and pass them to ``step_graphed`` with no device-to-device copy."""
+        g = self._graph_for(points_shape, gt_shape)
+        return g.s_points, g.s_gt
 
 
 class GraphedTrainStep:
@@ -212,7 +223,9 @@ class GraphedTrainStep:
         # the replay does not run Python: flip the mode here, so an eval forward
         # after it re-folds the updated weights (NDTNetSegmentation.train)
         self.tr.model.train()
-        self.s_points.copy_(points, non_blocking=True)
-        self.s_gt.copy_(gt_points, non_blocking=True)
+        if points.data_ptr() != self.s_points.data_ptr():
+            self.s_points.copy_(points, non_blocking=True)
+        if gt_points.data_ptr() != self.s_gt.data_ptr():
+            self.s_gt.copy_(gt_points, non_blocking=True)
         self.graph.replay()
         return self.loss, self.acc
