@@ -751,11 +751,11 @@ bool gemm_x6(bool a_kmajor, bool b_kmajor) {
 // NDNET_TR_BN1024=0 keeps 512 threads (read once like NDNET_TR_GEMM64: the
 // workgroup size sets the statistics' summation order).
 bool bn_wide_groups(int C) {
-  static const bool v = [] {
+  static const int v = [] {  // 0: never, 1: C < 512 (default), 2: every layer (A/B)
     const char* e = getenv("NDNET_TR_BN1024");
-    return !(e && e[0] == '0');
+    return e ? (e[0] == '0' ? 0 : e[0] == '2' ? 2 : 1) : 1;
   }();
-  return v && C < 512;
+  return v == 2 || (v == 1 && C < 512);
 }
 
 }  // namespace
