@@ -155,6 +155,9 @@ int ndnet_ndt_set_exact_counts(void *plan, int on);
  * random lines: ~2x the HBM write bytes).  Identical results either way;
  * float input with the plan's shapes in LDS only (otherwise direct). */
 int ndnet_ndt_set_front_staged(void *plan, int on);
+/* 1 when k_front's scatter of float input runs staged for this plan's shapes
+ * (and CU share), 0 when it runs direct; NDNET_ERR_ARG for a NULL plan. */
+int ndnet_ndt_get_front_staged(void *plan);
 
 /* k_welford_q computes the moments of an ND with at least min_samples points
  * on a whole wave (the mean recurrence alone on three lanes, the per-sample

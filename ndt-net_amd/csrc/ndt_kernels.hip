@@ -3081,7 +3081,14 @@ hipError_t front_config(Plan* P, int share) {
            ((sizeof(uint16_t) * (size_t)bpw * (1024 / rbs) * P->ndcap + 3) & ~(size_t)3);
   };
   const uint32_t rbs = (2 * bpw <= (uint32_t)kFrontWaves && lds_of(512) <= 150 * 1024) ? 512u : 1024u;
-  const size_t lds = lds_of(rbs);
+  size_t lds = lds_of(rbs);
+  // the staged scatter's records (16 bytes per point of the workgroup, over
+  // the whole dynamic LDS): reserved when they fit, else the direct scatter
+  // runs.  (Round 3's u16 histograms shrank lds_of below the records' need at
+  // B = 16, k = 1000, silently turning the staged scatter off: k_front's
+  // WRITE_SIZE 20.6 -> 39.5 MB, profiles/r04_pmc_summary.txt.)
+  const size_t staged_lds = (size_t)16 * 1024 * bpw;
+  if (bpw <= (uint32_t)kFrontR && staged_lds > lds && staged_lds <= 150 * 1024) lds = staged_lds;
   hipError_t e = hipSuccess;
   // (addv, the per-ND base words of the binning, live in the table region)
   int ok = lds <= 150 * 1024 && (G == 1 || (uint64_t)G * B <= (uint64_t)cus) && P->ndcap <= (uint32_t)kFrontTable;
@@ -3298,6 +3305,15 @@ int ndnet_ndt_set_front_staged(void* plan, int on) {
   if (!P || on < 0 || on > 1) return NDNET_ERR_ARG;
   P->front_staged = on;
   return NDNET_OK;
+}
+
+int ndnet_ndt_get_front_staged(void* plan) {
+  const Plan* P = (const Plan*)plan;
+  if (!P) return NDNET_ERR_ARG;
+  return P->front_ok && P->front_staged && P->fbpw <= (uint32_t)kFrontR && 2 * P->ndcap <= (uint32_t)kFrontTable &&
+                 (size_t)16 * 1024 * P->fbpw <= P->flds
+             ? 1
+             : 0;
 }
 
 int ndnet_ndt_set_heavy_threshold(void* plan, uint32_t min_samples) {

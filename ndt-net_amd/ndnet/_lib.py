@@ -70,6 +70,7 @@ EXPORTS = {
     "ndnet_ndt_set_cu_share": (_I, [_P, _I, _I]),
     "ndnet_ndt_set_exact_counts": (_I, [_P, _I]),
     "ndnet_ndt_set_front_staged": (_I, [_P, _I]),
+    "ndnet_ndt_get_front_staged": (_I, [_P]),
     "ndnet_ndt_set_run_part": (_I, [_P, _I]),
     "ndnet_ndt_set_lazy_list": (_I, [_P, _I]),
     "ndnet_ndt_set_heavy_threshold": (_I, [_P, ctypes.c_uint32]),

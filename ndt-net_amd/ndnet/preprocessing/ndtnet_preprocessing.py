@@ -86,6 +86,14 @@ class NdtPlan:
         include/ndnet_amd.h ndnet_ndt_set_front_staged; identical results)."""
         _lib.check(_lib.lib().ndnet_ndt_set_front_staged(self.handle, 1 if on else 0), "ndnet_ndt_set_front_staged")
 
+    @property
+    def front_staged(self) -> bool:
+        """Whether k_front's scatter runs staged for this plan's shapes (float input)."""
+        rc = _lib.lib().ndnet_ndt_get_front_staged(self.handle)
+        if rc < 0:
+            _lib.check(rc, "ndnet_ndt_get_front_staged")
+        return rc == 1
+
     def set_lazy_list(self, on: bool) -> None:
         """Defer the retained KL list of clouds whose level-1 prune cannot read
         it (num_nds <= k) until a prune or dump needs it (default on;

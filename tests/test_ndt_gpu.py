@@ -477,6 +477,18 @@ def test_merge_paths_match_oracle(k):
         assert np.array_equal(p[b], pc) and np.array_equal(c[b], cov)
 
 
+def test_front_staged_scatter_active_at_c2():
+    """The staged scatter actually runs for the C2 shape at CU share 1
+    (16 x 100k points -> 1000 NDs): round 3's u16 histograms had shrunk the
+    plan's LDS below the records' need and turned it off silently."""
+    import torch
+    from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
+    plan = NdtPlan(16, 100_000, 1000, -1, device=torch.device("cuda", 0))
+    assert plan.path == 2 and plan.front_staged
+    plan.set_front_staged(False)
+    assert not plan.front_staged
+
+
 @pytest.mark.parametrize("case", ["U", "L", "labelled"])
 def test_front_staged_scatter_equals_direct(case):
     """k_front's staged scatter (points placed in ND order in LDS, stored as
