@@ -1053,6 +1053,35 @@ __device__ inline void hv_block(double& m, double& acc, const double* __restrict
 typedef unsigned int hv_u16 __attribute__((ext_vector_type(16)));
 typedef double hv_d2 __attribute__((ext_vector_type(2)));  // native vector (HIP's double2 is a struct)
 
+#ifndef NDNET_WQ_HV_RLDS
+#define NDNET_WQ_HV_RLDS 1
+#endif
+#if NDNET_WQ_HV_RLDS
+// (rc, rl) of the 8 steps from the block's LDS row (every lane the same
+// address: a broadcast), written in phase 0 from the (rc, rl) each lane
+// loaded for its own sample three blocks ahead (HvRec::r) -- no scalar loads,
+// whose scalar-cache misses cost ~14 cycles per sample (profiles/r04_wq_rtab.txt)
+struct HvOps {
+  hv_d2 x[4];  // 8 steps' coordinates (lanes 0..2) or addends (lanes 3..8)
+  hv_d2 r[8];  // (rc, rl) of the 8 steps
+};
+
+template <int G>
+__device__ inline void hv_issue(HvOps& o, uint32_t rda, uint32_t rra) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(o.x[0]) : "v"(rda), "n"(64 * G));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(o.x[1]) : "v"(rda), "n"(64 * G + 16));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(o.x[2]) : "v"(rda), "n"(64 * G + 32));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(o.x[3]) : "v"(rda), "n"(64 * G + 48));
+#pragma unroll
+  for (int u = 0; u < 8; u++)
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(o.r[u]) : "v"(rra), "n"(128 * G + 16 * u));
+}
+__device__ inline void hv_wait(HvOps& o) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(o.x[0]), "+v"(o.x[1]), "+v"(o.x[2]), "+v"(o.x[3]), "+v"(o.r[0]), "+v"(o.r[1]), "+v"(o.r[2]),
+                 "+v"(o.r[3]), "+v"(o.r[4]), "+v"(o.r[5]), "+v"(o.r[6]), "+v"(o.r[7]));
+}
+#else
 struct HvOps {
   hv_d2 x[4];  // 8 steps' coordinates (lanes 0..2) or addends (lanes 3..8)
   hv_u16 r0, r1;  // (rc, rl) of the 8 steps, in scalar registers
@@ -1086,6 +1115,7 @@ __device__ inline void hv_wait(HvOps& o) {
   o.r0 = r0;
   o.r1 = r1;
 }
+#endif
 template <int G>
 __device__ inline void hv_put(uint32_t wra, const double (&mo)[8]) {
   const hv_d2 a = {mo[0], mo[1]}, b = {mo[2], mo[3]}, c = {mo[4], mo[5]}, d = {mo[6], mo[7]};
@@ -1101,23 +1131,32 @@ __device__ inline void hv_steps(double& m, double& acc, const HvOps& o, double (
 #pragma unroll
   for (int u = 0; u < 8; u++) {
     const double xv = o.x[u >> 1][u & 1];
+#if NDNET_WQ_HV_RLDS
+    const double rc = o.r[u][0], rl = o.r[u][1];
+#else
     const hv_u16& r = u < 4 ? o.r0 : o.r1;
     const double rc = hv_sd(r, 2 * (u & 3)), rl = hv_sd(r, 2 * (u & 3) + 1);
+#endif
     const double t = xv - m;
     m = m + fma(t, rc, t * rl);
     acc = acc + xv;
     mo[u] = m;
   }
 }
+#if NDNET_WQ_HV_RLDS
+typedef uint32_t HvRt;  // LDS byte address of the block's (rc, rl) row
+#else
+typedef const double2* HvRt;  // the block's first (rc, rl) in the global table
+#endif
 template <int G>  // group G of a full block: wait for its operands, write G - 1's means, issue G + 1's operands, step
 __device__ inline void hv_group(double& m, double& acc, HvOps& cur, HvOps& nxt, double (&mcur)[8],
-                                double (&mprev)[8], uint32_t rda, uint32_t wra, const double2* rtq) {
+                                double (&mprev)[8], uint32_t rda, uint32_t wra, HvRt rtq) {
   hv_wait(cur);
   if constexpr (G > 0) hv_put<G - 1>(wra, mprev);
   if constexpr (G < 7) hv_issue<G + 1>(nxt, rda, rtq);
   hv_steps(m, acc, cur, mcur);
 }
-__device__ inline void hv_block_asm(double& m, double& acc, uint32_t rda, uint32_t wra, const double2* rtq) {
+__device__ inline void hv_block_asm(double& m, double& acc, uint32_t rda, uint32_t wra, HvRt rtq) {
   HvOps A, B;
   double mA[8], mB[8];
   hv_issue<0>(A, rda, rtq);
@@ -1135,8 +1174,8 @@ __device__ inline void hv_block_asm(double& m, double& acc, uint32_t rda, uint32
 
 template <typename T, bool kStamp = false>  // kStamp: phase cycle totals to ph[0..2] (timing level 2)
 __device__ inline void wq_heavy(const T* __restrict__ rec, uint32_t cnt, const double2* __restrict__ rtab,
-                                double* __restrict__ lds, uint32_t lane, double& mean, double& m2, double& off,
-                                bool& bad, unsigned long long* ph = nullptr) {
+                                double* __restrict__ lds, double2* __restrict__ hr, uint32_t lane, double& mean,
+                                double& m2, double& off, bool& bad, unsigned long long* ph = nullptr) {
   unsigned long long ts = 0, c0 = 0, c1 = 0, c2 = 0;
   auto stamp = [&](unsigned long long& acc) __attribute__((always_inline)) {
     if constexpr (kStamp) {
@@ -1178,13 +1217,23 @@ __device__ inline void wq_heavy(const T* __restrict__ rec, uint32_t cnt, const d
     X[kHvS + lane] = x1;
     X[2 * kHvS + lane] = x2;
     if (lane < 3) M[a * kHvS + 1] = m;
+#if NDNET_WQ_HV_RLDS
+    hr[lane] = h.r;  // the block's (rc, rl) row for the loop's broadcast reads
+#endif
     asm volatile("" ::: "memory");  // one wave's LDS operations complete in order
     stamp(c0);
     // 1. the recurrence (lanes 0..2) + the previous block's ordered sums (lanes 3..8)
     if (lane < 9) {
       if (nb == 64)
         hv_block_asm(m, acc, (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const double*)rd,
-                     (uint32_t)(uintptr_t)(__attribute__((address_space(3))) double*)wr, rtab + q0 + 1);
+                     (uint32_t)(uintptr_t)(__attribute__((address_space(3))) double*)wr,
+#if NDNET_WQ_HV_RLDS
+                     (uint32_t)(uintptr_t)(__attribute__((address_space(3))) double2*)hr);
+#elif defined(NDNET_WQ_HV_FIXRT)  // timing experiment only (wrong results): every block reads block 0's (rc, rl)
+                     rtab + 1);
+#else
+                     rtab + q0 + 1);
+#endif
       else
         hv_block<true>(m, acc, rd, wr, rtab, q0, nb);
     }
@@ -1331,6 +1380,7 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
   extern __shared__ __attribute__((aligned(16))) unsigned char wq_smem[];
   // the quads' record transposes; a heavy item's wave uses its 16 rows (6400 B) as its wq_heavy stage
   __shared__ __attribute__((aligned(16))) float wq_stage[kWqNDs][kWqStageQ];
+  __shared__ double2 wq_hr[kWqThreads / 64][64];  // a heavy wave's block row of (rc, rl)
   static_assert(kHvLds * sizeof(double) <= 16 * kWqStageQ * sizeof(float), "heavy stage fits a wave's rows");
   static_assert((16 * kWqStageQ * sizeof(float)) % 16 == 0, "16-byte aligned heavy stage");
   double* lrt = (double*)wq_smem;                                // [kWqRt] refined reciprocals of 1..kWqRt
@@ -1652,8 +1702,8 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
     const T* rec = nd_pts + ((uint64_t)b * n + __builtin_amdgcn_readfirstlane(beg)) * 3;
     const uint32_t hc = __builtin_amdgcn_readfirstlane(c0);  // c0, beg: the same in every lane here
     double* hl = reinterpret_cast<double*>(&wq_stage[wave * 16][0]);
-    if (wq_marks) wq_heavy<T, true>(rec, hc, rtab, hl, lane, mean, m2, off, bad, ph);
-    else wq_heavy<T>(rec, hc, rtab, hl, lane, mean, m2, off, bad);
+    if (wq_marks) wq_heavy<T, true>(rec, hc, rtab, hl, wq_hr[wave], lane, mean, m2, off, bad, ph);
+    else wq_heavy<T>(rec, hc, rtab, hl, wq_hr[wave], lane, mean, m2, off, bad);
   } else
     run(mx, true, std::false_type{});
   if (wq_marks) mk_t1 = __builtin_amdgcn_s_memtime();
@@ -1790,7 +1840,10 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
       w[1] = mk_t0;
       w[2] = mk_t1;
       w[3] = t2;
-      w[4] = ((unsigned long long)hv << 63) | ((unsigned long long)mxc << 32) | (blockIdx.x * 4u + wave);
+      // placement: HW_ID (wave, SIMD, CU, SH, SE) and the XCC, to see which items shared a SIMD
+      const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+      const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;
+      w[4] = ((unsigned long long)hv << 63) | ((unsigned long long)xcc << 56) | ((unsigned long long)(mxc & 0xFFFFFFu) << 32) | hwid;
       w[5] = ph[0];
       w[6] = ph[1];
       w[7] = ph[2];

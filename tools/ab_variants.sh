@@ -10,7 +10,7 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 for V in "$@"; do
   if [ "$V" = base ]; then LIBV=""; else LIBV=$R/ndt-net_amd/lib/variants/libndnet_amd_$V.so; fi
-  NDNET_AMD_LIB=$LIBV timeout -k 10 150 python bench.py --no-cpu-baseline --no-other --steps 50 > $OUT/$V.log 2>&1 || { echo "$V failed"; tail -5 $OUT/$V.log; exit 1; }
+  NDNET_AMD_LIB=$LIBV timeout -k 10 150 python bench.py --no-cpu-baseline --no-other --steps 50 ${AB_ARGS} > $OUT/$V.log 2>&1 || { echo "$V failed"; tail -5 $OUT/$V.log; exit 1; }
   python3 - "$V" "$OUT/$V.log" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])

@@ -51,12 +51,15 @@ for r in range(a.reps):
     heavy = int((w[:, 4] >> np.uint64(63)).astype(bool)[: cap].sum())
     # the run's items: heavy first, then light; stale entries past them are ignored
     hv = (w[:, 4] >> np.uint64(63)).astype(bool)
-    cnt = ((w[:, 4] >> np.uint64(32)) & np.uint64(0x7fffffff)).astype(np.int64)
+    cnt = ((w[:, 4] >> np.uint64(32)) & np.uint64(0xFFFFFF)).astype(np.int64)
+    hwid = (w[:, 4] & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    xcc = ((w[:, 4] >> np.uint64(56)) & np.uint64(15)).astype(np.int64)
     rt0 = w[:, 0].astype(np.float64)
     t0, t1, t2 = (w[:, i].astype(np.int64) for i in (1, 2, 3))
     H = int(hv[: cap].sum())
     run = slice(0, H + light)
     hv, cnt, rt0, t0, t1, t2 = hv[run], cnt[run], rt0[run], t0[run], t1[run], t2[run]
+    hwid, xcc = hwid[run], xcc[run]
     start = rt0.min()
     end_rt = rt0 + (t2 - t0) / 2.1e9 * 1e8  # approximate: shader clock ~2.1 GHz -> 100 MHz ticks
     spans.append((end_rt.max() - start) * 0.01)
@@ -73,6 +76,38 @@ for r in range(a.reps):
         for i in order:
             print(f"  {'H' if hv[i] else 'L'} {cnt[i]:5d}  start {(rt0[i] - start) * 0.01:7.2f}  "
                   f"moments {t1[i] - t0[i]:7d}  epilogue {t2[i] - t1[i]:6d}")
+        # placement (HW_ID: simd 5:4, cu 11:8, sh 12, se 15:13, tg 19:16; + XCC)
+        simd = (hwid >> 4) & 3
+        cu_key = (xcc << 8) | (((hwid >> 13) & 7) << 5) | (((hwid >> 12) & 1) << 4) | ((hwid >> 8) & 15)
+        simd_key = cu_key * 4 + simd
+        tg = (hwid >> 16) & 15
+        ncu = len(np.unique(cu_key))
+        wgs = {}
+        for ck, g in zip(cu_key, tg):
+            wgs.setdefault(int(ck), set()).add(int(g))
+        per = np.bincount([len(v) for v in wgs.values()])
+        print(f"placement: {ncu} CUs used; workgroups per CU histogram {list(per)}")
+        end_m = rt0 + (t1 - t0) / 2.1e9 * 1e8
+        end_all = end_rt
+        share = []
+        for i in np.nonzero(hv)[0]:
+            same = (simd_key == simd_key[i])
+            same[i] = False
+            ov = np.clip(np.minimum(end_m[i], end_all[same]) - np.maximum(rt0[i], rt0[same]), 0, None)
+            share.append(ov.sum() / max(end_m[i] - rt0[i], 1e-9))
+        share = np.array(share) if share else np.zeros(1)
+        cps = ((t1 - t0)[hv] / np.maximum(cnt[hv], 1))
+        print("heavy items: mean other waves on the same SIMD during the moments: median %.2f p90 %.2f max %.2f"
+              % (np.median(share), np.percentile(share, 90), share.max()))
+        for lo_, hi_ in ((0, 0.05), (0.05, 0.5), (0.5, 1.0), (1.0, 9.0)):
+            sel = (share >= lo_) & (share < hi_)
+            if sel.any():
+                print(f"  sharing {lo_:.2f}-{hi_:.2f}: {sel.sum():4d} heavy items, cycles/sample median {np.median(cps[sel]):.1f}")
+        top = np.argsort(-cnt * hv)[: min(8, int(hv.sum()))]
+        for i in top:
+            j = list(np.nonzero(hv)[0]).index(i)
+            print(f"  heaviest: {cnt[i]:5d} samples, simd {simd[i]}, cu {cu_key[i]:4d}, cycles/sample {(t1[i] - t0[i]) / cnt[i]:.1f}, "
+                  f"other waves on SIMD {share[j]:.2f}")
         hc = np.sort(cnt[hv])[::-1][:5]
         print(f"heaviest heavy NDs: {list(hc)}; heaviest light group: {cnt[~hv].max() if (~hv).any() else 0}")
 _lib.lib().ndnet_ndt_set_timing(plan.handle, 0)
