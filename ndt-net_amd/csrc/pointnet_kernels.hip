@@ -119,6 +119,23 @@ __device__ inline float xor_row(float v) {
 // dynamic LDS of k_pn_chain: the two activation regions and the fused pair's
 // double buffer, addressed by float offsets so every access is a ds_* op
 extern __shared__ __attribute__((aligned(16))) float g_smem[];
+#ifndef NDNET_PN_TID_FRESH
+#define NDNET_PN_TID_FRESH 1
+#endif
+// threadIdx.x as a value the compiler cannot see through: a layer's lane /
+// wave / row / column offsets are derived from it where the layer runs
+// instead of being hoisted to the kernel's start and kept live through every
+// layer (they took ~48 of the 128 VGPRs the 16-wave build has, so the x6
+// loops could neither keep a plane's four A fragments nor the next weight
+// step in registers)
+__device__ inline int pn_tid() {
+  int t = (int)threadIdx.x;
+#if NDNET_PN_TID_FRESH
+  asm volatile("" : "+v"(t));
+#endif
+  return t;
+}
+
 
 // Timing build only (-DNDNET_PN_STAMPS, tools/pn_stamps.py): s_memrealtime
 // (100 MHz) of every workgroup at its start (0), after chain B's head
@@ -167,8 +184,8 @@ struct Pre {
 __device__ inline LayerCtx layer_ctx(const ndnet_pn_chain& A, int l, int b, const float* bias) {
   const ndnet_pn_layer& L = A.L[l];
   LayerCtx C;
-  C.w = reinterpret_cast<const f32x4*>(L.w + (int64_t)b * L.w_cloud_stride) + (threadIdx.x & 63);
-  C.w6 = reinterpret_cast<const bf16x8*>(L.w + (int64_t)b * L.w_cloud_stride) + (threadIdx.x & 63);
+  C.w = reinterpret_cast<const f32x4*>(L.w + (int64_t)b * L.w_cloud_stride) + (pn_tid() & 63);
+  C.w6 = reinterpret_cast<const bf16x8*>(L.w + (int64_t)b * L.w_cloud_stride) + (pn_tid() & 63);
   C.bias = bias;
   C.prec = L.prec;
   C.KG = L.prec ? L.K / 32 : L.K / 16;  // prec 1 and 2: 32-row k-groups
@@ -282,7 +299,7 @@ template <int RB, int NB>
 __device__ __attribute__((always_inline)) inline void store_cols(const f32x4 (&acc)[RB][NB],
                                                                  const float* __restrict__ bias, int col0, int relu,
                                                                  int row0, int out, int pout, int oc0) {
-  const int lane = threadIdx.x & 63;
+  const int lane = pn_tid() & 63;
   const int kq = lane >> 4, cl = lane & 15;
 #if NDNET_PN_SWAP
 #pragma unroll
@@ -323,7 +340,7 @@ template <int RB, int NB>
 __device__ __attribute__((always_inline)) inline void pool_cols(const f32x4 (&acc)[RB][NB],
                                                                 const float* __restrict__ bias, int col0, int relu,
                                                                 int row0, int rows_valid, float* gmax) {
-  const int lane = threadIdx.x & 63;
+  const int lane = pn_tid() & 63;
   const int kq = lane >> 4, cl = lane & 15;
 #if NDNET_PN_SWAP
   // lane (kq, cl): point cl of each row block, channels 4 kq + r; the max over
@@ -412,7 +429,7 @@ __device__ __attribute__((always_inline)) inline void store_cols_planes(const f3
                                                                         const float* __restrict__ bias, int col0,
                                                                         int relu, int row0, int out, int pitchb,
                                                                         int oc0) {
-  const int lane = threadIdx.x & 63;
+  const int lane = pn_tid() & 63;
   const int kq = lane >> 4, cl = lane & 15;
   __bf16* const base = reinterpret_cast<__bf16*>(g_smem + out);
   const int plane = kP * pitchb;
@@ -581,7 +598,7 @@ template <int RB, int NB>
 __device__ void plain_layer(const LayerCtx& C, int in, int pin, int out, int pout, float* gmax, int rows_valid,
                             bool out_planes, Pre pre = {}) {
   constexpr int WR = kRowBlocks / RB, WC = kWaves / WR, CB = WC * NB;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = pn_tid() & 63, wave = pn_tid() >> 6;
   const int wr = wave / WC, wc = wave % WC;
   const int kq = lane >> 4, cl = lane & 15;
   const int row0 = wr * RB * 16;
@@ -625,7 +642,7 @@ __device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin
                            float* gmax, int rows_valid, bool out_planes, Pre pre = {}) {
   constexpr int kFP = kFuseNC + kPadF;
   constexpr int WR = kRowBlocks / RB, WC = kWaves / WR;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = pn_tid() & 63, wave = pn_tid() >> 6;
   const int kq = lane >> 4, cl = lane & 15;
   // P: row block wave / PWC, PNB column blocks from 4 f + PNB (wave % PWC)
   constexpr int PWC = kWaves / kRowBlocks, PNB = 4 / PWC;

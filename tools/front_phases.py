@@ -25,11 +25,16 @@ ap.add_argument("--points", type=int, default=100_000)
 ap.add_argument("--nds", type=int, default=1000)
 ap.add_argument("--kind", default="U")
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--share", type=int, default=1, help="CU share of the NDT stage (the pipeline's is 2)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 pts = torch.from_numpy(make_batch(a.kind, a.batch, a.points, seed0=0)).to(dev)
 ndt_preprocessing(a.nds, pts)
 plan = get_plan(a.batch, a.points, a.nds, -1, dev)
+if a.share > 1:
+    from ndnet.pipeline import PIPE_WQ_SHARE  # noqa: E402
+    plan.set_cu_share(a.share, PIPE_WQ_SHARE)
+    ndt_preprocessing(a.nds, pts)
 _lib.check(_lib.lib().ndnet_ndt_set_timing(plan.handle, 2), "set_timing")
 names = {0: "start", 1: "limits in", 2: "limits out", 20: "accepted", 21: "dense ids", 22: "point NDs",
          23: "offsets in", 24: "offsets out", 25: "offsets", 26: "scattered"}
