@@ -50,7 +50,10 @@ constexpr int kFrontWaves = kFrontThreads / 64;
 #ifndef NDNET_FRONT_R
 #define NDNET_FRONT_R 8
 #endif
-constexpr int kFrontR = NDNET_FRONT_R;  // bins per workgroup whose points stay in registers
+constexpr int kFrontR = NDNET_FRONT_R;
+#ifndef NDNET_FRONT_LDSMATCH
+#define NDNET_FRONT_LDSMATCH 1
+#endif  // bins per workgroup whose points stay in registers
 constexpr int kFrontTable = 8192;   // LDS words: byte map of a small grid (32768 voxels) or hash slots
 constexpr int kFrontPhases = 40;    // record slots per cloud and run
 constexpr int kRecWords = 16;       // per-workgroup record: [0] count, [1] any bad, [2..9] first bad per worker
@@ -808,16 +811,39 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
     // m &= ~(ballot ^ mask) on both halves -- the lanes that agree on the bit.
     const uint32_t nbits = __builtin_amdgcn_readfirstlane(32u - (uint32_t)__clz((int)(ndcap > 1 ? ndcap - 1 : 1)));
     const unsigned long long below = (1ull << lane) - 1ull;
+#if NDNET_FRONT_LDSMATCH
+    // Round 4: the low 8 bits of the ND id matched through LDS instead of 8
+    // ballot rounds: each lane ORs its bit into its wave's slot d & 255
+    // (the table region is free once the point NDs are found: 16 waves x 256
+    // slots x 8 B = kFrontTable words) and reads the slot back; only the
+    // high bits are matched by ballots.  The loop is VALU-issue bound
+    // (~6 instructions per matched bit), not LDS bound.
+    unsigned long long* slots = reinterpret_cast<unsigned long long*>(table) + (uint64_t)wave * 256u;
+    static_assert(kFrontWaves * 256 * 2 <= kFrontTable, "a wave's 256 match slots fit the table region");
+#pragma unroll
+    for (int e = 0; e < 4; e++) slots[lane + 64 * e] = 0ull;
+    const unsigned long long mybit = 1ull << lane;
+#endif
     for (uint32_t r = wave; r < nrb; r += kFrontWaves) {
       uint16_t* hr = hist + (uint64_t)r * ndcap;
       uint32_t* br = binfo + (uint64_t)r * rbs;
       for (uint32_t st = 0; st < rbs / 64; st++) {
         const uint32_t d = br[st * 64 + lane];
         const bool valid = d != kInvalid;
+#if NDNET_FRONT_LDSMATCH
+        const uint32_t h = d & 255u;
+        if (valid) __hip_atomic_fetch_or(&slots[h], mybit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // the wave's ORs are one LDS instruction, executed before this read
+        const unsigned long long mv = valid ? __hip_atomic_load(&slots[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0ull;
+        uint32_t mlo = (uint32_t)mv, mhi = (uint32_t)(mv >> 32);
+        constexpr uint32_t kBit0 = 8;
+#else
         const unsigned long long mv = __ballot(valid);
         uint32_t mlo = (uint32_t)mv, mhi = (uint32_t)(mv >> 32);
+        constexpr uint32_t kBit0 = 0;
+#endif
 #pragma unroll
-        for (uint32_t bit = 0; bit < 15; bit++) {  // ndcap <= 16384 (k_front host check)
+        for (uint32_t bit = kBit0; bit < 15; bit++) {  // ndcap <= 16384 (k_front host check)
           if (bit < nbits) {
             const uint32_t mask = (uint32_t)__builtin_amdgcn_sbfe((int)d, bit, 1);
             const unsigned long long bb = __ballot(mask != 0u);
@@ -826,6 +852,11 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
           }
         }
         const unsigned long long m = ((unsigned long long)mhi << 32) | mlo;
+#if NDNET_FRONT_LDSMATCH
+        // every lane of the slot has read it (the read above is one
+        // instruction): cleared for the next step
+        if (valid) __hip_atomic_store(&slots[h], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
         if (valid) {
           const uint32_t rank = (uint32_t)__popcll(m & below), cnt = (uint32_t)__popcll(m);
           const uint32_t cur = hr[d];  // read by every lane of the set before its last lane writes
