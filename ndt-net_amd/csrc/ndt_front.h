@@ -50,10 +50,10 @@ constexpr int kFrontWaves = kFrontThreads / 64;
 #ifndef NDNET_FRONT_R
 #define NDNET_FRONT_R 8
 #endif
-constexpr int kFrontR = NDNET_FRONT_R;
+constexpr int kFrontR = NDNET_FRONT_R;  // bins per workgroup whose points stay in registers
 #ifndef NDNET_FRONT_LDSMATCH
-#define NDNET_FRONT_LDSMATCH 1
-#endif  // bins per workgroup whose points stay in registers
+#define NDNET_FRONT_LDSMATCH 1  // the rank loop's low ND-id bits matched through LDS slots
+#endif
 constexpr int kFrontTable = 8192;   // LDS words: byte map of a small grid (32768 voxels) or hash slots
 constexpr int kFrontPhases = 40;    // record slots per cloud and run
 constexpr int kRecWords = 16;       // per-workgroup record: [0] count, [1] any bad, [2..9] first bad per worker
@@ -421,6 +421,9 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
 
   // ---- bisection passes ----
   for (;;) {
+#ifndef NDNET_FRONT_BINMARKS
+    if (s.npass == 0) FRONT_MARK(27);
+#endif
     // grid of this guess (voxel.c:61-81), identical in every workgroup.
     // Thread 0 runs the passes a grid too small to count decides (hi = guess)
     // back to back, without a workgroup barrier per pass; after each such
@@ -470,6 +473,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
       }
     }
     __syncthreads();
+    if (s.npass == 0) FRONT_MARK(19);
     if (s.state != kSearching) break;
     const uint64_t V = s.V;
     const bool small = V <= (uint64_t)kBitsCap;
@@ -484,9 +488,6 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
     }
     if (t < (uint32_t)kWorkers) s_bad[t] = kInvalid;
     __syncthreads();
-#ifndef NDNET_FRONT_BINMARKS
-    if (s.npass == 0) FRONT_MARK(27);
-#endif
     const double vs = s.guess, inv_vs = 1.0 / vs;
     double off[3] = {s.off[0], s.off[1], s.off[2]};
     uint32_t len[3] = {s.len[0], s.len[1], s.len[2]};

@@ -326,6 +326,35 @@ def test_front_kernel_equals_multikernel_path(case):
             assert np.array_equal(o2[b, :, :3], pc) and np.array_equal(o2[b, :, 3:], cov)
 
 
+@pytest.mark.parametrize("vcap", [40, 120, 900, 6000])
+def test_voxel_capacity_overflow_paths_agree(vcap):
+    """A grid of more voxels than the plan's capacity fails the cloud (rc -1,
+    the reference's malloc of V NDs) at the iteration it appears: on a grid
+    too small to count (k_front's skipped iterations, run as lanes of one
+    wave) or on a counted one.  k_front and the one-launch-per-stage path
+    agree on every stats field, and U's clouds reach both kinds."""
+    import torch
+    from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
+    from ndnet.synthetic import make_batch
+    pts = np.concatenate([make_batch("U", 2, 20_000, seed0=3), make_batch("L", 1, 20_000, seed0=4)])
+    B, n, _ = pts.shape
+    k = 300
+    res = {}
+    for path in (1, 2):
+        plan = NdtPlan(B, n, k, -1, voxel_capacity=vcap)
+        plan.set_path(path)
+        assert plan.path == path
+        out = torch.empty((B, k, 12), dtype=torch.float32, device="cuda")
+        plan.run(torch.from_numpy(pts).cuda(), None, out, None)
+        torch.cuda.synchronize()
+        res[path] = (out.cpu().numpy(), plan.host_stats())
+    for b in range(B):
+        assert bytes(res[1][1][b]) == bytes(res[2][1][b]), f"cloud {b} stats (vcap {vcap})"
+    assert np.array_equal(res[1][0], res[2][0])
+    if vcap == 40:  # overflows while the grids are still too small to count
+        assert all(st.rc == -1 for st in res[2][1])
+
+
 @pytest.mark.parametrize("kind", ["U", "L"])
 def test_multiscale_batch_matches_oracle_chain(kind):
     """Config C5's path batched: downsample(600) -> prune(300) -> prune(150)

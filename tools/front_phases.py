@@ -38,7 +38,7 @@ if a.share > 1:
 _lib.check(_lib.lib().ndnet_ndt_set_timing(plan.handle, 2), "set_timing")
 names = {0: "start", 1: "limits in", 2: "limits out", 20: "accepted", 21: "dense ids", 22: "point NDs",
          23: "offsets in", 24: "offsets out", 25: "offsets", 26: "scattered"}
-names.update({27: "p1 cleared", 28: "p1 keys", 29: "p1 atomics", 30: "p1 sum", 31: "p1 counts read"})
+names.update({19: "p1 grid (thread 0)", 27: "p1 loop top", 28: "p1 keys", 29: "p1 atomics", 30: "p1 sum", 31: "p1 counts read"})
 if os.environ.get("NDNET_FRONT_BINMARKS"):
     names.update({27: "ranks done (wave 0)", 28: "ranks barrier", 29: "nd prefix done"})
     for i in (30, 31):
