@@ -125,9 +125,10 @@ void ndnet_ndt_plan_destroy(void *plan);
  * Concurrency: path 2's grid barrier assumes no other k_front grid competes
  * for the CUs at the same time (two partly resident grids wait for each
  * other until the ~2 s barrier timeout fails their clouds with
- * NDNET_ERR_SYNC).  Run at most one path-2 plan per device at a time, or
- * select path 1 for plans that run concurrently; the legacy entry points
- * above always use path 1. */
+ * NDNET_ERR_SYNC).  Run at most one path-2 plan per device at a time, give
+ * each of N path-2 plans that run concurrently front_share >= N
+ * (ndnet_ndt_set_cu_share; ndnet.pipeline does so for its N NDT streams), or
+ * select path 1 for them; the legacy entry points above always use path 1. */
 int ndnet_ndt_set_path(void *plan, int path);
 int ndnet_ndt_get_path(void *plan);
 

@@ -217,12 +217,33 @@ class PipelinedSegmentation:
         self.plan = self.plans[0]
         if cu_share is None:
             cu_share = PIPE_CU_SHARE
+        # k_front's workgroups of a cloud meet at cloud barriers, so all of them
+        # must be resident at once.  One NDT stream: k_front alone spans at most
+        # the chip (the other kernels never wait on anything, so they drain).
+        # N NDT streams run N k_front launches at once: each must take at most
+        # CUs / N, or their resident halves wait on each other until the
+        # barrier timeout fails the clouds (measured: 640 ms per step with two
+        # streams at share 1).  So the share is at least N, the largest that
+        # fits from the requested one down to N; a shape that fits none of them
+        # takes the one-launch-per-stage path (no cloud barriers).
+        self.front_share = []
         for plan in self.plans:
-            if cu_share > 1 and plan.path == 2:
-                try:
-                    plan.set_cu_share(cu_share, PIPE_WQ_SHARE)
-                except RuntimeError:  # k_front does not fit that share for this shape
-                    pass
+            applied = 1
+            if plan.path == 2:
+                want = [cu_share] if N == 1 else list(range(max(cu_share, N), N - 1, -1))
+                for sh in want:
+                    if sh <= 1:
+                        break
+                    try:
+                        plan.set_cu_share(sh, PIPE_WQ_SHARE)
+                        applied = sh
+                        break
+                    except RuntimeError:  # k_front does not fit that share for this shape
+                        continue
+                if N > 1 and applied < N:
+                    plan.set_path(1)
+                    applied = 0
+            self.front_share.append(applied)  # 0: the one-launch-per-stage path
         # stream priorities (NDNET_PIPE_PRIORITY): none by default, see PIPE_PRIORITY
         hi = torch.cuda.Stream.priority_range()[1] if PIPE_PRIORITY != "none" else 0
         self.s_ndts = [torch.cuda.Stream(device=dev, priority=hi if PIPE_PRIORITY == "ndt" else 0) for _ in range(N)]

@@ -142,6 +142,38 @@ def test_pipelined_free_running_steps_equal_sequential_batches(fwd_streams, ndt_
     assert torch.equal(out, expect[R - 1])
 
 
+def test_two_ndt_streams_keep_k_front_resident():
+    """Two NDT streams run two k_front launches at once; asked for CU share 1
+    (each launch would span the chip, their workgroups waiting on each other at
+    the cloud barriers) the pipeline takes share 2 instead, and every step's
+    clouds complete (no barrier timeout) with the one-graph-per-step path's
+    output, at the full C2 shape."""
+    import torch
+    from ndnet.models.ndtnet import NDTNetSegmentation
+    from ndnet.pipeline import GraphedSegmentation, PipelinedSegmentation
+    from ndnet.synthetic import make_batch
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    m = NDTNetSegmentation(3, 28, 768).to(dev).eval()
+    pipe = PipelinedSegmentation(m, 1000, 16, 100_000, device=dev, cu_share=1, ndt_streams=2)
+    assert pipe.front_share == [2, 2]
+    R = pipe.R
+    batches = [torch.from_numpy(make_batch("L" if j % 2 else "U", 16, 100_000, seed0=100 * j)).to(dev)
+               for j in range(R)]
+    ref = GraphedSegmentation(m, 1000, 16, 100_000, device=dev)
+    expect = [ref(b).clone() for b in batches]
+    for j, b in enumerate(batches):
+        pipe.inputs[j].copy_(b)
+    for _ in range(R):
+        pipe.replay()
+    pipe.replay_steps(2 * R)
+    torch.cuda.synchronize()
+    for plan in pipe.plans:
+        assert all(st.rc == 0 for st in plan.host_stats())
+    for j in range(R):
+        assert torch.equal(pipe.out[j], expect[(j - 1) % R]), f"slot {j}"
+
+
 def test_pipelined_levels_equal_graphed_levels():
     """C5-shaped pipeline (downsample + two prune levels, a forward per level):
     every step's per-level outputs, single-step and free-running, bit-equal the
