@@ -1154,6 +1154,17 @@ __device__ inline void hv_group(double& m, double& acc, HvOps& cur, HvOps& nxt, 
   hv_wait(cur);
   if constexpr (G > 0) hv_put<G - 1>(wra, mprev);
   if constexpr (G < 7) hv_issue<G + 1>(nxt, rda, rtq);
+  // the steps are plain VALU code, which the compiler may move above the
+  // asm statements before it: without this the next group's reads went out
+  // after this group's steps, right before their wait (the LDS latency
+  // exposed once per group).  m and acc pass through an asm statement placed
+  // after the reads, so the steps start only once they are issued.
+#ifndef NDNET_WQ_HV_ORDER
+#define NDNET_WQ_HV_ORDER 1
+#endif
+#if NDNET_WQ_HV_ORDER
+  asm volatile("" : "+v"(m), "+v"(acc));
+#endif
   hv_steps(m, acc, cur, mcur);
 }
 __device__ inline void hv_block_asm(double& m, double& acc, uint32_t rda, uint32_t wra, HvRt rtq) {
@@ -1440,6 +1451,9 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
   };
   for (uint32_t item = blockIdx.x * (kWqThreads / 64) + wave; item < total; item = next_item()) {
   const bool hv = item < H;  // a heavy ND (wave-uniform)
+#ifdef NDNET_WQ_EXP_HEAVYONLY  // timing experiment only (wrong results): light items skipped
+  if (!hv) continue;
+#endif
   unsigned long long mk_rt = 0, mk_t0 = 0, mk_t1 = 0;
   if (wq_marks) {
     mk_rt = __builtin_amdgcn_s_memrealtime();
