@@ -51,6 +51,9 @@ constexpr int kFrontWaves = kFrontThreads / 64;
 #define NDNET_FRONT_R 8
 #endif
 constexpr int kFrontR = NDNET_FRONT_R;  // bins per workgroup whose points stay in registers
+#ifndef NDNET_FRONT_BYTEMAP_READ
+#define NDNET_FRONT_BYTEMAP_READ 0  // 1: read a voxel's byte before marking it (round 1-4 form)
+#endif
 #ifndef NDNET_FRONT_LDSMATCH
 #define NDNET_FRONT_LDSMATCH 1  // the rank loop's low ND-id bits matched through LDS slots
 #endif
@@ -515,7 +518,11 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
         redo |= key == kKeyRedo;
         cold |= key == kInvalid;
         if (small && key < kKeyRedo) {
+#if NDNET_FRONT_BYTEMAP_READ
           if (!bytemap[key]) bytemap[key] = 1;  // read first: most lanes of a small grid hit set bytes
+#else
+          bytemap[key] = 1;  // a plain store: no LDS round trip per point before the next point's key
+#endif
         }
       }
       binfo[j * 1024 + t] = key;
