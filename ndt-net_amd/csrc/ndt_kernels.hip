@@ -847,7 +847,25 @@ constexpr int kWqThreads = 256;              // 4 waves x 16 quads
 constexpr int kWqNDs = kWqThreads / 4;
 constexpr int kWqU = 16;                     // samples per prefetch block
 constexpr int kWqNB = 4;                     // register blocks in the prefetch ring
-constexpr int kWqRt = 4096;                  // reciprocals tabled in LDS (32 KB)
+#ifndef NDNET_WQ_RT
+#define NDNET_WQ_RT 4096
+#endif
+#ifdef NDNET_WQ_WPE  // A/B: cap the registers (waves per SIMD) so other kernels' waves fit beside it
+#define NDNET_WQ_ATTR __attribute__((amdgpu_waves_per_eu(NDNET_WQ_WPE)))
+#else
+#define NDNET_WQ_ATTR
+#endif
+constexpr int kWqRt = NDNET_WQ_RT;           // reciprocals tabled in LDS at most (32 KB; larger counts compute theirs)
+// Entries of the table a run needs: the light quads' counts stay below the
+// heavy threshold, so 256 entries (2 KB) by default instead of 32 KB -- LDS
+// another stream's kernels can use beside k_welford_q (pipelined U +2 %,
+// profiles/r04_wq_lds.txt); counts past the table compute their reciprocal.
+__host__ __device__ inline uint32_t wq_rt_entries(uint32_t heavy_t) {
+#ifdef NDNET_WQ_RTFULL  // A/B: the whole table whatever the threshold (round 1-4 form)
+  return (uint32_t)kWqRt;
+#endif
+  return heavy_t < (uint32_t)kWqRt ? (heavy_t + 31u) & ~31u : (uint32_t)kWqRt;
+}
 constexpr int kWqHistMax = 64 * 1024;        // LDS class histograms up to this size, else global
 // Float input: a lane loads whole (x, y, z) records -- a quarter of its quad's
 // block, one dwordx3 each -- and the quad transposes them through LDS (lane j
@@ -1379,7 +1397,7 @@ __global__ void __launch_bounds__(64) k_debug_lu_chain(const double* A, uint32_t
 }
 
 template <typename T>
-__global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, int B, const T* __restrict__ nd_pts,
+__global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const CloudCtl* ctl, int B, const T* __restrict__ nd_pts,
                                                           const uint16_t* __restrict__ nd_lbl,
                                                           const uint32_t* __restrict__ nd_n,
                                                           const uint32_t* __restrict__ nd_base, double* nd_mean,
@@ -1394,12 +1412,13 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
   __shared__ double2 wq_hr[kWqThreads / 64][64];  // a heavy wave's block row of (rc, rl)
   static_assert(kHvLds * sizeof(double) <= 16 * kWqStageQ * sizeof(float), "heavy stage fits a wave's rows");
   static_assert((16 * kWqStageQ * sizeof(float)) % 16 == 0, "16-byte aligned heavy stage");
-  double* lrt = (double*)wq_smem;                                // [kWqRt] refined reciprocals of 1..kWqRt
+  const uint32_t rtn = wq_rt_entries(heavy_t);
+  double* lrt = (double*)wq_smem;                                // [rtn] refined reciprocals of 1..rtn
   const uint32_t bw = (uint32_t)((B + 1 + 3) & ~3);
-  uint32_t* pre = (uint32_t*)(wq_smem + kWqRt * sizeof(double));  // [B + 1] first light item of each cloud
+  uint32_t* pre = (uint32_t*)(wq_smem + rtn * sizeof(double));   // [B + 1] first light item of each cloud
   uint32_t* hpre = pre + bw;                                      // [B + 1] first heavy item of each cloud
   uint32_t* wq_hist = hpre + bw;                                  // labelled runs: [kWqNDs][ncls + 1]
-  for (uint32_t i = threadIdx.x; i < (uint32_t)kWqRt; i += kWqThreads) lrt[i] = recip_refined((double)(i + 1));
+  for (uint32_t i = threadIdx.x; i < rtn; i += kWqThreads) lrt[i] = recip_refined((double)(i + 1));
   // items: first the heavy NDs (>= kWqHeavy samples, listed by k_front /
   // k_bin_offsets), one per wave, so the longest work starts at once; then
   // (cloud, group of 16 NDs), in cloud order, whose heavy NDs are skipped.
@@ -1552,7 +1571,7 @@ __global__ void __launch_bounds__(kWqThreads) k_welford_q(const CloudCtl* ctl, i
   };
   // the block's reciprocals: broadcast LDS reads, computed past the table
   auto recips = [&](double (&cr)[kU], uint32_t q0) __attribute__((always_inline)) {
-    if (q0 + kU <= (uint32_t)kWqRt) {  // wave-uniform
+    if (q0 + kU <= rtn) {  // wave-uniform
 #pragma unroll
       for (int u = 0; u < kU; u++) cr[u] = lrt[q0 + u];
     } else {
@@ -3098,7 +3117,8 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
   }
 welford:
   P->lists_built = 0;
-  k_welford_q<T><<<P->wq_grid, kWqThreads, kWqRt * sizeof(double) + 8 * ((B + 1 + 3) & ~3) + (lbl ? P->wq_lds : 0),
+  k_welford_q<T><<<P->wq_grid, kWqThreads,
+                    wq_rt_entries(P->heavy_t) * sizeof(double) + 8 * ((B + 1 + 3) & ~3) + (lbl ? P->wq_lds : 0),
                     st>>>(
       P->ctl, B, (const T*)P->nd_pts, lbl ? P->nd_lbl : nullptr, P->nd_n, P->nd_base, P->nd_mean, P->nd_cov,
       P->nd_cls, P->hist, P->ncls, n, P->ndcap, P->wq_ctr, P->heavy, P->heavy_t, (const double2*)P->rtab,
