@@ -57,6 +57,10 @@ constexpr int kFrontR = NDNET_FRONT_R;  // bins per workgroup whose points stay 
 #ifndef NDNET_FRONT_LDSMATCH
 #define NDNET_FRONT_LDSMATCH 1  // the rank loop's low ND-id bits matched through LDS slots
 #endif
+#ifndef NDNET_FRONT_HEAVYSORT
+#define NDNET_FRONT_HEAVYSORT 1  // 0: heavy NDs in listing order (A/B)
+#endif
+constexpr int kHeavySort = 256;     // heavy NDs per cloud that k_front lists by descending count
 constexpr int kFrontTable = 8192;   // LDS words: byte map of a small grid (32768 voxels) or hash slots
 constexpr int kFrontPhases = 40;    // record slots per cloud and run
 constexpr int kRecWords = 16;       // per-workgroup record: [0] count, [1] any bad, [2..9] first bad per worker
@@ -272,6 +276,7 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
   __shared__ uint32_t scratch[32];
   __shared__ unsigned long long scratch64[16];
   __shared__ uint32_t s_heavy;  // workgroup 0: heavy NDs listed so far
+  __shared__ unsigned long long s_hkey[kHeavySort];  // workgroup 0: (~count, ND) of the first kHeavySort heavy NDs
   __shared__ uint32_t s_bad[kWorkers];
   // Workgroup -> (cloud, g).  Blocks are dealt round-robin over the 8 XCDs
   // (MI355X_MICROARCH.md, speed only: the barriers below hold whatever the
@@ -962,14 +967,28 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
         if (g == 0) {
           A.nd_n[(uint64_t)b * ndcap + d] = tot_d;
           A.nd_base[(uint64_t)b * ndcap + d] = start;
-          // k_welford_q gives these a wave each; their order does not matter
-          if (tot_d >= A.heavy_t) A.heavy[(uint64_t)b * ndcap + atomicAdd(&s_heavy, 1u)] = d;
+          // k_welford_q gives these a wave each (their order changes no result)
+          if (tot_d >= A.heavy_t) {
+            const uint32_t hi = atomicAdd(&s_heavy, 1u);
+            A.heavy[(uint64_t)b * ndcap + hi] = d;
+            if (hi < (uint32_t)kHeavySort) s_hkey[hi] = ((unsigned long long)~tot_d << 32) | d;
+          }
         }
         addv[d] = start + pre;  // a point's destination: addv[d] + hist[r][d] + its rank
       }
     }
     __syncthreads();
     if (g == 0 && t == 0) c.heavy_n = s_heavy;
+    if (NDNET_FRONT_HEAVYSORT && g == 0 && s_heavy > 1u && s_heavy <= (uint32_t)kHeavySort && t < s_heavy) {
+      // the cloud's heavy NDs by descending count: k_welford_q's first round
+      // gives item i to wave i % 4 of workgroup i / 4, so a cloud's longest
+      // NDs share a few workgroups (CUs) instead of each holding one CU to
+      // the end of the launch (profiles/r04_wq_heavy_order.txt)
+      const unsigned long long key = s_hkey[t];
+      uint32_t rank = 0;
+      for (uint32_t j = 0; j < s_heavy; j++) rank += s_hkey[j] < key ? 1u : 0u;
+      A.heavy[(uint64_t)b * ndcap + rank] = (uint32_t)key;
+    }
     FRONT_MARK(25);
     // ---- scatter: every point to its ND's run, in index order ----
     T* out = (T*)A.nd_pts + (uint64_t)b * n * 3;

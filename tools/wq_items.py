@@ -108,6 +108,14 @@ for r in range(a.reps):
             j = list(np.nonzero(hv)[0]).index(i)
             print(f"  heaviest: {cnt[i]:5d} samples, simd {simd[i]}, cu {cu_key[i]:4d}, cycles/sample {(t1[i] - t0[i]) / cnt[i]:.1f}, "
                   f"other waves on SIMD {share[j]:.2f}")
+        # CUs still holding a k_welford_q wave over time (a workgroup's CU is
+        # released when its last wave ends; items of one wave run back to back)
+        cu_end = {}
+        for ck, e in zip(cu_key, end_rt):
+            cu_end[int(ck)] = max(cu_end.get(int(ck), 0.0), float(e))
+        ends = np.array(sorted(cu_end.values()))
+        held = [(t_us, int((ends - start > t_us * 100).sum())) for t_us in (20, 30, 40, 50, 60)]
+        print("CUs still held after t us: " + ", ".join(f"{t}: {h}" for t, h in held))
         hc = np.sort(cnt[hv])[::-1][:5]
         print(f"heaviest heavy NDs: {list(hc)}; heaviest light group: {cnt[~hv].max() if (~hv).any() else 0}")
 _lib.lib().ndnet_ndt_set_timing(plan.handle, 0)
