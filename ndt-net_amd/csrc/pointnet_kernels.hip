@@ -595,7 +595,7 @@ __device__ __attribute__((always_inline)) inline void run_tiles_x6(f32x4 (&acc)[
 // One layer: RB row blocks x NB column blocks per wave; 4 / RB row groups x
 // 4 RB column groups of waves; N in chunks of (column groups x NB x 16).
 template <int RB, int NB>
-__device__ void plain_layer(const LayerCtx& C, int in, int pin, int out, int pout, float* gmax, int rows_valid,
+__device__ __attribute__((always_inline)) inline void plain_layer(const LayerCtx& C, int in, int pin, int out, int pout, float* gmax, int rows_valid,
                             bool out_planes, Pre pre = {}) {
   constexpr int WR = kRowBlocks / RB, WC = kWaves / WR, CB = WC * NB;
   const int lane = pn_tid() & 63, wave = pn_tid() >> 6;
@@ -638,7 +638,7 @@ __host__ __device__ inline int fbuf_floats(int qprec) {
 // (RB, NB) split), whose accumulators persist across the chunks: the N1-wide
 // activation never needs LDS of its own.  One barrier per chunk.
 template <int RB, int NB>
-__device__ void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin, int fbuf, int out, int pout,
+__device__ __attribute__((always_inline)) inline void fused_pair(const LayerCtx& P, const LayerCtx& Q, int in, int pin, int fbuf, int out, int pout,
                            float* gmax, int rows_valid, bool out_planes, Pre pre = {}) {
   constexpr int kFP = kFuseNC + kPadF;
   constexpr int WR = kRowBlocks / RB, WC = kWaves / WR;
