@@ -571,7 +571,7 @@ def main() -> None:
                     "algorithmic": f"{nbytes / 1e6:.2f} MB per launch: {what}", "ms": round(ms, 4),
                     "all_chains": chains_info}
         # HBM bytes per launch of that kernel from the committed rocprofv3 PMC
-        # passes (tools/pmc.sh -> tools/pmc_summary.py --json): FETCH_SIZE doubled
+        # passes (tools/gpu.sh pmc ndt -> tools/pmc_summary.py --json): FETCH_SIZE doubled
         # per MI355X_MICROARCH.md's gfx950 correction, plus WRITE_SIZE
         for kname, row in pmc.items():
             if kname != "_source" and roofline["kernel"].startswith(kname.split("<")[0]) and "hbm_bytes" in row:

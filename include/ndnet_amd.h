@@ -122,15 +122,30 @@ void ndnet_ndt_plan_destroy(void *plan);
  * cloud resident, so only where the plan's shape allows it), 0 = 2 where
  * allowed, else 1 (the default).  Both paths give identical results.
  * ndnet_ndt_get_path returns the path in use.
- * Concurrency: path 2's grid barrier assumes no other k_front grid competes
- * for the CUs at the same time (two partly resident grids wait for each
- * other until the ~2 s barrier timeout fails their clouds with
- * NDNET_ERR_SYNC).  Run at most one path-2 plan per device at a time, give
- * each of N path-2 plans that run concurrently front_share >= N
- * (ndnet_ndt_set_cu_share; ndnet.pipeline does so for its N NDT streams), or
- * select path 1 for them; the legacy entry points above always use path 1. */
+ * Concurrency: path 2's cloud barriers need every workgroup of a cloud
+ * resident at once, and two k_front grids that together want more workgroups
+ * than the chip holds could each hold part of the chip and wait on the other
+ * (until the ~2 s barrier timeout failed their clouds).  The library admits
+ * k_front launches itself: the chip is split into 4 front lanes, a plan's
+ * k_front occupies ceil(4 * workgroups / CUs) of them (4 at CU share 1, 2 at
+ * share 2), waits for the previous k_front of each of its lanes and records
+ * itself on them (HIP events; external event nodes when the stream is being
+ * captured, so graph replays are admitted the same way).  Any number of plans
+ * on any number of streams (or in graphs) on one device can therefore run
+ * concurrently; k_fronts whose lanes are disjoint (e.g. two share-2 plans) run
+ * side by side, the others in launch order.  (Processes sharing one GPU do not
+ * see each other's lanes.)  ndnet_ndt_get_front_lanes reports a plan's lanes
+ * (nlanes 0 on path 1). */
 int ndnet_ndt_set_path(void *plan, int path);
 int ndnet_ndt_get_path(void *plan);
+int ndnet_ndt_get_front_lanes(void *plan, int *lane0, int *nlanes);
+
+/* 1 if a k_front barrier of an earlier run of the plan timed out (a cloud
+ * failed with NDNET_ERR_SYNC) since the last call, else 0; clears the flag.
+ * k_front sets it in mapped host memory, so this reads it without
+ * synchronising: ndt_preprocessing raises on it at its next call (graph
+ * replays of ndnet.pipeline at theirs). */
+int ndnet_ndt_take_sync_failures(void *plan);
 
 /* CU shares of the plan's two widest kernels: k_front runs
  * CUs / (front_share * batch) workgroups per cloud and k_welford_q

@@ -98,6 +98,9 @@ struct FrontArgs {
   int staged;                   // 1: scatter through LDS records in ND order (float input; host checks the fit)
   int eval_all;                 // 1: count every bisection grid (debug / parity); 0: skip grids too small to matter
   uint64_t sync_ticks;          // cloud-barrier timeout in 100 MHz ticks (2e8 = 2 s; tests shorten it)
+  uint32_t* lu_done;            // [B][lu_gcap] k_welford_q's group counters, re-armed with the cloud
+  uint32_t lu_gcap;
+  uint32_t* sync_fail;          // mapped host word: set on a barrier timeout (ndnet_ndt_take_sync_failures), or null
 };
 
 // The shared bisection state of one workgroup (every workgroup of a cloud
@@ -978,7 +981,10 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
       }
     }
     __syncthreads();
-    if (g == 0 && t == 0) c.heavy_n = s_heavy;
+    if (g == 0 && t == 0) {
+      c.heavy_n = s_heavy;
+      c.heavy_t = A.heavy_t;
+    }
     if (NDNET_FRONT_HEAVYSORT && g == 0 && s_heavy > 1u && s_heavy <= (uint32_t)kHeavySort && t < s_heavy) {
       // the cloud's heavy NDs by descending count: k_welford_q's first round
       // gives item i to wave i % 4 of workgroup i / 4, so a cloud's longest
@@ -1084,14 +1090,18 @@ fail:
   if (t == 0) {
     c.state = kFailed;
     c.rc = kNdtErrSync;
+    // sticky, in host memory: the host raises it without synchronising
+    if (A.sync_fail) __hip_atomic_store(A.sync_fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 out:
   // The last workgroup of the cloud out (every one has passed its last
   // barrier poll) re-arms the cloud for the next run: barrier counter and
   // pass-sum slots zeroed, the epoch stored, the prune-list counters (set by
-  // the KL kernels, read by further prune levels) cleared.
+  // the KL kernels, read by further prune levels) and k_welford_q's group
+  // counters cleared (this run's k_welford_q follows in stream order).
   if (t == 0 && __hip_atomic_fetch_add(bar + 6, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1) {
     for (int i = 0; i < 7; i++) st_sc1(bar + i, 0u);
+    for (uint32_t i = 0; i < A.lu_gcap; i++) A.lu_done[(uint64_t)b * A.lu_gcap + i] = 0u;
     c.epoch = epoch;
     c.clear_stamps = clear_stamps ? 1u : 0u;
     c.num_valid = c.num_kl = c.num_phys = c.num_events = c.flag_count = 0;

@@ -27,6 +27,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
+#include <mutex>
 #include <type_traits>
 #include <vector>
 
@@ -97,6 +98,8 @@ struct CloudCtl {
                          // left shifts, ndt.c:69-72; always 0 on the global-memory prune path)
   uint32_t heavy_n;      // NDs of the accepted grid with >= kWqHeavy samples, listed in Plan::heavy
                          // (written by the binning of every run that accepts a grid)
+  uint32_t heavy_t;      // the threshold that list was built with: k_welford_q's light items skip
+                         // exactly the NDs it holds, whatever the plan's threshold is by then
 };
 
 struct Plan {
@@ -188,6 +191,12 @@ struct Plan {
   double* rtab;               // [n + 1][2] (rc, rl) per count for wq_heavy's divisions
   uint32_t* lu_done;          // [B][ceil(ndcap / 64)] k_welford_q's per-group completion counters (re-armed to 0)
   uint32_t heavy_t;           // NDs with >= heavy_t samples take wq_heavy (ndnet_ndt_set_heavy_threshold)
+  // k_front admission (front_gate): the device's front lanes this plan's
+  // k_front occupies, and the barrier-timeout flag k_front raises in host memory
+  int dev;                    // the device the plan lives on
+  int lane0, nlanes;          // lanes [lane0, lane0 + nlanes) mod kFrontLanes
+  uint32_t* sync_fail_h;      // pinned host word (mapped): nonzero after a k_front barrier timeout
+  uint32_t* sync_fail_d;      // its device address
 };
 
 // ------------------------------------------------------------------ helpers
@@ -280,9 +289,14 @@ __device__ inline void grid_from(const CloudCtl& c, double vs, uint32_t* len, do
 
 // ------------------------------------------------------------------ kernels
 
-__global__ void k_reset(CloudCtl* ctl, int B, uint32_t* bar) {
+__global__ void k_reset(CloudCtl* ctl, int B, uint32_t* bar, uint32_t* lu_done, uint32_t gcap) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
+  // k_welford_q's 64-ND group counters: re-armed by the wave that completes a
+  // group, and here at the start of every run (a run that failed half way
+  // cannot leave one non-zero)
+  if (lu_done)
+    for (uint32_t i = 0; i < gcap; i++) lu_done[(uint64_t)b * gcap + i] = 0;
   if (bar)  // k_front's cloud barrier counter and its two pass-sum slots (kBarStride)
     for (int i = 0; i < 6; i++) bar[(uint64_t)b * 16 + i] = 0;
   CloudCtl& c = ctl[b];
@@ -749,7 +763,10 @@ __global__ void __launch_bounds__(1024) k_bin_offsets(CloudCtl* ctl, uint32_t* c
     carry += tot;
   }
   __syncthreads();
-  if (threadIdx.x == 0) c.heavy_n = s_heavy;
+  if (threadIdx.x == 0) {
+    c.heavy_n = s_heavy;
+    c.heavy_t = heavy_t;
+  }
 }
 
 template <typename T>
@@ -1495,7 +1512,7 @@ __global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const Cl
   const uint32_t beg = nd_base[o];
   const uint32_t c0 = nd_n[o];
   // a light group's heavy NDs are done by their own items
-  const bool live = hv ? lane < 4 : (d < nd && c0 < heavy_t);
+  const bool live = hv ? lane < 4 : (d < nd && c0 < ctl[b].heavy_t);  // the heavy list's own threshold
   const uint32_t cnt = live ? c0 : 0u;
   const uint32_t last = cnt ? cnt - 1u : 0u;
   const uint32_t jj = j < 3 ? j : 0u;
@@ -2897,6 +2914,7 @@ static void plan_free(Plan* P) {
   if (P->kl_marks) (void)hipFree(P->kl_marks);
   if (P->wq_marks) (void)hipFree(P->wq_marks);
   if (P->fmarks) (void)hipFree(P->fmarks);
+  if (P->sync_fail_h) (void)hipHostFree(P->sync_fail_h);
   void* bufs[] = {P->flims, P->frec, P->fwgcnt, P->fbar, P->ctl, P->stamps, P->dense_of, P->vox, P->gbits, P->pkeys, P->did, P->bin_cnt, P->nd_base,
                   P->nd_pts, P->nd_lbl, P->nd_n,
                   P->nd_mean, P->nd_cov, P->nd_cov_post, P->nd_cls, P->hist, P->nb, P->keys, P->nkeys,
@@ -3038,6 +3056,72 @@ static int build_deferred_lists(Plan* P, hipStream_t st) {
 
 static size_t merge_lds_bytes(const Plan* P) { return 2 * (size_t)P->nchunk * kChunk * sizeof(unsigned long long); }
 
+// ---- k_front admission: the device's front lanes ----
+//
+// k_front's workgroups of a cloud meet at cloud barriers, so all of them must
+// be resident at once.  Two k_front grids that together want more workgroups
+// than the chip holds can each get part of their workgroups resident and then
+// wait on each other until the barrier timeout fails their clouds (measured:
+// 640 ms per step, profiles/r04_ndt_streams_guard.txt).  The library rules that
+// out itself, for any number of plans and streams, eager or captured in HIP
+// graphs: the chip is split into kFrontLanes lanes of CUs / kFrontLanes; a
+// plan's k_front occupies ceil(kFrontLanes * workgroups / CUs) of them (all four
+// at CU share 1, two at share 2); before its launch the stream waits for the
+// last k_front recorded on each of its lanes, and after it the launch is
+// recorded on them (one event per lane and device; external event nodes when
+// the stream is being captured, so a replayed graph waits for the k_front
+// launches before it, whatever stream they ran on).  So the k_front launches in
+// flight at any time never want more workgroups than there are CUs, and grids
+// on disjoint lanes (two share-2 plans: the pipeline's NDT streams) still run
+// concurrently.  The other kernels never wait on anything, so they drain.
+constexpr int kFrontLanes = 4;
+constexpr int kMaxDevices = 64;
+struct FrontLaneSet {
+  int init;
+  int next;  // the lane the next plan's lanes start at (round robin)
+  hipEvent_t ev[kFrontLanes];
+};
+static std::mutex g_lane_mu;
+static FrontLaneSet g_lanes[kMaxDevices];
+
+// Assigns the plan's lanes for its current k_front geometry (caller holds g_lane_mu).
+static hipError_t front_lanes_assign(Plan* P) {
+  if (P->dev < 0 || P->dev >= kMaxDevices) return hipErrorInvalidDevice;
+  FrontLaneSet& L = g_lanes[P->dev];
+  if (!L.init) {
+    for (int i = 0; i < kFrontLanes; i++) {
+      const hipError_t e = hipEventCreateWithFlags(&L.ev[i], hipEventDisableTiming);
+      if (e != hipSuccess) return e;
+    }
+    L.init = 1;
+  }
+  const uint64_t wgs = (uint64_t)P->fG * (uint64_t)P->B;
+  const int cus = P->cus > 0 ? P->cus : 1;
+  int nl = (int)((wgs * kFrontLanes + (uint64_t)cus - 1) / (uint64_t)cus);
+  nl = nl < 1 ? 1 : nl > kFrontLanes ? kFrontLanes : nl;
+  P->nlanes = nl;
+  P->lane0 = L.next;
+  L.next = (L.next + nl) % kFrontLanes;
+  return hipSuccess;
+}
+
+// Launches k_front between the lane waits and records (front_lanes_assign).
+template <typename T>
+static int front_launch(Plan* P, hipStream_t st, const T* pts, const FrontArgs& F) {
+  std::lock_guard<std::mutex> lk(g_lane_mu);  // waits, launch and records in one host order
+  FrontLaneSet& L = g_lanes[P->dev];
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  HIPCHK(hipStreamIsCapturing(st, &cs));
+  const bool cap = cs == hipStreamCaptureStatusActive;
+  for (int i = 0; i < P->nlanes; i++)
+    HIPCHK(hipStreamWaitEvent(st, L.ev[(P->lane0 + i) % kFrontLanes], cap ? hipEventWaitExternal : 0));
+  k_front<T><<<P->fG * P->B, kFrontThreads, P->flds, st>>>(pts, F);
+  HIPCHK(hipGetLastError());
+  for (int i = 0; i < P->nlanes; i++)
+    HIPCHK(hipEventRecordWithFlags(L.ev[(P->lane0 + i) % kFrontLanes], st, cap ? hipEventRecordExternal : 0));
+  return NDNET_OK;
+}
+
 template <typename T>
 static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, float* out, float* out_cls,
                     double* pc64, double* cov64, uint16_t* cls16, ndnet_ndt_stats* stats_dst) {
@@ -3048,7 +3132,7 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
   if (P->timing) HIPCHK(hipEventRecord(P->ev[0], st));
   P->lists_built = 0;
   // k_front re-arms its clouds itself (epoch, barrier words, list counters)
-  if (!P->front) k_reset<<<(B + 63) / 64, 64, 0, st>>>(P->ctl, B, nullptr);
+  if (!P->front) k_reset<<<(B + 63) / 64, 64, 0, st>>>(P->ctl, B, nullptr, P->lu_done, (P->ndcap + 63) / 64);
   P->calls++;
   if (P->front) {
     FrontArgs F;
@@ -3089,7 +3173,11 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
     F.nbins = P->nbins;
     F.xcd_local = (B % 8) == 0 ? 1 : 0;
     F.sync_ticks = P->front_sync_ticks;
-    k_front<T><<<P->fG * B, kFrontThreads, P->flds, st>>>(pts, F);
+    F.lu_done = P->lu_done;
+    F.lu_gcap = (P->ndcap + 63) / 64;
+    F.sync_fail = P->sync_fail_d;
+    const int frc = front_launch<T>(P, st, pts, F);
+    if (frc != NDNET_OK) return frc;
     if (P->timing)
       for (int e = 1; e <= 4; e++) HIPCHK(hipEventRecord(P->ev[e], st));
   } else {
@@ -3193,6 +3281,10 @@ hipError_t front_config(Plan* P, int share) {
   P->flds = lds;
   P->front_ok = e == hipSuccess && ok;
   P->cu_share = share;
+  if (e == hipSuccess && P->front_ok) {
+    std::lock_guard<std::mutex> lk(g_lane_mu);
+    e = front_lanes_assign(P);
+  }
   return e;
 }
 
@@ -3289,6 +3381,7 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
     if (e == hipSuccess) e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     P->cus = cus;
+    P->dev = dev;
     if (e == hipSuccess) e = front_config(P, 1);
     P->front = P->front_ok;
     const uint32_t G = P->fG;
@@ -3298,6 +3391,11 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
     A_(fbar, B * kBarStride);
   }
 #undef A_
+  if (e == hipSuccess) e = hipHostMalloc((void**)&P->sync_fail_h, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) {
+    *P->sync_fail_h = 0;
+    e = hipHostGetDevicePointer((void**)&P->sync_fail_d, P->sync_fail_h, 0);
+  }
   if (e == hipSuccess) e = hipMemset(P->ctl, 0, B * sizeof(CloudCtl));
   if (e == hipSuccess) e = hipMemset(P->fbar, 0, B * kBarStride * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(P->stamps, 0, B * P->vcap * sizeof(uint32_t));
@@ -3543,6 +3641,22 @@ int ndnet_ndt_debug_front_wg_marks(void* plan, unsigned long long* marks, int* G
   HIPCHK(hipMemcpy2D(marks, 2 * P->fG * sizeof(unsigned long long),
                      P->fmarks + 32, kFrontMarkStride * sizeof(unsigned long long),
                      2 * P->fG * sizeof(unsigned long long), P->B, hipMemcpyDeviceToHost));
+  return NDNET_OK;
+}
+
+int ndnet_ndt_take_sync_failures(void* plan) {
+  Plan* P = (Plan*)plan;
+  if (!P || !P->sync_fail_h) return NDNET_ERR_ARG;
+  const uint32_t v = __atomic_exchange_n(P->sync_fail_h, 0u, __ATOMIC_ACQ_REL);
+  return v ? 1 : 0;
+}
+
+int ndnet_ndt_get_front_lanes(void* plan, int* lane0, int* nlanes) {
+  Plan* P = (Plan*)plan;
+  if (!P || !lane0 || !nlanes) return NDNET_ERR_ARG;
+  std::lock_guard<std::mutex> lk(g_lane_mu);
+  *lane0 = P->lane0;
+  *nlanes = P->front ? P->nlanes : 0;
   return NDNET_OK;
 }
 

@@ -67,6 +67,8 @@ EXPORTS = {
     "ndnet_ndt_plan_destroy": (None, [_P]),
     "ndnet_ndt_set_path": (_I, [_P, _I]),
     "ndnet_ndt_get_path": (_I, [_P]),
+    "ndnet_ndt_get_front_lanes": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "ndnet_ndt_take_sync_failures": (_I, [_P]),
     "ndnet_ndt_set_cu_share": (_I, [_P, _I, _I]),
     "ndnet_ndt_set_exact_counts": (_I, [_P, _I]),
     "ndnet_ndt_set_front_staged": (_I, [_P, _I]),

@@ -75,6 +75,8 @@ class _Pinned:
         self._signature = lambda: pointnet_hip._signature(self.cache["tensors"])
 
     def check(self) -> None:
+        for plan in self.plans:  # a k_front barrier timeout of an earlier replay (no sync)
+            plan.raise_sync_failures()
         if self._signature() != self.sig:
             raise RuntimeError("the model's weights changed after the graph was captured: "
                                "build a new graph (the captured one replays the old fold)")

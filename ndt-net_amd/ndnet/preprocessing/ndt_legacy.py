@@ -90,7 +90,11 @@ class NDT_Sampler:
         return new_pcl, covs, new_cls
 
     def prune(self, new_desired_points: int):
-        """Prune the retained NDs further with the KL list of the first level."""
+        """Prune the retained NDs further with the KL list of the first level.
+
+        Returns ``(points [k,3] f64, covariances [k,9] f64, classes [k] i16)``:
+        the reference allocates the pruned classes as ``np.int16``
+        (ndt_legacy.py:211) where ``downsample`` uses ``np.uint16`` (:138)."""
         k = int(new_desired_points)
         core = _lib.lib()
         lx, ly, lz = self._grid()
@@ -104,7 +108,7 @@ class NDT_Sampler:
             raise RuntimeError(f"prune_nds failed with code {rc}")
         new_pcl = np.zeros((k, 3), dtype=np.float64)
         covs = np.zeros((k, 9), dtype=np.float64)
-        new_cls = np.zeros(k, dtype=np.uint16)
+        new_cls = np.zeros(k, dtype=np.int16)
         n_out = ctypes.c_ulong(0)
         rc2 = core.to_point_cloud(self.nd_array_ptr, lx, ly, lz, self.offset_x.contents.value,
                                   self.offset_y.contents.value, self.offset_z.contents.value,

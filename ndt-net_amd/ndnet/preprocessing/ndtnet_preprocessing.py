@@ -53,6 +53,7 @@ class NdtPlan:
         (include/ndnet_amd.h ndnet_ndt_set_run_part)."""
         assert points.is_contiguous() and points.dtype == torch.float32 and points.device == self.device
         assert out.is_contiguous() and out.shape == (self.batch, self.num_nds, 12)
+        self.raise_sync_failures()
         st = _lib.stream_ptr(self.device)
         _lib.check(_lib.lib().ndnet_ndt_set_run_part(self.handle, int(part)), "ndnet_ndt_set_run_part")
         rc = _lib.lib().ndnet_ndt_run(
@@ -111,6 +112,28 @@ class NdtPlan:
     def path(self) -> int:
         return int(_lib.lib().ndnet_ndt_get_path(self.handle))
 
+    @property
+    def front_lanes(self) -> Tuple[int, int]:
+        """(first lane, lane count) of the device's front lanes this plan's
+        k_front occupies (include/ndnet_amd.h ndnet_ndt_get_front_lanes;
+        count 0 on the one-launch-per-stage path)."""
+        l0, nl = ctypes.c_int(0), ctypes.c_int(0)
+        _lib.check(_lib.lib().ndnet_ndt_get_front_lanes(self.handle, ctypes.byref(l0), ctypes.byref(nl)),
+                   "ndnet_ndt_get_front_lanes")
+        return l0.value, nl.value
+
+    def raise_sync_failures(self) -> None:
+        """Raises ``NdtCloudError`` (rc -22) if a k_front cloud barrier of an
+        earlier run of this plan timed out -- read from mapped host memory,
+        without synchronising (include/ndnet_amd.h
+        ndnet_ndt_take_sync_failures).  Every ``run``, ``ndt_preprocessing``
+        call and pipeline replay checks it, whatever ``check`` says."""
+        rc = _lib.lib().ndnet_ndt_take_sync_failures(self.handle)
+        if rc < 0:
+            _lib.check(rc, "ndnet_ndt_take_sync_failures")
+        if rc:
+            raise NdtCloudError([_lib.NDNET_ERR_SYNC], sync=True)
+
     def prune(self, num_nds: int, out: torch.Tensor, out_classes: Optional[torch.Tensor] = None) -> None:
         st = _lib.stream_ptr(self.device)
         rc = _lib.lib().ndnet_ndt_prune(self.handle, st, num_nds, out.data_ptr(),
@@ -142,8 +165,12 @@ CHECK_RC = os.environ.get("NDNET_CHECK_RC", "0") == "1"
 class NdtCloudError(RuntimeError):
     """A cloud of the batch failed (``rcs``: per-cloud return codes)."""
 
-    def __init__(self, rcs):
+    def __init__(self, rcs, sync: bool = False):
         self.rcs = list(rcs)
+        if sync:
+            super().__init__("an earlier ndt_downsample run failed: a k_front cloud barrier timed out (rc -22, "
+                             "NDNET_ERR_SYNC); its clouds hold zero rows")
+            return
         bad = {b: rc for b, rc in enumerate(self.rcs) if rc != 0}
         super().__init__(f"ndt_downsample failed for clouds {bad} (rc -3: search hit 15 iterations, "
                          f"-1: grid above the voxel capacity, -22: front barrier timeout)")
@@ -153,6 +180,7 @@ def check_stats(plan: "NdtPlan") -> None:
     """Raises ``NdtCloudError`` if any cloud of the plan's last run failed
     (synchronises with the plan's stream)."""
     rcs = [s.rc for s in plan.host_stats()]
+    plan.raise_sync_failures()  # consumed here: the per-cloud codes below carry it
     if any(rc != 0 for rc in rcs):
         raise NdtCloudError(rcs)
 
@@ -182,7 +210,10 @@ def ndt_preprocessing(num_nds: int, points: torch.Tensor, classes: torch.Tensor 
     (default 2^22 voxels per cloud) fails the cloud with -1 where the
     reference would malloc it.  ``check=True`` (or ``NDNET_CHECK_RC=1``)
     synchronises and raises ``NdtCloudError`` instead; it is skipped while a
-    HIP graph is being captured.  Per-cloud codes: ``last_stats()``.
+    HIP graph is being captured.  Per-cloud codes: ``last_stats()``.  A
+    k_front barrier timeout (-22, no reference code) is never silent: it sets
+    a flag in host memory and the plan's next call raises ``NdtCloudError``
+    whatever ``check`` is (``NdtPlan.raise_sync_failures``).
     """
     _lib.require_gpu()
     src_device = points.device

@@ -92,7 +92,12 @@ def test_hip_forward_matches_torch_fp32(B, N):
     assert out.shape == (B, N, 29)
     assert (out - ref).abs().max().item() < TOL
     assert (out - emu).abs().max().item() < TOL
-    assert torch.equal(out.argmax(-1), ref.argmax(-1)) or (out.argmax(-1) != ref.argmax(-1)).float().mean() < 1e-3
+    # the predicted class agrees wherever the reference's top two classes are
+    # further apart than the two forwards can differ (a flip inside 2 TOL is a
+    # tie at fp32 rounding, which the abs bound above already covers)
+    top2 = ref.topk(2, dim=-1).values
+    clear = (top2[..., 0] - top2[..., 1]) > 2 * TOL
+    assert torch.equal(out.argmax(-1)[clear], ref.argmax(-1)[clear])
 
 
 @pytest.mark.gpu

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-kernel PMC summary from rocprofv3 --pmc passes (tools/pmc.sh).
+"""Per-kernel PMC summary from rocprofv3 --pmc passes (tools/gpu.sh pmc).
 
     python tools/pmc_summary.py gpurun_out/TAG [--json out.json]
 
