@@ -1364,13 +1364,9 @@ __device__ inline double ld_sc1_f64(const double* p) {
 // cloud whose list is deferred (lazy run, num_nds <= lazy_k) keeps only
 // which states have det != 0 and sgndet != 0 (chain_ok: all its event flags
 // read); k_kl_chains stores its states if the list is ever built.
-__device__ inline void wq_lu_group(const WqChainArgs& CA, int b, uint32_t u, uint32_t nd, uint32_t ndcap) {
-  if (u >= nd) return;
+__device__ inline void wq_lu_chain(const WqChainArgs& CA, int b, uint32_t u, uint32_t nd, uint32_t ndcap, double (&S)[9],
+                                   int nT) {
   const uint64_t ob = (uint64_t)b * ndcap;
-  double S[9];
-#pragma unroll
-  for (int q = 0; q < 9; q++) S[q] = ld_sc1_f64(&CA.cov_pre[9 * (ob + u) + q]);
-  const int nT = __popc(__hip_atomic_load(&CA.nkeys[ob + u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   const bool flags_only = CA.lazy_k && nd <= CA.lazy_k;  // a deferred cloud
   double* ch = CA.chain + ob * 108 + u;
   uint32_t* ps = CA.chain_ps + ob * 12 + u;
@@ -1390,6 +1386,16 @@ __device__ inline void wq_lu_group(const WqChainArgs& CA, int b, uint32_t u, uin
   if (flags_only) CA.chain_ok[ob + u] = okb;
 #pragma unroll
   for (int q = 0; q < 9; q++) CA.cov_post[9 * (ob + u) + q] = S[q];
+}
+
+__device__ inline void wq_lu_group(const WqChainArgs& CA, int b, uint32_t u, uint32_t nd, uint32_t ndcap) {
+  if (u >= nd) return;
+  const uint64_t ob = (uint64_t)b * ndcap;
+  double S[9];
+#pragma unroll
+  for (int q = 0; q < 9; q++) S[q] = ld_sc1_f64(&CA.cov_pre[9 * (ob + u) + q]);
+  const int nT = __popc(__hip_atomic_load(&CA.nkeys[ob + u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  wq_lu_chain(CA, b, u, nd, ndcap, S, nT);
 }
 
 // ndnet_debug_lu_chain: the device LU chain (lu3 + the event flags, as
@@ -1413,6 +1419,277 @@ __global__ void __launch_bounds__(64) k_debug_lu_chain(const double* A, uint32_t
   }
 }
 
+// ---- light NDs, one per lane (wq_light64, round 5) ----
+//
+// The lane-quad fold (one ND per quad, lane j = axis j) runs ~18 wave
+// instructions per sample for 16 NDs with only two independent dependency
+// chains per lane, ~9 cycles each: 227 cycles per sample (profiles/
+// r04_welford_ab.txt), and U's 16 x 1000 NDs filled every wave of the chip
+// for ~25 us (r04_wq_items_U.txt) -- while the FP64 work itself is ~5 us of
+// the chip.  Here a lane holds a whole ND (3 axes: three independent mean
+// recurrences, and the m2 / off-diagonal chains beside them), so a wave folds
+// 64 NDs, one 64-ND LU group, with ~33 FP64 instructions per sample and ILP
+// enough to issue them back to back: U needs 256 waves instead of 1008, the
+// persistent grid packs them four to a CU (items by workgroup), and the
+// other 192 CUs are free for another stream's kernels from the start.  The
+// group's LU chains (wq_lu_chain) run right after, from registers, in the
+// same wave -- no covariance hand-off through L2 and no group counter --
+// unless a heavy ND of the group is being folded by another wave; then the
+// round-4 protocol (sc1 stores, lu_done counter, the completing wave runs
+// wq_lu_group) applies.
+//
+// Per sample, in the reference's order (normal_distributions.c:75-103):
+//   t_j = x_j - mean_j;  mean_j += t_j / n;  u_j = x_j - mean_j;
+//   m2_j += t_j u_j;  off_jk += (u_j t_k) / n  (j < k: (0,1), (1,2), (0,2))
+// with t / n = fma(t, rc, t rl), (rc, rl) the per-count pair of Plan::rtab
+// (always the IEEE quotient: test_rtab_division_is_ieee), staged in LDS.  A
+// lane past its count folds x = mean (t = u = +0: an exact no-op, the sums
+// never being -0).  A lane whose coordinates leave the fast range (non-finite
+// floats; doubles outside [2^-300, 2^300]) refolds its ND with IEEE divisions
+// and the reference's per-step NaN -> 0 of the off-diagonal sums.
+#ifndef NDNET_WQ_LIGHT64
+#define NDNET_WQ_LIGHT64 1
+#endif
+constexpr uint32_t kWqLightNDs = NDNET_WQ_LIGHT64 ? 64u : 16u;  // NDs per light item (one wave)
+constexpr int kL64B = 8;                                      // samples per register block
+constexpr size_t kWqRtBytes = NDNET_WQ_LIGHT64 ? sizeof(double2) : sizeof(double);  // LDS table entry
+constexpr uint32_t kWqHistNDs = NDNET_WQ_LIGHT64 ? kWqThreads : kWqNDs;            // NDs of a workgroup at once
+
+template <typename T>
+struct L64Blk {
+  T v[kL64B][3];
+};
+
+template <typename T>
+__device__ __attribute__((always_inline)) inline void l64_load(L64Blk<T>& r, const T* __restrict__ src, uint32_t q0,
+                                                               uint32_t last) {
+#pragma unroll
+  for (int u = 0; u < kL64B; u++) {
+    const uint32_t q = q0 + (uint32_t)u < last ? q0 + (uint32_t)u : last;
+    const T* p = src + 3u * q;
+    r.v[u][0] = p[0];
+    r.v[u][1] = p[1];
+    r.v[u][2] = p[2];
+  }
+}
+
+// one block of kL64B samples of the lane's ND (kMask: some lane ends inside it)
+template <typename T, bool kMask>
+__device__ __attribute__((always_inline)) inline void l64_fold(const L64Blk<T>& r, const double2 (&rr)[kL64B],
+                                                               uint32_t q0, uint32_t cnt, double (&m)[3],
+                                                               double (&m2)[3], double (&of)[3], bool& bad) {
+#pragma unroll
+  for (int u = 0; u < kL64B; u++) {
+    const double rc = rr[u].x, rl = rr[u].y;
+    double x[3];
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      if constexpr (!std::is_same<T, float>::value) bad |= (q0 + (uint32_t)u < cnt) && !wq_in_range(r.v[u][a]);
+      x[a] = (double)r.v[u][a];
+    }
+    if constexpr (kMask) {
+      const unsigned long long lanes = __ballot(q0 + (uint32_t)u < cnt);
+#pragma unroll
+      for (int a = 0; a < 3; a++) x[a] = sel_d(lanes, x[a], m[a]);
+    }
+    double t[3], uu[3];
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      t[a] = x[a] - m[a];
+      m[a] = m[a] + fma(t[a], rc, t[a] * rl);
+      uu[a] = x[a] - m[a];
+      m2[a] = m2[a] + t[a] * uu[a];
+    }
+    const double p01 = uu[0] * t[1], p12 = uu[1] * t[2], p02 = uu[0] * t[2];
+    of[0] = of[0] + fma(p01, rc, p01 * rl);
+    of[1] = of[1] + fma(p12, rc, p12 * rl);
+    of[2] = of[2] + fma(p02, rc, p02 * rl);
+  }
+}
+
+template <typename T>
+__device__ __attribute__((always_inline)) inline void wq_light64(const CloudCtl* __restrict__ ctl, int b, uint32_t wd0,
+                                                     const T* __restrict__ nd_pts, const uint16_t* __restrict__ nd_lbl,
+                                                     const uint32_t* __restrict__ nd_n,
+                                                     const uint32_t* __restrict__ nd_base, double* nd_mean,
+                                                     double* nd_cov, uint16_t* nd_cls, uint32_t* hist_all, int ncls,
+                                                     uint64_t n, uint32_t ndcap, const double2* __restrict__ lrt2,
+                                                     uint32_t rtn, const double2* __restrict__ rtab,
+                                                     uint32_t* __restrict__ wq_hist, bool hist_lds,
+                                                     const WqChainArgs& CA, uint32_t lane) {
+  const uint32_t nd = ctl[b].num_nds, heavy_t = ctl[b].heavy_t;
+  const uint32_t d = wd0 + lane;
+  const bool inr = d < nd;
+  const uint64_t o = (uint64_t)b * ndcap + (inr ? d : wd0);
+  const uint32_t beg = nd_base[o], c0 = nd_n[o];
+  const bool live = inr && c0 < heavy_t;  // heavy NDs of the group are folded by their own items
+  const uint32_t cnt = live ? c0 : 0u;
+  const uint32_t last = cnt ? cnt - 1u : 0u;
+  const uint32_t mx = wave_max_u32(cnt);
+  const uint32_t full = wave_min_u32(live ? cnt : 0xffffffffu);  // blocks every live lane fills: no selects
+  const T* src = nd_pts + ((uint64_t)b * n + beg) * 3;
+  // the ND's neighbours (voxel.c:116-175: X+, X-, Y+, Y-, Z+, Z-), loaded behind the first point loads
+  int32_t nw[6];
+  uint32_t ncn[6];
+  {
+    const uint32_t lx = ctl[b].len[0], ly = ctl[b].len[1], lz = ctl[b].len[2];
+    const uint32_t lin = CA.vox[o];
+    const uint32_t zc = lin / (lx * ly), yc = (lin % (lx * ly)) / lx, xc = lin % lx;
+    const uint32_t* dense = CA.dense + (uint64_t)b * CA.vcap;
+    uint32_t dn[6];
+    bool in[6];
+#pragma unroll
+    for (int dd = 0; dd < 6; dd++) {
+      const uint32_t xx = xc + (dd == 0 ? 1u : dd == 1 ? ~0u : 0u);
+      const uint32_t yy = yc + (dd == 2 ? 1u : dd == 3 ? ~0u : 0u);
+      const uint32_t zz = zc + (dd == 4 ? 1u : dd == 5 ? ~0u : 0u);
+      in[dd] = xx < lx && yy < ly && zz < lz;
+      dn[dd] = dense[in[dd] ? zz * lx * ly + yy * lx + xx : lin];
+    }
+#pragma unroll
+    for (int dd = 0; dd < 6; dd++) {
+      nw[dd] = (in[dd] && dn[dd] != kInvalid) ? (int32_t)dn[dd] : -1;
+      ncn[dd] = nd_n[(uint64_t)b * ndcap + (nw[dd] >= 0 ? (uint32_t)nw[dd] : (uint32_t)(o - (uint64_t)b * ndcap))];
+    }
+  }
+  double m[3] = {0.0, 0.0, 0.0}, m2[3] = {0.0, 0.0, 0.0}, of[3] = {0.0, 0.0, 0.0};
+  bool bad = false;
+  // (rc, rl) of counts q0 + 1 .. q0 + kL64B: LDS broadcast reads, the global
+  // table past the LDS one (a threshold raised after the heavy list was built)
+  auto ldr = [&](double2 (&rr)[kL64B], uint32_t q0) __attribute__((always_inline)) {
+    const double2* tb = q0 + kL64B < rtn ? lrt2 : rtab;  // wave-uniform
+#pragma unroll
+    for (int u = 0; u < kL64B; u++) rr[u] = tb[q0 + (uint32_t)u + 1u];
+  };
+  // a ring of register blocks: kR - 1 blocks in flight while one is folded
+  constexpr int kR = std::is_same<T, float>::value ? 3 : 2;
+  L64Blk<T> rb[kR];
+#pragma unroll
+  for (int i = 0; i < kR; i++) l64_load(rb[i], src, (uint32_t)(i * kL64B), last);
+  double2 rr[kL64B];
+  ldr(rr, 0);
+  for (uint32_t q0 = 0; q0 < mx; q0 += kR * kL64B) {  // every branch below is wave-uniform
+#pragma unroll
+    for (int i = 0; i < kR; i++) {
+      const uint32_t qb = q0 + (uint32_t)(i * kL64B);
+      if (qb >= mx) break;
+      double2 cr[kL64B];
+#pragma unroll
+      for (int u = 0; u < kL64B; u++) cr[u] = rr[u];
+      if (qb + kL64B < mx) ldr(rr, qb + kL64B);
+      if (qb + kL64B <= full) l64_fold<T, false>(rb[i], cr, qb, cnt, m, m2, of, bad);
+      else l64_fold<T, true>(rb[i], cr, qb, cnt, m, m2, of, bad);
+      if (qb + kR * kL64B < mx) l64_load(rb[i], src, qb + kR * kL64B, last);
+    }
+  }
+  // float input: a non-finite coordinate leaves a non-finite mean
+  if constexpr (std::is_same<T, float>::value)
+    bad = live && !(fabs(m[0]) <= 0x1.fffffffffffffp+1023 && fabs(m[1]) <= 0x1.fffffffffffffp+1023 &&
+                    fabs(m[2]) <= 0x1.fffffffffffffp+1023);
+  bad = bad && live;
+  if (__any(bad) && bad) {  // the reference's exact steps (IEEE division, NaN -> 0 per off-diagonal step)
+#pragma unroll
+    for (int a = 0; a < 3; a++) m[a] = m2[a] = of[a] = 0.0;
+    for (uint32_t q = 0; q < cnt; q++) {
+      const double cn = (double)(q + 1u);
+      double t[3], uu[3];
+#pragma unroll
+      for (int a = 0; a < 3; a++) {
+        const double x = (double)src[3u * q + a];
+        t[a] = x - m[a];
+        m[a] = m[a] + t[a] / cn;
+        uu[a] = x - m[a];
+        m2[a] = m2[a] + t[a] * uu[a];
+      }
+      const double c01 = of[0] + (uu[0] * t[1]) / cn, c12 = of[1] + (uu[1] * t[2]) / cn,
+                   c02 = of[2] + (uu[0] * t[2]) / cn;
+      of[0] = c01 != c01 ? 0.0 : c01;
+      of[1] = c12 != c12 ? 0.0 : c12;
+      of[2] = c02 != c02 ? 0.0 : c02;
+    }
+  }
+  double S[9];
+  {
+    const double cn = (double)cnt;
+    double vd[3];
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      const double v = m2[a] / cn;
+      vd[a] = v != v ? 0.0 : v;
+    }
+    S[0] = vd[0];
+    S[4] = vd[1];
+    S[8] = vd[2];
+    S[1] = S[3] = of[0];
+    S[5] = S[7] = of[1];
+    S[2] = S[6] = of[2];
+  }
+  // the group's LU chains need every ND of the group: a heavy ND among them is
+  // folded by another wave, which then meets this one at the group counter
+  const bool grp_heavy = __any(inr && c0 >= heavy_t);
+  uint32_t el = 0;
+#pragma unroll
+  for (int dd = 0; dd < 6; dd++)
+    if (nw[dd] >= 0 && cnt > 1 && ncn[dd] > 1) el |= 1u << dd;
+  const uint32_t mask = chain_mask(el);
+  if (live) {
+#pragma unroll
+    for (int a = 0; a < 3; a++) nd_mean[3 * o + a] = m[a];
+#pragma unroll
+    for (int q = 0; q < 9; q++) st_sc1_f64(&nd_cov[9 * o + q], S[q]);
+#pragma unroll
+    for (int dd = 0; dd < 6; dd++) CA.nb[6 * o + dd] = nw[dd];
+    __hip_atomic_store(&CA.nkeys[o], mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // labelled runs: the ND's class histogram (first index of the max, normal_distributions.c:107-121)
+  if (nd_lbl) {
+    const uint32_t nbins = (uint32_t)ncls + 1u;
+    const uint16_t* l = nd_lbl + (uint64_t)b * n + beg;
+    uint32_t* hist = hist_lds ? wq_hist + (threadIdx.x & (kWqThreads - 1)) * nbins : hist_all + o * nbins;
+    if (live) {
+      for (uint32_t k = 0; k < nbins; k++) hist[k] = 0;
+      if (hist_lds) {
+        for (uint32_t s = 0; s < cnt; s++)
+          if (l[s] < nbins) atomicAdd(&hist[l[s]], 1u);  // return-less LDS adds: no read-modify-write wait
+        __builtin_amdgcn_s_waitcnt(0xc07f);            // lgkmcnt(0)
+      } else {
+        for (uint32_t s = 0; s < cnt; s++)
+          if (l[s] < nbins) hist[l[s]]++;
+      }
+      uint32_t best = 0;
+      uint16_t cls = 0;
+      for (uint32_t k = 0; k < nbins; k++) {
+        const uint32_t h = hist[k];
+        if (h > best) {
+          best = h;
+          cls = (uint16_t)k;
+        }
+      }
+      nd_cls[o] = cls;
+    }
+  } else if (live) {
+    nd_cls[o] = 0;
+  }
+  if (!grp_heavy) {
+    if (live) wq_lu_chain(CA, b, d, nd, ndcap, S, __popc(mask));
+    return;
+  }
+  const uint32_t nlive = (uint32_t)__popcll(__ballot(live));
+  if (nlive) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores are done
+    const uint32_t g = wd0 / 64u, gcap = (ndcap + 63u) / 64u;
+    const uint32_t total = nd - 64u * g < 64u ? nd - 64u * g : 64u;
+    uint32_t* gc = CA.lu_done + (uint64_t)b * gcap + g;
+    uint32_t old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(gc, nlive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old + nlive == total) {
+      if (lane == 0) __hip_atomic_store(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+      wq_lu_group(CA, b, 64u * g + lane, nd, ndcap);
+    }
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const CloudCtl* ctl, int B, const T* __restrict__ nd_pts,
                                                           const uint16_t* __restrict__ nd_lbl,
@@ -1430,12 +1707,18 @@ __global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const Cl
   static_assert(kHvLds * sizeof(double) <= 16 * kWqStageQ * sizeof(float), "heavy stage fits a wave's rows");
   static_assert((16 * kWqStageQ * sizeof(float)) % 16 == 0, "16-byte aligned heavy stage");
   const uint32_t rtn = wq_rt_entries(heavy_t);
-  double* lrt = (double*)wq_smem;                                // [rtn] refined reciprocals of 1..rtn
+  double* lrt = (double*)wq_smem;                                // quads: [rtn] refined reciprocals of 1..rtn
+  double2* lrt2 = (double2*)wq_smem;                             // light64: [rtn] (rc, rl) of counts 0..rtn - 1
   const uint32_t bw = (uint32_t)((B + 1 + 3) & ~3);
-  uint32_t* pre = (uint32_t*)(wq_smem + rtn * sizeof(double));   // [B + 1] first light item of each cloud
+  uint32_t* pre = (uint32_t*)(wq_smem + rtn * kWqRtBytes);       // [B + 1] first light item of each cloud
   uint32_t* hpre = pre + bw;                                      // [B + 1] first heavy item of each cloud
-  uint32_t* wq_hist = hpre + bw;                                  // labelled runs: [kWqNDs][ncls + 1]
-  for (uint32_t i = threadIdx.x; i < rtn; i += kWqThreads) lrt[i] = recip_refined((double)(i + 1));
+  uint32_t* wq_hist = hpre + bw;                                  // labelled runs: [kWqHistNDs][ncls + 1]
+  if constexpr (NDNET_WQ_LIGHT64) {
+    const uint32_t rte = rtn < n + 1 ? rtn : (uint32_t)(n + 1);  // rtab holds counts 0..n
+    for (uint32_t i = threadIdx.x; i < rte; i += kWqThreads) lrt2[i] = rtab[i];
+  } else {
+    for (uint32_t i = threadIdx.x; i < rtn; i += kWqThreads) lrt[i] = recip_refined((double)(i + 1));
+  }
   // items: first the heavy NDs (>= kWqHeavy samples, listed by k_front /
   // k_bin_offsets), one per wave, so the longest work starts at once; then
   // (cloud, group of 16 NDs), in cloud order, whose heavy NDs are skipped.
@@ -1443,7 +1726,7 @@ __global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const Cl
   // per SIMD), so no SIMD holds two ND groups while another idles.
   for (int i = threadIdx.x; i < B; i += kWqThreads) {
     const bool acc = ctl[i].state == kAccepted;
-    pre[i + 1] = acc ? (ctl[i].num_nds + 15u) / 16u : 0u;
+    pre[i + 1] = acc ? (ctl[i].num_nds + kWqLightNDs - 1u) / kWqLightNDs : 0u;
     hpre[i + 1] = acc ? ctl[i].heavy_n : 0u;
   }
   __syncthreads();
@@ -1504,6 +1787,24 @@ __global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const Cl
     else hi = mid - 1;
   }
   const int b = lo;
+  if (NDNET_WQ_LIGHT64 && !hv) {  // 64 NDs, one per lane
+    wq_light64<T>(ctl, b, (li - pre[b]) * kWqLightNDs, nd_pts, nd_lbl, nd_n, nd_base, nd_mean, nd_cov, nd_cls,
+                  hist_all, ncls, n, ndcap, lrt2, rtn, rtab, wq_hist,
+                  (size_t)kWqHistNDs * ((uint32_t)ncls + 1u) * sizeof(uint32_t) <= (size_t)kWqHistMax, CA, lane);
+    if (wq_marks && lane == 0) {
+      unsigned long long* w = wq_marks + (uint64_t)item * kWqMarkW;
+      const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+      w[0] = mk_rt;
+      w[1] = mk_t0;
+      w[2] = t2;
+      w[3] = t2;
+      const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+      const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;
+      w[4] = ((unsigned long long)xcc << 56) | hwid;
+      w[5] = w[6] = w[7] = 0;
+    }
+    continue;
+  }
   const uint32_t nd = ctl[b].num_nds;
   // heavy: quad 0 holds the ND, the other quads idle; light: 16 NDs
   const uint32_t wd0 = hv ? heavy[(uint64_t)b * ndcap + (li - hpre[b])] : (li - pre[b]) * 16u;
@@ -1754,8 +2055,9 @@ __global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const Cl
     double* hl = reinterpret_cast<double*>(&wq_stage[wave * 16][0]);
     if (wq_marks) wq_heavy<T, true>(rec, hc, rtab, hl, wq_hr[wave], lane, mean, m2, off, bad, ph);
     else wq_heavy<T>(rec, hc, rtab, hl, wq_hr[wave], lane, mean, m2, off, bad);
-  } else
+  } else if constexpr (!NDNET_WQ_LIGHT64) {  // (light64: light items never reach this point)
     run(mx, true, std::false_type{});
+  }
   if (wq_marks) mk_t1 = __builtin_amdgcn_s_memtime();
   // float input: every finite coordinate is in div_fast's exact range, and a
   // non-finite one makes the running mean non-finite from then on (x - mean
@@ -1803,7 +2105,7 @@ __global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const Cl
     if (live && j == 0) __hip_atomic_store(&CA.nkeys[o], chain_mask(el), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   const uint32_t nbins = (uint32_t)ncls + 1u;
-  const bool hist_lds = (size_t)kWqNDs * nbins * sizeof(uint32_t) <= (size_t)kWqHistMax;
+  const bool hist_lds = (size_t)kWqHistNDs * nbins * sizeof(uint32_t) <= (size_t)kWqHistMax;
   if (live && nd_lbl && hist_lds) {
     // the whole quad counts: lane j takes the 8-label runs j, j + 4, ... of
     // each 128-label round (the quad reads 256 contiguous bytes per round, 32
@@ -3206,7 +3508,7 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
 welford:
   P->lists_built = 0;
   k_welford_q<T><<<P->wq_grid, kWqThreads,
-                    wq_rt_entries(P->heavy_t) * sizeof(double) + 8 * ((B + 1 + 3) & ~3) + (lbl ? P->wq_lds : 0),
+                    wq_rt_entries(P->heavy_t) * kWqRtBytes + 8 * ((B + 1 + 3) & ~3) + (lbl ? P->wq_lds : 0),
                     st>>>(
       P->ctl, B, (const T*)P->nd_pts, lbl ? P->nd_lbl : nullptr, P->nd_n, P->nd_base, P->nd_mean, P->nd_cov,
       P->nd_cls, P->hist, P->ncls, n, P->ndcap, P->wq_ctr, P->heavy, P->heavy_t, (const double2*)P->rtab,
@@ -3413,7 +3715,7 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
     e = hipMemcpy(P->rtab, rt.data(), rt.size() * sizeof(double), hipMemcpyHostToDevice);
   }
   {
-    const size_t hb = (size_t)kWqNDs * (size_t)nb * sizeof(uint32_t);
+    const size_t hb = (size_t)kWqHistNDs * (size_t)nb * sizeof(uint32_t);
     P->wq_lds = num_classes >= 0 && hb <= (size_t)kWqHistMax ? hb : 0;
     int dv = 0, ncu = 0;
     if (e == hipSuccess) e = hipGetDevice(&dv);
@@ -3428,10 +3730,10 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   }
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_welford_q<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(kWqRt * sizeof(double) + 8 * ((batch + 1 + 3) & ~3) + kWqHistMax));
+                            (int)(kWqRt * kWqRtBytes + 8 * ((batch + 1 + 3) & ~3) + kWqHistMax));
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_welford_q<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(kWqRt * sizeof(double) + 8 * ((batch + 1 + 3) & ~3) + kWqHistMax));
+                            (int)(kWqRt * kWqRtBytes + 8 * ((batch + 1 + 3) & ~3) + kWqHistMax));
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_kl_merge<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(2 * kMergeLdsChunks * kChunk * sizeof(unsigned long long)));

@@ -518,7 +518,7 @@ __device__ __attribute__((always_inline)) inline void mma_kgroup_x6(f32x4 (&acc)
 // run_tiles for split-bf16 layers: 32-row k-groups; A from the three planes
 // (abase: this lane's row / k offset in plane 0, in bf16), B three 1 KB
 // fragment pieces per column block, prefetched kDepth6 steps ahead.
-template <int RB, int NB, class Epi>
+template <int RB, int NB, class Epi, int kD = kDepth6>
 __device__ __attribute__((always_inline)) inline void run_tiles_x6(f32x4 (&acc)[RB][NB],
                                                                    const bf16x8* __restrict__ w, int KG, int kg0,
                                                                    int nkg, int cb0, int cbs, int nchunk,
@@ -569,9 +569,9 @@ __device__ __attribute__((always_inline)) inline void run_tiles_x6(f32x4 (&acc)[
       if (++c == nchunk) c = 0;
     }
   };
-  bf16x8 bq[kDepth6][NB][3];
+  bf16x8 bq[kD][NB][3];
 #pragma unroll
-  for (int i = 0; i < kDepth6; i++) {
+  for (int i = 0; i < kD; i++) {
     if (NB == 1 && i == 0 && pre.on) {  // the first step, prefetched by the caller
       bq[0][0][0] = __builtin_bit_cast(bf16x8, pre.r0);
       bq[0][0][1] = __builtin_bit_cast(bf16x8, pre.r1);
@@ -581,12 +581,12 @@ __device__ __attribute__((always_inline)) inline void run_tiles_x6(f32x4 (&acc)[
       load(bq[i]);
     }
   }
-  for (int t = 0; t < T; t += kDepth6) {
+  for (int t = 0; t < T; t += kD) {
 #pragma unroll
-    for (int i = 0; i < kDepth6; i++) {
+    for (int i = 0; i < kD; i++) {
       if (t + i < T) {
         step(bq[i]);
-        load(bq[i]);
+        if (t + i + kD < T) load(bq[i]);  // no reload past the last step
       }
     }
   }
@@ -618,8 +618,16 @@ __device__ __attribute__((always_inline)) inline void plain_layer(const LayerCtx
   if (C.prec) {  // input: three bf16 planes of pitch K + kPadB (the producer's N + kPadB)
     const int pb = 32 * C.KG + kPadB;
     const __bf16* abase6 = reinterpret_cast<const __bf16*>(g_smem + in) + (row0 + cl) * pb + 8 * kq;
-    run_tiles_x6<RB, NB>(acc, C.w6, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase6, pb, epi, pre,
-                              kChunkRot ? (int)((blockIdx.x + blockIdx.y) % nchunk) : 0);
+#ifndef NDNET_PN_SHORT_D2
+#define NDNET_PN_SHORT_D2 1
+#endif
+    // a layer of two k-group steps (K = 64, one chunk: the narrow 64 -> 64 /
+    // 64 -> 128 layers) loads both up front, so only one L2 latency is exposed
+    if (NDNET_PN_SHORT_D2 && nchunk * C.KG == 2)
+      run_tiles_x6<RB, NB, decltype(epi), 2>(acc, C.w6, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase6, pb, epi, pre, 0);
+    else
+      run_tiles_x6<RB, NB>(acc, C.w6, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase6, pb, epi, pre,
+                           kChunkRot ? (int)((blockIdx.x + blockIdx.y) % nchunk) : 0);
   } else {
     const float* abase = g_smem + in + (row0 + cl) * pin + 4 * kq;
     run_tiles<RB, NB>(acc, C.w, C.KG, 0, C.KG, wc * NB, CB, nchunk, abase, pin, epi, pre);
@@ -691,6 +699,78 @@ __device__ __attribute__((always_inline)) inline void fused_pair(const LayerCtx&
   if (gmax) pool_cols<RB, NB>(acc2, Q.bias, 16 * qwc * NB, Q.relu, qrow0, rows_valid, gmax);
   else if (out_planes) store_cols_planes<RB, NB>(acc2, Q.bias, 16 * qwc * NB, Q.relu, qrow0, out, Q.N + kPadB, 16 * qwc * NB);
   else store_cols<RB, NB>(acc2, Q.bias, 16 * qwc * NB, Q.relu, qrow0, out, pout, 16 * qwc * NB);
+}
+
+// The fused pair with both layers split-bf16 and P's K = 64 (the seg head's
+// 64 -> 512 -> 256, ndtnet.py:233-234), software-pipelined across chunks.
+// fused_pair loads each chunk's weights at the start of the chunk's GEMM, so
+// every chunk exposes the L2 latency of P's and Q's first steps -- with all 16
+// waves in lockstep between the chunk barriers, nothing covers it (chain D's
+// pair ran at ~0.42 of the issued peak against ~0.55 for the plain x6 layers,
+// profiles/r04_chain_vgpr_ab.txt).  Here a chunk's weights (P: 2 k-groups, Q:
+// 2 k-groups, 3 planes each: 48 VGPRs) are loaded one chunk ahead, right after
+// the previous chunk's MFMAs consumed the registers, so each load has a whole
+// phase and a barrier to arrive.  Same products, same accumulation order.
+template <int RB>
+__device__ __attribute__((always_inline)) inline void fused_pair_x6p(const LayerCtx& P, const LayerCtx& Q, int in,
+                                                                     int fbuf, int out, int pout, float* gmax,
+                                                                     int rows_valid, bool out_planes) {
+  constexpr int WR = kRowBlocks / RB, WC = kWaves / WR;  // Q: NB = 1
+  constexpr int PWC = kWaves / kRowBlocks;                // P: 4 column groups of one block
+  static_assert(PWC == 4 && kFuseNC == 64, "16 waves, 64-column chunks");
+  const int lane = pn_tid() & 63, wave = pn_tid() >> 6;
+  const int kq = lane >> 4, cl = lane & 15;
+  const int prow0 = (wave / PWC) * 16, pwc = wave % PWC;
+  const int pinb = 32 * P.KG + kPadB;  // P.KG == 2
+  const __bf16* ain6 = reinterpret_cast<const __bf16*>(g_smem + in) + (prow0 + cl) * pinb + 8 * kq;
+  const int qrow0 = (wave / WC) * RB * 16, qwc = wave % WC;
+  const int nf = P.N / kFuseNC;
+  const int fbsz = fbuf_floats(1) / 2;
+  constexpr int fpb = kFuseNC + kPadB;
+  // chunk f's weights: P column block 4 f + pwc, k-groups 0, 1; Q column block qwc, k-groups 2 f, 2 f + 1
+  bf16x8 wp[2][1][3], wq[2][1][3];
+  auto load_p = [&](int f) {
+    const bf16x8* s = P.w6 + ((int64_t)(4 * f + pwc) * P.KG) * 3 * 64;
+#pragma unroll
+    for (int k = 0; k < 2; k++)
+#pragma unroll
+      for (int p = 0; p < 3; p++) wp[k][0][p] = s[(k * 3 + p) * 64];
+  };
+  auto load_q = [&](int f) {
+    const bf16x8* s = Q.w6 + ((int64_t)qwc * Q.KG + 2 * f) * 3 * 64;
+#pragma unroll
+    for (int k = 0; k < 2; k++)
+#pragma unroll
+      for (int p = 0; p < 3; p++) wq[k][0][p] = s[(k * 3 + p) * 64];
+  };
+  auto p_chunk = [&](int f) {
+    f32x4 acc1[1][1];
+    zero_acc(acc1);
+#pragma unroll
+    for (int k = 0; k < 2; k++) mma_kgroup_x6<1, 1>(acc1, ain6 + 32 * k, kP * pinb, 16 * pinb, wp[k]);
+    store_cols_planes<1, 1>(acc1, P.bias, 64 * f + 16 * pwc, P.relu, prow0, fbuf + (f & 1) * fbsz, fpb, 16 * pwc);
+  };
+  f32x4 acc2[RB][1];
+  zero_acc(acc2);
+  load_p(0);
+  load_q(0);
+  p_chunk(0);
+  if (nf > 1) load_p(1);
+  __syncthreads();
+  for (int f = 0; f < nf; f++) {
+    const __bf16* af6 = reinterpret_cast<const __bf16*>(g_smem + fbuf + (f & 1) * fbsz) + (qrow0 + cl) * fpb + 8 * kq;
+#pragma unroll
+    for (int k = 0; k < 2; k++) mma_kgroup_x6<RB, 1>(acc2, af6 + 32 * k, kP * fpb, 16 * fpb, wq[k]);
+    if (f + 1 < nf) {
+      load_q(f + 1);
+      p_chunk(f + 1);
+      if (f + 2 < nf) load_p(f + 2);
+    }
+    __syncthreads();
+  }
+  if (gmax) pool_cols<RB, 1>(acc2, Q.bias, 16 * qwc, Q.relu, qrow0, rows_valid, gmax);
+  else if (out_planes) store_cols_planes<RB, 1>(acc2, Q.bias, 16 * qwc, Q.relu, qrow0, out, Q.N + kPadB, 16 * qwc);
+  else store_cols<RB, 1>(acc2, Q.bias, 16 * qwc, Q.relu, qrow0, out, pout, 16 * qwc);
 }
 
 // Loads the first weight step this wave runs in layer l (the 16-wave 64-point
@@ -1006,7 +1086,12 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
         if (Q.N == 256) fused_pair<2, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op);
         else fused_pair<1, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op);
       } else {
-        if (Q.N == 256) fused_pair<4, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op, pre);
+#ifndef NDNET_PN_FUSED_PIPE
+#define NDNET_PN_FUSED_PIPE 1
+#endif
+        if (NDNET_PN_FUSED_PIPE && kWaves == 16 && Q.N == 256 && P.prec && Q.prec && P.KG == 2)
+          fused_pair_x6p<4>(P, Q, in, fbuf, out, pout, gm, rows_valid, op);
+        else if (Q.N == 256) fused_pair<4, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op, pre);
         else if (Q.N > 64) fused_pair<2, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op, pre);
         else fused_pair<1, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op, pre);
       }
