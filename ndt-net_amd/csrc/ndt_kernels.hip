@@ -1516,7 +1516,8 @@ __device__ __attribute__((always_inline)) inline void wq_light64(const CloudCtl*
                                                      uint64_t n, uint32_t ndcap, const double2* __restrict__ lrt2,
                                                      uint32_t rtn, const double2* __restrict__ rtab,
                                                      uint32_t* __restrict__ wq_hist, bool hist_lds,
-                                                     const WqChainArgs& CA, uint32_t lane) {
+                                                     const WqChainArgs& CA, uint32_t lane,
+                                                     unsigned long long& t_mom, uint32_t& mx_out) {
   const uint32_t nd = ctl[b].num_nds, heavy_t = ctl[b].heavy_t;
   const uint32_t d = wd0 + lane;
   const bool inr = d < nd;
@@ -1582,6 +1583,8 @@ __device__ __attribute__((always_inline)) inline void wq_light64(const CloudCtl*
       if (qb + kR * kL64B < mx) l64_load(rb[i], src, qb + kR * kL64B, last);
     }
   }
+  t_mom = __builtin_amdgcn_s_memtime();  // timing level 2: the moments are done
+  mx_out = mx;
   // float input: a non-finite coordinate leaves a non-finite mean
   if constexpr (std::is_same<T, float>::value)
     bad = live && !(fabs(m[0]) <= 0x1.fffffffffffffp+1023 && fabs(m[1]) <= 0x1.fffffffffffffp+1023 &&
@@ -1788,19 +1791,21 @@ __global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const Cl
   }
   const int b = lo;
   if (NDNET_WQ_LIGHT64 && !hv) {  // 64 NDs, one per lane
+    unsigned long long t_mom = 0;
+    uint32_t lmx = 0;
     wq_light64<T>(ctl, b, (li - pre[b]) * kWqLightNDs, nd_pts, nd_lbl, nd_n, nd_base, nd_mean, nd_cov, nd_cls,
                   hist_all, ncls, n, ndcap, lrt2, rtn, rtab, wq_hist,
-                  (size_t)kWqHistNDs * ((uint32_t)ncls + 1u) * sizeof(uint32_t) <= (size_t)kWqHistMax, CA, lane);
+                  (size_t)kWqHistNDs * ((uint32_t)ncls + 1u) * sizeof(uint32_t) <= (size_t)kWqHistMax, CA, lane,
+                  t_mom, lmx);
     if (wq_marks && lane == 0) {
       unsigned long long* w = wq_marks + (uint64_t)item * kWqMarkW;
-      const unsigned long long t2 = __builtin_amdgcn_s_memtime();
       w[0] = mk_rt;
       w[1] = mk_t0;
-      w[2] = t2;
-      w[3] = t2;
+      w[2] = t_mom;
+      w[3] = __builtin_amdgcn_s_memtime();
       const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
       const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;
-      w[4] = ((unsigned long long)xcc << 56) | hwid;
+      w[4] = ((unsigned long long)xcc << 56) | ((unsigned long long)(lmx & 0xFFFFFFu) << 32) | hwid;
       w[5] = w[6] = w[7] = 0;
     }
     continue;

@@ -1089,9 +1089,15 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
 #ifndef NDNET_PN_FUSED_PIPE
 #define NDNET_PN_FUSED_PIPE 1
 #endif
-        if (NDNET_PN_FUSED_PIPE && kWaves == 16 && Q.N == 256 && P.prec && Q.prec && P.KG == 2)
-          fused_pair_x6p<4>(P, Q, in, fbuf, out, pout, gm, rows_valid, op);
-        else if (Q.N == 256) fused_pair<4, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op, pre);
+        bool piped = false;
+        if constexpr (kWaves == 16) {
+          if (NDNET_PN_FUSED_PIPE && Q.N == 256 && P.prec && Q.prec && P.KG == 2) {
+            fused_pair_x6p<4>(P, Q, in, fbuf, out, pout, gm, rows_valid, op);
+            piped = true;
+          }
+        }
+        if (piped) {
+        } else if (Q.N == 256) fused_pair<4, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op, pre);
         else if (Q.N > 64) fused_pair<2, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op, pre);
         else fused_pair<1, kQ>(P, Q, in, pin, fbuf, out, pout, gm, rows_valid, op, pre);
       }

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Per-item timing inside k_welford_q (timing level 2 stamps): heavy items
-(a whole wave per long ND, wq_heavy) and light items (16 NDs on lane quads),
+(a whole wave per long ND, wq_heavy) and light items (64 NDs one per lane,
+wq_light64; --light-nds 16 for a build with the round-4 lane quads),
 cycles per sample of each, the epilogue (neighbours, LU chain, classes), and
 which items end last.
 
@@ -28,6 +29,7 @@ ap.add_argument("--nds", type=int, default=1000)
 ap.add_argument("--kind", default="L")
 ap.add_argument("--heavy", type=int, default=256)
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--light-nds", type=int, default=64)
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 B, n, k = a.batch, a.points, a.nds
@@ -37,7 +39,7 @@ plan.set_heavy_threshold(a.heavy)
 out = torch.empty((B, k, 12), dtype=torch.float32, device=dev)
 plan.run(pts, None, out, None)
 _lib.check(_lib.lib().ndnet_ndt_set_timing(plan.handle, 2), "set_timing")
-cap = B * (int(1.2 * k) + 1 + (int(1.2 * k) + 1 + 15) // 16)
+cap = B * (int(1.2 * k) + 1 + (int(1.2 * k) + 1 + 15) // 16)  # the plan's item capacity (16-ND quads' bound)
 m = np.zeros(cap * 8, np.uint64)
 items = ctypes.c_uint32(0)
 per_sample_h, per_sample_l, epi_h, epi_l, spans, phases = [], [], [], [], [], []
@@ -45,7 +47,8 @@ for r in range(a.reps):
     plan.run(pts, None, out, None)
     torch.cuda.synchronize()
     st = plan.host_stats()
-    light = sum((s.num_nds + 15) // 16 for s in st if s.rc == 0 or s.num_nds)
+    L = a.light_nds
+    light = sum((s.num_nds + L - 1) // L for s in st if s.rc == 0 or s.num_nds)
     _lib.check(_lib.lib().ndnet_ndt_debug_wq_marks(plan.handle, m.ctypes.data, ctypes.byref(items)), "wq_marks")
     w = m.reshape(-1, 8)
     heavy = int((w[:, 4] >> np.uint64(63)).astype(bool)[: cap].sum())
