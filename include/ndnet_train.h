@@ -7,6 +7,8 @@
  *
  * Replaces, in train mode:
  *   ndnet/models/ndtnet.py:48-50   TNet conv1..3 + bn1..3 + ReLU
+ *   ndnet/models/ndtnet.py:53-60   TNet fc1 + bn4 + ReLU, fc2 + bn5 + ReLU, fc3 + identity
+ *   ndnet/models/ndtnet.py:153-155 the x^T t2 product (ndnet_tr_gemm, per cloud)
  *   ndnet/models/ndtnet.py:148-152 NDTNet conv1 + bn1 (no ReLU), conv2/conv3 + bn2/bn3
  *   ndnet/models/ndtnet.py:233-239 seg head conv1..3 + bn1..3 + ReLU, conv4
  * and the autograd backward torch runs through them.  Host side:
@@ -96,6 +98,34 @@ int ndnet_tr_argmax_match(const float *pred, const float *gt, int64_t rows, int 
  * maximum, as torch.argmax): the labelled NDT path's class of each point from
  * its one-hot label (ndtnet_preprocessing.py:34), batched over the clouds. */
 int ndnet_row_argmax(const float *x, int64_t rows, int cols, int32_t *out, void *stream);
+
+/* TNet FC heads in train mode (ndtnet.py:53-60: fc1 + bn4 + ReLU, fc2 + bn5 +
+ * ReLU, fc3 + identity), B <= 16 rows (one per cloud), x [B][K] and W [N][K]
+ * row-major (torch's Linear layout), K % 4 == 0, 16-byte aligned rows.
+ * Forward, one wave per output channel:
+ *   y[b][n] = x[b] . W[n] + bias[n], + 1 where eye > 0 and n is a diagonal
+ *   entry of the eye x eye transform (added after the bias, as torch adds the
+ *   identity); with gamma: z = relu?(BatchNorm1d(y)) over the B rows (batch
+ *   statistics summed in double, biased variance; mean / invstd [N] saved;
+ *   running stats updated with `momentum` and the unbiased variance;
+ *   batches_tracked incremented), y kept for the backward; without gamma
+ *   z = y (relu and batches_tracked must be 0 / NULL).
+ * Backward: ndnet_tr_fc_bwd_w (one wave per channel) -- the BatchNorm and
+ * ReLU backward of channel n (as ndnet_tr_bn_bwd over B rows), dpre [B][N]
+ * (the gradient of y), db = sum_b dpre, dgamma, dbeta, and the weight
+ * gradient dW[n][k] = sum_b dpre[b][n] x[b][k] (any output may be NULL);
+ * ndnet_tr_fc_bwd_x -- dx[b][k] = sum_n dpre[b][n] W[n][k], over `nsplit`
+ * channel ranges of at most 256 (partials part [nsplit][B][K], summed in split
+ * order into dx; part may be NULL with nsplit == 1). */
+int ndnet_tr_fc_fwd(const float *x, const float *W, const float *bias, float *y, float *z, float *mean,
+                    float *invstd, float *running_mean, float *running_var, const float *gamma, const float *beta,
+                    int B, int K, int N, float eps, float momentum, int relu, int eye, int64_t *batches_tracked,
+                    void *stream);
+int ndnet_tr_fc_bwd_w(const float *dz, const float *x, const float *y, const float *mean, const float *invstd,
+                      const float *gamma, const float *beta, float *dpre, float *dW, float *db, float *dgamma,
+                      float *dbeta, int B, int K, int N, int relu, void *stream);
+int ndnet_tr_fc_bwd_x(const float *dpre, const float *W, float *dx, float *part, int B, int K, int N, int nsplit,
+                      void *stream);
 
 #ifdef __cplusplus
 }

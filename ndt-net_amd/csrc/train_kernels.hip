@@ -697,6 +697,202 @@ __global__ __launch_bounds__(256) void k_row_argmax_staged(const float* __restri
   if ((int)threadIdx.x < nr) out[r0 + threadIdx.x] = row_argmax(s + threadIdx.x * cols, cols);
 }
 
+// ---- TNet FC heads in train mode (ndtnet.py:53-60): Linear [+ BatchNorm1d
+// over the batch + ReLU] on B <= 16 rows (one row per cloud) ----
+//
+// torch runs each head layer as a 16-row GEMM (hipBLASLt), then BatchNorm's
+// batch statistics and ReLU as separate launches, and the same again
+// backward.  Here a wave owns one output channel n: its lanes split K in
+// float4 pieces with one partial sum per row (the weight row is read once for
+// every row), a reduce-scatter over the lanes leaves row b's sum in lanes
+// 4 b .. 4 b + 3, and BatchNorm's statistics over the B rows, the affine step
+// and ReLU follow in the same wave -- one launch per layer forward.  Backward:
+// one wave per channel for BatchNorm's backward, the bias / gamma / beta
+// gradients and the weight-gradient row (dW[n] = sum_b dpre[b][n] x[b]); the
+// input gradient by k-column blocks and N-splits summed in split order.
+constexpr int kFcB = 16;  // rows (clouds) per launch at most
+
+// sums of 16 per-row values over the wave's 64 lanes; lane L ends with row
+// ((L >> 2) & 15)'s total (a reduce-scatter: 8 + 4 + 2 + 1 exchanges, then 2)
+__device__ inline float fc_reduce16(float (&a)[kFcB], int lane) {
+  float v8[8], v4[4], v2[2], v1;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {  // xor 32: the low half keeps rows 0..7, the high half 8..15
+    const bool hi = lane & 32;
+    const float send = hi ? a[i] : a[8 + i], keep = hi ? a[8 + i] : a[i];
+    v8[i] = keep + __shfl_xor(send, 32);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const bool hi = lane & 16;
+    const float send = hi ? v8[i] : v8[4 + i], keep = hi ? v8[4 + i] : v8[i];
+    v4[i] = keep + __shfl_xor(send, 16);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    const bool hi = lane & 8;
+    const float send = hi ? v4[i] : v4[2 + i], keep = hi ? v4[2 + i] : v4[i];
+    v2[i] = keep + __shfl_xor(send, 8);
+  }
+  {
+    const bool hi = lane & 4;
+    const float send = hi ? v2[0] : v2[1], keep = hi ? v2[1] : v2[0];
+    v1 = keep + __shfl_xor(send, 4);
+  }
+  v1 += __shfl_xor(v1, 2);
+  v1 += __shfl_xor(v1, 1);
+  return v1;
+}
+
+__device__ inline double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// y[b][n] = x[b] . W[n] + bias[n] (+1 on the diagonal of an eye x eye transform:
+// TNet's fc3 + identity, ndtnet.py:59, added after the bias as torch does);
+// gamma != null: z = relu?(BatchNorm1d(y)) with batch statistics over the B
+// rows (double sums, biased variance; running stats with the unbiased one).
+__global__ __launch_bounds__(256) void k_tr_fc_fwd(const float* __restrict__ x, const float* __restrict__ W,
+                                                   const float* __restrict__ bias, float* __restrict__ y,
+                                                   float* __restrict__ z, float* __restrict__ mean,
+                                                   float* __restrict__ invstd, float* __restrict__ rmean,
+                                                   float* __restrict__ rvar, const float* __restrict__ gamma,
+                                                   const float* __restrict__ beta, int Bn, int K, int N, float eps,
+                                                   float momentum, int relu, int eye,
+                                                   long long* __restrict__ batches_tracked) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (batches_tracked && blockIdx.x == 0 && threadIdx.x == 0) batches_tracked[0] += 1;
+  if (n >= N) return;
+  const f32x4* w = reinterpret_cast<const f32x4*>(W + (int64_t)n * K);
+  float acc[kFcB];
+#pragma unroll
+  for (int b = 0; b < kFcB; b++) acc[b] = 0.0f;
+  for (int f = lane; f < K / 4; f += 64) {
+    const f32x4 wv = w[f];
+#pragma unroll
+    for (int b = 0; b < kFcB; b++) {
+      const f32x4 xv = reinterpret_cast<const f32x4*>(x + (int64_t)(b < Bn ? b : 0) * K)[f];
+      const f32x4 p = xv * wv;
+      acc[b] += (p[0] + p[1]) + (p[2] + p[3]);
+    }
+  }
+  const int row = (lane >> 2) & 15;  // the row this lane holds after the reduction
+  float v = fc_reduce16(acc, lane) + bias[n];
+  if (eye > 0 && n < eye * eye && n % (eye + 1) == 0) v += 1.0f;
+  const bool mine = (lane & 3) == 0 && row < Bn;
+  if (!gamma) {
+    if (mine) z[(int64_t)row * N + n] = v;
+    return;
+  }
+  const double mu = wave_sum_d(mine ? (double)v : 0.0) / (double)Bn;
+  const double dv = (double)v - mu;
+  const double var = wave_sum_d(mine ? dv * dv : 0.0) / (double)Bn;
+  const float inv = (float)(1.0 / sqrt(var + (double)eps));
+  const float fm = (float)mu;
+  if (lane == 0) {
+    mean[n] = fm;
+    invstd[n] = inv;
+    if (rmean) rmean[n] = (1.0f - momentum) * rmean[n] + momentum * fm;
+    if (rvar) {
+      const double unb = Bn > 1 ? var * (double)Bn / (double)(Bn - 1) : var;
+      rvar[n] = (1.0f - momentum) * rvar[n] + momentum * (float)unb;
+    }
+  }
+  float o = bn_apply(v, fm, inv, gamma[n], beta[n]);
+  if (relu) o = fmaxf(o, 0.0f);
+  if (mine) {
+    y[(int64_t)row * N + n] = v;
+    z[(int64_t)row * N + n] = o;
+  }
+}
+
+// Backward through BatchNorm (+ ReLU mask) of channel n and its weight row:
+// dpre[b][n] (the gradient of y), db[n] = sum_b dpre, dgamma / dbeta, and
+// dW[n][k] = sum_b dpre[b][n] x[b][k] in row order.  gamma == null: dpre = dz.
+__global__ __launch_bounds__(256) void k_tr_fc_bwd_w(const float* __restrict__ dz, const float* __restrict__ x,
+                                                     const float* __restrict__ y, const float* __restrict__ mean,
+                                                     const float* __restrict__ invstd,
+                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                     float* __restrict__ dpre, float* __restrict__ dW,
+                                                     float* __restrict__ db, float* __restrict__ dgamma,
+                                                     float* __restrict__ dbeta, int Bn, int K, int N, int relu) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= N) return;
+  const bool mine = lane < Bn;  // lane b: row b
+  float d = 0.0f;
+  if (!gamma) {
+    d = mine ? dz[(int64_t)lane * N + n] : 0.0f;
+  } else {
+    const float mu = mean[n], inv = invstd[n], gm = gamma[n], bt = beta[n];
+    float g = 0.0f, xh = 0.0f;
+    if (mine) {
+      const float yv = y[(int64_t)lane * N + n];
+      g = dz[(int64_t)lane * N + n];
+      if (relu && !(bn_apply(yv, mu, inv, gm, bt) > 0.0f)) g = 0.0f;
+      xh = (yv - mu) * inv;
+    }
+    const double sg = wave_sum_d(g), sgx = wave_sum_d((double)g * xh);
+    const float k1 = (float)(sg / (double)Bn), k2 = (float)(sgx / (double)Bn);
+    if (mine) d = gm * inv * (g - k1 - xh * k2);
+    if (lane == 0) {
+      if (dgamma) dgamma[n] = (float)sgx;
+      if (dbeta) dbeta[n] = (float)sg;
+    }
+  }
+  const double sd = wave_sum_d(d);
+  if (lane == 0 && db) db[n] = (float)sd;
+  if (mine && dpre) dpre[(int64_t)lane * N + n] = d;
+  if (!dW) return;
+  float dv[kFcB];
+#pragma unroll
+  for (int b = 0; b < kFcB; b++) dv[b] = __shfl(d, b);  // 0 past the rows
+  f32x4* wrow = reinterpret_cast<f32x4*>(dW + (int64_t)n * K);
+  for (int f = lane; f < K / 4; f += 64) {
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int b = 0; b < kFcB; b++) {
+      if (b < Bn) {
+        const f32x4 xv = reinterpret_cast<const f32x4*>(x + (int64_t)b * K)[f];
+        s = s + xv * dv[b];
+      }
+    }
+    wrow[f] = s;
+  }
+}
+
+// dx[b][k] = sum_n dpre[b][n] W[n][k]: workgroup (k block of 256 columns, N
+// split s); part[s][b][k] (or dx itself with one split), summed in split order.
+constexpr int kFcXMaxN = 256;  // channels of a split staged in LDS
+__global__ __launch_bounds__(256) void k_tr_fc_bwd_x(const float* __restrict__ dpre, const float* __restrict__ W,
+                                                     float* __restrict__ out, int Bn, int K, int N, int nsplit) {
+  __shared__ float s_d[kFcXMaxN][kFcB];
+  const int s = blockIdx.y;
+  const int n0 = (int)((int64_t)N * s / nsplit), n1 = (int)((int64_t)N * (s + 1) / nsplit);
+  for (int e = threadIdx.x; e < (n1 - n0) * kFcB; e += 256) {
+    const int nn = e / kFcB, b = e % kFcB;
+    s_d[nn][b] = b < Bn ? dpre[(int64_t)b * N + n0 + nn] : 0.0f;
+  }
+  __syncthreads();
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= K) return;
+  float acc[kFcB];
+#pragma unroll
+  for (int b = 0; b < kFcB; b++) acc[b] = 0.0f;
+  for (int nn = n0; nn < n1; nn++) {
+    const float wv = W[(int64_t)nn * K + k];
+#pragma unroll
+    for (int b = 0; b < kFcB; b++) acc[b] = fmaf(s_d[nn - n0][b], wv, acc[b]);
+  }
+  float* o = out + (int64_t)s * Bn * K;
+#pragma unroll
+  for (int b = 0; b < kFcB; b++)
+    if (b < Bn) o[(int64_t)b * K + k] = acc[b];
+}
+
 int launched() { return hipGetLastError() == hipSuccess ? 0 : -21; }
 
 bool getenv_flag(const char* name) {
@@ -879,5 +1075,44 @@ extern "C" int ndnet_row_argmax(const float* x, int64_t rows, int cols, int32_t*
     k_row_argmax_staged<<<(unsigned)((rows + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, rows, cols, out);
   else
     k_row_argmax<<<(unsigned)((rows + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, rows, cols, out);
+  return launched();
+}
+
+extern "C" int ndnet_tr_fc_fwd(const float* x, const float* W, const float* bias, float* y, float* z, float* mean,
+                               float* invstd, float* running_mean, float* running_var, const float* gamma,
+                               const float* beta, int B, int K, int N, float eps, float momentum, int relu, int eye,
+                               int64_t* batches_tracked, void* stream) {
+  if (!x || !W || !bias || !z || B <= 0 || B > kFcB || K <= 0 || K % 4 || N <= 0) return -20;
+  if (gamma && (!y || !mean || !invstd || !beta)) return -20;
+  if (!gamma && (relu || batches_tracked)) return -20;
+  if ((((uintptr_t)x | (uintptr_t)W) & 15) != 0) return -20;  // float4 rows
+  k_tr_fc_fwd<<<(N + 3) / 4, 256, 0, (hipStream_t)stream>>>(x, W, bias, y, z, mean, invstd, running_mean,
+                                                              running_var, gamma, beta, B, K, N, eps, momentum, relu,
+                                                              eye, reinterpret_cast<long long*>(batches_tracked));
+  return launched();
+}
+
+extern "C" int ndnet_tr_fc_bwd_w(const float* dz, const float* x, const float* y, const float* mean,
+                                 const float* invstd, const float* gamma, const float* beta, float* dpre, float* dW,
+                                 float* db, float* dgamma, float* dbeta, int B, int K, int N, int relu, void* stream) {
+  if (!dz || !x || B <= 0 || B > kFcB || K <= 0 || K % 4 || N <= 0) return -20;
+  if (gamma && (!y || !mean || !invstd || !beta)) return -20;
+  if (!gamma && relu) return -20;
+  if ((((uintptr_t)x | (uintptr_t)dW) & 15) != 0) return -20;
+  k_tr_fc_bwd_w<<<(N + 3) / 4, 256, 0, (hipStream_t)stream>>>(dz, x, y, mean, invstd, gamma, beta, dpre, dW, db,
+                                                                dgamma, dbeta, B, K, N, relu);
+  return launched();
+}
+
+extern "C" int ndnet_tr_fc_bwd_x(const float* dpre, const float* W, float* dx, float* part, int B, int K, int N,
+                                 int nsplit, void* stream) {
+  if (!dpre || !W || !dx || B <= 0 || B > kFcB || K <= 0 || N <= 0 || nsplit <= 0 || nsplit > N) return -20;
+  if ((N + nsplit - 1) / nsplit > kFcXMaxN || (nsplit > 1 && !part)) return -20;
+  float* out = nsplit > 1 ? part : dx;
+  k_tr_fc_bwd_x<<<dim3((K + 255) / 256, nsplit), 256, 0, (hipStream_t)stream>>>(dpre, W, out, B, K, N, nsplit);
+  if (nsplit > 1) {
+    const int64_t count = (int64_t)B * K;
+    k_tr_sum_parts<<<(unsigned)((count + 1023) / 1024), 256, 0, (hipStream_t)stream>>>(part, dx, count, nsplit);
+  }
   return launched();
 }

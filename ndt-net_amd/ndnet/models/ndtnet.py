@@ -18,7 +18,9 @@ Two forward paths:
   * train mode on the GPU -> every Conv1d(k=1) + BatchNorm1d (batch
     statistics) [+ ReLU] block forward and backward on the train kernels of
     lib/libndnet_amd.so (``ndnet.models.train_hip``, include/ndnet_train.h);
-    the max-pools, transforms, TNet FC heads and log-softmax stay torch ops.
+    the TNet FC heads (Linear + BatchNorm1d + ReLU fused per layer) and the
+    x^T t2 product also run on HIP kernels; the point transform t1 (one bmm)
+    and log-softmax stay torch ops.
     ``NDNET_TRAIN_PATH=torch`` selects the torch composition instead (A/B).
   * anything else (eval-mode autograd, CPU) -> the PyTorch composition below,
     which is also the fp32 reference the kernels are tested against.
@@ -45,6 +47,14 @@ def _hip_train(conv: nn.Conv1d, bn, x: torch.Tensor) -> bool:
     return (x.is_cuda and conv.training and (bn is None or bn.training) and not _TRAIN_TORCH
             and x.dtype == torch.float32 and conv.weight.dtype == torch.float32
             and not torch.is_autocast_enabled("cuda"))
+
+
+def _hip_fc(t: "TNet", g: torch.Tensor) -> bool:
+    """The TNet head on the HIP FC kernels: train mode, fp32 on the GPU, at most
+    16 clouds (train_hip.FC_MAX_ROWS), every layer's sizes a multiple of 4."""
+    return (_hip_train(t.conv1, t.bn1, g) and t.fc1.training and t.bn4.training and t.bn5.training
+            and 2 <= g.shape[0] <= 16 and g.dim() == 2 and all(fc.weight.dtype == torch.float32 and
+                                                                 fc.in_features % 4 == 0 for fc in (t.fc1, t.fc2, t.fc3)))
 
 
 def _block_pool(conv: nn.Conv1d, bn, x: torch.Tensor, relu: bool) -> torch.Tensor:
@@ -85,6 +95,14 @@ class TNet(nn.Module):
         x = _block(self.conv1, self.bn1, x, True)
         x = _block(self.conv2, self.bn2, x, True)
         g = _block_pool(self.conv3, self.bn3, x, True)
+        if _hip_fc(self, g):
+            # the FC head on the HIP train kernels (train_hip.fc_bn_act): one launch
+            # per layer forward, Linear + BatchNorm's batch statistics + ReLU fused
+            from . import train_hip
+            g = train_hip.fc_bn_act(self.fc1, self.bn4, g, True)
+            g = train_hip.fc_bn_act(self.fc2, self.bn5, g, True)
+            t = train_hip.fc_bn_act(self.fc3, None, g, False, eye=self.in_dim)
+            return t.view(-1, self.in_dim, self.in_dim)
         g = self.relu(self.bn4(self.fc1(g)))
         g = self.relu(self.bn5(self.fc2(g)))
         t = self.fc3(g) + torch.eye(self.in_dim, device=g.device, dtype=g.dtype).reshape(1, -1)
@@ -138,7 +156,11 @@ class NDTNet(nn.Module):
             x = torch.cat((xyz.transpose(1, 2), cov), dim=2).transpose(1, 2)  # [B,12,N]
         x = _block(self.conv1, self.bn1, x, False)        # no ReLU (reference ndtnet.py:149)
         t2 = self.t2(x)                                   # [B,64,64]
-        x = torch.bmm(x.transpose(1, 2), t2).transpose(1, 2)  # x^T t2
+        if _hip_train(self.conv2, self.bn2, x):
+            from . import train_hip
+            x = train_hip.transform_t(x, t2)              # x^T t2 on the HIP GEMM (ndtnet.py:153-155)
+        else:
+            x = torch.bmm(x.transpose(1, 2), t2).transpose(1, 2)  # x^T t2
         x_t2 = x
         x = _block(self.conv2, self.bn2, x, False)
         if pooled:

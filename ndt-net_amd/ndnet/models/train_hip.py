@@ -302,3 +302,125 @@ def conv_bn_act_pool(conv: torch.nn.Conv1d, bn: torch.nn.BatchNorm1d, x: torch.T
         bn.num_batches_tracked.add_(1)
     return out
 
+
+
+# ---- TNet FC heads (ndtnet.py:53-60) and the x^T t2 product (:153-155) ----
+
+FC_MAX_ROWS = 16  # clouds per batch the FC kernels take (include/ndnet_train.h ndnet_tr_fc_fwd)
+
+
+def _fc_splits(N: int) -> int:
+    """Channel splits of the input-gradient kernel: about 128 workgroups over
+    the k blocks, at most 256 channels (the kernel's LDS stage) per split."""
+    return max(-(-N // 256), min(N, 32))
+
+
+class _FcBNAct(torch.autograd.Function):
+    """Linear [-> BatchNorm1d over the batch rows -> ReLU] (or + identity, fc3),
+    on x [B,K] with B <= 16 (ndnet_tr_fc_fwd / _bwd_w / _bwd_x)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, gamma, beta, run_mean, run_var, eps, momentum, relu, eye, nbt=None):
+        x = x.contiguous()
+        w2 = w.detach().contiguous()
+        _check_f32(x, w2)
+        Bn, K = x.shape
+        N = w2.shape[0]
+        z = torch.empty(Bn, N, device=x.device, dtype=torch.float32)
+        bn = gamma is not None
+        y = torch.empty_like(z) if bn else None
+        mean = torch.empty(N, device=x.device, dtype=torch.float32) if bn else None
+        invstd = torch.empty_like(mean) if bn else None
+        g = gamma.detach().contiguous() if bn else None
+        bt = beta.detach().contiguous() if bn else None
+        rc = _lib.lib().ndnet_tr_fc_fwd(x.data_ptr(), w2.data_ptr(), b.detach().contiguous().data_ptr(), _ptr(y),
+                                        z.data_ptr(), _ptr(mean), _ptr(invstd), _ptr(run_mean), _ptr(run_var),
+                                        _ptr(g), _ptr(bt), Bn, K, N, float(eps), float(momentum), int(relu), int(eye),
+                                        _ptr(nbt), _stream())
+        _lib.check(rc, "ndnet_tr_fc_fwd")
+        ctx.relu, ctx.bn = bool(relu), bn
+        ctx.save_for_backward(x, w2, y, mean, invstd, g, bt)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        dz = dz.contiguous()
+        need = ctx.needs_input_grad
+        x, w2, y, mean, invstd, g, bt = ctx.saved_tensors
+        Bn, K = x.shape
+        N = w2.shape[0]
+        dev = x.device
+        dpre = torch.empty(Bn, N, device=dev, dtype=torch.float32)
+        dw = torch.empty(N, K, device=dev, dtype=torch.float32) if need[1] else None
+        db = torch.empty(N, device=dev, dtype=torch.float32) if need[2] else None
+        dgamma = torch.empty(N, device=dev, dtype=torch.float32) if ctx.bn and need[3] else None
+        dbeta = torch.empty(N, device=dev, dtype=torch.float32) if ctx.bn and need[4] else None
+        rc = _lib.lib().ndnet_tr_fc_bwd_w(dz.data_ptr(), x.data_ptr(), _ptr(y), _ptr(mean), _ptr(invstd), _ptr(g),
+                                          _ptr(bt), dpre.data_ptr(), _ptr(dw), _ptr(db), _ptr(dgamma), _ptr(dbeta),
+                                          Bn, K, N, int(ctx.relu), _stream())
+        _lib.check(rc, "ndnet_tr_fc_bwd_w")
+        dx = None
+        if need[0]:
+            dx = torch.empty(Bn, K, device=dev, dtype=torch.float32)
+            ns = _fc_splits(N)
+            part = torch.empty(ns, Bn, K, device=dev, dtype=torch.float32) if ns > 1 else None
+            rc = _lib.lib().ndnet_tr_fc_bwd_x(dpre.data_ptr(), w2.data_ptr(), dx.data_ptr(), _ptr(part), Bn, K, N, ns,
+                                              _stream())
+            _lib.check(rc, "ndnet_tr_fc_bwd_x")
+        return dx, dw, db, dgamma, dbeta, None, None, None, None, None, None, None
+
+
+def fc_bn_act(fc: torch.nn.Linear, bn: Optional[torch.nn.BatchNorm1d], x: torch.Tensor, relu: bool,
+              eye: int = 0) -> torch.Tensor:
+    """``relu(bn(fc(x)))`` in training mode on the HIP kernels (x [B,K], B <= 16;
+    the TNet heads' fc1 / fc2), or ``fc(x) + eye(eye).flatten()`` without
+    ``bn`` (fc3, ndtnet.py:57-59).  Same results (fp32, within summation
+    order) and side effects (running statistics, num_batches_tracked) as the
+    torch modules."""
+    if bn is None:
+        return _FcBNAct.apply(x, fc.weight, fc.bias, None, None, None, None, 0.0, 0.0, False, eye)
+    if not bn.affine or bn.momentum is None:
+        raise ValueError("the FC kernels take affine BatchNorm1d with a fixed momentum (the model's defaults)")
+    track = bn.track_running_stats and bn.running_mean is not None
+    nbt = _batches_tracked(bn) if track else None
+    out = _FcBNAct.apply(x, fc.weight, fc.bias, bn.weight, bn.bias, bn.running_mean if track else None,
+                         bn.running_var if track else None, bn.eps, bn.momentum, relu, 0, nbt)
+    if track and nbt is None:
+        bn.num_batches_tracked.add_(1)
+    return out
+
+
+class _TransformT(torch.autograd.Function):
+    """x_t2 = (x^T t2)^T per cloud (ndtnet.py:153-155) on ndnet_tr_gemm: x
+    [B,C,N] (NCL), t [B,C,C] -> [B,C,N] with x_t2[b] = t[b]^T x[b]."""
+
+    @staticmethod
+    def forward(ctx, x, t):
+        x, t = x.contiguous(), t.contiguous()
+        _check_f32(x, t)
+        Bn, C, N = x.shape
+        y = torch.empty_like(x)
+        # A(m, k) = t[b][k][m] (not k-major, lda C), B(k, n) = x[b][k][n]
+        gemm(t, x, y, None, C, N, C, C, N, N, C * C, C * N, C * N, Bn, False, False)
+        ctx.save_for_backward(x, t)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        x, t = ctx.saved_tensors
+        Bn, C, N = x.shape
+        dx = dt = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)  # dx[b] = t[b] dy[b]: A(m, k) = t[b][m][k] (k-major)
+            gemm(t, dy, dx, None, C, N, C, C, N, N, C * C, C * N, C * N, Bn, True, False)
+        if ctx.needs_input_grad[1]:
+            # dt[b][i][j] = sum_p x[b][i][p] dy[b][j][p]: A = x[b] (k-major, lda N), B(k, n) = dy[b][n][k] (k-major)
+            dt = torch.empty_like(t)
+            gemm(x, dy, dt, None, C, C, N, N, N, C, C * N, C * N, C * C, Bn, True, True)
+        return dx, dt
+
+
+def transform_t(x: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
+    """``torch.bmm(x.transpose(1, 2), t).transpose(1, 2)`` for x [B,C,N], t [B,C,C]."""
+    return _TransformT.apply(x, t)

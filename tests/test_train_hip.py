@@ -130,6 +130,80 @@ def test_block_matches_torch(cin, cout, bn, relu, B, N):
         _close(conv.bias.grad, conv2.bias.grad, 1e-4, "db")
 
 
+@pytest.mark.parametrize("K,N,bn,relu,eye,B", [
+    (1024, 512, True, True, 0, 16),   # TNet fc1 + bn4 + ReLU, the bench's batch
+    (512, 256, True, True, 0, 16),    # fc2 + bn5 + ReLU
+    (256, 9, False, False, 3, 16),    # TNet(3) fc3 + identity
+    (256, 4096, False, False, 64, 16),  # TNet(64) fc3 + identity (16 channel splits in dx)
+    (512, 256, True, True, 0, 5),     # a ragged batch
+    (1024, 512, True, True, 0, 2),    # two clouds: BatchNorm over two rows
+])
+def test_fc_head_matches_torch(K, N, bn, relu, eye, B):
+    """VERDICT r4 (next 6): the TNet FC heads (ndtnet.py:53-60) on the HIP
+    train kernels -- Linear [+ BatchNorm1d over the batch + ReLU] or fc3 +
+    identity -- against the torch modules: output, running statistics,
+    num_batches_tracked and every gradient."""
+    from ndnet.models import train_hip
+    torch.manual_seed(K + N + B)
+    fc = torch.nn.Linear(K, N).cuda()
+    norm = torch.nn.BatchNorm1d(N).cuda() if bn else None
+    if norm is not None:
+        with torch.no_grad():
+            norm.weight.uniform_(0.5, 1.5)
+            norm.bias.uniform_(-0.3, 0.3)
+            norm.running_mean.uniform_(-1, 1)
+            norm.running_var.uniform_(0.5, 2)
+    fc2, norm2 = copy.deepcopy(fc), copy.deepcopy(norm)
+    x = (torch.randn(B, K, device="cuda") * 2 + 0.5).requires_grad_(True)
+    x2 = x.detach().clone().requires_grad_(True)
+    out = train_hip.fc_bn_act(fc, norm, x, relu, eye=eye)
+    ref = fc2(x2)
+    if norm2 is not None:
+        ref = norm2(ref)
+    if relu:
+        ref = torch.relu(ref)
+    if eye:
+        ref = ref + torch.eye(eye, device="cuda").reshape(1, -1)
+    # BatchNorm over two rows normalises each channel to +-1 exactly: a near-tie of
+    # the two rows amplifies fp32 summation order (|y0 - y1| ~ 1e-3 |y|), so the bound
+    # is on the pre-normalisation error scale there
+    torch.testing.assert_close(out, ref, rtol=0, atol=1e-4 if B > 2 else 5e-3)
+    if norm is not None:
+        torch.testing.assert_close(norm.running_mean, norm2.running_mean, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(norm.running_var, norm2.running_var, rtol=1e-4, atol=1e-4)
+        assert int(norm.num_batches_tracked) == int(norm2.num_batches_tracked) == 1
+    up = torch.randn_like(ref)
+    out.backward(up)
+    ref.backward(up)
+    tol = 1e-4 if B > 2 else 5e-3
+    _close(x.grad, x2.grad, tol, "dx")
+    _close(fc.weight.grad, fc2.weight.grad, tol, "dW")
+    if norm is not None:
+        _close(norm.weight.grad, norm2.weight.grad, tol, "dgamma")
+        _close(norm.bias.grad, norm2.bias.grad, tol, "dbeta")
+        assert (fc.bias.grad - fc2.bias.grad).abs().max().item() <= 1e-3  # sum(dy) ~ 0 under BN
+    else:
+        _close(fc.bias.grad, fc2.bias.grad, tol, "db")
+
+
+def test_transform_t_matches_bmm():
+    """x^T t2 (ndtnet.py:153-155) on the HIP GEMM against torch's bmm, forward
+    and both gradients."""
+    from ndnet.models import train_hip
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.randn(16, 64, 1000, device="cuda", generator=g).requires_grad_(True)
+    t = (torch.randn(16, 64, 64, device="cuda", generator=g) * 0.2 + torch.eye(64, device="cuda")).requires_grad_(True)
+    x2, t2 = x.detach().clone().requires_grad_(True), t.detach().clone().requires_grad_(True)
+    out = train_hip.transform_t(x, t)
+    ref = torch.bmm(x2.transpose(1, 2), t2).transpose(1, 2)
+    _close(out, ref, 1e-5, "x_t2")
+    up = torch.randn_like(ref)
+    out.backward(up)
+    ref.backward(up)
+    _close(x.grad, x2.grad, 1e-5, "dx")
+    _close(t.grad, t2.grad, 1e-5, "dt")
+
+
 def test_block_input_without_grad_skips_dx():
     from ndnet.models import train_hip
     conv, norm = _pair(3, 64, True, 5)
@@ -243,15 +317,29 @@ def test_segmentation_train_forward_backward_matches_torch(monkeypatch):
         calls.append(2)
         return real_pool(*a, **k)
 
+    real_fc, real_tt = train_hip.fc_bn_act, train_hip.transform_t
+
+    def spy_fc(*a, **k):
+        calls.append(3)
+        return real_fc(*a, **k)
+
+    def spy_tt(*a, **k):
+        calls.append(4)
+        return real_tt(*a, **k)
+
     monkeypatch.setattr(train_hip, "conv_bn_act", spy)
     monkeypatch.setattr(train_hip, "conv_bn_act_pool", spy_pool)
+    monkeypatch.setattr(train_hip, "fc_bn_act", spy_fc)
+    monkeypatch.setattr(train_hip, "transform_t", spy_tt)
     out = model(pts, cov)
-    # 3 + 3 TNet blocks (the last of each pooled), 3 NDTNet (conv3 pooled), 3 seg head + conv4
-    assert len(calls) == 13 and calls.count(2) == 3
+    # 3 + 3 TNet blocks (the last of each pooled), 3 NDTNet (conv3 pooled), 3 seg head + conv4;
+    # 3 + 3 TNet FC layers; one x^T t2
+    assert calls.count(1) + calls.count(2) == 13 and calls.count(2) == 3
+    assert calls.count(3) == 6 and calls.count(4) == 1
     monkeypatch.setattr(ndtnet, "_TRAIN_TORCH", True)
     f64_model = copy.deepcopy(ref_model).double()
     ref = ref_model(pts, cov)
-    assert len(calls) == 13
+    assert len(calls) == 20
     torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4)
     # and as close to a float64 evaluation as torch's own fp32 forward is
     f64 = f64_model(pts.double(), cov.double())
