@@ -1558,9 +1558,16 @@ __device__ __attribute__((always_inline)) inline void wq_light64(const CloudCtl*
   // (rc, rl) of counts q0 + 1 .. q0 + kL64B: LDS broadcast reads, the global
   // table past the LDS one (a threshold raised after the heavy list was built)
   auto ldr = [&](double2 (&rr)[kL64B], uint32_t q0) __attribute__((always_inline)) {
-    const double2* tb = q0 + kL64B < rtn ? lrt2 : rtab;  // wave-uniform
+    if (q0 + kL64B < rtn) {  // wave-uniform
 #pragma unroll
-    for (int u = 0; u < kL64B; u++) rr[u] = tb[q0 + (uint32_t)u + 1u];
+      for (int u = 0; u < kL64B; u++) rr[u] = lrt2[q0 + (uint32_t)u + 1u];
+    } else {  // counts past the table (clamped to the plan's n: a masked step only needs a finite pair)
+#pragma unroll
+      for (int u = 0; u < kL64B; u++) {
+        const uint64_t c = (uint64_t)q0 + (uint32_t)u + 1u;
+        rr[u] = rtab[c <= n ? c : n];
+      }
+    }
   };
   // a ring of register blocks: kR - 1 blocks in flight while one is folded
   constexpr int kR = std::is_same<T, float>::value ? 3 : 2;
@@ -1717,8 +1724,9 @@ __global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const Cl
   uint32_t* hpre = pre + bw;                                      // [B + 1] first heavy item of each cloud
   uint32_t* wq_hist = hpre + bw;                                  // labelled runs: [kWqHistNDs][ncls + 1]
   if constexpr (NDNET_WQ_LIGHT64) {
-    const uint32_t rte = rtn < n + 1 ? rtn : (uint32_t)(n + 1);  // rtab holds counts 0..n
-    for (uint32_t i = threadIdx.x; i < rte; i += kWqThreads) lrt2[i] = rtab[i];
+    // every entry finite: a masked step past a lane's count reads one (x = mean
+    // makes t = +0, and 0 * rl must not be 0 * inf); rtab holds counts 0..n
+    for (uint32_t i = threadIdx.x; i < rtn; i += kWqThreads) lrt2[i] = rtab[i <= n ? i : n];
   } else {
     for (uint32_t i = threadIdx.x; i < rtn; i += kWqThreads) lrt[i] = recip_refined((double)(i + 1));
   }
