@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <mutex>
 #include <type_traits>
@@ -3421,6 +3422,37 @@ static hipError_t front_lanes_assign(Plan* P) {
 }
 
 // Launches k_front between the lane waits and records (front_lanes_assign).
+// How a stream being captured is admitted (NDNET_LANE_CAPTURE, read once;
+// tools/capture_lane_probe.py tries each form): 0 no lane nodes in the graph,
+// 1 external wait nodes only, 2 external record nodes only, 3 both, 4 both as
+// explicit graph nodes (hipGraphAddEventWaitNode / hipGraphAddEventRecordNode
+// on the capture's graph, then the capture's dependencies moved past them).
+static int lane_capture_mode() {
+  static const int v = [] {
+    const char* e = getenv("NDNET_LANE_CAPTURE");
+    return e ? atoi(e) : 3;
+  }();
+  return v;
+}
+
+// Adds an event node (wait or record) after the capture's current
+// dependencies and makes it the capture's only dependency.
+static hipError_t capture_event_node(hipStream_t st, hipEvent_t ev, bool wait) {
+  hipStreamCaptureStatus cs;
+  unsigned long long id = 0;
+  hipGraph_t g = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t nd = 0;
+  hipError_t e = hipStreamGetCaptureInfo_v2(st, &cs, &id, &g, &deps, &nd);
+  if (e != hipSuccess) return e;
+  std::vector<hipGraphNode_t> dv(deps, deps + nd);
+  hipGraphNode_t node;
+  e = wait ? hipGraphAddEventWaitNode(&node, g, dv.data(), dv.size(), ev)
+           : hipGraphAddEventRecordNode(&node, g, dv.data(), dv.size(), ev);
+  if (e != hipSuccess) return e;
+  return hipStreamUpdateCaptureDependencies(st, &node, 1, hipStreamSetCaptureDependencies);
+}
+
 template <typename T>
 static int front_launch(Plan* P, hipStream_t st, const T* pts, const FrontArgs& F) {
   std::lock_guard<std::mutex> lk(g_lane_mu);  // waits, launch and records in one host order
@@ -3428,12 +3460,21 @@ static int front_launch(Plan* P, hipStream_t st, const T* pts, const FrontArgs& 
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   HIPCHK(hipStreamIsCapturing(st, &cs));
   const bool cap = cs == hipStreamCaptureStatusActive;
-  for (int i = 0; i < P->nlanes; i++)
-    HIPCHK(hipStreamWaitEvent(st, L.ev[(P->lane0 + i) % kFrontLanes], cap ? hipEventWaitExternal : 0));
+  const int mode = cap ? lane_capture_mode() : 3;
+  for (int i = 0; i < P->nlanes; i++) {
+    hipEvent_t ev = L.ev[(P->lane0 + i) % kFrontLanes];
+    if (!cap) HIPCHK(hipStreamWaitEvent(st, ev, 0));
+    else if (mode == 1 || mode == 3) HIPCHK(hipStreamWaitEvent(st, ev, hipEventWaitExternal));
+    else if (mode == 4) HIPCHK(capture_event_node(st, ev, true));
+  }
   k_front<T><<<P->fG * P->B, kFrontThreads, P->flds, st>>>(pts, F);
   HIPCHK(hipGetLastError());
-  for (int i = 0; i < P->nlanes; i++)
-    HIPCHK(hipEventRecordWithFlags(L.ev[(P->lane0 + i) % kFrontLanes], st, cap ? hipEventRecordExternal : 0));
+  for (int i = 0; i < P->nlanes; i++) {
+    hipEvent_t ev = L.ev[(P->lane0 + i) % kFrontLanes];
+    if (!cap) HIPCHK(hipEventRecord(ev, st));
+    else if (mode == 2 || mode == 3) HIPCHK(hipEventRecordWithFlags(ev, st, hipEventRecordExternal));
+    else if (mode == 4) HIPCHK(capture_event_node(st, ev, false));
+  }
   return NDNET_OK;
 }
 
@@ -3622,6 +3663,10 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   P->front_sync_ticks = 200000000ull;  // 2 s at the 100 MHz constant clock
   P->front_staged = 1;
   P->heavy_t = kWqHeavy;
+  if (const char* e = getenv("NDNET_HEAVY_T")) {  // A/B of the default threshold (tools/gpu.sh ab)
+    const long v = atol(e);
+    if (v >= 1) P->heavy_t = (uint32_t)v;
+  }
   const double upper = (double)num_desired * (1 + 0.2);
   P->ndcap = (uint32_t)upper + 1;
   P->ecap = 6 * P->ndcap;

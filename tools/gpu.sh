@@ -15,6 +15,7 @@
 #   bash tools/gpu.sh pmc     TAG ndt|pn|chain|cache|issue    PMC passes, one counter group per run
 #   bash tools/gpu.sh train   TAG                 train-path tests + the eager / graphed train step
 #   bash tools/gpu.sh stamps  TAG                 per-layer chain stamps (variant "stamps")
+#   bash tools/gpu.sh py      TAG tool.py [args]  a python tool under a time limit (output kept)
 set -o pipefail
 CMD=${1:?command}
 TAG=${2:?tag}
@@ -143,6 +144,11 @@ train)
   tail -1 $OUT/train_eager.log
   step graph 200 $OUT/train_graph.log python -u tools/bench_train.py --steps 20 --warmup 5 --graph
   tail -1 $OUT/train_graph.log
+  ;;
+py)  # a python tool (e.g. tools/wq_items.py --kind L), output to gpurun_out/TAG/<tool>.txt
+  NAME=$(basename ${1%.py})
+  step $NAME 300 $OUT/$NAME.txt python -u "$@"
+  cat $OUT/$NAME.txt
   ;;
 stamps)
   export NDNET_AMD_LIB=$R/ndt-net_amd/lib/variants/libndnet_amd_stamps.so
