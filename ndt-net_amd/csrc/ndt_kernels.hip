@@ -2127,7 +2127,10 @@ __global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const Cl
     // return-less LDS atomics, so no increment waits on the previous one.
     // One lane counting alone waited on a load and an LDS read-modify-write
     // per label: L's 1675-label ND took ~100 us of a labelled run.
-    uint32_t* hist = wq_hist + (threadIdx.x >> 2) * nbins;
+    // light64: a lane per slot, [wave * 64, wave * 64 + 64) per wave, so a heavy
+    // wave's quad 0 takes its own wave's first slot (a quad index would land
+    // in another wave's range while that wave's light64 item counts into it)
+    uint32_t* hist = wq_hist + (NDNET_WQ_LIGHT64 ? (threadIdx.x & ~3u) : (threadIdx.x >> 2)) * nbins;
     for (uint32_t k = j; k < nbins; k += 4) hist[k] = 0;
     __builtin_amdgcn_wave_barrier();
     const uint16_t* l = nd_lbl + (uint64_t)b * n + beg;
@@ -3427,10 +3430,14 @@ static hipError_t front_lanes_assign(Plan* P) {
 // 1 external wait nodes only, 2 external record nodes only, 3 both, 4 both as
 // explicit graph nodes (hipGraphAddEventWaitNode / hipGraphAddEventRecordNode
 // on the capture's graph, then the capture's dependencies moved past them).
+// On ROCm 7.2 only 4 works: hipStreamWaitEvent(hipEventWaitExternal) in a
+// capture throws std::bad_alloc inside HIP (modes 1, 3) and
+// hipEventRecordWithFlags(hipEventRecordExternal) fails (mode 2, -21)
+// (profiles/r05_capture_lane_probe.txt).  4 is the default.
 static int lane_capture_mode() {
   static const int v = [] {
     const char* e = getenv("NDNET_LANE_CAPTURE");
-    return e ? atoi(e) : 3;
+    return e ? atoi(e) : 4;
   }();
   return v;
 }

@@ -472,6 +472,9 @@ def test_two_plans_on_two_streams_are_admitted(graphs):
         ins.append(torch.from_numpy(make_batch(kind, B, n)).cuda())
         outs.append(torch.zeros((B, k, 12), dtype=torch.float32, device="cuda"))
         shas.append(z[f"C2_{kind}_sha"])
+    from ndnet import _lib
+    for pl in plans:  # k_front's per-workgroup start / end stamps (s_memrealtime: one clock for the chip)
+        assert _lib.lib().ndnet_ndt_set_timing(pl.handle, 2) == 0
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     for s in streams:
         s.wait_stream(torch.cuda.current_stream())
@@ -499,12 +502,22 @@ def test_two_plans_on_two_streams_are_admitted(graphs):
                     else:
                         plans[i].run(ins[i], None, outs[i], None)
         torch.cuda.synchronize()
+        span = []
         for i in range(2):
             assert [st.rc for st in plans[i].host_stats()] == [0] * B, (graphs, rnd, i)
             plans[i].raise_sync_failures()
             rows = outs[i].cpu().numpy()
             for b in range(B):
                 assert _sha_rows(rows[b]) == shas[i][b, 0].tobytes(), (graphs, rnd, i, b)
+            G = ctypes.c_int(0)
+            m = np.zeros(B * 256 * 2, np.uint64)
+            assert _lib.lib().ndnet_ndt_debug_front_wg_marks(plans[i].handle, m.ctypes.data, ctypes.byref(G)) == 0
+            m = m[: B * G.value * 2].reshape(B, G.value, 2).astype(np.int64)
+            span.append((int(m[..., 0].min()), int(m[..., 1].max())))
+        # the two plans' last k_front launches (each at CU share 1: all four front
+        # lanes) were admitted one after the other: their spans do not overlap
+        (a0, a1), (b0, b1) = span
+        assert a1 <= b0 or b1 <= a0, (graphs, rnd, span)
 
 
 def test_front_lanes_follow_the_cu_share():

@@ -33,6 +33,19 @@ def one(mode: int) -> None:
         p.run(x, None, o, None)
         torch.cuda.synchronize()
         plans.append(p), ins.append(x), outs.append(o), refs.append(o.clone())
+    import ctypes
+    import numpy as np
+    from ndnet import _lib
+    for p in plans:  # per-workgroup k_front stamps: do the two launches overlap in time?
+        _lib.lib().ndnet_ndt_set_timing(p.handle, 2)
+
+    def span(p):
+        G = ctypes.c_int(0)
+        m = np.zeros(B * 256 * 2, np.uint64)
+        _lib.lib().ndnet_ndt_debug_front_wg_marks(p.handle, m.ctypes.data, ctypes.byref(G))
+        m = m[: B * G.value * 2].reshape(B, G.value, 2).astype(np.int64)
+        return int(m[..., 0].min()), int(m[..., 1].max())
+
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     for s in streams:
         s.wait_stream(torch.cuda.current_stream())
@@ -58,17 +71,21 @@ def one(mode: int) -> None:
         dt = time.time() - t0
         ok = [torch.equal(outs[i], refs[i]) for i in range(2)]
         rcs = [sorted({s.rc for s in p.host_stats()}) for p in plans]
-        print(f"mode {mode}: round {rnd}: {dt * 1e3:.1f} ms, rows equal {ok}, rcs {rcs}", flush=True)
+        (a0, a1), (b0, b1) = span(plans[0]), span(plans[1])
+        overlap = max(0, min(a1, b1) - max(a0, b0)) * 0.01  # 100 MHz ticks -> us
+        print(f"mode {mode}: round {rnd}: {dt * 1e3:.1f} ms, rows equal {ok}, rcs {rcs}, "
+              f"k_front spans {(a1 - a0) * 0.01:.1f} / {(b1 - b0) * 0.01:.1f} us, overlap {overlap:.1f} us", flush=True)
 
 
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", type=int, default=None)
+    ap.add_argument("--modes", type=int, nargs="*", default=None)
     a = ap.parse_args()
     if a.mode is not None:
         one(a.mode)
         return
-    for mode in (3, 1, 2, 4, 0):  # 0 (no admission) last: its concurrent share-1 replays wait out the barrier timeout
+    for mode in (a.modes or (3, 1, 2, 4, 0)):  # 0 (no admission) last: concurrent share-1 replays may wait out the barrier timeout
         r = subprocess.run([sys.executable, "-u", __file__, "--mode", str(mode)], capture_output=True, text=True,
                            timeout=120)
         tail = (r.stdout + r.stderr).strip().splitlines()[-6:]
