@@ -3460,8 +3460,23 @@ static hipError_t capture_event_node(hipStream_t st, hipEvent_t ev, bool wait) {
   return hipStreamUpdateCaptureDependencies(st, &node, 1, hipStreamSetCaptureDependencies);
 }
 
+// NDNET_FRONT_LANES=0 (A/B only, read once): no admission at all -- the round-4
+// behaviour, concurrent path-2 plans then need front_share >= N
+static bool lanes_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("NDNET_FRONT_LANES");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 template <typename T>
 static int front_launch(Plan* P, hipStream_t st, const T* pts, const FrontArgs& F) {
+  if (!lanes_enabled()) {
+    k_front<T><<<P->fG * P->B, kFrontThreads, P->flds, st>>>(pts, F);
+    HIPCHK(hipGetLastError());
+    return NDNET_OK;
+  }
   std::lock_guard<std::mutex> lk(g_lane_mu);  // waits, launch and records in one host order
   FrontLaneSet& L = g_lanes[P->dev];
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;

@@ -36,8 +36,10 @@ line() {  # the bench line's headline fields
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
 r = d.get("roofline", {})
+st = {k.split(" ")[0]: v for k, v in (d.get("stages_ms") or {}).items()}
+cl = {k: v.get("value") for k, v in (d.get("config_lines") or {}).items()}
 print(f"{sys.argv[1]:12s} {d['value']:10.1f} {d['unit']}  {d['ms_per_step']:.4f} ms/step  "
-      f"frac {r.get('frac')}  chains {r.get('all_chains', {}).get('ms')}")
+      f"frac {r.get('frac')}  chains {r.get('all_chains', {}).get('ms')}  stages {st}  {cl}")
 PY
 }
 
