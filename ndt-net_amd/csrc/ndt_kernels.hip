@@ -196,6 +196,7 @@ struct Plan {
   // k_front occupies, and the barrier-timeout flag k_front raises in host memory
   int dev;                    // the device the plan lives on
   int lane0, nlanes;          // lanes [lane0, lane0 + nlanes) mod kFrontLanes
+  hipEvent_t front_ev;        // records this plan's k_front launches (the lanes' admission)
   uint32_t* sync_fail_h;      // pinned host word (mapped): nonzero after a k_front barrier timeout
   uint32_t* sync_fail_d;      // its device address
 };
@@ -882,7 +883,8 @@ __host__ __device__ inline uint32_t wq_rt_entries(uint32_t heavy_t) {
 #ifdef NDNET_WQ_RTFULL  // A/B: the whole table whatever the threshold (round 1-4 form)
   return (uint32_t)kWqRt;
 #endif
-  return heavy_t < (uint32_t)kWqRt ? (heavy_t + 31u) & ~31u : (uint32_t)kWqRt;
+  // + 16: a light64 group's last block reads the pairs of up to 2 x 8 counts past its longest ND
+  return heavy_t + 16u < (uint32_t)kWqRt ? (heavy_t + 16u + 31u) & ~31u : (uint32_t)kWqRt;
 }
 constexpr int kWqHistMax = 64 * 1024;        // LDS class histograms up to this size, else global
 // Float input: a lane loads whole (x, y, z) records -- a quarter of its quad's
@@ -1453,6 +1455,10 @@ __global__ void __launch_bounds__(64) k_debug_lu_chain(const double* A, uint32_t
 #endif
 constexpr uint32_t kWqLightNDs = NDNET_WQ_LIGHT64 ? 64u : 16u;  // NDs per light item (one wave)
 constexpr int kL64B = 8;                                      // samples per register block
+static_assert(2 * kL64B <= 16, "wq_rt_entries' margin covers a light64 group's last blocks");
+#ifndef NDNET_WQ_L64_COALESCE
+#define NDNET_WQ_L64_COALESCE 1
+#endif
 constexpr size_t kWqRtBytes = NDNET_WQ_LIGHT64 ? sizeof(double2) : sizeof(double);  // LDS table entry
 constexpr uint32_t kWqHistNDs = NDNET_WQ_LIGHT64 ? kWqThreads : kWqNDs;            // NDs of a workgroup at once
 
@@ -1472,6 +1478,55 @@ __device__ __attribute__((always_inline)) inline void l64_load(L64Blk<T>& r, con
     r.v[u][1] = p[1];
     r.v[u][2] = p[2];
   }
+}
+
+// Float records, coalesced: a lane owning a whole ND reading its own records
+// sends the wave's 64 loads to 64 cache lines ~1.2 KB apart, and with four
+// waves per CU each holding a ring of 3 blocks the lines are evicted from the
+// 32 KB L1 before their next sample is read -- r05f: 490 cycles per sample
+// against ~132 of FP64 work (profiles/r05_wq_items_U.txt).  Here load k of a
+// block reads sample q0 + (lane & 7) of ND 8k + (lane >> 3): eight NDs' 96-byte
+// runs per instruction.  kL64Pitch dwords per ND row: conflict-free reads.
+constexpr int kL64Pitch = 3 * kL64B + 1;
+static_assert(64 * kL64Pitch * sizeof(float) <= 16 * kWqStageQ * sizeof(float), "a block fits a wave's stage rows");
+
+// the 8 NDs a lane loads for, as record offsets from the cloud's first record and last samples
+struct L64Src {
+  uint32_t off[8], last[8];
+};
+
+__device__ __attribute__((always_inline)) inline void l64_sload(L64Blk<float>& r, const float* __restrict__ cloud,
+                                                                const L64Src& s, uint32_t q0, uint32_t lane) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint32_t q0u = q0 + (lane & 7u);
+    const uint32_t q = q0u < s.last[k] ? q0u : s.last[k];
+    const float* p = cloud + 3u * (s.off[k] + q);
+    r.v[k][0] = p[0];
+    r.v[k][1] = p[1];
+    r.v[k][2] = p[2];
+  }
+}
+
+// the coalesced block (load k: ND 8k + lane / 8, sample lane % 8) -> the lane's own ND's 8 samples
+__device__ __attribute__((always_inline)) inline void l64_transpose(const L64Blk<float>& r, L64Blk<float>& x,
+                                                                    float* __restrict__ stg, uint32_t lane) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    float* w = stg + (8u * (uint32_t)k + (lane >> 3)) * kL64Pitch + 3u * (lane & 7u);
+    w[0] = r.v[k][0];
+    w[1] = r.v[k][1];
+    w[2] = r.v[k][2];
+  }
+  asm volatile("" ::: "memory");  // one wave's LDS operations complete in order
+  const float* rd = stg + lane * kL64Pitch;
+#pragma unroll
+  for (int u = 0; u < kL64B; u++) {
+    x.v[u][0] = rd[3 * u];
+    x.v[u][1] = rd[3 * u + 1];
+    x.v[u][2] = rd[3 * u + 2];
+  }
+  asm volatile("" ::: "memory");
 }
 
 // one block of kL64B samples of the lane's ND (kMask: some lane ends inside it)
@@ -1517,8 +1572,9 @@ __device__ __attribute__((always_inline)) inline void wq_light64(const CloudCtl*
                                                      uint64_t n, uint32_t ndcap, const double2* __restrict__ lrt2,
                                                      uint32_t rtn, const double2* __restrict__ rtab,
                                                      uint32_t* __restrict__ wq_hist, bool hist_lds,
-                                                     const WqChainArgs& CA, uint32_t lane,
-                                                     unsigned long long& t_mom, uint32_t& mx_out) {
+                                                     const WqChainArgs& CA, uint32_t lane, float* __restrict__ stg,
+                                                     unsigned long long& t_loop, unsigned long long& t_mom,
+                                                     uint32_t& mx_out) {
   const uint32_t nd = ctl[b].num_nds, heavy_t = ctl[b].heavy_t;
   const uint32_t d = wd0 + lane;
   const bool inr = d < nd;
@@ -1571,13 +1627,59 @@ __device__ __attribute__((always_inline)) inline void wq_light64(const CloudCtl*
     }
   };
   // a ring of register blocks: kR - 1 blocks in flight while one is folded
+  constexpr bool kCo = std::is_same<T, float>::value && NDNET_WQ_L64_COALESCE;  // coalesced loads + LDS transpose
   constexpr int kR = std::is_same<T, float>::value ? 3 : 2;
   L64Blk<T> rb[kR];
+  L64Src ss;
+  const T* const cloud = nd_pts + (uint64_t)b * n * 3;
+  if constexpr (kCo) {
 #pragma unroll
-  for (int i = 0; i < kR; i++) l64_load(rb[i], src, (uint32_t)(i * kL64B), last);
+    for (int k = 0; k < 8; k++) {
+      const int sl = 8 * k + (int)(lane >> 3);
+      ss.off[k] = (uint32_t)__shfl((int)beg, sl);
+      ss.last[k] = (uint32_t)__shfl((int)last, sl);
+    }
+  }
+  auto blk_load = [&](L64Blk<T>& r, uint32_t q0) __attribute__((always_inline)) {
+    if constexpr (kCo) l64_sload(r, cloud, ss, q0, lane);
+    else l64_load(r, src, q0, last);
+  };
+#pragma unroll
+  for (int i = 0; i < kR; i++) blk_load(rb[i], (uint32_t)(i * kL64B));
+  bool slow = false;  // the exact refold below for every live lane
+  t_loop = __builtin_amdgcn_s_memtime();  // timing level 2: the prologue is done
+  if constexpr (kCo) {
+    // The loop has no load under a branch and takes (rc, rl) from the LDS
+    // table only, so the compiler's waits stay counted: block i waits for its
+    // own loads, issued kR blocks earlier, with the later ones in flight.  (A
+    // conditional refill, or the global-table fallback's loads, left it one
+    // vmcnt(0) per block: every block paid a memory latency, r05g ~440 cycles
+    // per sample.)  A group past the table (a threshold raised between a
+    // front call and this one) takes the exact path.
+    if (mx + 2u * kL64B <= rtn) {
+      for (uint32_t q0 = 0; q0 < mx; q0 += kR * kL64B) {
+#pragma unroll
+        for (int i = 0; i < kR; i++) {
+          const uint32_t qb = q0 + (uint32_t)(i * kL64B);
+          if (qb < mx) {  // wave-uniform
+            double2 cr[kL64B];
+#pragma unroll
+            for (int u = 0; u < kL64B; u++) cr[u] = lrt2[qb + (uint32_t)u + 1u];
+            L64Blk<T> xb;
+            l64_transpose(rb[i], xb, stg, lane);
+            if (qb + kL64B <= full) l64_fold<T, false>(xb, cr, qb, cnt, m, m2, of, bad);
+            else l64_fold<T, true>(xb, cr, qb, cnt, m, m2, of, bad);
+          }
+          blk_load(rb[i], qb + kR * kL64B);
+        }
+      }
+    } else {
+      slow = true;
+    }
+  }
   double2 rr[kL64B];
-  ldr(rr, 0);
-  for (uint32_t q0 = 0; q0 < mx; q0 += kR * kL64B) {  // every branch below is wave-uniform
+  if constexpr (!kCo) ldr(rr, 0);
+  for (uint32_t q0 = 0; !kCo && q0 < mx; q0 += kR * kL64B) {  // every branch below is wave-uniform
 #pragma unroll
     for (int i = 0; i < kR; i++) {
       const uint32_t qb = q0 + (uint32_t)(i * kL64B);
@@ -1588,7 +1690,7 @@ __device__ __attribute__((always_inline)) inline void wq_light64(const CloudCtl*
       if (qb + kL64B < mx) ldr(rr, qb + kL64B);
       if (qb + kL64B <= full) l64_fold<T, false>(rb[i], cr, qb, cnt, m, m2, of, bad);
       else l64_fold<T, true>(rb[i], cr, qb, cnt, m, m2, of, bad);
-      if (qb + kR * kL64B < mx) l64_load(rb[i], src, qb + kR * kL64B, last);
+      if (qb + kR * kL64B < mx) blk_load(rb[i], qb + kR * kL64B);
     }
   }
   t_mom = __builtin_amdgcn_s_memtime();  // timing level 2: the moments are done
@@ -1597,7 +1699,7 @@ __device__ __attribute__((always_inline)) inline void wq_light64(const CloudCtl*
   if constexpr (std::is_same<T, float>::value)
     bad = live && !(fabs(m[0]) <= 0x1.fffffffffffffp+1023 && fabs(m[1]) <= 0x1.fffffffffffffp+1023 &&
                     fabs(m[2]) <= 0x1.fffffffffffffp+1023);
-  bad = bad && live;
+  bad = (bad || slow) && live;
   if (__any(bad) && bad) {  // the reference's exact steps (IEEE division, NaN -> 0 per off-diagonal step)
 #pragma unroll
     for (int a = 0; a < 3; a++) m[a] = m2[a] = of[a] = 0.0;
@@ -1800,12 +1902,12 @@ __global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const Cl
   }
   const int b = lo;
   if (NDNET_WQ_LIGHT64 && !hv) {  // 64 NDs, one per lane
-    unsigned long long t_mom = 0;
+    unsigned long long t_mom = 0, t_loop = 0;
     uint32_t lmx = 0;
     wq_light64<T>(ctl, b, (li - pre[b]) * kWqLightNDs, nd_pts, nd_lbl, nd_n, nd_base, nd_mean, nd_cov, nd_cls,
                   hist_all, ncls, n, ndcap, lrt2, rtn, rtab, wq_hist,
                   (size_t)kWqHistNDs * ((uint32_t)ncls + 1u) * sizeof(uint32_t) <= (size_t)kWqHistMax, CA, lane,
-                  t_mom, lmx);
+                  &wq_stage[(threadIdx.x >> 6) * 16][0], t_loop, t_mom, lmx);
     if (wq_marks && lane == 0) {
       unsigned long long* w = wq_marks + (uint64_t)item * kWqMarkW;
       w[0] = mk_rt;
@@ -1815,7 +1917,8 @@ __global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const Cl
       const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
       const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;
       w[4] = ((unsigned long long)xcc << 56) | ((unsigned long long)(lmx & 0xFFFFFFu) << 32) | hwid;
-      w[5] = w[6] = w[7] = 0;
+      w[5] = t_loop - mk_t0;  // light items: the prologue's cycles
+      w[6] = w[7] = 0;
     }
     continue;
   }
@@ -3226,6 +3329,9 @@ static hipError_t alloc(T** p, size_t count) {
   return hipMalloc((void**)p, (count ? count : 1) * sizeof(T));
 }
 
+static std::mutex g_lane_mu;
+static void front_lanes_forget(Plan* P);
+
 static void plan_free(Plan* P) {
   if (!P) return;
   if (P->ev_created)
@@ -3234,7 +3340,15 @@ static void plan_free(Plan* P) {
   if (P->wq_marks) (void)hipFree(P->wq_marks);
   if (P->fmarks) (void)hipFree(P->fmarks);
   if (P->sync_fail_h) (void)hipHostFree(P->sync_fail_h);
-  void* bufs[] = {P->flims, P->frec, P->fwgcnt, P->fbar, P->ctl, P->stamps, P->dense_of, P->vox, P->gbits, P->pkeys, P->did, P->bin_cnt, P->nd_base,
+  if (P->front_ev) {
+    (void)hipEventSynchronize(P->front_ev);
+    {
+      std::lock_guard<std::mutex> lk(g_lane_mu);
+      front_lanes_forget(P);
+    }
+    (void)hipEventDestroy(P->front_ev);
+  }
+  void* bufs[]= {P->flims, P->frec, P->fwgcnt, P->fbar, P->ctl, P->stamps, P->dense_of, P->vox, P->gbits, P->pkeys, P->did, P->bin_cnt, P->nd_base,
                   P->nd_pts, P->nd_lbl, P->nd_n,
                   P->nd_mean, P->nd_cov, P->nd_cov_post, P->nd_cls, P->hist, P->nb, P->keys, P->nkeys,
                   P->chain, P->chain_ps, P->chain_ok, P->slot_val, P->slot_flag, P->ev_val, P->ev_p, P->ev_q, P->ev_min,
@@ -3386,33 +3500,45 @@ static size_t merge_lds_bytes(const Plan* P) { return 2 * (size_t)P->nchunk * kC
 // graphs: the chip is split into kFrontLanes lanes of CUs / kFrontLanes; a
 // plan's k_front occupies ceil(kFrontLanes * workgroups / CUs) of them (all four
 // at CU share 1, two at share 2); before its launch the stream waits for the
-// last k_front recorded on each of its lanes, and after it the launch is
-// recorded on them (one event per lane and device; external event nodes when
-// the stream is being captured, so a replayed graph waits for the k_front
-// launches before it, whatever stream they ran on).  So the k_front launches in
-// flight at any time never want more workgroups than there are CUs, and grids
-// on disjoint lanes (two share-2 plans: the pipeline's NDT streams) still run
-// concurrently.  The other kernels never wait on anything, so they drain.
+// last k_front launched on each of its lanes, and after it the launch is
+// recorded in the plan's own event, which becomes those lanes' last launch
+// (explicit event graph nodes when the stream is being captured, so a replayed
+// graph waits for the k_front launches before it, whatever stream they ran
+// on).  A wait is left out when stream order already gives it (the lane's last
+// launch came from the same stream in the same capture, or both eager), and
+// lanes whose last launch shares an event are waited on once: one plan on one
+// stream -- the common case -- pays one event record per run and no waits
+// (round-5 r05e: four waits + four records per run cost 19 us of k_front
+// stage).  So the k_front launches in flight at any time never want more
+// workgroups than there are CUs, and grids on disjoint lanes (two share-2
+// plans: the pipeline's NDT streams) still run concurrently.  The other kernels
+// never wait on anything, so they drain.
 constexpr int kFrontLanes = 4;
 constexpr int kMaxDevices = 64;
 struct FrontLaneSet {
-  int init;
-  int next;  // the lane the next plan's lanes start at (round robin)
-  hipEvent_t ev[kFrontLanes];
+  int next;                          // the lane the next plan's lanes start at (round robin)
+  hipEvent_t ev[kFrontLanes];        // the event of the lane's last k_front launch (null: none yet)
+  hipStream_t st[kFrontLanes];       // the stream it was launched on
+  unsigned long long cap[kFrontLanes];  // the capture it was launched in (0: eager)
 };
-static std::mutex g_lane_mu;
 static FrontLaneSet g_lanes[kMaxDevices];
+
+// Drops a freed plan's event from the lanes (caller holds g_lane_mu; the
+// event has completed, so nothing left to wait for).
+static void front_lanes_forget(Plan* P) {
+  if (P->dev < 0 || P->dev >= kMaxDevices || !P->front_ev) return;
+  FrontLaneSet& L = g_lanes[P->dev];
+  for (int i = 0; i < kFrontLanes; i++)
+    if (L.ev[i] == P->front_ev) L.ev[i] = nullptr;
+}
 
 // Assigns the plan's lanes for its current k_front geometry (caller holds g_lane_mu).
 static hipError_t front_lanes_assign(Plan* P) {
   if (P->dev < 0 || P->dev >= kMaxDevices) return hipErrorInvalidDevice;
   FrontLaneSet& L = g_lanes[P->dev];
-  if (!L.init) {
-    for (int i = 0; i < kFrontLanes; i++) {
-      const hipError_t e = hipEventCreateWithFlags(&L.ev[i], hipEventDisableTiming);
-      if (e != hipSuccess) return e;
-    }
-    L.init = 1;
+  if (!P->front_ev) {
+    const hipError_t e = hipEventCreateWithFlags(&P->front_ev, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
   }
   const uint64_t wgs = (uint64_t)P->fG * (uint64_t)P->B;
   const int cus = P->cus > 0 ? P->cus : 1;
@@ -3480,22 +3606,37 @@ static int front_launch(Plan* P, hipStream_t st, const T* pts, const FrontArgs& 
   std::lock_guard<std::mutex> lk(g_lane_mu);  // waits, launch and records in one host order
   FrontLaneSet& L = g_lanes[P->dev];
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  HIPCHK(hipStreamIsCapturing(st, &cs));
+  unsigned long long cap_id = 0;
+  HIPCHK(hipStreamGetCaptureInfo(st, &cs, &cap_id));
   const bool cap = cs == hipStreamCaptureStatusActive;
+  if (!cap) cap_id = 0;
   const int mode = cap ? lane_capture_mode() : 3;
+  hipEvent_t waited[kFrontLanes];
+  int nw = 0;
   for (int i = 0; i < P->nlanes; i++) {
-    hipEvent_t ev = L.ev[(P->lane0 + i) % kFrontLanes];
+    const int l = (P->lane0 + i) % kFrontLanes;
+    hipEvent_t ev = L.ev[l];
+    if (!ev || (L.st[l] == st && L.cap[l] == cap_id)) continue;  // nothing yet / stream order covers it
+    bool dup = false;
+    for (int j = 0; j < nw; j++) dup |= waited[j] == ev;
+    if (dup) continue;
+    waited[nw++] = ev;
     if (!cap) HIPCHK(hipStreamWaitEvent(st, ev, 0));
     else if (mode == 1 || mode == 3) HIPCHK(hipStreamWaitEvent(st, ev, hipEventWaitExternal));
     else if (mode == 4) HIPCHK(capture_event_node(st, ev, true));
   }
   k_front<T><<<P->fG * P->B, kFrontThreads, P->flds, st>>>(pts, F);
   HIPCHK(hipGetLastError());
-  for (int i = 0; i < P->nlanes; i++) {
-    hipEvent_t ev = L.ev[(P->lane0 + i) % kFrontLanes];
-    if (!cap) HIPCHK(hipEventRecord(ev, st));
-    else if (mode == 2 || mode == 3) HIPCHK(hipEventRecordWithFlags(ev, st, hipEventRecordExternal));
-    else if (mode == 4) HIPCHK(capture_event_node(st, ev, false));
+  if (!cap) HIPCHK(hipEventRecord(P->front_ev, st));
+  else if (mode == 2 || mode == 3) HIPCHK(hipEventRecordWithFlags(P->front_ev, st, hipEventRecordExternal));
+  else if (mode == 4) HIPCHK(capture_event_node(st, P->front_ev, false));
+  if (!cap || mode == 2 || mode == 3 || mode == 4) {  // mode 0/1 captures record nothing: the lanes keep their last launch
+    for (int i = 0; i < P->nlanes; i++) {
+      const int l = (P->lane0 + i) % kFrontLanes;
+      L.ev[l] = P->front_ev;
+      L.st[l] = st;
+      L.cap[l] = cap_id;
+    }
   }
   return NDNET_OK;
 }

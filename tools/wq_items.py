@@ -42,7 +42,7 @@ _lib.check(_lib.lib().ndnet_ndt_set_timing(plan.handle, 2), "set_timing")
 cap = B * (int(1.2 * k) + 1 + (int(1.2 * k) + 1 + 15) // 16)  # the plan's item capacity (16-ND quads' bound)
 m = np.zeros(cap * 8, np.uint64)
 items = ctypes.c_uint32(0)
-per_sample_h, per_sample_l, epi_h, epi_l, spans, phases = [], [], [], [], [], []
+per_sample_h, per_sample_l, epi_h, epi_l, spans, phases, pro_l, loop_l = [], [], [], [], [], [], [], []
 for r in range(a.reps):
     plan.run(pts, None, out, None)
     torch.cuda.synchronize()
@@ -72,6 +72,8 @@ for r in range(a.reps):
     per_sample_l += list((t1 - t0)[~hv] / np.maximum(cnt[~hv], 1))
     epi_h += list((t2 - t1)[hv])
     epi_l += list((t2 - t1)[~hv])
+    pro_l += list(w[run, 5].astype(np.int64)[~hv])
+    loop_l += list(((t1 - t0) - w[run, 5].astype(np.int64))[~hv] / np.maximum(cnt[~hv], 1))
     if r == a.reps - 1:
         order = np.argsort(-(end_rt - start))[:8]
         print(f"items: {H} heavy + {light} light; span ~{spans[-1]:.1f} us (end stamps from the shader clock at 2.1 GHz)")
@@ -104,7 +106,7 @@ for r in range(a.reps):
               % (np.median(share), np.percentile(share, 90), share.max()))
         for lo_, hi_ in ((0, 0.05), (0.05, 0.5), (0.5, 1.0), (1.0, 9.0)):
             sel = (share >= lo_) & (share < hi_)
-            if sel.any():
+            if sel.any() and hv.any():
                 print(f"  sharing {lo_:.2f}-{hi_:.2f}: {sel.sum():4d} heavy items, cycles/sample median {np.median(cps[sel]):.1f}")
         top = np.argsort(-cnt * hv)[: min(8, int(hv.sum()))]
         for i in top:
@@ -125,6 +127,8 @@ _lib.lib().ndnet_ndt_set_timing(plan.handle, 0)
 q = lambda v: f"median {np.median(v):.1f} p90 {np.percentile(v, 90):.1f} max {np.max(v):.1f}" if len(v) else "-"  # noqa: E731
 print(f"cycles per sample, heavy items: {q(per_sample_h)}")
 print(f"cycles per sample (of the group's longest ND), light items: {q(per_sample_l)}")
+if pro_l:
+    print(f"light items: prologue cycles (item start -> first block) {q(pro_l)}; loop cycles per sample {q(loop_l)}")
 if phases and len(np.concatenate(phases)):
     P = np.concatenate(phases)
     print("heavy items, cycles per sample by phase (median): 0+2 loads/products %.1f, 1 mean recurrence + "
