@@ -883,8 +883,8 @@ __host__ __device__ inline uint32_t wq_rt_entries(uint32_t heavy_t) {
 #ifdef NDNET_WQ_RTFULL  // A/B: the whole table whatever the threshold (round 1-4 form)
   return (uint32_t)kWqRt;
 #endif
-  // + 16: a light64 group's last block reads the pairs of up to 2 x 8 counts past its longest ND
-  return heavy_t + 16u < (uint32_t)kWqRt ? (heavy_t + 16u + 31u) & ~31u : (uint32_t)kWqRt;
+  // + 32: a light64 group's last round reads the pairs of up to 3 x 8 counts past its longest ND
+  return heavy_t + 32u < (uint32_t)kWqRt ? (heavy_t + 32u + 31u) & ~31u : (uint32_t)kWqRt;
 }
 constexpr int kWqHistMax = 64 * 1024;        // LDS class histograms up to this size, else global
 // Float input: a lane loads whole (x, y, z) records -- a quarter of its quad's
@@ -1455,7 +1455,7 @@ __global__ void __launch_bounds__(64) k_debug_lu_chain(const double* A, uint32_t
 #endif
 constexpr uint32_t kWqLightNDs = NDNET_WQ_LIGHT64 ? 64u : 16u;  // NDs per light item (one wave)
 constexpr int kL64B = 8;                                      // samples per register block
-static_assert(2 * kL64B <= 16, "wq_rt_entries' margin covers a light64 group's last blocks");
+static_assert(4 * kL64B <= 32, "wq_rt_entries' margin covers a light64 group's last round (ring <= 4)");
 #ifndef NDNET_WQ_L64_COALESCE
 #define NDNET_WQ_L64_COALESCE 1
 #endif
@@ -1628,7 +1628,10 @@ __device__ __attribute__((always_inline)) inline void wq_light64(const CloudCtl*
   };
   // a ring of register blocks: kR - 1 blocks in flight while one is folded
   constexpr bool kCo = std::is_same<T, float>::value && NDNET_WQ_L64_COALESCE;  // coalesced loads + LDS transpose
-  constexpr int kR = std::is_same<T, float>::value ? 3 : 2;
+#ifndef NDNET_WQ_L64_RING
+#define NDNET_WQ_L64_RING 3
+#endif
+  constexpr int kR = std::is_same<T, float>::value ? NDNET_WQ_L64_RING : 2;
   L64Blk<T> rb[kR];
   L64Src ss;
   const T* const cloud = nd_pts + (uint64_t)b * n * 3;
@@ -1656,21 +1659,23 @@ __device__ __attribute__((always_inline)) inline void wq_light64(const CloudCtl*
     // vmcnt(0) per block: every block paid a memory latency, r05g ~440 cycles
     // per sample.)  A group past the table (a threshold raised between a
     // front call and this one) takes the exact path.
-    if (mx + 2u * kL64B <= rtn) {
-      for (uint32_t q0 = 0; q0 < mx; q0 += kR * kL64B) {
+    // whole rounds of kR blocks: a block past every lane's count folds x = mean
+    // (exact no-ops), so the round has no branch around its loads and waits
+    constexpr uint32_t kRound = (uint32_t)(kR * kL64B);
+    const uint32_t qend = (mx + kRound - 1u) / kRound * kRound;
+    if (qend < rtn) {
+      for (uint32_t q0 = 0; q0 < qend; q0 += kRound) {
 #pragma unroll
         for (int i = 0; i < kR; i++) {
           const uint32_t qb = q0 + (uint32_t)(i * kL64B);
-          if (qb < mx) {  // wave-uniform
-            double2 cr[kL64B];
+          double2 cr[kL64B];
 #pragma unroll
-            for (int u = 0; u < kL64B; u++) cr[u] = lrt2[qb + (uint32_t)u + 1u];
-            L64Blk<T> xb;
-            l64_transpose(rb[i], xb, stg, lane);
-            if (qb + kL64B <= full) l64_fold<T, false>(xb, cr, qb, cnt, m, m2, of, bad);
-            else l64_fold<T, true>(xb, cr, qb, cnt, m, m2, of, bad);
-          }
-          blk_load(rb[i], qb + kR * kL64B);
+          for (int u = 0; u < kL64B; u++) cr[u] = lrt2[qb + (uint32_t)u + 1u];
+          L64Blk<T> xb;
+          l64_transpose(rb[i], xb, stg, lane);
+          blk_load(rb[i], qb + kRound);
+          if (qb + kL64B <= full) l64_fold<T, false>(xb, cr, qb, cnt, m, m2, of, bad);
+          else l64_fold<T, true>(xb, cr, qb, cnt, m, m2, of, bad);
         }
       }
     } else {

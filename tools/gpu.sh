@@ -147,6 +147,13 @@ train)
   step graph 200 $OUT/train_graph.log python -u tools/bench_train.py --steps 20 --warmup 5 --graph
   tail -1 $OUT/train_graph.log
   ;;
+trtrace)  # kernel trace of the graphed train step + per-kernel summary
+  cd /tmp && export TMPDIR=/tmp
+  step trtrace 300 $OUT/trprof.log rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trprof -o run \
+    -- python3 $R/tools/bench_train.py --steps 10 --warmup 3 --graph
+  tail -1 $OUT/trprof.log | cut -c1-300
+  cd $R && python3 tools/trace_summary.py $OUT/trprof > $OUT/trprof_summary.txt && head -60 $OUT/trprof_summary.txt
+  ;;
 py)  # a python tool (e.g. tools/wq_items.py --kind L), output to gpurun_out/TAG/<tool>.txt
   NAME=$(basename ${1%.py})
   step $NAME 300 $OUT/$NAME.txt python -u "$@"

@@ -27,10 +27,12 @@ def main():
         k = m.group(1) if m else r["Kernel_Name"][:40]
         dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0)
     tot = 0.0
-    print(f"{'kernel':34s} {'n':>5s} {'median us':>10s} {'p10':>8s} {'p90':>8s}")
+    print(f"{'kernel':34s} {'n':>5s} {'median us':>10s} {'p10':>8s} {'p90':>8s} {'sum us':>9s}")
     for k, v in sorted(dur.items(), key=lambda kv: -np.median(kv[1][skip:] or kv[1]) * len(kv[1])):
         v = np.array(v[skip:] or v)
-        print(f"{k:34s} {len(v):5d} {np.median(v):10.1f} {np.percentile(v, 10):8.1f} {np.percentile(v, 90):8.1f}")
+        tot += v.sum()
+        print(f"{k:34s} {len(v):5d} {np.median(v):10.1f} {np.percentile(v, 10):8.1f} {np.percentile(v, 90):8.1f} {v.sum():9.1f}")
+    print(f"sum of kernel time {tot:.1f} us")
 
 
 def timeline(d, anchor="k_front", which=-2, span=1):
