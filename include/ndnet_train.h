@@ -101,7 +101,8 @@ int ndnet_row_argmax(const float *x, int64_t rows, int cols, int32_t *out, void 
 
 /* TNet FC heads in train mode (ndtnet.py:53-60: fc1 + bn4 + ReLU, fc2 + bn5 +
  * ReLU, fc3 + identity), B <= 16 rows (one per cloud), x [B][K] and W [N][K]
- * row-major (torch's Linear layout), K % 4 == 0, 16-byte aligned rows.
+ * row-major (torch's Linear layout), K % 4 == 0, 16-byte aligned rows, and
+ * B * K <= 16384 (x is staged whole in LDS: K <= 1024 at 16 rows).
  * Forward, one wave per output channel:
  *   y[b][n] = x[b] . W[n] + bias[n], + 1 where eye > 0 and n is a diagonal
  *   entry of the eye x eye transform (added after the bias, as torch adds the

@@ -1767,9 +1767,19 @@ __device__ __attribute__((always_inline)) inline void wq_light64(const CloudCtl*
     if (live) {
       for (uint32_t k = 0; k < nbins; k++) hist[k] = 0;
       if (hist_lds) {
-        for (uint32_t s = 0; s < cnt; s++)
-          if (l[s] < nbins) atomicAdd(&hist[l[s]], 1u);  // return-less LDS adds: no read-modify-write wait
-        __builtin_amdgcn_s_waitcnt(0xc07f);            // lgkmcnt(0)
+        // 32 labels in flight per lane (clamped loads, then the adds): one
+        // memory latency per 32 samples, not one per sample (r05k: the
+        // per-sample loop took 69 of the labelled launch's 106 us)
+        const uint32_t lastl = cnt - 1u;
+        for (uint32_t s0 = 0; s0 < cnt; s0 += 32) {
+          uint16_t v[32];
+#pragma unroll
+          for (int j = 0; j < 32; j++) v[j] = l[s0 + j < lastl ? s0 + j : lastl];
+#pragma unroll
+          for (int j = 0; j < 32; j++)
+            if (s0 + j < cnt && v[j] < nbins) atomicAdd(&hist[v[j]], 1u);  // return-less LDS adds
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
       } else {
         for (uint32_t s = 0; s < cnt; s++)
           if (l[s] < nbins) hist[l[s]]++;

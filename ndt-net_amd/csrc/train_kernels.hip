@@ -361,28 +361,26 @@ __global__ __launch_bounds__(256) void k_tr_gemm_x6(const float* __restrict__ A,
     }
 }
 
-// out[i] = part[0][i] + part[1][i] + ... in part order; 4 elements per thread,
-// eight parts' loads issued before their sums
+// out[i] = part[0][i] + part[1][i] + ... in part order; one element per
+// thread, up to 32 parts' loads issued before their sums (one memory latency
+// per launch at the weight gradients' <= 32 parts: round 4's 4 elements and 8
+// parts per round left the small layers' launches at 4 workgroups and 4
+// dependent rounds, 178 us a step over 19 launches, r05k)
+constexpr int kSumParts = 32;
 __global__ __launch_bounds__(256) void k_tr_sum_parts(const float* __restrict__ part, float* __restrict__ out,
                                                       int64_t count, int nparts) {
-  const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  if (i0 >= count) return;
-  const int w = (int)min<int64_t>(4, count - i0);
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int p0 = 0; p0 < nparts; p0 += 8) {
-    float v[8][4];
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= count) return;
+  float s = 0.0f;
+  for (int p0 = 0; p0 < nparts; p0 += kSumParts) {
+    float v[kSumParts];
 #pragma unroll
-    for (int u = 0; u < 8; u++)
+    for (int u = 0; u < kSumParts; u++) v[u] = p0 + u < nparts ? part[(int64_t)(p0 + u) * count + i] : 0.0f;
 #pragma unroll
-      for (int e = 0; e < 4; e++)
-        v[u][e] = (p0 + u < nparts && e < w) ? part[(int64_t)(p0 + u) * count + i0 + e] : 0.0f;
-#pragma unroll
-    for (int u = 0; u < 8; u++)
-#pragma unroll
-      for (int e = 0; e < 4; e++)
-        if (p0 + u < nparts) s[e] = (p0 + u == 0) ? v[u][e] : s[e] + v[u][e];
+    for (int u = 0; u < kSumParts; u++)
+      if (p0 + u < nparts) s = (p0 + u == 0) ? v[u] : s + v[u];
   }
-  for (int e = 0; e < w; e++) out[i0 + e] = s[e];
+  out[i] = s;
 }
 
 // sum over the workgroup in a fixed order (wave shuffles, then the waves in order)
@@ -754,7 +752,20 @@ __device__ inline double wave_sum_d(double v) {
 // TNet's fc3 + identity, ndtnet.py:59, added after the bias as torch does);
 // gamma != null: z = relu?(BatchNorm1d(y)) with batch statistics over the B
 // rows (double sums, biased variance; running stats with the unbiased one).
-__global__ __launch_bounds__(256) void k_tr_fc_fwd(const float* __restrict__ x, const float* __restrict__ W,
+constexpr int kFcWaves = 8;           // channels in flight per workgroup (a wave each)
+constexpr int kFcMaxLds = 64 * 1024;  // the staged input rows: B x K floats
+
+// The workgroup's input rows x [B][K] staged in LDS with float4 loads (one
+// memory latency), then each wave's weight row loaded whole (<= 4 float4 per
+// lane, issued together) -- round 5: a wave reading its own copy of x from L2
+// K / 256 times in sequence took 12.7 us per launch (r05k trace).
+__device__ inline void fc_stage_x(f32x4* s_x, const float* __restrict__ x, int Bn, int K4) {
+  const f32x4* xv = reinterpret_cast<const f32x4*>(x);
+  for (int e = threadIdx.x; e < Bn * K4; e += kFcWaves * 64) s_x[e] = xv[e];
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kFcWaves * 64) void k_tr_fc_fwd(const float* __restrict__ x, const float* __restrict__ W,
                                                    const float* __restrict__ bias, float* __restrict__ y,
                                                    float* __restrict__ z, float* __restrict__ mean,
                                                    float* __restrict__ invstd, float* __restrict__ rmean,
@@ -762,105 +773,117 @@ __global__ __launch_bounds__(256) void k_tr_fc_fwd(const float* __restrict__ x, 
                                                    const float* __restrict__ beta, int Bn, int K, int N, float eps,
                                                    float momentum, int relu, int eye,
                                                    long long* __restrict__ batches_tracked) {
+  extern __shared__ f32x4 s_x[];  // [Bn][K / 4]
   const int lane = threadIdx.x & 63;
-  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int K4 = K / 4;
   if (batches_tracked && blockIdx.x == 0 && threadIdx.x == 0) batches_tracked[0] += 1;
-  if (n >= N) return;
-  const f32x4* w = reinterpret_cast<const f32x4*>(W + (int64_t)n * K);
-  float acc[kFcB];
+  fc_stage_x(s_x, x, Bn, K4);
+  for (int n = blockIdx.x * kFcWaves + (threadIdx.x >> 6); n < N; n += gridDim.x * kFcWaves) {
+    const f32x4* w = reinterpret_cast<const f32x4*>(W + (int64_t)n * K);
+    float acc[kFcB];
 #pragma unroll
-  for (int b = 0; b < kFcB; b++) acc[b] = 0.0f;
-  for (int f = lane; f < K / 4; f += 64) {
-    const f32x4 wv = w[f];
+    for (int b = 0; b < kFcB; b++) acc[b] = 0.0f;
+    for (int f0 = 0; f0 < K4; f0 += 256) {  // (one round for K <= 1024)
+      f32x4 wv[4];
 #pragma unroll
-    for (int b = 0; b < kFcB; b++) {
-      const f32x4 xv = reinterpret_cast<const f32x4*>(x + (int64_t)(b < Bn ? b : 0) * K)[f];
-      const f32x4 p = xv * wv;
-      acc[b] += (p[0] + p[1]) + (p[2] + p[3]);
+      for (int i = 0; i < 4; i++) {
+        const int f = f0 + lane + 64 * i;
+        if (f < K4) wv[i] = w[f];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int f = f0 + lane + 64 * i;
+        if (f >= K4) break;
+#pragma unroll
+        for (int b = 0; b < kFcB; b++) {
+          const f32x4 xv = s_x[(b < Bn ? b : 0) * K4 + f];
+          const f32x4 pr = xv * wv[i];
+          acc[b] += (pr[0] + pr[1]) + (pr[2] + pr[3]);
+        }
+      }
     }
-  }
-  const int row = (lane >> 2) & 15;  // the row this lane holds after the reduction
-  float v = fc_reduce16(acc, lane) + bias[n];
-  if (eye > 0 && n < eye * eye && n % (eye + 1) == 0) v += 1.0f;
-  const bool mine = (lane & 3) == 0 && row < Bn;
-  if (!gamma) {
-    if (mine) z[(int64_t)row * N + n] = v;
-    return;
-  }
-  const double mu = wave_sum_d(mine ? (double)v : 0.0) / (double)Bn;
-  const double dv = (double)v - mu;
-  const double var = wave_sum_d(mine ? dv * dv : 0.0) / (double)Bn;
-  const float inv = (float)(1.0 / sqrt(var + (double)eps));
-  const float fm = (float)mu;
-  if (lane == 0) {
-    mean[n] = fm;
-    invstd[n] = inv;
-    if (rmean) rmean[n] = (1.0f - momentum) * rmean[n] + momentum * fm;
-    if (rvar) {
-      const double unb = Bn > 1 ? var * (double)Bn / (double)(Bn - 1) : var;
-      rvar[n] = (1.0f - momentum) * rvar[n] + momentum * (float)unb;
+    const int row = (lane >> 2) & 15;  // the row this lane holds after the reduction
+    float v = fc_reduce16(acc, lane) + bias[n];
+    if (eye > 0 && n < eye * eye && n % (eye + 1) == 0) v += 1.0f;
+    const bool mine = (lane & 3) == 0 && row < Bn;
+    if (!gamma) {
+      if (mine) z[(int64_t)row * N + n] = v;
+      continue;
     }
-  }
-  float o = bn_apply(v, fm, inv, gamma[n], beta[n]);
-  if (relu) o = fmaxf(o, 0.0f);
-  if (mine) {
-    y[(int64_t)row * N + n] = v;
-    z[(int64_t)row * N + n] = o;
+    const double mu = wave_sum_d(mine ? (double)v : 0.0) / (double)Bn;
+    const double dv = (double)v - mu;
+    const double var = wave_sum_d(mine ? dv * dv : 0.0) / (double)Bn;
+    const float inv = (float)(1.0 / sqrt(var + (double)eps));
+    const float fm = (float)mu;
+    if (lane == 0) {
+      mean[n] = fm;
+      invstd[n] = inv;
+      if (rmean) rmean[n] = (1.0f - momentum) * rmean[n] + momentum * fm;
+      if (rvar) {
+        const double unb = Bn > 1 ? var * (double)Bn / (double)(Bn - 1) : var;
+        rvar[n] = (1.0f - momentum) * rvar[n] + momentum * (float)unb;
+      }
+    }
+    float o = bn_apply(v, fm, inv, gamma[n], beta[n]);
+    if (relu) o = fmaxf(o, 0.0f);
+    if (mine) {
+      y[(int64_t)row * N + n] = v;
+      z[(int64_t)row * N + n] = o;
+    }
   }
 }
 
 // Backward through BatchNorm (+ ReLU mask) of channel n and its weight row:
 // dpre[b][n] (the gradient of y), db[n] = sum_b dpre, dgamma / dbeta, and
 // dW[n][k] = sum_b dpre[b][n] x[b][k] in row order.  gamma == null: dpre = dz.
-__global__ __launch_bounds__(256) void k_tr_fc_bwd_w(const float* __restrict__ dz, const float* __restrict__ x,
+__global__ __launch_bounds__(kFcWaves * 64) void k_tr_fc_bwd_w(const float* __restrict__ dz, const float* __restrict__ x,
                                                      const float* __restrict__ y, const float* __restrict__ mean,
                                                      const float* __restrict__ invstd,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      float* __restrict__ dpre, float* __restrict__ dW,
                                                      float* __restrict__ db, float* __restrict__ dgamma,
                                                      float* __restrict__ dbeta, int Bn, int K, int N, int relu) {
+  extern __shared__ f32x4 s_x[];  // [Bn][K / 4] (dW only)
   const int lane = threadIdx.x & 63;
-  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (n >= N) return;
-  const bool mine = lane < Bn;  // lane b: row b
-  float d = 0.0f;
-  if (!gamma) {
-    d = mine ? dz[(int64_t)lane * N + n] : 0.0f;
-  } else {
-    const float mu = mean[n], inv = invstd[n], gm = gamma[n], bt = beta[n];
-    float g = 0.0f, xh = 0.0f;
-    if (mine) {
-      const float yv = y[(int64_t)lane * N + n];
-      g = dz[(int64_t)lane * N + n];
-      if (relu && !(bn_apply(yv, mu, inv, gm, bt) > 0.0f)) g = 0.0f;
-      xh = (yv - mu) * inv;
-    }
-    const double sg = wave_sum_d(g), sgx = wave_sum_d((double)g * xh);
-    const float k1 = (float)(sg / (double)Bn), k2 = (float)(sgx / (double)Bn);
-    if (mine) d = gm * inv * (g - k1 - xh * k2);
-    if (lane == 0) {
-      if (dgamma) dgamma[n] = (float)sgx;
-      if (dbeta) dbeta[n] = (float)sg;
-    }
-  }
-  const double sd = wave_sum_d(d);
-  if (lane == 0 && db) db[n] = (float)sd;
-  if (mine && dpre) dpre[(int64_t)lane * N + n] = d;
-  if (!dW) return;
-  float dv[kFcB];
-#pragma unroll
-  for (int b = 0; b < kFcB; b++) dv[b] = __shfl(d, b);  // 0 past the rows
-  f32x4* wrow = reinterpret_cast<f32x4*>(dW + (int64_t)n * K);
-  for (int f = lane; f < K / 4; f += 64) {
-    f32x4 s = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int b = 0; b < kFcB; b++) {
-      if (b < Bn) {
-        const f32x4 xv = reinterpret_cast<const f32x4*>(x + (int64_t)b * K)[f];
-        s = s + xv * dv[b];
+  const int K4 = K / 4;
+  if (dW) fc_stage_x(s_x, x, Bn, K4);
+  for (int n = blockIdx.x * kFcWaves + (threadIdx.x >> 6); n < N; n += gridDim.x * kFcWaves) {
+    const bool mine = lane < Bn;  // lane b: row b
+    float d = 0.0f;
+    if (!gamma) {
+      d = mine ? dz[(int64_t)lane * N + n] : 0.0f;
+    } else {
+      const float mu = mean[n], inv = invstd[n], gm = gamma[n], bt = beta[n];
+      float g = 0.0f, xh = 0.0f;
+      if (mine) {
+        const float yv = y[(int64_t)lane * N + n];
+        g = dz[(int64_t)lane * N + n];
+        if (relu && !(bn_apply(yv, mu, inv, gm, bt) > 0.0f)) g = 0.0f;
+        xh = (yv - mu) * inv;
+      }
+      const double sg = wave_sum_d(g), sgx = wave_sum_d((double)g * xh);
+      const float k1 = (float)(sg / (double)Bn), k2 = (float)(sgx / (double)Bn);
+      if (mine) d = gm * inv * (g - k1 - xh * k2);
+      if (lane == 0) {
+        if (dgamma) dgamma[n] = (float)sgx;
+        if (dbeta) dbeta[n] = (float)sg;
       }
     }
-    wrow[f] = s;
+    const double sd = wave_sum_d(d);
+    if (lane == 0 && db) db[n] = (float)sd;
+    if (mine && dpre) dpre[(int64_t)lane * N + n] = d;
+    if (!dW) continue;
+    float dv[kFcB];
+#pragma unroll
+    for (int b = 0; b < kFcB; b++) dv[b] = __shfl(d, b);  // 0 past the rows
+    f32x4* wrow = reinterpret_cast<f32x4*>(dW + (int64_t)n * K);
+    for (int f = lane; f < K4; f += 64) {
+      f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int b = 0; b < kFcB; b++)
+        if (b < Bn) sacc = sacc + s_x[b * K4 + f] * dv[b];
+      wrow[f] = sacc;
+    }
   }
 }
 
@@ -882,7 +905,17 @@ __global__ __launch_bounds__(256) void k_tr_fc_bwd_x(const float* __restrict__ d
   float acc[kFcB];
 #pragma unroll
   for (int b = 0; b < kFcB; b++) acc[b] = 0.0f;
-  for (int nn = n0; nn < n1; nn++) {
+  int nn = n0;
+  for (; nn + 8 <= n1; nn += 8) {  // 8 weight loads in flight, summed in channel order
+    float wv[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) wv[j] = W[(int64_t)(nn + j) * K + k];
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+#pragma unroll
+      for (int b = 0; b < kFcB; b++) acc[b] = fmaf(s_d[nn + j - n0][b], wv[j], acc[b]);
+  }
+  for (; nn < n1; nn++) {
     const float wv = W[(int64_t)nn * K + k];
 #pragma unroll
     for (int b = 0; b < kFcB; b++) acc[b] = fmaf(s_d[nn - n0][b], wv, acc[b]);
@@ -1015,7 +1048,7 @@ extern "C" int ndnet_tr_gemm(const float* A, const float* B, float* C, const flo
 
 extern "C" int ndnet_tr_sum_parts(const float* part, float* out, int64_t count, int nparts, void* stream) {
   if (!part || !out || count <= 0 || nparts <= 0) return -20;
-  const int64_t blocks = (count + 1023) / 1024;
+  const int64_t blocks = (count + 255) / 256;
   if (blocks > (int64_t)INT32_MAX) return -20;
   k_tr_sum_parts<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(part, out, count, nparts);
   return launched();
@@ -1078,6 +1111,13 @@ extern "C" int ndnet_row_argmax(const float* x, int64_t rows, int cols, int32_t*
   return launched();
 }
 
+// workgroups of the FC kernels: a wave per channel, at most 256 workgroups
+// (each stages x once; the waves loop over the channels past the grid)
+static unsigned fc_grid(int N) {
+  const int g = (N + kFcWaves - 1) / kFcWaves;
+  return (unsigned)(g < 256 ? g : 256);
+}
+
 extern "C" int ndnet_tr_fc_fwd(const float* x, const float* W, const float* bias, float* y, float* z, float* mean,
                                float* invstd, float* running_mean, float* running_var, const float* gamma,
                                const float* beta, int B, int K, int N, float eps, float momentum, int relu, int eye,
@@ -1086,7 +1126,9 @@ extern "C" int ndnet_tr_fc_fwd(const float* x, const float* W, const float* bias
   if (gamma && (!y || !mean || !invstd || !beta)) return -20;
   if (!gamma && (relu || batches_tracked)) return -20;
   if ((((uintptr_t)x | (uintptr_t)W) & 15) != 0) return -20;  // float4 rows
-  k_tr_fc_fwd<<<(N + 3) / 4, 256, 0, (hipStream_t)stream>>>(x, W, bias, y, z, mean, invstd, running_mean,
+  const size_t lds = (size_t)B * K * sizeof(float);
+  if (lds > (size_t)kFcMaxLds) return -20;  // x staged whole (K <= 1024 at 16 rows)
+  k_tr_fc_fwd<<<fc_grid(N), kFcWaves * 64, lds, (hipStream_t)stream>>>(x, W, bias, y, z, mean, invstd, running_mean,
                                                               running_var, gamma, beta, B, K, N, eps, momentum, relu,
                                                               eye, reinterpret_cast<long long*>(batches_tracked));
   return launched();
@@ -1099,7 +1141,9 @@ extern "C" int ndnet_tr_fc_bwd_w(const float* dz, const float* x, const float* y
   if (gamma && (!y || !mean || !invstd || !beta)) return -20;
   if (!gamma && relu) return -20;
   if ((((uintptr_t)x | (uintptr_t)dW) & 15) != 0) return -20;
-  k_tr_fc_bwd_w<<<(N + 3) / 4, 256, 0, (hipStream_t)stream>>>(dz, x, y, mean, invstd, gamma, beta, dpre, dW, db,
+  const size_t lds = dW ? (size_t)B * K * sizeof(float) : 0;
+  if (lds > (size_t)kFcMaxLds) return -20;
+  k_tr_fc_bwd_w<<<fc_grid(N), kFcWaves * 64, lds, (hipStream_t)stream>>>(dz, x, y, mean, invstd, gamma, beta, dpre, dW, db,
                                                                 dgamma, dbeta, B, K, N, relu);
   return launched();
 }
@@ -1112,7 +1156,7 @@ extern "C" int ndnet_tr_fc_bwd_x(const float* dpre, const float* W, float* dx, f
   k_tr_fc_bwd_x<<<dim3((K + 255) / 256, nsplit), 256, 0, (hipStream_t)stream>>>(dpre, W, out, B, K, N, nsplit);
   if (nsplit > 1) {
     const int64_t count = (int64_t)B * K;
-    k_tr_sum_parts<<<(unsigned)((count + 1023) / 1024), 256, 0, (hipStream_t)stream>>>(part, dx, count, nsplit);
+    k_tr_sum_parts<<<(unsigned)((count + 255) / 256), 256, 0, (hipStream_t)stream>>>(part, dx, count, nsplit);
   }
   return launched();
 }

@@ -51,10 +51,12 @@ def _hip_train(conv: nn.Conv1d, bn, x: torch.Tensor) -> bool:
 
 def _hip_fc(t: "TNet", g: torch.Tensor) -> bool:
     """The TNet head on the HIP FC kernels: train mode, fp32 on the GPU, at most
-    16 clouds (train_hip.FC_MAX_ROWS), every layer's sizes a multiple of 4."""
+    16 clouds (train_hip.FC_MAX_ROWS), every layer's input width a multiple of
+    4 and its rows small enough for the kernels' LDS stage (B * K <= 16384)."""
     return (_hip_train(t.conv1, t.bn1, g) and t.fc1.training and t.bn4.training and t.bn5.training
-            and 2 <= g.shape[0] <= 16 and g.dim() == 2 and all(fc.weight.dtype == torch.float32 and
-                                                                 fc.in_features % 4 == 0 for fc in (t.fc1, t.fc2, t.fc3)))
+            and 2 <= g.shape[0] <= 16 and g.dim() == 2
+            and all(fc.weight.dtype == torch.float32 and fc.in_features % 4 == 0
+                    and g.shape[0] * fc.in_features <= 16384 for fc in (t.fc1, t.fc2, t.fc3)))
 
 
 def _block_pool(conv: nn.Conv1d, bn, x: torch.Tensor, relu: bool) -> torch.Tensor:
