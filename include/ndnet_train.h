@@ -128,6 +128,31 @@ int ndnet_tr_fc_bwd_w(const float *dz, const float *x, const float *y, const flo
 int ndnet_tr_fc_bwd_x(const float *dpre, const float *W, float *dx, float *part, int B, int K, int N, int nsplit,
                       void *stream);
 
+/* The seg head's log_softmax over the class dim (ndtnet.py:241; x, out
+ * [B][C][N]) and its backward (dx = dy - exp(y) sum_c dy, y the forward's
+ * output); the training loss -sum(gt * logp) / (B N) of the one-hot target gt
+ * [B][N][C] (ndnet.training.segmentation_loss) -- part: (B N + 63) / 64
+ * doubles of scratch, summed in a fixed order -- and its gradient
+ * dlogp[b][c][n] = -gt[b][n][c] dloss / (B N) (dloss a 1-element device
+ * tensor); C <= 32. */
+int ndnet_tr_log_softmax_c(const float *x, float *out, int B, int C, int N, void *stream);
+int ndnet_tr_log_softmax_c_bwd(const float *y, const float *dy, float *dx, int B, int C, int N, void *stream);
+int ndnet_tr_nll_onehot(const float *logp, const float *gt, double *part, float *loss, int B, int C, int N,
+                        void *stream);
+int ndnet_tr_nll_onehot_bwd(const float *gt, const float *dloss, float *dlogp, int B, int C, int N, void *stream);
+
+/* Adam, torch.optim.Adam's fused capturable form (tools/train.py's
+ * optimizer): for each of the n tensors i, steps[i][0] += 1 (device float,
+ * torch's capturable step state), then m = b1 m + (1 - b1) g, v = b2 v +
+ * (1 - b2) g^2, p -= (lr / (1 - b1^t)) m / (sqrt(v) / sqrt(1 - b2^t) + eps)
+ * with t the new step and lr a device float (g += wd p first when
+ * weight_decay != 0).  The arrays are host arrays of device pointers; the
+ * launches take them by value (graph-capturable, no table upload).  The betas
+ * come as doubles: 1 - beta is rounded from double, as torch's kernel gets it. */
+int ndnet_tr_adam(int n, float *const *params, const float *const *grads, float *const *exp_avg,
+                  float *const *exp_avg_sq, float *const *steps, const int64_t *numel, const float *lr, double beta1,
+                  double beta2, float eps, float weight_decay, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1574,7 +1574,7 @@ __device__ __attribute__((always_inline)) inline void wq_light64(const CloudCtl*
                                                      uint32_t* __restrict__ wq_hist, bool hist_lds,
                                                      const WqChainArgs& CA, uint32_t lane, float* __restrict__ stg,
                                                      unsigned long long& t_loop, unsigned long long& t_mom,
-                                                     uint32_t& mx_out) {
+                                                     unsigned long long& t_lbl, uint32_t& mx_out) {
   const uint32_t nd = ctl[b].num_nds, heavy_t = ctl[b].heavy_t;
   const uint32_t d = wd0 + lane;
   const bool inr = d < nd;
@@ -1760,30 +1760,71 @@ __device__ __attribute__((always_inline)) inline void wq_light64(const CloudCtl*
     __hip_atomic_store(&CA.nkeys[o], mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   // labelled runs: the ND's class histogram (first index of the max, normal_distributions.c:107-121)
+  const unsigned long long t_l0 = __builtin_amdgcn_s_memtime();
   if (nd_lbl) {
     const uint32_t nbins = (uint32_t)ncls + 1u;
     const uint16_t* l = nd_lbl + (uint64_t)b * n + beg;
     uint32_t* hist = hist_lds ? wq_hist + (threadIdx.x & (kWqThreads - 1)) * nbins : hist_all + o * nbins;
-    if (live) {
+    if (live)
       for (uint32_t k = 0; k < nbins; k++) hist[k] = 0;
-      if (hist_lds) {
-        // 32 labels in flight per lane (clamped loads, then the adds): one
-        // memory latency per 32 samples, not one per sample (r05k: the
-        // per-sample loop took 69 of the labelled launch's 106 us)
-        const uint32_t lastl = cnt - 1u;
-        for (uint32_t s0 = 0; s0 < cnt; s0 += 32) {
-          uint16_t v[32];
+    if (hist_lds) {
+      // Coalesced, as the records: load k of a 32-sample block reads samples
+      // q0 .. q0 + 31 of NDs 2k and 2k + 1 (lanes 0..31, 32..63: one or two
+      // 64-byte runs per instruction), staged in the wave's rows (pitch
+      // kLblPitch dwords: conflict-free reads), then each lane counts its own
+      // ND's 32 with return-less LDS adds.  (Per-lane loads sent each
+      // instruction to 64 lines: ~225 cycles per sample, r05m.)
+      constexpr uint32_t kLblPitch = 17;  // dwords per ND row (32 labels + 1)
+      static_assert(64 * kLblPitch * 4 <= 16 * kWqStageQ * sizeof(float), "label block fits the stage rows");
+      const uint16_t* lc = nd_lbl + (uint64_t)b * n;
+      uint16_t* st16 = reinterpret_cast<uint16_t*>(stg);
+      const uint32_t* st32 = reinterpret_cast<const uint32_t*>(stg) + lane * kLblPitch;
+      const uint32_t lastl = cnt ? cnt - 1u : 0u;
+      const uint32_t half = lane >> 5, ql = lane & 31u;
+      // two 32-sample blocks in registers: block j + 1's loads are in flight
+      // while block j is staged and counted (one exposed latency per item,
+      // not per block: 34k cycles per light item before, r05o)
+      auto ld = [&](uint16_t (&v)[32], uint32_t q0) __attribute__((always_inline)) {
 #pragma unroll
-          for (int j = 0; j < 32; j++) v[j] = l[s0 + j < lastl ? s0 + j : lastl];
-#pragma unroll
-          for (int j = 0; j < 32; j++)
-            if (s0 + j < cnt && v[j] < nbins) atomicAdd(&hist[v[j]], 1u);  // return-less LDS adds
+        for (int k = 0; k < 32; k++) {
+          const uint32_t b0 = __builtin_amdgcn_readlane(beg, 2 * k), b1 = __builtin_amdgcn_readlane(beg, 2 * k + 1);
+          const uint32_t e0 = __builtin_amdgcn_readlane(lastl, 2 * k), e1 = __builtin_amdgcn_readlane(lastl, 2 * k + 1);
+          const uint32_t bb = half ? b1 : b0, ee = half ? e1 : e0;
+          const uint32_t q = q0 + ql < ee ? q0 + ql : ee;
+          v[k] = lc[bb + q];
         }
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-      } else {
-        for (uint32_t s = 0; s < cnt; s++)
-          if (l[s] < nbins) hist[l[s]]++;
+      };
+      auto count = [&](const uint16_t (&v)[32], uint32_t q0) __attribute__((always_inline)) {
+        asm volatile("" ::: "memory");  // the previous block's reads are issued (one wave's LDS ops run in order)
+#pragma unroll
+        for (int k = 0; k < 32; k++) st16[2u * ((2u * (uint32_t)k + half) * kLblPitch) + ql] = v[k];
+        asm volatile("" ::: "memory");
+        uint32_t w[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) w[i] = st32[i];
+        asm volatile("" ::: "memory");
+        if (live) {
+#pragma unroll
+          for (int j = 0; j < 32; j++) {
+            const uint32_t lb = (w[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+            if (q0 + (uint32_t)j < cnt && lb < nbins) atomicAdd(&hist[lb], 1u);  // return-less LDS adds
+          }
+        }
+      };
+      uint16_t va[32], vb[32];
+      ld(va, 0);
+      for (uint32_t q0 = 0; q0 < mx; q0 += 64) {  // wave-uniform; loads past mx are clamped (unused)
+        ld(vb, q0 + 32);
+        count(va, q0);
+        ld(va, q0 + 64);
+        if (q0 + 32 < mx) count(vb, q0 + 32);
       }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    } else if (live) {
+      for (uint32_t s = 0; s < cnt; s++)
+        if (l[s] < nbins) hist[l[s]]++;
+    }
+    if (live) {
       uint32_t best = 0;
       uint16_t cls = 0;
       for (uint32_t k = 0; k < nbins; k++) {
@@ -1798,6 +1839,7 @@ __device__ __attribute__((always_inline)) inline void wq_light64(const CloudCtl*
   } else if (live) {
     nd_cls[o] = 0;
   }
+  t_lbl = __builtin_amdgcn_s_memtime() - t_l0;  // timing level 2: the class histogram's cycles
   if (!grp_heavy) {
     if (live) wq_lu_chain(CA, b, d, nd, ndcap, S, __popc(mask));
     return;
@@ -1917,12 +1959,12 @@ __global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const Cl
   }
   const int b = lo;
   if (NDNET_WQ_LIGHT64 && !hv) {  // 64 NDs, one per lane
-    unsigned long long t_mom = 0, t_loop = 0;
+    unsigned long long t_mom = 0, t_loop = 0, t_lbl = 0;
     uint32_t lmx = 0;
     wq_light64<T>(ctl, b, (li - pre[b]) * kWqLightNDs, nd_pts, nd_lbl, nd_n, nd_base, nd_mean, nd_cov, nd_cls,
                   hist_all, ncls, n, ndcap, lrt2, rtn, rtab, wq_hist,
                   (size_t)kWqHistNDs * ((uint32_t)ncls + 1u) * sizeof(uint32_t) <= (size_t)kWqHistMax, CA, lane,
-                  &wq_stage[(threadIdx.x >> 6) * 16][0], t_loop, t_mom, lmx);
+                  &wq_stage[(threadIdx.x >> 6) * 16][0], t_loop, t_mom, t_lbl, lmx);
     if (wq_marks && lane == 0) {
       unsigned long long* w = wq_marks + (uint64_t)item * kWqMarkW;
       w[0] = mk_rt;
@@ -1933,7 +1975,8 @@ __global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const Cl
       const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;
       w[4] = ((unsigned long long)xcc << 56) | ((unsigned long long)(lmx & 0xFFFFFFu) << 32) | hwid;
       w[5] = t_loop - mk_t0;  // light items: the prologue's cycles
-      w[6] = w[7] = 0;
+      w[6] = t_lbl;           // and the class histogram's
+      w[7] = 0;
     }
     continue;
   }

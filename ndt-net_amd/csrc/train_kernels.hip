@@ -480,7 +480,10 @@ __global__ __launch_bounds__(T) void k_tr_bn_fwd(const float* __restrict__ y, fl
   }
   const float fm = (float)mu, g = gamma[c], bt = beta[c];
   // pool mode: no z; this thread's running max per cloud (its elements visit the
-  // clouds in order), merged into pk when the cloud changes
+  // clouds in order), merged into pk when the cloud changes.  (A wave-level
+  // merge -- the leaving lanes' maxima reduced over the wave, one atomic --
+  // measured slower: 39 -> 46 us per 1024-channel launch, r05o; the per-lane
+  // atomics cost ~10 of the 39, NDNET_TR_EXP_NOPOOLATOMIC, r05n.)
   unsigned long long best = 0ull;
   int cur = -1;
   auto emit = [&](const ChanWalk<T>& w, float o) {
@@ -489,7 +492,9 @@ __global__ __launch_bounds__(T) void k_tr_bn_fwd(const float* __restrict__ y, fl
       return;
     }
     if (w.b != cur) {
+#ifndef NDNET_TR_EXP_NOPOOLATOMIC  // timing experiment only (wrong pooled values): no LDS atomics
       if (cur >= 0) atomicMax(&pk[cur], best);
+#endif
       cur = w.b;
       best = 0ull;
     }
@@ -544,6 +549,19 @@ __global__ __launch_bounds__(T) void k_tr_bn_bwd(const float* __restrict__ dz, c
   const float mu = mean[c], inv = invstd[c], gm = gamma[c], bt = beta[c];
   float gv[kCache], xv[kCache];
   double sg = 0.0, sgx = 0.0;
+  // pool mode: the channel's per-cloud argmax and pooled gradient, staged once
+  // (the element loop read both from global memory per element: three vector
+  // loads per element instead of one)
+  __shared__ int s_pidx[kPoolMaxB];
+  __shared__ float s_pdz[kPoolMaxB];
+  if (pool_idx) {
+    if (threadIdx.x < Bn) {
+      const int64_t bc = (int64_t)threadIdx.x * C + c;
+      s_pidx[threadIdx.x] = pool_idx[bc];
+      s_pdz[threadIdx.x] = dz[bc];
+    }
+    __syncthreads();
+  }
   // g = dz where the forward's output was > 0 (ReLU), xhat = (y - mean) invstd;
   // pool mode: dz is [B][C], the gradient of the max over points, all of it at
   // the forward's first maximum
@@ -552,8 +570,7 @@ __global__ __launch_bounds__(T) void k_tr_bn_bwd(const float* __restrict__ dz, c
     const float yv = y[off];
     float g;
     if (pool_idx) {
-      const int64_t bc = (int64_t)w.b * C + c;
-      g = w.n == pool_idx[bc] ? dz[bc] : 0.0f;
+      g = w.n == s_pidx[w.b] ? s_pdz[w.b] : 0.0f;
     } else {
       g = dz[off];
     }
@@ -926,6 +943,207 @@ __global__ __launch_bounds__(256) void k_tr_fc_bwd_x(const float* __restrict__ d
     if (b < Bn) o[(int64_t)b * K + k] = acc[b];
 }
 
+// ---- the seg head's log_softmax over the class dim (ndtnet.py:241) and the
+// training loss (NLL of the one-hot target, ndnet.training.segmentation_loss)
+// ----
+//
+// torch runs log_softmax(dim=1) on [B][C][N] as cunn_SpatialSoftMax (~20 us
+// each way at 16 x 29 x 1000) and the loss as ~8 small elementwise / reduce
+// launches (r05l trace).  Here one thread per point (b, n) holds its C <=
+// kLsmC classes in registers (stride-N loads: consecutive threads read
+// consecutive addresses; all of them issued at once -- a loop over C with a
+// load per step waited once per class: 18 us, r05o).
+constexpr int kLsmC = 32;
+// 64-thread workgroups: the B N = 16000 points then spread over ~250 CUs
+// (256-thread groups left them on 63 CUs, each waiting on its loads)
+constexpr int kLsmT = 64;
+
+__global__ __launch_bounds__(kLsmT) void k_tr_log_softmax_c(const float* __restrict__ x, float* __restrict__ out,
+                                                            int Bn, int C, int N) {
+  const int64_t t = (int64_t)blockIdx.x * kLsmT + threadIdx.x;
+  if (t >= (int64_t)Bn * N) return;
+  const int64_t base = t / N * C * N + t % N;
+  float v[kLsmC];
+#pragma unroll
+  for (int c = 0; c < kLsmC; c++) v[c] = c < C ? x[base + (int64_t)c * N] : -__builtin_huge_valf();
+  float mx = v[0];
+#pragma unroll
+  for (int c = 1; c < kLsmC; c++) mx = fmaxf(mx, v[c]);
+  float sum = 0.0f;
+#pragma unroll
+  for (int c = 0; c < kLsmC; c++)
+    if (c < C) sum += expf(v[c] - mx);
+  const float lse = logf(sum);
+#pragma unroll
+  for (int c = 0; c < kLsmC; c++)
+    if (c < C) out[base + (int64_t)c * N] = (v[c] - mx) - lse;
+}
+
+// dx[c] = dy[c] - exp(y[c]) * sum_c' dy[c'] (y the forward's log-probs)
+__global__ __launch_bounds__(kLsmT) void k_tr_log_softmax_c_bwd(const float* __restrict__ y,
+                                                                const float* __restrict__ dy, float* __restrict__ dx,
+                                                                int Bn, int C, int N) {
+  const int64_t t = (int64_t)blockIdx.x * kLsmT + threadIdx.x;
+  if (t >= (int64_t)Bn * N) return;
+  const int64_t base = t / N * C * N + t % N;
+  float d[kLsmC], yv[kLsmC];
+#pragma unroll
+  for (int c = 0; c < kLsmC; c++) {
+    d[c] = c < C ? dy[base + (int64_t)c * N] : 0.0f;
+    yv[c] = c < C ? y[base + (int64_t)c * N] : 0.0f;
+  }
+  float s = 0.0f;
+#pragma unroll
+  for (int c = 0; c < kLsmC; c++) s += d[c];
+#pragma unroll
+  for (int c = 0; c < kLsmC; c++)
+    if (c < C) dx[base + (int64_t)c * N] = d[c] - expf(yv[c]) * s;
+}
+
+// the workgroup's gt rows [t0, t0 + kLsmT) x C, staged in LDS with coalesced
+// loads (a thread reading its own 116-byte row sent every load instruction to
+// 64 lines); row pitch C (odd at C = 29: conflict-free reads)
+__device__ inline const float* nll_stage_gt(float* s_gt, const float* __restrict__ gt, int64_t pts, int C) {
+  const int64_t t0 = (int64_t)blockIdx.x * kLsmT;
+  const int64_t n = (pts - t0 < kLsmT ? pts - t0 : kLsmT) * C;
+  const float* src = gt + t0 * C;
+  for (int64_t i = threadIdx.x; i < n; i += kLsmT) s_gt[i] = src[i];
+  __syncthreads();
+  return s_gt + threadIdx.x * C;
+}
+
+// Per-workgroup partial of sum_{b,n,c} gt[b][n][c] * logp[b][c][n] (gt
+// [B][N][C] one-hot rows, logp the log-softmax output [B][C][N]); a point
+// per thread, then the workgroup's sum in a fixed order.
+__global__ __launch_bounds__(kLsmT) void k_tr_nll_part(const float* __restrict__ logp, const float* __restrict__ gt,
+                                                       double* __restrict__ part, int Bn, int C, int N) {
+  __shared__ float s_gt[kLsmT * kLsmC];
+  const int64_t pts = (int64_t)Bn * N;
+  const int64_t t = (int64_t)blockIdx.x * kLsmT + threadIdx.x;
+  // this point's log-probs first, in flight with the gt stage's loads
+  const int64_t tc = t < pts ? t : pts - 1;
+  const int64_t base = tc / N * C * N + tc % N;
+  float lp[kLsmC];
+#pragma unroll
+  for (int c = 0; c < kLsmC; c++) lp[c] = c < C ? logp[base + (int64_t)c * N] : 0.0f;
+  const float* g = nll_stage_gt(s_gt, gt, pts, C);
+  double v = 0.0;
+  if (t < pts) {
+    float a = 0.0f;
+#pragma unroll
+    for (int c = 0; c < kLsmC; c++)
+      if (c < C) a += g[c] * lp[c];
+    v = a;
+  }
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if (threadIdx.x == 0) part[blockIdx.x] = v;
+}
+
+// loss = -(sum of the parts in order) / (B N)
+__global__ __launch_bounds__(64) void k_tr_nll_sum(const double* __restrict__ part, int nparts, float* __restrict__ loss,
+                                                   int64_t count) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 64) s += part[i];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (threadIdx.x == 0) loss[0] = (float)(-s / (double)count);
+}
+
+// dlogp[b][c][n] = -gt[b][n][c] * dloss / (B N)
+__global__ __launch_bounds__(kLsmT) void k_tr_nll_bwd(const float* __restrict__ gt, const float* __restrict__ dloss,
+                                                      float* __restrict__ dlogp, int Bn, int C, int N) {
+  __shared__ float s_gt[kLsmT * kLsmC];
+  const int64_t pts = (int64_t)Bn * N;
+  const float* g = nll_stage_gt(s_gt, gt, pts, C);
+  const int64_t t = (int64_t)blockIdx.x * kLsmT + threadIdx.x;
+  if (t >= pts) return;
+  const int64_t base = t / N * C * N + t % N;
+  const float s = -dloss[0] / (float)pts;
+#pragma unroll
+  for (int c = 0; c < kLsmC; c++)
+    if (c < C) dlogp[base + (int64_t)c * N] = g[c] * s;
+}
+
+// ---- Adam (torch.optim.Adam's fused, capturable form; tools/train.py's
+// optimizer) over up to kAdamMax tensors per launch, the tensors' pointers in
+// the kernel arguments (captured by value into a graph: no pointer table to
+// upload) ----
+//
+// torch's fused Adam ran as two multi_tensor_apply launches of ~46 us each on
+// the 3.37 M parameters (94 MB of state traffic: ~15 us at HBM speed, r05p).
+// Per element, torch's order of operations (ATen fused_adam_utils,
+// ADAM_MODE::ORIGINAL): m = b1 m + (1 - b1) g; v = b2 v + (1 - b2) g^2;
+// p -= (lr / (1 - b1^t)) m / (sqrt(v) / sqrt(1 - b2^t) + eps), t the step
+// after its increment (k_tr_adam_steps runs first).
+constexpr int kAdamMax = 32;
+constexpr int kAdamChunk = 4096;  // elements per workgroup (256 threads x 16)
+struct AdamArgs {
+  float* p[kAdamMax];
+  const float* g[kAdamMax];
+  float* m[kAdamMax];
+  float* v[kAdamMax];
+  const float* step[kAdamMax];
+  int64_t numel[kAdamMax];
+  int chunk0[kAdamMax + 1];  // first chunk of each tensor; chunk0[n] = total
+  int n;
+  float beta1, beta2, omb1, omb2, eps, wd;  // omb = 1 - beta, rounded from double (as torch passes it)
+  double beta1d, beta2d;                    // the bias corrections' powers, in double as torch's kernel
+  const float* lr;
+};
+
+constexpr int kAdamStepsMax = 128;
+struct AdamSteps {
+  float* s[kAdamStepsMax];
+  int n;
+};
+__global__ __launch_bounds__(64) void k_tr_adam_steps(AdamSteps S) {
+  for (int i = threadIdx.x; i < S.n; i += 64) S.s[i][0] += 1.0f;
+}
+
+__global__ __launch_bounds__(256) void k_tr_adam(AdamArgs A) {
+  const int chunk = blockIdx.x;
+  int ti = 0;
+  while (ti + 1 < A.n && A.chunk0[ti + 1] <= chunk) ti++;
+  const int64_t e0 = (int64_t)(chunk - A.chunk0[ti]) * kAdamChunk;
+  const int64_t ne = A.numel[ti];
+  const float t = A.step[ti][0];
+  const float lr = A.lr[0];
+  const float bc1 = (float)(1.0 - pow(A.beta1d, (double)t)), bc2 = (float)(1.0 - pow(A.beta2d, (double)t));
+  const float step_size = lr / bc1, bc2s = sqrtf(bc2);
+  float* __restrict__ p = A.p[ti];
+  const float* __restrict__ g = A.g[ti];
+  float* __restrict__ m = A.m[ti];
+  float* __restrict__ v = A.v[ti];
+  // four elements per thread at a time, their 16 loads issued together
+  // (clamped indices; the stores past the tensor are skipped)
+#pragma unroll
+  for (int k0 = 0; k0 < kAdamChunk / 256; k0 += 4) {
+    float gv[4], pv[4], mv[4], vv[4];
+    int64_t ix[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      ix[u] = e0 + (int64_t)(k0 + u) * 256 + threadIdx.x;
+      const int64_t ic = ix[u] < ne ? ix[u] : ne - 1;
+      gv[u] = g[ic];
+      pv[u] = p[ic];
+      mv[u] = m[ic];
+      vv[u] = v[ic];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      float gi = gv[u];
+      if (A.wd != 0.0f) gi = gi + pv[u] * A.wd;
+      const float mi = A.beta1 * mv[u] + A.omb1 * gi;
+      const float vi = A.beta2 * vv[u] + A.omb2 * gi * gi;
+      const float denom = sqrtf(vi) / bc2s + A.eps;
+      if (ix[u] < ne) {
+        m[ix[u]] = mi;
+        v[ix[u]] = vi;
+        p[ix[u]] = pv[u] - step_size * mi / denom;
+      }
+    }
+  }
+}
+
 int launched() { return hipGetLastError() == hipSuccess ? 0 : -21; }
 
 bool getenv_flag(const char* name) {
@@ -1074,6 +1292,7 @@ extern "C" int ndnet_tr_bn_bwd(const float* dz, const float* y, const float* mea
                                const float* gamma, const float* beta, float* dy, float* dgamma, float* dbeta,
                                float* dbias, int B, int C, int N, int relu, const int32_t* pool_idx, void* stream) {
   if (!dz || !y || !mean || !invstd || !gamma || !beta || !dy || B <= 0 || C <= 0 || N <= 0) return -20;
+  if (pool_idx && B > kPoolMaxB) return -20;  // the pooled gradients are staged per cloud
   if (bn_wide_groups(C))
     k_tr_bn_bwd<1024><<<C, 1024, 0, (hipStream_t)stream>>>(dz, y, mean, invstd, gamma, beta, dy, dgamma, dbeta,
                                                            dbias, B, C, N, relu, pool_idx);
@@ -1160,3 +1379,87 @@ extern "C" int ndnet_tr_fc_bwd_x(const float* dpre, const float* W, float* dx, f
   }
   return launched();
 }
+
+extern "C" int ndnet_tr_log_softmax_c(const float* x, float* out, int B, int C, int N, void* stream) {
+  if (!x || !out || B <= 0 || C <= 0 || N <= 0) return -20;
+  if (C > kLsmC) return -20;  // the classes of a point are held in registers
+  const int64_t pts = (int64_t)B * N;
+  k_tr_log_softmax_c<<<(unsigned)((pts + kLsmT - 1) / kLsmT), kLsmT, 0, (hipStream_t)stream>>>(x, out, B, C, N);
+  return launched();
+}
+
+extern "C" int ndnet_tr_log_softmax_c_bwd(const float* y, const float* dy, float* dx, int B, int C, int N,
+                                          void* stream) {
+  if (!y || !dy || !dx || B <= 0 || C <= 0 || N <= 0) return -20;
+  if (C > kLsmC) return -20;  // the classes of a point are held in registers
+  const int64_t pts = (int64_t)B * N;
+  k_tr_log_softmax_c_bwd<<<(unsigned)((pts + kLsmT - 1) / kLsmT), kLsmT, 0, (hipStream_t)stream>>>(y, dy, dx, B, C, N);
+  return launched();
+}
+
+extern "C" int ndnet_tr_nll_onehot(const float* logp, const float* gt, double* part, float* loss, int B, int C, int N,
+                                   void* stream) {
+  if (!logp || !gt || !part || !loss || B <= 0 || C <= 0 || N <= 0) return -20;
+  if (C > kLsmC) return -20;  // the classes of a point are held in registers
+  const int64_t pts = (int64_t)B * N;
+  const unsigned blocks = (unsigned)((pts + kLsmT - 1) / kLsmT);
+  k_tr_nll_part<<<blocks, kLsmT, 0, (hipStream_t)stream>>>(logp, gt, part, B, C, N);
+  k_tr_nll_sum<<<1, 64, 0, (hipStream_t)stream>>>(part, (int)blocks, loss, pts);
+  return launched();
+}
+
+extern "C" int ndnet_tr_nll_onehot_bwd(const float* gt, const float* dloss, float* dlogp, int B, int C, int N,
+                                       void* stream) {
+  if (!gt || !dloss || !dlogp || B <= 0 || C <= 0 || N <= 0) return -20;
+  if (C > kLsmC) return -20;  // the classes of a point are held in registers
+  const int64_t pts = (int64_t)B * N;
+  k_tr_nll_bwd<<<(unsigned)((pts + kLsmT - 1) / kLsmT), kLsmT, 0, (hipStream_t)stream>>>(gt, dloss, dlogp, B, C, N);
+  return launched();
+}
+
+extern "C" int ndnet_tr_adam(int n, float* const* params, const float* const* grads, float* const* exp_avg,
+                             float* const* exp_avg_sq, float* const* steps, const int64_t* numel, const float* lr,
+                             double beta1, double beta2, float eps, float weight_decay, void* stream) {
+  if (n <= 0 || !params || !grads || !exp_avg || !exp_avg_sq || !steps || !numel || !lr) return -20;
+  hipStream_t st = (hipStream_t)stream;
+  for (int b0 = 0; b0 < n; b0 += kAdamStepsMax) {  // one launch for every step count (<= 128 tensors)
+    AdamSteps S;
+    S.n = n - b0 < kAdamStepsMax ? n - b0 : kAdamStepsMax;
+    for (int i = 0; i < S.n; i++) {
+      if (!steps[b0 + i]) return -20;
+      S.s[i] = steps[b0 + i];
+    }
+    k_tr_adam_steps<<<1, 64, 0, st>>>(S);
+  }
+  for (int b0 = 0; b0 < n; b0 += kAdamMax) {
+    AdamArgs A;
+    A.n = n - b0 < kAdamMax ? n - b0 : kAdamMax;
+    int64_t chunks = 0;
+    for (int i = 0; i < A.n; i++) {
+      const int j = b0 + i;
+      if (!params[j] || !grads[j] || !exp_avg[j] || !exp_avg_sq[j] || !steps[j] || numel[j] <= 0) return -20;
+      A.p[i] = params[j];
+      A.g[i] = grads[j];
+      A.m[i] = exp_avg[j];
+      A.v[i] = exp_avg_sq[j];
+      A.step[i] = steps[j];
+      A.numel[i] = numel[j];
+      A.chunk0[i] = (int)chunks;
+      chunks += (numel[j] + kAdamChunk - 1) / kAdamChunk;
+      if (chunks > INT32_MAX) return -20;
+    }
+    A.chunk0[A.n] = (int)chunks;
+    A.beta1 = (float)beta1;
+    A.beta2 = (float)beta2;
+    A.omb1 = (float)(1.0 - beta1);
+    A.omb2 = (float)(1.0 - beta2);
+    A.beta1d = beta1;
+    A.beta2d = beta2;
+    A.eps = eps;
+    A.wd = weight_decay;
+    A.lr = lr;
+    k_tr_adam<<<(unsigned)chunks, 256, 0, st>>>(A);
+  }
+  return launched();
+}
+

@@ -147,6 +147,12 @@ TRAIN_EXPORTS: dict = {
                              _I, _I, _P, _P]),
     "ndnet_tr_fc_bwd_w": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "ndnet_tr_fc_bwd_x": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "ndnet_tr_log_softmax_c": (_I, [_P, _P, _I, _I, _I, _P]),
+    "ndnet_tr_log_softmax_c_bwd": (_I, [_P, _P, _P, _I, _I, _I, _P]),
+    "ndnet_tr_nll_onehot": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),
+    "ndnet_tr_nll_onehot_bwd": (_I, [_P, _P, _P, _I, _I, _I, _P]),
+    "ndnet_tr_adam": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, ctypes.c_double, ctypes.c_double, ctypes.c_float,
+                           ctypes.c_float, _P]),
 }
 
 

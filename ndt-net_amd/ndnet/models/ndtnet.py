@@ -221,7 +221,12 @@ class NDTNetSegmentation(nn.Module):
             x = torch.cat((x_t2, g), dim=1)
         for conv, bn in blocks:
             x = _block(conv, bn, x, True)
-        x = torch.nn.functional.log_softmax(_block(self.conv4, None, x, False), dim=1)
+        x = _block(self.conv4, None, x, False)
+        if hip and x.shape[1] <= 32:  # one HIP launch each way (torch's spatial softmax: ~20 us each)
+            from . import train_hip
+            x = train_hip.log_softmax_c(x)
+        else:
+            x = torch.nn.functional.log_softmax(x, dim=1)
         return x.transpose(2, 1)
 
     def _needs_autograd(self, points: torch.Tensor, covariances: torch.Tensor) -> bool:

@@ -537,7 +537,9 @@ def _folded(model):
         tensors = _tensors(model)
         cache = model._hip = {"tensors": tensors, "sig": None, "stale": False}
     sig = _signature(cache["tensors"])
-    if cache["sig"] != sig or cache["stale"]:
+    cur = _tensors(model)  # a parameter or buffer replaced by another tensor is a change too
+    replaced = len(cur) != len(cache["tensors"]) or any(a is not b for a, b in zip(cur, cache["tensors"]))
+    if replaced or cache["sig"] != sig or cache["stale"]:
         # stale: the model was in train mode since the last fold, where a
         # replayed training graph updates the weights without bumping their
         # versions (ndnet.training.GraphedTrainStep)

@@ -424,3 +424,68 @@ class _TransformT(torch.autograd.Function):
 def transform_t(x: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
     """``torch.bmm(x.transpose(1, 2), t).transpose(1, 2)`` for x [B,C,N], t [B,C,C]."""
     return _TransformT.apply(x, t)
+
+
+class _LogSoftmaxC(torch.autograd.Function):
+    """log_softmax over dim 1 of [B,C,N] (ndtnet.py:241; ndnet_tr_log_softmax_c)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        _check_f32(x)
+        Bn, C, N = x.shape
+        y = torch.empty_like(x)
+        _lib.check(_lib.lib().ndnet_tr_log_softmax_c(x.data_ptr(), y.data_ptr(), Bn, C, N, _stream()),
+                   "ndnet_tr_log_softmax_c")
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        Bn, C, N = y.shape
+        dx = torch.empty_like(y)
+        _lib.check(_lib.lib().ndnet_tr_log_softmax_c_bwd(y.data_ptr(), dy.data_ptr(), dx.data_ptr(), Bn, C, N,
+                                                         _stream()), "ndnet_tr_log_softmax_c_bwd")
+        return dx
+
+
+def log_softmax_c(x: torch.Tensor) -> torch.Tensor:
+    """``torch.nn.functional.log_softmax(x, dim=1)`` for x [B,C,N] (fp32, cuda)
+    on the HIP kernels: one launch each way instead of torch's spatial softmax."""
+    return _LogSoftmaxC.apply(x)
+
+
+class _NllOneHot(torch.autograd.Function):
+    """-(gt * logp^T).sum(-1).mean() for logp [B,C,N] and one-hot gt [B,N,C]."""
+
+    @staticmethod
+    def forward(ctx, logp, gt):
+        logp, gt = logp.contiguous(), gt.contiguous()
+        _check_f32(logp, gt)
+        Bn, C, N = logp.shape
+        part = torch.empty(-(-(Bn * N) // 64), device=logp.device, dtype=torch.float64)
+        loss = torch.empty((), device=logp.device, dtype=torch.float32)
+        _lib.check(_lib.lib().ndnet_tr_nll_onehot(logp.data_ptr(), gt.data_ptr(), part.data_ptr(), loss.data_ptr(),
+                                                  Bn, C, N, _stream()), "ndnet_tr_nll_onehot")
+        ctx.save_for_backward(gt)
+        ctx.shape = logp.shape
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        (gt,) = ctx.saved_tensors
+        Bn, C, N = ctx.shape
+        dl = dloss.contiguous().float().reshape(1)
+        dlogp = torch.empty(Bn, C, N, device=gt.device, dtype=torch.float32)
+        _lib.check(_lib.lib().ndnet_tr_nll_onehot_bwd(gt.data_ptr(), dl.data_ptr(), dlogp.data_ptr(), Bn, C, N,
+                                                      _stream()), "ndnet_tr_nll_onehot_bwd")
+        return dlogp, None
+
+
+def nll_onehot(logp: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
+    """The training loss of ndnet.training.segmentation_loss on the HIP kernels:
+    logp [B,C,N] (the model's log-softmax before its transpose), gt [B,N,C]."""
+    return _NllOneHot.apply(logp, gt)
+

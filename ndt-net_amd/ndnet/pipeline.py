@@ -60,10 +60,19 @@ PIPE_PRIORITY = os.environ.get("NDNET_PIPE_PRIORITY", "none")
 class _Pinned:
     """What a captured graph reads through raw pointers, kept alive for the
     graph's lifetime: the model's folded-weight cache (weights, workspace,
-    prebuilt argument blocks) and the NDT plans.  ``check()`` raises when the
-    model's weights changed since capture (the graph would replay the old
-    fold): ``model.train()``, a re-fold by an eager forward or an in-place
-    update no longer free or silently bypass the captured buffers."""
+    prebuilt argument blocks) and the NDT plans.
+
+    Captured graphs follow the model's weights (one behaviour,
+    whatever changed them).  ``check()`` runs before every replay: when a
+    weight changed since the last fold -- an in-place update, an optimizer
+    step, ``model.train()`` then ``eval()`` around a replayed training graph
+    that changes weights without bumping their versions -- it re-folds in
+    place (one ``ndnet_pn_fold_run`` launch on the caller's stream: after the
+    previous replays, which the caller's stream has joined, and before this
+    one, whose streams fork from it), so the replay computes with the current
+    weights.  A fold that cannot be redone in place (a parameter tensor
+    replaced, a dtype change) leaves the graph pointing at the old buffers:
+    the replay raises, and a new graph must be built."""
 
     def __init__(self, model, plans) -> None:
         from .models import pointnet_hip
@@ -75,11 +84,20 @@ class _Pinned:
         self._signature = lambda: pointnet_hip._signature(self.cache["tensors"])
 
     def check(self) -> None:
+        from .models import pointnet_hip
         for plan in self.plans:  # a k_front barrier timeout of an earlier replay (no sync)
             plan.raise_sync_failures()
-        if self._signature() != self.sig:
-            raise RuntimeError("the model's weights changed after the graph was captured: "
-                               "build a new graph (the captured one replays the old fold)")
+        if self.model.training:
+            raise RuntimeError("replaying an eval-mode graph with the model in train mode: call model.eval()")
+        cur = pointnet_hip._tensors(self.model)
+        same = len(cur) == len(self.cache["tensors"]) and all(a is b for a, b in zip(cur, self.cache["tensors"]))
+        if same and self.cache.get("W") is self.W and self._signature() == self.sig and not self.cache.get("stale"):
+            return
+        pointnet_hip._folded(self.model)  # re-folds in place when it can
+        if self.cache.get("W") is not self.W:
+            raise RuntimeError("the model's weights changed after the graph was captured in a way the fold "
+                               "cannot follow in place (a parameter replaced?): build a new graph")
+        self.sig = self.cache["sig"]
 
 
 class GraphedSegmentation:
@@ -87,8 +105,9 @@ class GraphedSegmentation:
 
     Args:
         model: an ``NDTNetSegmentation`` in eval mode on a cuda device.  Its
-            weights are folded at capture time; after changing them, build a
-            new ``GraphedSegmentation``.
+            weights are folded at capture time; the replays follow later
+            in-place weight changes (re-folded before the replay, see
+            ``_Pinned``); a replaced parameter tensor makes the replay raise.
         num_nds: NDs per cloud (the reference's ``n_desired_nds``).
         batch, num_points: the static input shape ``[batch, num_points, 3]``.
         warmup: eager runs before capture (plan / workspace creation, kernel

@@ -28,8 +28,69 @@ import torch
 
 def segmentation_loss(pred: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
     """Mean NLL of one-hot ``gt`` [B,N,C+1] under log-probs ``pred`` [B,N,C+1]
-    (= cross_entropy over the class dim of the pre-log-softmax logits)."""
+    (= cross_entropy over the class dim of the pre-log-softmax logits).  On the
+    GPU, for the model's output (the transposed view of a [B,C+1,N] tensor),
+    one HIP reduction and one HIP gradient launch (train_hip.nll_onehot)
+    instead of torch's ~8 elementwise / reduce launches."""
+    if (pred.is_cuda and gt.is_cuda and pred.dtype == torch.float32 and gt.dtype == torch.float32
+            and pred.dim() == 3 and pred.shape == gt.shape and pred.shape[-1] <= 32
+            and pred.transpose(1, 2).is_contiguous()
+            and gt.is_contiguous()):
+        from .models import train_hip
+        return train_hip.nll_onehot(pred.transpose(1, 2), gt)
     return -(gt * pred).sum(dim=-1).mean()
+
+
+class HipAdam(torch.optim.Adam):
+    """``torch.optim.Adam(..., capturable=True, fused=True)`` -- the graphed
+    step's optimizer -- with the update of every parameter on one HIP launch
+    per 32 tensors (``ndnet_tr_adam``, include/ndnet_train.h: torch's fused
+    order of operations, the step counts and moments kept in torch's state
+    layout, so ``state_dict`` round-trips).  torch's fused kernel took two
+    ~46 us launches per step on the 3.37 M parameters (r05p trace).  Falls
+    back to torch's own step for anything the kernel does not cover (amsgrad,
+    maximize, non-float32 or sparse gradients, a closure)."""
+
+    def __init__(self, params, lr, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0) -> None:
+        super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, capturable=True, fused=True)
+
+    @staticmethod
+    def _covered(group, ps) -> bool:
+        lr = group["lr"]
+        return (not group.get("amsgrad") and not group.get("maximize") and not group.get("differentiable")
+                and not group.get("decoupled_weight_decay", False)
+                and torch.is_tensor(lr) and lr.is_cuda and lr.dtype == torch.float32 and lr.numel() == 1
+                and all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and not p.grad.is_sparse
+                        and p.grad.dtype == torch.float32 and p.grad.is_contiguous() for p in ps))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        if closure is not None:
+            return super().step(closure)
+        groups = [(g, [p for p in g["params"] if p.grad is not None]) for g in self.param_groups]
+        if not all(self._covered(g, ps) for g, ps in groups):
+            return super().step()
+        import ctypes
+        from . import _lib
+        for group, ps in groups:
+            if not ps:
+                continue
+            for p in ps:
+                st = self.state[p]
+                if len(st) == 0:  # torch's capturable fused initial state
+                    st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            n = len(ps)
+            arr = lambda ts: (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])  # noqa: E731
+            b1, b2 = group["betas"]
+            rc = _lib.lib().ndnet_tr_adam(
+                n, arr(ps), arr([p.grad for p in ps]), arr([self.state[p]["exp_avg"] for p in ps]),
+                arr([self.state[p]["exp_avg_sq"] for p in ps]), arr([self.state[p]["step"] for p in ps]),
+                (ctypes.c_int64 * n)(*[p.numel() for p in ps]), group["lr"].data_ptr(), float(b1), float(b2),
+                float(group["eps"]), float(group["weight_decay"]), torch.cuda.current_stream(ps[0].device).cuda_stream)
+            _lib.check(rc, "ndnet_tr_adam")
+        return None
 
 
 def accuracy_tensor(pred: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
@@ -67,8 +128,9 @@ class Trainer:
     ``graphs=True`` (one GPU, no DDP): ``step`` replays the whole training step
     -- labelled NDT, train forward, loss, backward, Adam -- as one HIP graph per
     input shape (``GraphedTrainStep``).  The optimizer is then Adam's fused,
-    capturable form with the learning rate in a device tensor, so
-    ``set_epoch`` still takes effect inside the graph."""
+    capturable form (``HipAdam``: its update on the HIP kernel) with the
+    learning rate in a device tensor, so ``set_epoch`` still takes effect
+    inside the graph."""
 
     def __init__(self, model: torch.nn.Module, lr: float, num_nds: int, num_classes: int,
                  device: torch.device, ddp: Optional[bool] = None, bucket_cap_mb: float = 4.0,
@@ -92,8 +154,7 @@ class Trainer:
         else:
             self.net = self.model
         if self.graphs:
-            self.opt = torch.optim.Adam(self.model.parameters(), lr=torch.tensor(self.base_lr, device=device),
-                                        capturable=True, fused=True)
+            self.opt = HipAdam(self.model.parameters(), lr=torch.tensor(self.base_lr, device=device))
         else:
             self.opt = torch.optim.Adam(self.model.parameters(), lr=self.base_lr)
 

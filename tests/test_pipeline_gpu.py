@@ -232,7 +232,9 @@ def test_pipelined_streamed_host_batches():
 def test_graph_keeps_captured_fold_alive():
     """a captured graph reads the model's folded weights and
     workspace through raw pointers.  A redundant eval() or an eager forward
-    after capture must not free them; a weight change must be refused."""
+    after capture must not free them.  ADVICE r4: the replays follow an
+    in-place weight change (re-folded before the replay: equal to the eager
+    forward with the new weights); a replaced parameter is refused."""
     import torch
     from ndnet.synthetic import make_batch
     from ndnet.pipeline import GraphedSegmentation
@@ -255,7 +257,13 @@ def test_graph_keeps_captured_fold_alive():
     assert torch.equal(again, first) and torch.equal(eager, first)
     with torch.no_grad():
         m.conv4.bias.add_(1.0)
-    with pytest.raises(RuntimeError, match="weights changed"):
+    followed = g(pts).clone()        # no eager forward in between: the replay re-folds itself
+    with torch.no_grad():
+        eager2 = m(p, c).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(followed, eager2) and not torch.equal(followed, first)
+    m.conv4.bias = torch.nn.Parameter(m.conv4.bias.detach().clone())  # a new tensor: no in-place fold
+    with pytest.raises(RuntimeError, match="build a new graph"):
         g(pts)
 
 

@@ -77,6 +77,52 @@ def test_gemm_layouts(case):
     _close(got, ref, 2e-6, "gemm")
 
 
+@pytest.mark.parametrize("scale_a, scale_b", [(1e-30, 1e30), (1e30, 1e-30), (1e-12, 1e-12), ("rows", "rows")])
+def test_gemm_x6_dynamic_range(scale_a, scale_b):
+    """The weight-gradient GEMM (both operands k-major: split-bf16 by default)
+    on operands far from unit scale: every bf16 plane keeps fp32's exponent
+    range, so the split stays fp32-accurate for operands down to ~1e-30 as long
+    as the products stay normal in fp32 (a product below ~1e-30 loses its
+    residual terms to fp32 subnormals: ADVICE r4); "rows" scales every operand
+    row / column by its own 10^U(-15, 15)."""
+    from ndnet.models import train_hip
+    Bn, M, N, K = 3, 64, 96, 1000
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(17)
+    A = torch.randn(Bn, M, K, device=dev, generator=g, dtype=torch.float64)
+    B = torch.randn(Bn, K, N, device=dev, generator=g, dtype=torch.float64)
+    if scale_a == "rows":
+        A = A * 10.0 ** (torch.rand(Bn, M, 1, device=dev, generator=g, dtype=torch.float64) * 30 - 15)
+        B = B * 10.0 ** (torch.rand(Bn, 1, N, device=dev, generator=g, dtype=torch.float64) * 30 - 15)
+    else:
+        A, B = A * scale_a, B * scale_b
+    A, B = A.float(), B.float()
+    C = torch.full((Bn, M, N), float("nan"), device=dev)
+    train_hip.gemm(A.contiguous(), B.transpose(1, 2).contiguous(), C, None, M, N, K, K, K, N, M * K, K * N, M * N, Bn,
+                   True, True)
+    torch.cuda.synchronize()
+    ref = torch.bmm(A.double(), B.double())
+    assert torch.isfinite(C).all()
+    for z in range(Bn):  # per element, relative to its row / column scale: |err| <= 1e-5 |A_m| |B_n|
+        scale = A[z].double().norm(dim=1)[:, None] * B[z].double().norm(dim=0)[None, :]
+        err = ((C[z].double() - ref[z]).abs() / scale).max().item()
+        assert err <= 1e-5, f"cloud {z}: max relative error {err:.3e}"
+
+
+def test_gemm_layouts_all_split_bf16():
+    """NDNET_TR_X6=all (read once per process) runs every GEMM layout on the
+    split-bf16 kernel, including the non-k-major loads no default layout
+    uses: the layout cases again in a child process."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, NDNET_TR_X6="all")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", __file__,
+                        "-k", "test_gemm_layouts and not all_split"], env=env, capture_output=True, text=True,
+                       timeout=300, cwd=os.path.dirname(__file__))
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+
+
 def _pair(cin, cout, bn, seed):
     torch.manual_seed(seed)
     conv = torch.nn.Conv1d(cin, cout, 1).cuda()
@@ -501,3 +547,68 @@ def test_accuracy_shape_mismatch_does_not_take_kernel():
     gt = torch.nn.functional.one_hot(pred[0].argmax(-1), 5).float()  # [10, 5]: broadcasts
     ref = (pred.argmax(dim=-1) == gt.argmax(dim=-1)).float().mean()
     assert accuracy_tensor(pred, gt).item() == ref.item()
+
+
+def test_log_softmax_c_matches_torch():
+    """The seg head's log_softmax over the class dim (ndtnet.py:241) on the HIP
+    kernels: forward and backward against torch in float64."""
+    from ndnet.models import train_hip
+    torch.manual_seed(5)
+    x = (torch.randn(3, 29, 1000, device="cuda") * 4).requires_grad_()
+    x64 = x.detach().double().requires_grad_()
+    y = train_hip.log_softmax_c(x)
+    y64 = torch.nn.functional.log_softmax(x64, dim=1)
+    _close(y, y64, 1e-6, "log_softmax")
+    g = torch.randn_like(y)
+    y.backward(g)
+    y64.backward(g.double())
+    _close(x.grad, x64.grad, 1e-5, "log_softmax backward")
+
+
+def test_nll_onehot_matches_torch():
+    """ndnet.training.segmentation_loss on the HIP kernels (the model's output
+    view) against the torch formula in float64: value and gradient."""
+    from ndnet.training import segmentation_loss
+    torch.manual_seed(6)
+    logp = torch.nn.functional.log_softmax(torch.randn(4, 29, 1000, device="cuda"), dim=1).requires_grad_()
+    gt = torch.nn.functional.one_hot(torch.randint(0, 29, (4, 1000), device="cuda"), 29).float()
+    gt[0, :10] = 0.0  # rows without a class
+    loss = segmentation_loss(logp.transpose(1, 2), gt)
+    lp64 = logp.detach().double().requires_grad_()
+    ref = -(gt.double() * lp64.transpose(1, 2)).sum(dim=-1).mean()
+    assert abs(loss.item() - ref.item()) <= 1e-6 * abs(ref.item())
+    (loss * 3.0).backward()
+    (ref * 3.0).backward()
+    _close(logp.grad, lp64.grad, 1e-6, "nll backward")
+
+
+def test_hip_adam_matches_torch_fused_adam():
+    """ndnet.training.HipAdam (the graphed trainer's optimizer, one HIP launch
+    per 32 tensors) against torch's own fused capturable Adam: five steps on
+    tensors of several sizes (one without a gradient), weight decay on and off."""
+    from ndnet.training import HipAdam
+    for wd in (0.0, 0.01):
+        torch.manual_seed(8)
+        shapes = [(64, 3, 1), (64,), (1024, 128), (29,), (7, 5)] * 8  # 40 tensors: two launches
+        ps = [torch.randn(s, device="cuda") for s in shapes]
+        qs = [p.clone() for p in ps]
+        for t in ps + qs:
+            t.requires_grad_(True)
+        lr = 1e-3
+        a = HipAdam(ps, lr=torch.tensor(lr, device="cuda"), weight_decay=wd)
+        b = torch.optim.Adam(qs, lr=torch.tensor(lr, device="cuda"), weight_decay=wd, capturable=True, fused=True)
+        for it in range(5):
+            for i, (p, q) in enumerate(zip(ps, qs)):
+                if i == 3:
+                    p.grad = q.grad = None
+                    continue
+                g = torch.randn_like(p) * (10.0 ** (i % 5 - 2))
+                p.grad, q.grad = g.clone(), g.clone()
+            a.step()
+            b.step()
+        torch.cuda.synchronize()
+        for i, (p, q) in enumerate(zip(ps, qs)):
+            torch.testing.assert_close(p, q, rtol=1e-6, atol=1e-7, msg=f"tensor {i} wd {wd}")
+            if i != 3:
+                assert a.state[p]["step"].item() == b.state[q]["step"].item() == 5.0
+                torch.testing.assert_close(a.state[p]["exp_avg_sq"], b.state[q]["exp_avg_sq"], rtol=1e-6, atol=0)

@@ -30,21 +30,26 @@ ap.add_argument("--kind", default="L")
 ap.add_argument("--heavy", type=int, default=256)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--light-nds", type=int, default=64)
+ap.add_argument("--classes", type=int, default=-1, help="labelled run with this many classes (random labels)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 B, n, k = a.batch, a.points, a.nds
 pts = torch.from_numpy(make_batch(a.kind, B, n, seed0=0)).to(dev)
-plan = NdtPlan(B, n, k, -1)
+plan = NdtPlan(B, n, k, a.classes)
 plan.set_heavy_threshold(a.heavy)
 out = torch.empty((B, k, 12), dtype=torch.float32, device=dev)
-plan.run(pts, None, out, None)
+lbl = ocls = None
+if a.classes > 0:
+    lbl = torch.randint(0, a.classes + 1, (B, n), dtype=torch.int32, device=dev)
+    ocls = torch.empty((B, k, a.classes + 1), dtype=torch.float32, device=dev)
+plan.run(pts, lbl, out, ocls)
 _lib.check(_lib.lib().ndnet_ndt_set_timing(plan.handle, 2), "set_timing")
 cap = B * (int(1.2 * k) + 1 + (int(1.2 * k) + 1 + 15) // 16)  # the plan's item capacity (16-ND quads' bound)
 m = np.zeros(cap * 8, np.uint64)
 items = ctypes.c_uint32(0)
-per_sample_h, per_sample_l, epi_h, epi_l, spans, phases, pro_l, loop_l = [], [], [], [], [], [], [], []
+per_sample_h, per_sample_l, epi_h, epi_l, spans, phases, pro_l, loop_l, lbl_l = [], [], [], [], [], [], [], [], []
 for r in range(a.reps):
-    plan.run(pts, None, out, None)
+    plan.run(pts, lbl, out, ocls)
     torch.cuda.synchronize()
     st = plan.host_stats()
     L = a.light_nds
@@ -74,6 +79,7 @@ for r in range(a.reps):
     epi_l += list((t2 - t1)[~hv])
     pro_l += list(w[run, 5].astype(np.int64)[~hv])
     loop_l += list(((t1 - t0) - w[run, 5].astype(np.int64))[~hv] / np.maximum(cnt[~hv], 1))
+    lbl_l += list(w[run, 6].astype(np.int64)[~hv])
     if r == a.reps - 1:
         order = np.argsort(-(end_rt - start))[:8]
         print(f"items: {H} heavy + {light} light; span ~{spans[-1]:.1f} us (end stamps from the shader clock at 2.1 GHz)")
@@ -129,6 +135,7 @@ print(f"cycles per sample, heavy items: {q(per_sample_h)}")
 print(f"cycles per sample (of the group's longest ND), light items: {q(per_sample_l)}")
 if pro_l:
     print(f"light items: prologue cycles (item start -> first block) {q(pro_l)}; loop cycles per sample {q(loop_l)}")
+    print(f"light items: class histogram cycles (labelled runs) {q(lbl_l)}")
 if phases and len(np.concatenate(phases)):
     P = np.concatenate(phases)
     print("heavy items, cycles per sample by phase (median): 0+2 loads/products %.1f, 1 mean recurrence + "
