@@ -260,6 +260,23 @@ __device__ inline void front_point(const T* p, uint64_t i, T& x, T& y, T& z) {
   z = p[3 * i + 2];
 }
 
+#ifndef NDNET_FRONT_XB
+#define NDNET_FRONT_XB 4
+#endif
+constexpr int kFrontXB = NDNET_FRONT_XB;  // bins past kFrontR loaded together
+
+// the points of bins j0 .. j0 + kFrontXB - 1 of this thread (index clamped to
+// the cloud's last point: every load valid, all of them in flight together)
+template <typename T>
+__device__ inline void front_points_xb(const T* p, uint64_t bin0, uint32_t j0, uint32_t t, uint64_t n,
+                                       T (&xs)[kFrontXB], T (&ys)[kFrontXB], T (&zs)[kFrontXB]) {
+#pragma unroll
+  for (int u = 0; u < kFrontXB; u++) {
+    const uint64_t i = (bin0 + j0 + u) * 1024 + t;
+    front_point(p, i < n ? i : n - 1, xs[u], ys[u], zs[u]);
+  }
+}
+
 // phase stamp (s_memrealtime, 100 MHz) of workgroup 0 of the cloud
 #define FRONT_MARK(i)                                                                                  \
   do {                                                                                                 \
@@ -376,12 +393,16 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
       px[j] = py[j] = pz[j] = T(0);
     }
   }
-  for (uint32_t j = kFrontR; j < bpw; j++) {
-    const uint64_t i = (bin0 + j) * 1024 + t;
-    if (i < iend) {
-      T x, y, z;
-      front_point(p, i, x, y, z);
-      lim_acc(x, y, z);
+  // bins past kFrontR (a CU share > 1: 13 bins per workgroup at share 2) are
+  // re-read in every phase; their loads go out kFrontXB at a time (clamped
+  // addresses), not one dependent round trip per bin
+  for (uint32_t j0 = kFrontR; j0 < bpw; j0 += kFrontXB) {
+    T xs[kFrontXB], ys[kFrontXB], zs[kFrontXB];
+    front_points_xb(p, bin0, j0, t, n, xs, ys, zs);
+#pragma unroll
+    for (int u = 0; u < kFrontXB; u++) {
+      const uint64_t i = (bin0 + j0 + u) * 1024 + t;
+      if (j0 + u < bpw && i < iend) lim_acc(xs[u], ys[u], zs[u]);
     }
   }
   {
@@ -538,11 +559,12 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
 #pragma unroll
     for (int j = 0; j < kFrontR; j++)
       if ((uint32_t)j < bpw) visit(j, (bin0 + j) * 1024 + t, px[j], py[j], pz[j]);
-    for (uint32_t j = kFrontR; j < bpw; j++) {
-      const uint64_t i = (bin0 + j) * 1024 + t;
-      T x = 0, y = 0, z = 0;
-      if (i < iend8) front_point(p, i, x, y, z);
-      visit(j, i, x, y, z);
+    for (uint32_t j0 = kFrontR; j0 < bpw; j0 += kFrontXB) {
+      T xs[kFrontXB], ys[kFrontXB], zs[kFrontXB];
+      front_points_xb(p, bin0, j0, t, n, xs, ys, zs);
+#pragma unroll
+      for (int u = 0; u < kFrontXB; u++)
+        if (j0 + u < bpw) visit(j0 + u, (bin0 + j0 + u) * 1024 + t, xs[u], ys[u], zs[u]);  // (visit checks iend8)
     }
     if (__any(redo)) {
 #pragma unroll 1
@@ -1073,12 +1095,13 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
 #pragma unroll
     for (int j = 0; j < kFrontR; j++)
       if ((uint32_t)j < bpw) put(j, (bin0 + j) * 1024 + t, px[j], py[j], pz[j]);
-    for (uint32_t j = kFrontR; j < bpw; j++) {
-      const uint64_t i = (bin0 + j) * 1024 + t;
-      if (i < iend8) {
-        T x, y, z;
-        front_point(p, i, x, y, z);
-        put(j, i, x, y, z);
+    for (uint32_t j0 = kFrontR; j0 < bpw; j0 += kFrontXB) {
+      T xs[kFrontXB], ys[kFrontXB], zs[kFrontXB];
+      front_points_xb(p, bin0, j0, t, n, xs, ys, zs);
+#pragma unroll
+      for (int u = 0; u < kFrontXB; u++) {
+        const uint64_t i = (bin0 + j0 + u) * 1024 + t;
+        if (j0 + u < bpw && i < iend8) put(j0 + u, i, xs[u], ys[u], zs[u]);
       }
     }
     }

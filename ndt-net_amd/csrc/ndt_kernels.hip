@@ -49,6 +49,7 @@ constexpr int kBitsCap = 32768;      // grids up to this many voxels count throu
 constexpr int kBitsWords = kBitsCap / 32;
 constexpr int kKLThreads = 1024;
 constexpr int kChunk = 256;          // slots per chunk of the chip-wide event sort
+constexpr int kKLMarks = 32;  // phase stamps per cloud of the KL kernels (timing level 2)
 constexpr int kMergeLdsChunks = 34;  // k_kl_merge stages score + NaN keys in LDS up to this many chunks (136 KB)
 constexpr int kMergeScoreChunks = 72; // ... and the score runs alone up to this many (144 KB; k <= 2440)
 constexpr int kMaxChunks = 6 * 16384 / kChunk;  // ndcap <= 16384
@@ -118,7 +119,7 @@ struct Plan {
   int timing;          // 0 off, 1 stage events, 2 + k_kl phase marks
   int ev_created;
   hipEvent_t ev[8];
-  unsigned long long* kl_marks;  // [B][16] s_memrealtime stamps (timing level 2)
+  unsigned long long* kl_marks;  // [B][kKLMarks] s_memrealtime stamps (timing level 2)
   unsigned long long* wq_marks;  // [wq_items][kWqMarkW] k_welford_q per-item stamps (timing level 2)
   // device buffers
   CloudCtl* ctl;
@@ -2386,11 +2387,11 @@ __global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const Cl
 // phase stamp of k_kl (timing level 2): 100 MHz constant clock
 #define KL_MARK(i)                                                                   \
   do {                                                                               \
-    if (A.marks && threadIdx.x == 0) A.marks[(uint64_t)b * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    if (A.marks && threadIdx.x == 0) A.marks[(uint64_t)b * kKLMarks + (i)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
 struct KLArgs {
-  unsigned long long* marks;  // [B][16] phase stamps of k_kl, or null
+  unsigned long long* marks;  // [B][kKLMarks] phase stamps of the KL kernels, or null
   CloudCtl* ctl;
   uint32_t* wq_ctr;           // k_welford_q's item counter, re-armed by k_kl_rank_chunks
   const uint32_t* dense_all;
@@ -2879,6 +2880,12 @@ __global__ void __launch_bounds__(kChunk) k_kl_rank_chunks(KLArgs A) {
   const uint32_t t = threadIdx.x;
   const uint32_t sl = ch * kChunk + t;
   const bool deferred = kl_list_deferrable(A, c);
+  // phase stamps of chunk 0 (timing level 2): start, scores done, end
+#define RANK_MARK(i)                                                                               \
+  do {                                                                                             \
+    if (A.marks && ch == 0 && t == 0) A.marks[(uint64_t)b * kKLMarks + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+  RANK_MARK(3);
   uint32_t fl = 0;
   double vl = 0.0;
   if (deferred) {
@@ -2897,6 +2904,7 @@ __global__ void __launch_bounds__(kChunk) k_kl_rank_chunks(KLArgs A) {
                              __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
+  RANK_MARK(4);
   if (sl < nslots) A.slot_flag_all[eb + sl] = fl;
   if (sl < nslots) A.slot_val_all[eb + sl] = vl;
   const bool f = sl < nslots && fl;
@@ -2956,6 +2964,8 @@ __global__ void __launch_bounds__(kChunk) k_kl_rank_chunks(KLArgs A) {
     A.chunk_cnt[(uint64_t)b * A.nchunk + ch] = ctot;
     A.chunk_min[(uint64_t)b * A.nchunk + ch] = mtot;
   }
+  RANK_MARK(15);
+#undef RANK_MARK
 }
 
 // NaN keys need the min over all earlier chunks: one pass writes every NaN
@@ -3113,7 +3123,7 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
   const uint32_t ch = blockIdx.x * kMergeRuns + lc;
 #define MERGE_MARK(i)                                                                              \
   do {                                                                                             \
-    if (A.marks && blockIdx.x == 0 && tid == 0) A.marks[(uint64_t)b * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    if (A.marks && blockIdx.x == 0 && tid == 0) A.marks[(uint64_t)b * kKLMarks + (i)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
   MERGE_MARK(12);
   extern __shared__ __attribute__((aligned(16))) unsigned long long dynk[];
@@ -3173,6 +3183,7 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
     }
   }
   __syncthreads();
+  MERGE_MARK(16);
   if (kLds) {
     // the NaN bases and the min over earlier chunks (k_kl_nan_keys' scans),
     // one lane per chunk (nch <= kMergeLdsChunks < 64)
@@ -3200,6 +3211,7 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
       if (tid + 1 == nch) s_nb[nch] = nn;
     }
     __syncthreads();
+    MERGE_MARK(17);
   }
   const uint32_t nnan_tot = s_nb[nch];
   const uint32_t cc = ch < nch ? s_cnt[ch] : 0u;
@@ -4127,8 +4139,8 @@ int ndnet_ndt_set_timing(void* plan, int enable) {
     HIPCHK(hipMemset(P->wq_marks, 0, items * kWqMarkW * sizeof(unsigned long long)));
   }
   if (enable >= 2 && !P->kl_marks) {
-    HIPCHK(hipMalloc(&P->kl_marks, (size_t)P->B * 16 * sizeof(unsigned long long)));
-    HIPCHK(hipMemset(P->kl_marks, 0, (size_t)P->B * 16 * sizeof(unsigned long long)));
+    HIPCHK(hipMalloc(&P->kl_marks, (size_t)P->B * kKLMarks * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(P->kl_marks, 0, (size_t)P->B * kKLMarks * sizeof(unsigned long long)));
   }
   P->timing = enable;
   return NDNET_OK;
@@ -4182,7 +4194,7 @@ int ndnet_ndt_debug_kl_marks(void* plan, unsigned long long* marks) {
   Plan* P = (Plan*)plan;
   if (!P || !marks || !P->kl_marks) return NDNET_ERR_ARG;
   HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpy(marks, P->kl_marks, (size_t)P->B * 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(marks, P->kl_marks, (size_t)P->B * kKLMarks * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return NDNET_OK;
 }
 

@@ -36,15 +36,17 @@ pts = torch.from_numpy(make_batch(a.kind, a.batch, a.points, seed0=0)).to(dev)
 ndt_preprocessing(a.nds, pts)
 plan = get_plan(a.batch, a.points, a.nds, -1, dev)
 _lib.check(_lib.lib().ndnet_ndt_set_timing(plan.handle, 2), "set_timing")
-# k_kl_merge, workgroup 0 of each cloud (marks 12-14): staging, searches; then the gap to k_kl
-MPHASES = [(12, 13, "merge: stage runs"), (13, 14, "merge: searches+writes"), (14, 0, "merge end -> k_kl start")]
+# k_kl_rank_chunks, chunk 0 of each cloud (marks 3, 4, 15); k_kl_merge, workgroup 0 of each cloud
+# (marks 12-14): staging, searches; then the gap to k_kl
+MPHASES = [(3, 4, "rank: chunk 0 scores"), (4, 15, "rank: scans, rank, writes"), (15, 12, "rank end -> merge start"),
+           (12, 16, "merge: stage runs"), (16, 17, "merge: NaN bases"), (17, 13, "merge: NaN keys"), (13, 14, "merge: searches+writes"), (14, 0, "merge end -> k_kl start")]
 acc = np.zeros(len(PHASES))
 macc = np.zeros(len(MPHASES))
 for _ in range(a.reps):
     ndt_preprocessing(a.nds, pts)
-    m = np.zeros(a.batch * 16, np.uint64)
+    m = np.zeros(a.batch * 32, np.uint64)
     _lib.check(_lib.lib().ndnet_ndt_debug_kl_marks(plan.handle, m.ctypes.data), "kl_marks")
-    m = m.reshape(a.batch, 16).astype(np.float64)
+    m = m.reshape(a.batch, 32).astype(np.float64)
     acc += np.array([((m[:, j] - m[:, i]) * 0.01).mean() for i, j, _ in PHASES])  # 100 MHz ticks -> us
     macc += np.array([((m[:, j] - m[:, i]) * 0.01).mean() for i, j, _ in MPHASES])
 _lib.lib().ndnet_ndt_set_timing(plan.handle, 0)
@@ -54,3 +56,22 @@ for (_, _, nm), v in zip(PHASES, acc):
 print(f"  {'total':20s} {acc.sum():8.2f} us (mean over clouds)")
 for (_, _, nm), v in zip(MPHASES, macc / a.reps):
     print(f"  {nm:24s} {v:8.2f} us")
+# the event census behind the stages: events, NaN scores, chunks per cloud
+st = plan.host_stats()
+ev = np.array([s.num_events for s in st])
+nds = np.array([s.num_nds for s in st])
+nan = []
+for b in range(a.batch):
+    ne = int(st[b].num_kl)
+    v = np.zeros(max(ne, 1))
+    z = lambda n, t=np.uint32: np.zeros(max(n, 1), t)  # noqa: E731
+    p = lambda x: x.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    n = int(nds[b])
+    bufs = [z(n), z(3 * n, np.float64), z(9 * n, np.float64), z(9 * n, np.float64), z(n), v, z(ne), z(ne),
+            np.zeros(16), z(16), None, z(n, np.uint8)]
+    it = ctypes.c_uint32(0)
+    args = [p(x) if x is not None else ctypes.byref(it) for x in bufs]
+    _lib.check(_lib.lib().ndnet_ndt_debug_dump(plan.handle, b, *args), "dump")
+    nan.append(int(np.isnan(v[:ne]).sum()))
+print(f"  events per cloud: mean {ev.mean():.0f} max {ev.max()}; NDs mean {nds.mean():.0f}; "
+      f"chunks {int(np.ceil(6 * nds.max() / 256))}; NaN scores in the retained lists: mean {np.mean(nan):.1f} max {max(nan)}")
