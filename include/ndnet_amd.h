@@ -247,12 +247,17 @@ int ndnet_ndt_debug_set_sync_timeout(void *plan, uint64_t ticks);
  * stamps itself; tests use this to reach the wrap. */
 int ndnet_ndt_debug_set_epoch(void *plan, uint32_t epoch);
 
+/* The run's prune and rows on the merge launch's last workgroup per cloud
+ * (on = 1, the default; NDNET_KL_FUSE=0 in the environment at plan creation
+ * turns it off) or on a k_kl launch of their own (0).  Same outputs either way. */
+int ndnet_ndt_debug_set_kl_fuse(void *plan, int on);
+
 /* KL-stage phase stamps of the last run at timing level 2: marks[cloud * 32 + i],
  * 100 MHz s_memrealtime ticks.  k_kl: 0 start, 1 cloud state checked, 2 event
  * count, 5 list initialised, 6 first occurrences, 7 walk scan, 8 kills, 9 shift,
  * 10 rows emitted, 11 end; k_kl_rank_chunks (chunk 0): 3 start, 4 scores, 15 end;
  * k_kl_merge (workgroup 0): 12 start, 16 runs staged, 17 NaN bases scanned,
- * 13 NaN keys, 14 end; the rest unused.  marks holds B * 32 values; synchronises. */
+ * 13 NaN keys, 14 end; 18 / 19 the last rank / merge workgroup's end; the rest unused.  marks holds B * 32 values; synchronises. */
 int ndnet_ndt_debug_kl_marks(void *plan, unsigned long long *marks);
 
 /* k_front phase stamps of the last run at timing level 2 (workgroup 0 of each

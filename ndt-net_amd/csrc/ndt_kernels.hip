@@ -102,6 +102,7 @@ struct CloudCtl {
                          // (written by the binning of every run that accepts a grid)
   uint32_t heavy_t;      // the threshold that list was built with: k_welford_q's light items skip
                          // exactly the NDs it holds, whatever the plan's threshold is by then
+  uint32_t kl_arrive;    // k_kl_merge<.., kTail> workgroups of the cloud done (re-armed by the last)
 };
 
 struct Plan {
@@ -185,6 +186,7 @@ struct Plan {
   int cu_share;               // k_front / k_welford_q use CUs / cu_share (ndnet_ndt_set_cu_share)
   uint32_t* wq_ctr;           // [8][16] k_welford_q dynamic item counters, one per XCD (re-armed by k_kl_rank_chunks)
   int eager_list;             // build every cloud's retained list in the run (ndnet_ndt_set_lazy_list(plan, 0))
+  int kl_fuse;                // the run's prune rides on the merge launch (kl_fusable; NDNET_KL_FUSE=0: k_kl)
   uint64_t front_sync_ticks;  // k_front's cloud-barrier timeout (ndnet_ndt_debug_set_sync_timeout)
   int lists_built;            // the deferred lists of the last run are built (no further build launches)
   int front_staged;           // k_front's scatter through LDS records (ndnet_ndt_set_front_staged; default 1)
@@ -329,6 +331,7 @@ __global__ void k_reset(CloudCtl* ctl, int B, uint32_t* bar, uint32_t* lu_done, 
   c.num_phys = 0;
   c.num_events = 0;
   c.flag_count = 0;
+  c.kl_arrive = 0;
   c.prune_rc = 0;
   c.num_out = 0;
   c.last_k = 0;
@@ -2468,8 +2471,11 @@ __device__ inline bool kl_list_skipped(const KLArgs& A, const CloudCtl& c) {
 // ND column, the per-ND first occurrences / alive flags and the walk's
 // scratch live in LDS (lds: 5 ndcap + 8 ecap bytes, dynamic), else in global
 // scratch.
-template <bool kLds>
+// kCoh: the list's p column was stored in this launch by workgroups on other
+// XCDs (sc1): read it with sc1 loads (k_kl_merge's tail).
+template <bool kLds, bool kCoh = false>
 __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t* s_u32, uint32_t* scratch) {
+  static_assert(kLds || !kCoh, "the coherent prune stages the list in LDS");
   extern __shared__ __attribute__((aligned(16))) uint32_t kl_smem[];
   CloudCtl& c = A.ctl[b];
   const uint32_t nd = c.num_nds;
@@ -2534,8 +2540,12 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
       if constexpr (kLds) {
         // logical entry i is physical entry off + i; past the entries ever
         // written it is poison (the reference's uninitialised tail)
-        for (uint32_t i = base + threadIdx.x; i < bend; i += blockDim.x)
-          s_op[i] = i + off < nphys ? g_op[i + off] : kInvalid;
+        for (uint32_t i = base + threadIdx.x; i < bend; i += blockDim.x) {
+          uint32_t v = kInvalid;
+          if (i + off < nphys)
+            v = kCoh ? __hip_atomic_load(&g_op[i + off], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : g_op[i + off];
+          s_op[i] = v;
+        }
         __syncthreads();
       }
       for (uint32_t i = base + threadIdx.x; i < bend; i += blockDim.x) {
@@ -2577,10 +2587,13 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
       __syncthreads();
       return carry >= to_remove;  // uniform: carry is the block's total
     };
-    // a first block of one entry per thread (the kills usually end there:
-    // ~120 of ~1120 NDs at C2-L, ~200 of ~2200 at C5), then 8 per thread
-    if (!walk_block(std::integral_constant<int, 1>{}, 0u))
-      for (uint32_t base = blockDim.x; base < nkl0; base += blockDim.x * 8)
+    // a first block of 1024 entries (one or two per thread; the kills usually
+    // end there: ~120 of ~1120 NDs at C2-L, ~200 of ~2200 at C5), then 8 per thread
+    const bool wide = blockDim.x >= 1024;
+    const bool found = wide ? walk_block(std::integral_constant<int, 1>{}, 0u)
+                            : walk_block(std::integral_constant<int, 2>{}, 0u);
+    if (!found)
+      for (uint32_t base = wide ? blockDim.x : 2 * blockDim.x; base < nkl0; base += blockDim.x * 8)
         if (walk_block(std::integral_constant<int, 8>{}, base)) break;
     KL_MARK(7);
     const uint32_t F = carry;
@@ -2679,16 +2692,30 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
       for (uint32_t u = threadIdx.x; u < nd; u += blockDim.x) g_alive[u] = alive[u];
   }
   const uint32_t nrows = carry < kout ? carry : (uint32_t)kout;
-  for (uint32_t rw = threadIdx.x; rw < nrows; rw += blockDim.x) {
-    const uint32_t u = identity ? rw : rowmap[rw];
+  // two rows per thread per round, their loads issued together
+  for (uint32_t rw0 = threadIdx.x; rw0 < nrows; rw0 += 2 * blockDim.x) {
+    double v2[2][12];
+    uint32_t u2[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint32_t rw = rw0 + h * blockDim.x;
+      const uint32_t rc2 = rw < nrows ? rw : rw0;
+      const uint32_t u = identity ? rc2 : rowmap[rc2];
+      u2[h] = u;
+      const double* m = A.nd_mean + 3 * (ob + u);
+      const double* cv = A.nd_cov_post + 9 * (ob + u);
+#pragma unroll
+      for (int q = 0; q < 3; q++) v2[h][q] = m[q];
+#pragma unroll
+      for (int q = 0; q < 9; q++) v2[h][3 + q] = cv[q];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+    const uint32_t rw = rw0 + h * blockDim.x;
+    if (rw >= nrows) break;
+    const uint32_t u = u2[h];
     const uint64_t o = (uint64_t)b * kout + rw;
-    const double* m = A.nd_mean + 3 * (ob + u);
-    const double* cv = A.nd_cov_post + 9 * (ob + u);
-    double v[12];
-#pragma unroll
-    for (int q = 0; q < 3; q++) v[q] = m[q];
-#pragma unroll
-    for (int q = 0; q < 9; q++) v[3 + q] = cv[q];
+    const double(&v)[12] = v2[h];
     if (A.out) {
       float* r = A.out + 12 * o;
 #pragma unroll
@@ -2707,6 +2734,7 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
       for (int q = 0; q < 9; q++) A.out_cov64[9 * o + q] = v[3 + q];
     }
     if (A.out_cls16) A.out_cls16[o] = A.nd_cls[ob + u];
+    }
   }
   __syncthreads();
   KL_MARK(10);
@@ -2965,6 +2993,9 @@ __global__ void __launch_bounds__(kChunk) k_kl_rank_chunks(KLArgs A) {
     A.chunk_min[(uint64_t)b * A.nchunk + ch] = mtot;
   }
   RANK_MARK(15);
+  if (A.marks && t == 0)  // the cloud's last chunk to end (the stamps only grow, so no reset is needed)
+    __hip_atomic_fetch_max(&A.marks[(uint64_t)b * kKLMarks + 18], (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #undef RANK_MARK
 }
 
@@ -3109,10 +3140,11 @@ constexpr int kMergeRuns1 = NDNET_MERGE_RUNS1;
 // kMode 2: score runs and NaN keys in LDS, the NaN keys computed here (up to
 // kMergeLdsChunks chunks); 1: score runs in LDS, NaN keys from k_kl_nan_keys
 // (up to kMergeScoreChunks); 0: everything from global memory.
-template <int kMode, int kMergeRuns = ::kMergeRuns>
-__global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
+// kCoh: the list entries are stored write-through (sc1) for a last
+// workgroup on another XCD to read in the same launch (k_kl_merge's tail).
+template <int kMode, int kMergeRuns, bool kCoh>
+__device__ inline void merge_runs(const KLArgs& A, const int b) {
   constexpr bool kLds = kMode == 2;
-  const int b = blockIdx.y;
   const CloudCtl& c = A.ctl[b];
   if (c.state != kAccepted || kl_list_skipped(A, c)) return;
   const uint32_t nch = (6 * c.num_nds + kChunk - 1) / kChunk;
@@ -3135,6 +3167,12 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
   constexpr int kStageU = (kMergeLdsChunks * kChunk / 2 + kChunk * kMergeRuns - 1) / (kChunk * kMergeRuns);
   const uint32_t nv = kLds ? nch * kChunk / 2 : 0u;
   ulonglong2 sv[kStageU];
+  // mode 2 also loads, in the same round, its chunk's NaN slots and the first
+  // kNanPre NaN minima of every chunk (indices clamped into the cloud's
+  // slots), which the NaN keys below would otherwise fetch after the scans
+  constexpr uint32_t kNanPre = kChunk * kMergeRuns / kMergeLdsChunks;
+  uint32_t own_nan = 0;
+  double pre_min = 0.0;
   if (kLds) {
     const ulonglong2* src = reinterpret_cast<const ulonglong2*>(gK);
 #pragma unroll
@@ -3142,6 +3180,9 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
       const uint32_t i = u * blockDim.x + tid;
       sv[u] = src[i < nv ? i : 0];
     }
+    const uint32_t os = ch * kChunk + t, ps = (tid / kNanPre) * kChunk + tid % kNanPre;
+    own_nan = A.nan_list_all[eb + (os < A.ecap ? os : A.ecap - 1)];
+    pre_min = A.ev_min_all[eb + (ps < A.ecap ? ps : A.ecap - 1)];
   } else if (kMode == 1) {  // score runs only: eight 16-byte loads in flight per thread
     const uint32_t nv1 = nch * kChunk / 2;
     const ulonglong2* src = reinterpret_cast<const ulonglong2*>(gK);
@@ -3166,6 +3207,8 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
   __shared__ double s_pm[kMergeLdsChunks];
   __shared__ uint32_t s_own_num_slot[kMergeRuns][kChunk];
   __shared__ uint32_t s_own_nan_slot[kMergeRuns][kChunk];
+  __shared__ double s_pre_min[kLds ? kChunk * kMergeRuns : 1];
+  if (kLds && tid < nch * kNanPre) s_pre_min[tid] = pre_min;
   for (uint32_t c2 = tid; c2 < nch; c2 += blockDim.x) {
     s_cnt[c2] = A.chunk_cnt[cb + c2];
     if (kLds) s_pm[c2] = A.chunk_min[cb + c2];
@@ -3217,7 +3260,7 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
   const uint32_t cc = ch < nch ? s_cnt[ch] : 0u;
   const uint32_t nnum = cc >> 16, nnan = cc & 0xffffu;
   const uint32_t nb0 = ch < nch ? s_nb[ch] : 0u;
-  if (t < nnan) s_own_nan_slot[lc][t] = kLds ? A.nan_list_all[eb + ch * kChunk + t] : A.nan_slot_all[eb + nb0 + t];
+  if (t < nnan) s_own_nan_slot[lc][t] = kLds ? own_nan : A.nan_slot_all[eb + nb0 + t];
   // mode 1: the NaN keys (from k_kl_nan_keys) join the score runs in LDS when they fit
   const bool nan_lds = kMode == 1 && (uint64_t)nch * kChunk + nnan_tot <= A.merge_lds_keys;
   if (nan_lds) {
@@ -3232,7 +3275,9 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
         if (s_nb[mid] <= i) lo = mid;
         else hi = mid;
       }
-      lN[i] = score_key(MinF64()(s_pm[lo], A.ev_min_all[eb + lo * kChunk + (i - s_nb[lo])]));
+      const uint32_t j = i - s_nb[lo];
+      const double em = j < kNanPre ? s_pre_min[lo * kNanPre + j] : A.ev_min_all[eb + lo * kChunk + j];
+      lN[i] = score_key(MinF64()(s_pm[lo], em));
     }
   }
   __syncthreads();
@@ -3276,9 +3321,17 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
       for (int q = 0; q < kMergeQ; q++)
         if (c0 + q < nch && c0 + q != ch) pos += add[q];
     }
-    A.ord_val_all[eb + pos] = A.slot_val_all[eb + sl];
-    A.ord_p_all[eb + pos] = sl / 6;
-    A.ord_q_all[eb + pos] = (uint32_t)A.nb_all[6 * (uint64_t)b * A.ndcap + sl];
+    const double ov = A.slot_val_all[eb + sl];
+    const uint32_t oq = (uint32_t)A.nb_all[6 * (uint64_t)b * A.ndcap + sl];
+    if constexpr (kCoh) {
+      st_sc1_f64(&A.ord_val_all[eb + pos], ov);
+      __hip_atomic_store(&A.ord_p_all[eb + pos], sl / 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&A.ord_q_all[eb + pos], oq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      A.ord_val_all[eb + pos] = ov;
+      A.ord_p_all[eb + pos] = sl / 6;
+      A.ord_q_all[eb + pos] = oq;
+    }
   };
   if (kLds) body(static_cast<const unsigned long long*>(lK), static_cast<const unsigned long long*>(lN));
   else if (kMode == 1 && nan_lds)
@@ -3286,6 +3339,9 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
   else if (kMode == 1) body(static_cast<const unsigned long long*>(lK), gN);
   else body(gK, gN);
   MERGE_MARK(14);
+  if (A.marks && t == 0)  // the cloud's last merge workgroup to end
+    __hip_atomic_fetch_max(&A.marks[(uint64_t)b * kKLMarks + 19], (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #undef MERGE_MARK
 }
 
@@ -3312,9 +3368,10 @@ __global__ void __launch_bounds__(256) k_kl_list_done(KLArgs A) {
   if (threadIdx.x == 0) c.kl_deferred = 0;
 }
 
-// Prune and output rows: one workgroup per cloud.
-__global__ void __launch_bounds__(kKLThreads) k_kl(KLArgs A) {
-  const int b = blockIdx.x;
+// Prune and output rows of cloud b by one workgroup (k_kl, or the last
+// k_kl_merge workgroup of the cloud: kCoh).
+template <bool kCoh>
+__device__ void kl_cloud(const KLArgs& A, const int b) {
   CloudCtl& c = A.ctl[b];
   __shared__ uint32_t s_u32[16];
   KL_MARK(0);
@@ -3358,12 +3415,38 @@ __global__ void __launch_bounds__(kKLThreads) k_kl(KLArgs A) {
   }
   __syncthreads();
   KL_MARK(5);
-  const uint32_t nout = A.kl_lds ? prune_and_emit<true>(A, b, A.k, s_u32, s_u32)
-                                 : prune_and_emit<false>(A, b, A.k, s_u32, s_u32);
+  uint32_t nout;
+  if constexpr (kCoh) nout = prune_and_emit<true, true>(A, b, A.k, s_u32, s_u32);  // the host fuses only kl_lds plans
+  else nout = A.kl_lds ? prune_and_emit<true>(A, b, A.k, s_u32, s_u32) : prune_and_emit<false>(A, b, A.k, s_u32, s_u32);
   fill_tail(A, b, A.k, nout < A.k ? nout : (uint32_t)A.k);
   __syncthreads();
   if (threadIdx.x == 0) write_stats(A, b);
   KL_MARK(11);
+}
+
+__global__ void __launch_bounds__(kKLThreads) k_kl(KLArgs A) { kl_cloud<false>(A, blockIdx.x); }
+
+// The event order of every cloud (merge_runs); with kTail the cloud's last
+// workgroup to finish then prunes it and writes its rows (kl_cloud), which
+// saves k_kl's launch and the kernel boundary.  The list entries are stored
+// and read write-through (sc1, as k_welford_q's LU groups hand over their
+// covariances); each wave drains its stores before the workgroup's ticket.
+template <int kMode, int kMergeRuns = ::kMergeRuns, bool kTail = false>
+__global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
+  const int b = blockIdx.y;
+  merge_runs<kMode, kMergeRuns, kTail>(A, b);
+  if constexpr (kTail) {
+    __shared__ uint32_t s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's list stores are done
+    __syncthreads();
+    if (threadIdx.x == 0)
+      s_last = __hip_atomic_fetch_add(&A.ctl[b].kl_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    if (threadIdx.x == 0) __hip_atomic_store(&A.ctl[b].kl_arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    kl_cloud<true>(A, b);
+  }
 }
 
 __global__ void __launch_bounds__(kKLThreads) k_prune(KLArgs A) {
@@ -3524,23 +3607,44 @@ __global__ void __launch_bounds__(256) k_kl_chains(KLArgs A) {
   }
 }
 
-static void launch_list_sort(Plan* P, const KLArgs& A, hipStream_t st) {
+// The dynamic LDS of the fused merge + prune launches (k_kl_merge<.., true>):
+// the larger of the merge's and the LDS-resident prune's (kl_lds_bytes).
+constexpr size_t kKLFusedLds = kMergeScoreChunks * kChunk * sizeof(unsigned long long);  // 144 KB
+static size_t kl_lds_bytes(const Plan* P);
+
+// tail: the merge's last workgroup per cloud also prunes and emits the rows
+// (k_kl's work; the caller checked kl_fusable).
+static void launch_list_sort(Plan* P, const KLArgs& A, hipStream_t st, bool tail = false) {
   const int B = P->B;
   k_kl_rank_chunks<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
   const uint32_t mg = (P->nchunk + kMergeRuns - 1) / kMergeRuns;
+  const size_t kl = tail ? kl_lds_bytes(P) : 0;
+  auto dyn = [&](size_t m) { return m > kl ? m : kl; };
   if (P->nchunk <= (uint32_t)kMergeLdsChunks) {  // the merge computes the NaN keys itself
-    k_kl_merge<2><<<dim3(mg, B), kChunk * kMergeRuns, merge_lds_bytes(P), st>>>(A);
+    if (tail) k_kl_merge<2, kMergeRuns, true><<<dim3(mg, B), kChunk * kMergeRuns, dyn(merge_lds_bytes(P)), st>>>(A);
+    else k_kl_merge<2><<<dim3(mg, B), kChunk * kMergeRuns, merge_lds_bytes(P), st>>>(A);
   } else if (P->nchunk <= (uint32_t)kMergeScoreChunks) {
     k_kl_nan_keys<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
     KLArgs A1 = A;
     const size_t keys = kMergeScoreChunks * kChunk;  // the launch's dynamic LDS, in 64-bit keys (144 KB)
     A1.merge_lds_keys = (uint32_t)keys;
     const uint32_t mg1 = (P->nchunk + kMergeRuns1 - 1) / kMergeRuns1;
-    k_kl_merge<1, kMergeRuns1><<<dim3(mg1, B), kChunk * kMergeRuns1, keys * sizeof(unsigned long long), st>>>(A1);
+    if (tail)
+      k_kl_merge<1, kMergeRuns1, true><<<dim3(mg1, B), kChunk * kMergeRuns1, dyn(keys * sizeof(unsigned long long)),
+                                          st>>>(A1);
+    else
+      k_kl_merge<1, kMergeRuns1><<<dim3(mg1, B), kChunk * kMergeRuns1, keys * sizeof(unsigned long long), st>>>(A1);
   } else {
     k_kl_nan_keys<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
-    k_kl_merge<0><<<dim3(mg, B), kChunk * kMergeRuns, 0, st>>>(A);
+    if (tail) k_kl_merge<0, kMergeRuns, true><<<dim3(mg, B), kChunk * kMergeRuns, dyn(0), st>>>(A);
+    else k_kl_merge<0><<<dim3(mg, B), kChunk * kMergeRuns, 0, st>>>(A);
   }
+}
+
+// The run's prune can ride on the merge launch: the prune's arrays fit the
+// fused launch's LDS (the LDS-resident prune) and NDNET_KL_FUSE is not 0.
+static bool kl_fusable(const Plan* P, const KLArgs& A) {
+  return P->kl_fuse && A.kl_lds && kl_lds_bytes(P) <= kKLFusedLds;
 }
 
 // Builds the retained lists a lazy run deferred (no-op for the others).
@@ -3805,8 +3909,12 @@ welford:
   if (P->timing) HIPCHK(hipEventRecord(P->ev[5], st));
   KLArgs A = kl_args(P, P->k, out, out_cls, pc64, cov64, cls16);
   A.stats_out = stats_dst;
-  launch_list_sort(P, A, st);
-  k_kl<<<B, kKLThreads, A.kl_lds ? kl_lds_bytes(P) : 0, st>>>(A);
+  if (kl_fusable(P, A)) {
+    launch_list_sort(P, A, st, true);
+  } else {
+    launch_list_sort(P, A, st);
+    k_kl<<<B, kKLThreads, A.kl_lds ? kl_lds_bytes(P) : 0, st>>>(A);
+  }
   if (P->timing) HIPCHK(hipEventRecord(P->ev[6], st));
   HIPCHK(hipGetLastError());
   return NDNET_OK;
@@ -3900,6 +4008,8 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
     const long v = atol(e);
     if (v >= 1) P->heavy_t = (uint32_t)v;
   }
+  P->kl_fuse = 1;
+  if (const char* e = getenv("NDNET_KL_FUSE")) P->kl_fuse = atoi(e) != 0;  // A/B: 0 launches k_kl
   const double upper = (double)num_desired * (1 + 0.2);
   P->ndcap = (uint32_t)upper + 1;
   P->ecap = 6 * P->ndcap;
@@ -4031,6 +4141,15 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_kl_merge<1, kMergeRuns1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(kMergeScoreChunks * kChunk * sizeof(unsigned long long)));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_kl_merge<2, kMergeRuns, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)kKLFusedLds);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_kl_merge<1, kMergeRuns1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)kKLFusedLds);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_kl_merge<0, kMergeRuns, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)kKLFusedLds);
   if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_kl, hipFuncAttributeMaxDynamicSharedMemorySize, kKLLdsMax);
   if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_prune, hipFuncAttributeMaxDynamicSharedMemorySize, kKLLdsMax);
   if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_bin_count, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -4267,6 +4386,13 @@ int ndnet_ndt_debug_set_epoch(void* plan, uint32_t epoch) {
   k_set_epoch<<<(P->B + 63) / 64, 64>>>(P->ctl, P->B, epoch);
   HIPCHK(hipGetLastError());
   HIPCHK(hipDeviceSynchronize());
+  return NDNET_OK;
+}
+
+int ndnet_ndt_debug_set_kl_fuse(void* plan, int on) {
+  Plan* P = (Plan*)plan;
+  if (!P) return NDNET_ERR_ARG;
+  P->kl_fuse = on ? 1 : 0;
   return NDNET_OK;
 }
 

@@ -652,6 +652,56 @@ def test_front_staged_scatter_equals_direct(case):
             assert np.array_equal(d1[b][key], d0[b][key], equal_nan=True), (b, key)
 
 
+@pytest.mark.parametrize("case", ["U", "L", "labelled", "L1300", "C5"])
+def test_fused_prune_equals_k_kl(case):
+    """The prune + rows on the merge launch's last workgroup per cloud (the
+    default) against k_kl's own launch: rows, classes, stats and every dumped
+    intermediate (the built list, alive flags, post-KL covariances) equal.
+    k = 1000 fuses into the all-LDS merge, k = 1300 into the score-runs-in-LDS
+    merge; C5 runs two further prune levels off the fused level-1 list."""
+    import torch
+    from ndnet import _lib
+    from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
+    from ndnet.synthetic import make_batch
+    kind = "U" if case == "U" else "L"
+    pts = make_batch(kind, 6, 60_000, seed0=47)
+    B, n, _ = pts.shape
+    k = 1300 if case == "L1300" else (1000 if case == "C5" else 800)
+    ncls = 27 if case == "labelled" else -1
+    lbl = None
+    if case == "labelled":
+        lbl = torch.from_numpy(np.random.default_rng(5).integers(0, ncls + 1, size=(B, n)).astype(np.int32)).cuda()
+    res = {}
+    for fuse in (1, 0):
+        plan = NdtPlan(B, n, k, ncls)
+        plan.set_lazy_list(case == "U")  # U: the deferred lists through the fused launch too
+        _lib.check(_lib.lib().ndnet_ndt_debug_set_kl_fuse(plan.handle, fuse), "set_kl_fuse")
+        out = torch.empty((B, k, 12), dtype=torch.float32, device="cuda")
+        oc = None if lbl is None else torch.empty((B, k, ncls + 1), dtype=torch.float32, device="cuda")
+        plan.run(torch.from_numpy(pts).cuda(), lbl, out, oc)
+        levels = []
+        if case == "C5":
+            for k2 in (700, 400):
+                o2 = torch.empty((B, k2, 12), dtype=torch.float32, device="cuda")
+                plan.prune(k2, o2)
+                levels.append(o2.cpu().numpy())
+        torch.cuda.synchronize()
+        stats = plan.host_stats()
+        dumps = [_dump(plan, b, int(stats[b].num_nds), int(stats[b].num_events)) for b in range(B)]
+        res[fuse] = (out.cpu().numpy(), None if oc is None else oc.cpu().numpy(), stats, dumps, levels)
+    (o1, c1, s1, d1, l1), (o0, c0, s0, d0, l0) = res[1], res[0]
+    assert np.array_equal(o1, o0)
+    if c1 is not None:
+        assert np.array_equal(c1, c0)
+    for a, b_ in zip(l1, l0):
+        assert np.array_equal(a, b_)
+    for b in range(B):
+        assert s1[b].rc == 0
+        assert bytes(s1[b]) == bytes(s0[b]), f"cloud {b} stats"
+        for key in d1[b]:
+            assert np.array_equal(d1[b][key], d0[b][key], equal_nan=True), (b, key)
+
+
 def test_run_parts_equal_whole_run():
     """ndnet_ndt_set_run_part: the front (part 1) and the rest (part 2) as two
     stream-ordered calls give the rows and stats of one whole run."""

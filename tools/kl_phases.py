@@ -38,8 +38,8 @@ plan = get_plan(a.batch, a.points, a.nds, -1, dev)
 _lib.check(_lib.lib().ndnet_ndt_set_timing(plan.handle, 2), "set_timing")
 # k_kl_rank_chunks, chunk 0 of each cloud (marks 3, 4, 15); k_kl_merge, workgroup 0 of each cloud
 # (marks 12-14): staging, searches; then the gap to k_kl
-MPHASES = [(3, 4, "rank: chunk 0 scores"), (4, 15, "rank: scans, rank, writes"), (15, 12, "rank end -> merge start"),
-           (12, 16, "merge: stage runs"), (16, 17, "merge: NaN bases"), (17, 13, "merge: NaN keys"), (13, 14, "merge: searches+writes"), (14, 0, "merge end -> k_kl start")]
+MPHASES = [(3, 4, "rank: chunk 0 scores"), (4, 15, "rank: scans, rank, writes"), (4, 18, "rank: chunk 0 scores -> last chunk end"), (18, 12, "last rank end -> merge start"),
+           (12, 16, "merge: stage runs"), (16, 17, "merge: NaN bases"), (17, 13, "merge: NaN keys"), (13, 14, "merge: searches+writes"), (14, 19, "merge wg 0 end -> last merge end"), (19, 0, "last merge end -> k_kl start")]
 acc = np.zeros(len(PHASES))
 macc = np.zeros(len(MPHASES))
 for _ in range(a.reps):
@@ -62,7 +62,7 @@ ev = np.array([s.num_events for s in st])
 nds = np.array([s.num_nds for s in st])
 nan = []
 for b in range(a.batch):
-    ne = int(st[b].num_kl)
+    ne = int(st[b].num_events)  # the dump writes the physical list (num_events entries)
     v = np.zeros(max(ne, 1))
     z = lambda n, t=np.uint32: np.zeros(max(n, 1), t)  # noqa: E731
     p = lambda x: x.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
@@ -72,6 +72,6 @@ for b in range(a.batch):
     it = ctypes.c_uint32(0)
     args = [p(x) if x is not None else ctypes.byref(it) for x in bufs]
     _lib.check(_lib.lib().ndnet_ndt_debug_dump(plan.handle, b, *args), "dump")
-    nan.append(int(np.isnan(v[:ne]).sum()))
+    nan.append(int(np.isnan(v[:int(st[b].num_kl)]).sum()))
 print(f"  events per cloud: mean {ev.mean():.0f} max {ev.max()}; NDs mean {nds.mean():.0f}; "
       f"chunks {int(np.ceil(6 * nds.max() / 256))}; NaN scores in the retained lists: mean {np.mean(nan):.1f} max {max(nan)}")
