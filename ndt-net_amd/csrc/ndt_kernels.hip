@@ -2471,14 +2471,27 @@ __device__ inline bool kl_list_skipped(const KLArgs& A, const CloudCtl& c) {
 // ND column, the per-ND first occurrences / alive flags and the walk's
 // scratch live in LDS (lds: 5 ndcap + 8 ecap bytes, dynamic), else in global
 // scratch.
+// The cloud's stats as kl_cloud's thread 0 knows them by the end (its ctl
+// fields loaded at the start, the prune's results recorded here as they are
+// set), so the stats need no read-back of the ctl words just written.
+struct KLStatsSnap {
+  int32_t rc, prune_rc;
+  uint32_t iters, num_nds, num_valid, num_kl, num_events, num_out;
+  uint32_t list_off, num_phys;  // (not stats: the prune's starting list state)
+  uint32_t len[3];
+  double off[3], vs;
+};
+
 // kCoh: the list's p column was stored in this launch by workgroups on other
-// XCDs (sc1): read it with sc1 loads (k_kl_merge's tail).
+// XCDs (sc1): read it with sc1 loads (k_kl_merge's tail).  sn: where thread 0
+// records the prune's stats fields (kl_cloud), or null.
 template <bool kLds, bool kCoh = false>
-__device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t* s_u32, uint32_t* scratch) {
+__device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t* s_u32, uint32_t* scratch,
+                                   KLStatsSnap* sn = nullptr) {
   static_assert(kLds || !kCoh, "the coherent prune stages the list in LDS");
   extern __shared__ __attribute__((aligned(16))) uint32_t kl_smem[];
   CloudCtl& c = A.ctl[b];
-  const uint32_t nd = c.num_nds;
+  const uint32_t nd = sn ? sn->num_nds : c.num_nds;
   const uint64_t ob = (uint64_t)b * A.ndcap, eb = (uint64_t)b * A.ecap;
   uint8_t* const g_alive = A.alive_all + ob;
   const uint32_t* const g_op = A.ord_p_all + eb;
@@ -2487,8 +2500,8 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
   const uint32_t* op;
   uint32_t* s_op = nullptr;  // kLds: the list's p column in LDS
   uint8_t* alive;
-  const uint32_t nv0 = c.num_valid, nkl0 = c.num_kl;
-  const uint32_t off = c.list_off, nphys = c.num_phys;
+  const uint32_t nv0 = sn ? sn->num_valid : c.num_valid, nkl0 = sn ? sn->num_kl : c.num_kl;
+  const uint32_t off = sn ? sn->list_off : c.list_off, nphys = sn ? sn->num_phys : c.num_phys;
   const bool walk = k < nv0;  // the prune removes something: the walk reads the list
   // no ND dead and none to remove: the survivors are every ND, the rows the
   // NDs in order (the level-1 prune of a cloud with num_nds == k)
@@ -2517,7 +2530,10 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
   } else if (!walk) {
     // to_remove = 0: the loop of ndt.c:44-67 runs no iteration, the shift
     // moves nothing; list, counts and flags stay as they are
-    if (threadIdx.x == 0) c.num_kl = nkl0;
+    if (threadIdx.x == 0) {
+      c.num_kl = nkl0;
+      if (sn) sn->num_kl = nkl0;
+    }
   } else {
     const uint32_t to_remove = (uint32_t)(nv0 - k);
     for (uint32_t u = threadIdx.x; u < nd; u += blockDim.x) first[u] = kInvalid;
@@ -2628,6 +2644,7 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
       if (threadIdx.x == 0) {
         c.list_off = off + s_kpos + 1;
         c.num_kl = nkl0 - to_remove;
+        if (sn) sn->num_kl = nkl0 - to_remove;
       }
     } else if (rc == 0 && to_remove > 0) {
       // shift left by idx_to_remove = f_{to_remove} + 1 (ndt.c:69-72)
@@ -2657,11 +2674,18 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
         oq[i] = tq[i];
       }
       __syncthreads();
-      if (threadIdx.x == 0) c.num_kl = nkl1;
+      if (threadIdx.x == 0) {
+        c.num_kl = nkl1;
+        if (sn) sn->num_kl = nkl1;
+      }
     } else if (threadIdx.x == 0) {
       c.num_kl = nkl0 - kills;
+      if (sn) sn->num_kl = nkl0 - kills;
     }
-    if (threadIdx.x == 0) c.num_valid = nv0 - kills;
+    if (threadIdx.x == 0) {
+      c.num_valid = nv0 - kills;
+      if (sn) sn->num_valid = nv0 - kills;
+    }
   }
   __syncthreads();
   KL_MARK(9);
@@ -2742,12 +2766,31 @@ __device__ uint32_t prune_and_emit(const KLArgs& A, int b, uint64_t k, uint32_t*
     c.prune_rc = rc;
     c.num_out = carry;
     c.last_k = (uint32_t)k;
+    if (sn) {
+      sn->prune_rc = rc;
+      sn->num_out = carry;
+    }
   }
   (void)s_u32;
   return carry;  // survivors (block-uniform)
 }
 
 __device__ void write_stats_to(const KLArgs& A, int b, ndnet_ndt_stats& s);
+__device__ inline void write_snap_to(const KLStatsSnap& v, ndnet_ndt_stats& s) {
+  s.rc = v.rc;
+  s.prune_rc = v.prune_rc;
+  s.iters = v.iters;
+  for (int a = 0; a < 3; a++) {
+    s.len[a] = v.len[a];
+    s.offset[a] = v.off[a];
+  }
+  s.voxel_size = v.vs;
+  s.num_nds = v.num_nds;
+  s.num_valid = v.num_valid;
+  s.num_kl = v.num_kl;
+  s.num_events = v.num_events;
+  s.num_out = v.num_out;
+}
 __device__ void write_stats(const KLArgs& A, int b) {
   write_stats_to(A, b, A.stats[b]);
   if (A.stats_out) write_stats_to(A, b, A.stats_out[b]);
@@ -3374,6 +3417,7 @@ template <bool kCoh>
 __device__ void kl_cloud(const KLArgs& A, const int b) {
   CloudCtl& c = A.ctl[b];
   __shared__ uint32_t s_u32[16];
+  __shared__ KLStatsSnap s_sn;
   KL_MARK(0);
   if (c.state != kAccepted) {
     zero_outputs(A, b, A.k);
@@ -3390,6 +3434,16 @@ __device__ void kl_cloud(const KLArgs& A, const int b) {
   const uint64_t ob = (uint64_t)b * A.ndcap, eb = (uint64_t)b * A.ecap;
   const uint32_t nch = (6 * nd + kChunk - 1) / kChunk;
   const bool deferred = kl_list_deferrable(A, c);
+  if (threadIdx.x == 0) {  // the stats fields the KL stage does not change, loaded with the chunk counters
+    s_sn.rc = c.rc;
+    s_sn.iters = c.iter;
+    for (int a = 0; a < 3; a++) {
+      s_sn.len[a] = c.len[a];
+      s_sn.off[a] = c.off[a];
+    }
+    s_sn.vs = c.vs;
+    s_sn.num_nds = nd;
+  }
   // event count: from the chunk counters, or (deferred list) k_kl_rank_chunks' count
   uint32_t e_part = 0;
   if (!deferred) {
@@ -3412,15 +3466,23 @@ __device__ void kl_cloud(const KLArgs& A, const int b) {
     c.num_kl = E;
     c.num_phys = E;
     c.num_valid = nd;
+    s_sn.list_off = 0;
+    s_sn.num_events = s_sn.num_kl = s_sn.num_phys = E;
+    s_sn.num_valid = nd;
   }
   __syncthreads();
   KL_MARK(5);
   uint32_t nout;
-  if constexpr (kCoh) nout = prune_and_emit<true, true>(A, b, A.k, s_u32, s_u32);  // the host fuses only kl_lds plans
-  else nout = A.kl_lds ? prune_and_emit<true>(A, b, A.k, s_u32, s_u32) : prune_and_emit<false>(A, b, A.k, s_u32, s_u32);
+  if constexpr (kCoh) nout = prune_and_emit<true, true>(A, b, A.k, s_u32, s_u32, &s_sn);  // the host fuses only kl_lds plans
+  else
+    nout = A.kl_lds ? prune_and_emit<true>(A, b, A.k, s_u32, s_u32, &s_sn)
+                    : prune_and_emit<false>(A, b, A.k, s_u32, s_u32, &s_sn);
   fill_tail(A, b, A.k, nout < A.k ? nout : (uint32_t)A.k);
   __syncthreads();
-  if (threadIdx.x == 0) write_stats(A, b);
+  if (threadIdx.x == 0) {
+    write_snap_to(s_sn, A.stats[b]);
+    if (A.stats_out) write_snap_to(s_sn, A.stats_out[b]);
+  }
   KL_MARK(11);
 }
 

@@ -654,11 +654,11 @@ __global__ __launch_bounds__(256) void k_tr_row_sum(const float* __restrict__ x,
 }
 
 // first index of the row's maximum, NaN counting as the maximum (torch.argmax)
-__device__ __forceinline__ int row_argmax(const float* __restrict__ r, int cols) {
+__device__ __forceinline__ int row_argmax(const float* __restrict__ r, int cols, int64_t stride = 1) {
   int bi = 0;
   float bv = r[0];
   for (int j = 1; j < cols; j++) {
-    const float v = r[j];
+    const float v = r[j * stride];
     if (!(bv != bv) && (v > bv || v != v)) {
       bv = v;
       bi = j;
@@ -673,6 +673,20 @@ __global__ __launch_bounds__(256) void k_tr_argmax_match(const float* __restrict
                                                          int64_t rows, int cols, unsigned* __restrict__ count) {
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
   unsigned n = r < rows ? (row_argmax(pred + r * cols, cols) == row_argmax(gt + r * cols, cols)) : 0u;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
+  if ((threadIdx.x & 63) == 0 && n) atomicAdd(count, n);
+}
+
+// the same with pred channel-major [B][C][N] (the seg head's log-probs before
+// their transposed view): a thread per point, the classes N apart
+__global__ __launch_bounds__(256) void k_tr_argmax_match_cm(const float* __restrict__ pred,
+                                                            const float* __restrict__ gt, int64_t rows, int C, int N,
+                                                            unsigned* __restrict__ count) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  unsigned n = 0;
+  if (r < rows)
+    n = row_argmax(pred + r / N * C * N + r % N, C, N) == row_argmax(gt + r * C, C);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
   if ((threadIdx.x & 63) == 0 && n) atomicAdd(count, n);
@@ -1063,6 +1077,89 @@ __global__ __launch_bounds__(kLsmT) void k_tr_nll_bwd(const float* __restrict__ 
     if (c < C) dlogp[base + (int64_t)c * N] = g[c] * s;
 }
 
+// ---- the point transform t1 (reference ndtnet.py:141-147: t . p and
+// t . C, left product only) of the train forward ----
+//
+// x[b, i, n] = sum_j t[b,i,j] p[b,n,j] and x[b, 3 + 3 i + k, n] = sum_j
+// t[b,i,j] C[b,n,j,k], x [B,12,N] channel-major as the first conv reads it:
+// one thread per point (the torch composition: two cats, a permute and a
+// batched GEMM).  Backward to t only (the points and covariances are data):
+// dt[b,i,j] = sum_n dx[b,i,n] p[n,j] + sum_{n,k} dx[b,3+3i+k,n] C[n,j,k], one
+// workgroup per cloud.
+constexpr int kPtT = 256;
+constexpr int kPtBwdT = 1024;
+__global__ __launch_bounds__(kPtT) void k_tr_point_transform(const float* __restrict__ t,
+                                                             const float* __restrict__ pts,
+                                                             const float* __restrict__ extra, float* __restrict__ x,
+                                                             int N) {
+  const int b = blockIdx.y;
+  const int n = blockIdx.x * kPtT + threadIdx.x;
+  if (n >= N) return;
+  float tm[9], p[3], c[9];
+#pragma unroll
+  for (int q = 0; q < 9; q++) tm[q] = t[9 * b + q];
+  const float* pp = pts + 3 * ((int64_t)b * N + n);
+  const float* cc = extra + 9 * ((int64_t)b * N + n);
+#pragma unroll
+  for (int q = 0; q < 3; q++) p[q] = pp[q];
+#pragma unroll
+  for (int q = 0; q < 9; q++) c[q] = cc[q];
+  float* xo = x + (int64_t)b * 12 * N + n;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    xo[(int64_t)i * N] = fmaf(tm[3 * i + 2], p[2], fmaf(tm[3 * i + 1], p[1], tm[3 * i] * p[0]));
+#pragma unroll
+    for (int kk = 0; kk < 3; kk++)
+      xo[(int64_t)(3 + 3 * i + kk) * N] =
+          fmaf(tm[3 * i + 2], c[6 + kk], fmaf(tm[3 * i + 1], c[3 + kk], tm[3 * i] * c[kk]));
+  }
+}
+
+__global__ __launch_bounds__(kPtBwdT) void k_tr_point_transform_bwd(const float* __restrict__ dx,
+                                                                    const float* __restrict__ pts,
+                                                                    const float* __restrict__ extra,
+                                                                    float* __restrict__ dt, int N) {
+  const int b = blockIdx.x;
+  float acc[9];
+#pragma unroll
+  for (int q = 0; q < 9; q++) acc[q] = 0.f;
+  const float* d = dx + (int64_t)b * 12 * N;
+  for (int n = threadIdx.x; n < N; n += kPtBwdT) {
+    float p[3], c[9], g[12];
+    const float* pp = pts + 3 * ((int64_t)b * N + n);
+    const float* cc = extra + 9 * ((int64_t)b * N + n);
+#pragma unroll
+    for (int q = 0; q < 3; q++) p[q] = pp[q];
+#pragma unroll
+    for (int q = 0; q < 9; q++) c[q] = cc[q];
+#pragma unroll
+    for (int r = 0; r < 12; r++) g[r] = d[(int64_t)r * N + n];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+      for (int j = 0; j < 3; j++) {
+        float a = g[i] * p[j];
+#pragma unroll
+        for (int kk = 0; kk < 3; kk++) a = fmaf(g[3 + 3 * i + kk], c[3 * j + kk], a);
+        acc[3 * i + j] += a;
+      }
+  }
+  __shared__ float s_red[kPtBwdT / 64][9];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < 9; q++) {
+    float v = acc[q];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) s_red[w][q] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 9) {
+    float v = 0.f;
+    for (int i = 0; i < kPtBwdT / 64; i++) v += s_red[i][threadIdx.x];
+    dt[9 * b + threadIdx.x] = v;
+  }
+}
+
 // ---- Adam (torch.optim.Adam's fused, capturable form; tools/train.py's
 // optimizer) over up to kAdamMax tensors per launch, the tensors' pointers in
 // the kernel arguments (captured by value into a graph: no pointer table to
@@ -1321,6 +1418,14 @@ extern "C" int ndnet_tr_argmax_match(const float* pred, const float* gt, int64_t
   return launched();
 }
 
+extern "C" int ndnet_tr_argmax_match_cm(const float* pred, const float* gt, int B, int C, int N, uint32_t* count,
+                                        void* stream) {
+  const int64_t rows = (int64_t)B * N;
+  if (!pred || !gt || !count || B <= 0 || C <= 0 || N <= 0 || (rows + 255) / 256 > (int64_t)INT32_MAX) return -20;
+  k_tr_argmax_match_cm<<<(unsigned)((rows + 255) / 256), 256, 0, (hipStream_t)stream>>>(pred, gt, rows, C, N, count);
+  return launched();
+}
+
 extern "C" int ndnet_row_argmax(const float* x, int64_t rows, int cols, int32_t* out, void* stream) {
   if (!x || !out || rows <= 0 || cols <= 0 || (rows + 255) / 256 > (int64_t)INT32_MAX) return -20;
   if (cols <= kArgmaxStagedCols)
@@ -1394,6 +1499,21 @@ extern "C" int ndnet_tr_log_softmax_c_bwd(const float* y, const float* dy, float
   if (C > kLsmC) return -20;  // the classes of a point are held in registers
   const int64_t pts = (int64_t)B * N;
   k_tr_log_softmax_c_bwd<<<(unsigned)((pts + kLsmT - 1) / kLsmT), kLsmT, 0, (hipStream_t)stream>>>(y, dy, dx, B, C, N);
+  return launched();
+}
+
+extern "C" int ndnet_tr_point_transform(const float* t, const float* pts, const float* extra, float* x, int B, int N,
+                                        void* stream) {
+  if (!t || !pts || !extra || !x || B <= 0 || N <= 0) return -20;
+  k_tr_point_transform<<<dim3((unsigned)((N + kPtT - 1) / kPtT), (unsigned)B), kPtT, 0, (hipStream_t)stream>>>(
+      t, pts, extra, x, N);
+  return launched();
+}
+
+extern "C" int ndnet_tr_point_transform_bwd(const float* dx, const float* pts, const float* extra, float* dt, int B,
+                                            int N, void* stream) {
+  if (!dx || !pts || !extra || !dt || B <= 0 || N <= 0) return -20;
+  k_tr_point_transform_bwd<<<(unsigned)B, kPtBwdT, 0, (hipStream_t)stream>>>(dx, pts, extra, dt, N);
   return launched();
 }
 

@@ -144,8 +144,12 @@ class NDTNet(nn.Module):
         d = self.point_dim
         xyz = points.transpose(1, 2)                      # [B,3,N]
         t = self.t1(xyz)                                  # [B,3,3]
-        if extra.shape[-1] == d * d and _hip_train(self.conv1, self.bn1, points):
+        if (extra.shape[-1] == d * d and d == 3 and _hip_train(self.conv1, self.bn1, points)
+                and not points.requires_grad and not extra.requires_grad):
             # (HIP train path; the torch composition below stays the reference's op for op)
+            from . import train_hip
+            x = train_hip.point_transform(t, points, extra)   # t . p and t . C, one launch each way
+        elif extra.shape[-1] == d * d and _hip_train(self.conv1, self.bn1, points):
             # t . p and t . C (left only, ndtnet.py:141-147) as ONE bmm per cloud: each point
             # contributes 4 columns (p, C[:, 0], C[:, 1], C[:, 2]) of a [3, 4N] matrix -- torch's
             # batched matmul of 16000 3x3 products costs ~85 us each way on this GPU
@@ -211,10 +215,7 @@ class NDTNetSegmentation(nn.Module):
             # conv with the global feature's term a per-cloud bias: W[:, 64:] g + b -- 1/13 of the
             # layer's FLOPs forward and backward; the gradient reaches g through the bias
             from . import train_hip
-            c = x_t2.shape[1]
-            w = self.conv1.weight
-            cb = torch.addmm(self.conv1.bias, x, w[:, c:, 0].t())  # x: the pooled global feature [B,F]
-            x = train_hip.conv_bn_act(self.conv1, self.bn1, x_t2, True, weight=w[:, :c], cloud_bias=cb)
+            x = train_hip.seg_conv1(self.conv1, self.bn1, x_t2, x)  # x: the pooled global feature [B,F]
             blocks = blocks[1:]
         else:
             g = x.amax(dim=2, keepdim=True).expand(-1, -1, x_t2.shape[2])

@@ -230,6 +230,85 @@ def conv_bn_act(conv: torch.nn.Conv1d, bn: Optional[torch.nn.BatchNorm1d], x: to
     return out
 
 
+class _SegConv1(torch.autograd.Function):
+    """The segmentation head's first block (ndtnet.py:230-234): relu(bn(conv1(
+    cat(x_t2, g broadcast over the points)))) as a conv over x_t2's c channels
+    with the per-cloud bias cb = b + W[:, c:] g.  The whole weight W [Cout,
+    c + F, 1] is one operand: the conv reads its first c columns in place (row
+    stride c + F) and the backward returns the whole dW, so no slice of the
+    weight is copied forward and no zero-filled gradient is summed backward."""
+
+    @staticmethod
+    def forward(ctx, x, g, w, b, gamma, beta, run_mean, run_var, eps, momentum, nbt):
+        x, g = x.contiguous(), g.contiguous()
+        W = w.detach().reshape(w.shape[0], -1)
+        _check_f32(x, g, W)
+        Bn, c, N = x.shape
+        Cout, Ct = W.shape
+        if Ct != c + g.shape[1]:
+            raise ValueError(f"conv1 expects {Ct} input channels, got {c} + {g.shape[1]}")
+        cb = torch.addmm(b.detach(), g.detach(), W[:, c:].t())     # [B,Cout]
+        y = torch.empty(Bn, Cout, N, device=x.device, dtype=torch.float32)
+        gemm(W, x, y, cb, Cout, N, c, Ct, N, N, 0, c * N, Cout * N, Bn, True, False, sbias=Cout)
+        z = torch.empty_like(y)
+        mean = torch.empty(Cout, device=y.device, dtype=torch.float32)
+        invstd = torch.empty_like(mean)
+        gm, bt = gamma.detach().contiguous(), beta.detach().contiguous()
+        rc = _lib.lib().ndnet_tr_bn_fwd(y.data_ptr(), z.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                                        _ptr(run_mean), _ptr(run_var), gm.data_ptr(), bt.data_ptr(), Bn, Cout, N,
+                                        float(eps), float(momentum), 1, None, None, _ptr(nbt), _stream())
+        _lib.check(rc, "ndnet_tr_bn_fwd")
+        ctx.w_shape = w.shape
+        ctx.save_for_backward(x, g, W, y, mean, invstd, gm, bt)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        x, g, W, y, mean, invstd, gm, bt = ctx.saved_tensors
+        dz = dz.contiguous()
+        need = ctx.needs_input_grad
+        Bn, Cout, N = y.shape
+        c, Ct = x.shape[1], W.shape[1]
+        dy = torch.empty_like(y)
+        dgamma = torch.empty(Cout, device=y.device, dtype=torch.float32)
+        dbeta, dbias = torch.empty_like(dgamma), torch.empty_like(dgamma)
+        rc = _lib.lib().ndnet_tr_bn_bwd(dz.data_ptr(), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                                        gm.data_ptr(), bt.data_ptr(), dy.data_ptr(), dgamma.data_ptr(),
+                                        dbeta.data_ptr(), dbias.data_ptr(), Bn, Cout, N, 1, None, _stream())
+        _lib.check(rc, "ndnet_tr_bn_bwd")
+        dx = None
+        if need[0]:  # W[:, :c]^T dy, the weight read in place
+            dx = torch.empty(Bn, c, N, device=dy.device, dtype=torch.float32)
+            gemm(W, dy, dx, None, c, N, Cout, Ct, N, N, 0, Cout * N, c * N, Bn, False, False)
+        dcb = row_sum(dy)                                            # [B,Cout]: the per-cloud bias gradient
+        dW = None
+        if need[2]:
+            dW = torch.empty(Cout, Ct, device=dy.device, dtype=torch.float32)
+            dW[:, :c].copy_(conv_weight_grad(dy, x))
+            torch.mm(dcb.t(), g, out=dW[:, c:])
+            dW = dW.view(ctx.w_shape)
+        db = chan_sum(dcb.view(Bn, Cout, 1)) if need[3] else None
+        dg = torch.mm(dcb, W[:, c:]) if need[1] else None
+        return (dx, dg, dW, db, dgamma if need[4] else None, dbeta if need[5] else None,
+                None, None, None, None, None)
+
+
+def seg_conv1(conv: torch.nn.Conv1d, bn: torch.nn.BatchNorm1d, x_t2: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
+    """``relu(bn(conv(cat(x_t2, g[:, :, None].expand(-1, -1, N)))))`` in
+    training mode (the segmentation head's first block, ndtnet.py:230-234):
+    x_t2 [B,c,N], the pooled global feature g [B,F]."""
+    if conv.kernel_size != (1,) or conv.groups != 1 or conv.bias is None or not bn.affine or bn.momentum is None:
+        raise ValueError("seg_conv1 takes the model's pointwise conv1 with bias and affine bn1")
+    track = bn.track_running_stats and bn.running_mean is not None
+    nbt = _batches_tracked(bn) if track else None
+    out = _SegConv1.apply(x_t2, g, conv.weight, conv.bias, bn.weight, bn.bias,
+                          bn.running_mean if track else None, bn.running_var if track else None,
+                          bn.eps, bn.momentum, nbt)
+    if track and nbt is None:
+        bn.num_batches_tracked.add_(1)
+    return out
+
+
 class _ConvBNPool(torch.autograd.Function):
     """``amax(relu(bn(conv(x))), dim=2)`` -> [B,C] without the [B,C,N]
     activation: the BatchNorm kernel's pool mode keeps each cloud's first
@@ -424,6 +503,41 @@ class _TransformT(torch.autograd.Function):
 def transform_t(x: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
     """``torch.bmm(x.transpose(1, 2), t).transpose(1, 2)`` for x [B,C,N], t [B,C,C]."""
     return _TransformT.apply(x, t)
+
+
+class _PointTransform(torch.autograd.Function):
+    """x [B,12,N] = (t . p, t . C) of the point transform t1 (ndtnet.py:141-147);
+    the gradient reaches t only (ndnet_tr_point_transform / _bwd)."""
+
+    @staticmethod
+    def forward(ctx, t, points, extra):
+        t, points, extra = t.contiguous(), points.contiguous(), extra.contiguous()
+        _check_f32(t, points, extra)
+        Bn, N, _ = points.shape
+        x = torch.empty((Bn, 12, N), device=points.device, dtype=torch.float32)
+        _lib.check(_lib.lib().ndnet_tr_point_transform(t.data_ptr(), points.data_ptr(), extra.data_ptr(), x.data_ptr(),
+                                                       Bn, N, _stream()), "ndnet_tr_point_transform")
+        ctx.save_for_backward(points, extra)
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        points, extra = ctx.saved_tensors
+        dx = dx.contiguous()
+        Bn, N, _ = points.shape
+        dt = torch.empty((Bn, 3, 3), device=points.device, dtype=torch.float32)
+        _lib.check(_lib.lib().ndnet_tr_point_transform_bwd(dx.data_ptr(), points.data_ptr(), extra.data_ptr(),
+                                                           dt.data_ptr(), Bn, N, _stream()),
+                   "ndnet_tr_point_transform_bwd")
+        return dt, None, None
+
+
+def point_transform(t: torch.Tensor, points: torch.Tensor, extra: torch.Tensor) -> torch.Tensor:
+    """The first conv's input [B,12,N] = cat(t . p, t . C) for t [B,3,3], points
+    [B,N,3], extra [B,N,9] (fp32, cuda; points and extra without gradient):
+    one launch each way instead of two cats, a permute and a batched GEMM."""
+    assert not points.requires_grad and not extra.requires_grad
+    return _PointTransform.apply(t, points, extra)
 
 
 class _LogSoftmaxC(torch.autograd.Function):

@@ -101,13 +101,20 @@ def accuracy_tensor(pred: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
             and pred.dtype == torch.float32 and gt.dtype == torch.float32):
         # the kernel indexes gt with pred's rows and columns: only for equal shapes
         from . import _lib
-        p, g = pred.contiguous(), gt.contiguous()
+        g = gt.contiguous()
         cnt = torch.zeros((), device=pred.device, dtype=torch.int32)
-        cols = p.shape[-1]
-        rows = p.numel() // cols
-        _lib.check(_lib.lib().ndnet_tr_argmax_match(p.data_ptr(), g.data_ptr(), rows, cols, cnt.data_ptr(),
-                                                    torch.cuda.current_stream().cuda_stream),
-                   "ndnet_tr_argmax_match")
+        cols = pred.shape[-1]
+        rows = pred.numel() // cols
+        st = torch.cuda.current_stream().cuda_stream
+        if pred.dim() == 3 and not pred.is_contiguous() and pred.transpose(1, 2).is_contiguous():
+            # the model's [B,N,C] view of its [B,C,N] log-probs: read in place
+            Bn, N, C = pred.shape
+            _lib.check(_lib.lib().ndnet_tr_argmax_match_cm(pred.data_ptr(), g.data_ptr(), Bn, C, N, cnt.data_ptr(),
+                                                           st), "ndnet_tr_argmax_match_cm")
+        else:
+            p = pred.contiguous()
+            _lib.check(_lib.lib().ndnet_tr_argmax_match(p.data_ptr(), g.data_ptr(), rows, cols, cnt.data_ptr(), st),
+                       "ndnet_tr_argmax_match")
         return cnt.float() / rows
     return (pred.argmax(dim=-1) == gt.argmax(dim=-1)).float().mean()
 

@@ -492,6 +492,10 @@ def test_accuracy_kernel_matches_torch_argmax():
     ref = (pred.argmax(dim=-1) == gt.argmax(dim=-1)).float().mean()
     got = accuracy_tensor(pred, gt)
     assert abs(got.item() - ref.item()) <= 1e-7
+    # the model's layout: a [B,N,C] view of channel-major [B,C,N] log-probs (read in place)
+    view = pred.transpose(1, 2).contiguous().transpose(1, 2)
+    assert not view.is_contiguous()
+    assert abs(accuracy_tensor(view, gt).item() - ref.item()) <= 1e-7
 
 
 
@@ -563,6 +567,55 @@ def test_log_softmax_c_matches_torch():
     y.backward(g)
     y64.backward(g.double())
     _close(x.grad, x64.grad, 1e-5, "log_softmax backward")
+
+
+def test_point_transform_matches_torch():
+    """The point transform t1 (ndtnet.py:141-147: t . p and t . C, left only)
+    on the HIP kernels against the reference's torch composition in float64:
+    the first conv's input and the gradient reaching t."""
+    from ndnet.models import train_hip
+    torch.manual_seed(8)
+    B, N = 4, 1000
+    t = (torch.eye(3, device="cuda") + 0.3 * torch.randn(B, 3, 3, device="cuda")).requires_grad_()
+    p = torch.randn(B, N, 3, device="cuda") * 20
+    c = torch.randn(B, N, 9, device="cuda")
+    x = train_hip.point_transform(t, p, c)
+    t64 = t.detach().double().requires_grad_()
+    xyz = torch.bmm(t64, p.double().transpose(1, 2))
+    cov = torch.matmul(t64.unsqueeze(1), c.double().reshape(B, N, 3, 3)).reshape(B, N, 9)
+    x64 = torch.cat((xyz.transpose(1, 2), cov), dim=2).transpose(1, 2)
+    _close(x, x64, 1e-6, "point transform")
+    g = torch.randn_like(x)
+    x.backward(g)
+    x64.backward(g.double())
+    _close(t.grad, t64.grad, 1e-5, "point transform backward")
+
+
+def test_seg_conv1_matches_torch():
+    """The segmentation head's first block over cat(x_t2, g broadcast) as one
+    Function over the whole conv1 weight (ndtnet.py:230-234): output, running
+    statistics and every gradient (x_t2, g, the whole weight, bias, BN affine)
+    against the torch block on the concatenated input."""
+    from ndnet.models import train_hip
+    conv, norm = _pair(64 + 768, 512, True, 21)
+    conv2, norm2 = copy.deepcopy(conv), copy.deepcopy(norm)
+    B, N = 4, 1000
+    x = (torch.randn(B, 64, N, device="cuda") * 2).requires_grad_()
+    g = torch.randn(B, 768, device="cuda").requires_grad_()
+    x2, g2 = x.detach().clone().requires_grad_(), g.detach().clone().requires_grad_()
+    out = train_hip.seg_conv1(conv, norm, x, g)
+    ref = torch.relu(norm2(conv2(torch.cat((x2, g2[:, :, None].expand(-1, -1, N)), dim=1))))
+    torch.testing.assert_close(out, ref, rtol=0, atol=1e-4)
+    torch.testing.assert_close(norm.running_mean, norm2.running_mean, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(norm.running_var, norm2.running_var, rtol=1e-5, atol=1e-5)
+    assert int(norm.num_batches_tracked) == int(norm2.num_batches_tracked)
+    dz = torch.randn_like(out)
+    out.backward(dz)
+    ref.backward(dz)
+    for a, b, what in ((x.grad, x2.grad, "x_t2"), (g.grad, g2.grad, "g"), (conv.weight.grad, conv2.weight.grad, "W"),
+                       (conv.bias.grad, conv2.bias.grad, "b"), (norm.weight.grad, norm2.weight.grad, "gamma"),
+                       (norm.bias.grad, norm2.bias.grad, "beta")):
+        _close(a, b, 1e-4, what)
 
 
 def test_nll_onehot_matches_torch():
