@@ -706,10 +706,16 @@ __global__ __launch_bounds__(256) void k_row_argmax(const float* __restrict__ x,
 // rows -- one contiguous block -- are loaded as 16-byte vectors by consecutive
 // lanes into LDS, then each thread scans its row there (an odd row pitch is
 // bank-conflict free).
+// The LDS is sized to the rows (dynamic: 256 * cols floats, 29.7 KB for the
+// train step's 29 classes, five workgroups per CU) and each thread issues its
+// share of the 16-byte loads together, so a CU keeps ~150 KB of the stream in
+// flight (the static 48-column buffer held three workgroups: 52 us for the
+// step's 186 MB, r05u).
 constexpr int kArgmaxStagedCols = 48;
+constexpr int kArgmaxLoads = 256 * kArgmaxStagedCols / 4 / 256;  // 16-byte loads per thread at most
 __global__ __launch_bounds__(256) void k_row_argmax_staged(const float* __restrict__ x, int64_t rows, int cols,
                                                            int* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) float s[256 * kArgmaxStagedCols];
+  extern __shared__ __attribute__((aligned(16))) float s[];
   const int64_t r0 = (int64_t)blockIdx.x * 256;
   const int nr = (int)min<int64_t>(256, rows - r0);
   const int count = nr * cols;
@@ -717,7 +723,17 @@ __global__ __launch_bounds__(256) void k_row_argmax_staged(const float* __restri
   if (((uintptr_t)src & 15) == 0) {
     const int n4 = count >> 2;
     const f32x4* s4 = reinterpret_cast<const f32x4*>(src);
-    for (int i = threadIdx.x; i < n4; i += 256) reinterpret_cast<f32x4*>(s)[i] = __builtin_nontemporal_load(s4 + i);
+    f32x4 v[kArgmaxLoads];
+#pragma unroll
+    for (int u = 0; u < kArgmaxLoads; u++) {
+      const int i = u * 256 + threadIdx.x;
+      if (i < n4) v[u] = __builtin_nontemporal_load(s4 + i);
+    }
+#pragma unroll
+    for (int u = 0; u < kArgmaxLoads; u++) {
+      const int i = u * 256 + threadIdx.x;
+      if (i < n4) reinterpret_cast<f32x4*>(s)[i] = v[u];
+    }
     for (int i = (n4 << 2) + threadIdx.x; i < count; i += 256) s[i] = src[i];
   } else {
     for (int i = threadIdx.x; i < count; i += 256) s[i] = src[i];
@@ -1429,7 +1445,8 @@ extern "C" int ndnet_tr_argmax_match_cm(const float* pred, const float* gt, int 
 extern "C" int ndnet_row_argmax(const float* x, int64_t rows, int cols, int32_t* out, void* stream) {
   if (!x || !out || rows <= 0 || cols <= 0 || (rows + 255) / 256 > (int64_t)INT32_MAX) return -20;
   if (cols <= kArgmaxStagedCols)
-    k_row_argmax_staged<<<(unsigned)((rows + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, rows, cols, out);
+    k_row_argmax_staged<<<(unsigned)((rows + 255) / 256), 256, 256 * cols * sizeof(float), (hipStream_t)stream>>>(
+        x, rows, cols, out);
   else
     k_row_argmax<<<(unsigned)((rows + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, rows, cols, out);
   return launched();

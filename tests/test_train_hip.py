@@ -297,9 +297,10 @@ def test_train_forward_matches_reference_fixture(monkeypatch, name):
     m = m.cuda().train()
     p, c = torch.from_numpy(z["points"]), torch.from_numpy(z["covs"])
     calls = []
-    real, real_pool = train_hip.conv_bn_act, train_hip.conv_bn_act_pool
+    real, real_pool, real_seg = train_hip.conv_bn_act, train_hip.conv_bn_act_pool, train_hip.seg_conv1
     monkeypatch.setattr(train_hip, "conv_bn_act", lambda *a, **k: calls.append(1) or real(*a, **k))
     monkeypatch.setattr(train_hip, "conv_bn_act_pool", lambda *a, **k: calls.append(2) or real_pool(*a, **k))
+    monkeypatch.setattr(train_hip, "seg_conv1", lambda *a, **k: calls.append(1) or real_seg(*a, **k))
     out = m(p.cuda(), c.cuda()).detach().cpu().double().numpy()
     assert len(calls) == 13, "the train forward must run on the HIP kernels"
     monkeypatch.setattr(ndtnet, "_TRAIN_TORCH", True)
@@ -331,9 +332,10 @@ def test_train_forward_matches_reference_fixture_b16(monkeypatch):
     m.load_state_dict(deterministic_state(m.state_dict()))
     m = m.cuda().train()
     calls = []
-    real, real_pool = train_hip.conv_bn_act, train_hip.conv_bn_act_pool
+    real, real_pool, real_seg = train_hip.conv_bn_act, train_hip.conv_bn_act_pool, train_hip.seg_conv1
     monkeypatch.setattr(train_hip, "conv_bn_act", lambda *a, **k: calls.append(1) or real(*a, **k))
     monkeypatch.setattr(train_hip, "conv_bn_act_pool", lambda *a, **k: calls.append(2) or real_pool(*a, **k))
+    monkeypatch.setattr(train_hip, "seg_conv1", lambda *a, **k: calls.append(1) or real_seg(*a, **k))
     out = m(torch.from_numpy(z["points"]).cuda(), torch.from_numpy(z["covs"]).cuda()).detach().cpu().double().numpy()
     assert len(calls) == 13, "the train forward must run on the HIP kernels"
     ref, ref64 = z["out_train"].astype(np.float64), z["out_train64"]
@@ -363,7 +365,16 @@ def test_segmentation_train_forward_backward_matches_torch(monkeypatch):
         calls.append(2)
         return real_pool(*a, **k)
 
-    real_fc, real_tt = train_hip.fc_bn_act, train_hip.transform_t
+    real_fc, real_tt, real_seg, real_pt = train_hip.fc_bn_act, train_hip.transform_t, train_hip.seg_conv1, \
+        train_hip.point_transform
+
+    def spy_seg(*a, **k):
+        calls.append(1)
+        return real_seg(*a, **k)
+
+    def spy_pt(*a, **k):
+        calls.append(5)
+        return real_pt(*a, **k)
 
     def spy_fc(*a, **k):
         calls.append(3)
@@ -377,15 +388,17 @@ def test_segmentation_train_forward_backward_matches_torch(monkeypatch):
     monkeypatch.setattr(train_hip, "conv_bn_act_pool", spy_pool)
     monkeypatch.setattr(train_hip, "fc_bn_act", spy_fc)
     monkeypatch.setattr(train_hip, "transform_t", spy_tt)
+    monkeypatch.setattr(train_hip, "seg_conv1", spy_seg)
+    monkeypatch.setattr(train_hip, "point_transform", spy_pt)
     out = model(pts, cov)
-    # 3 + 3 TNet blocks (the last of each pooled), 3 NDTNet (conv3 pooled), 3 seg head + conv4;
-    # 3 + 3 TNet FC layers; one x^T t2
+    # 3 + 3 TNet blocks (the last of each pooled), 3 NDTNet (conv3 pooled), 3 seg head (conv1 over
+    # the whole weight) + conv4; 3 + 3 TNet FC layers; one x^T t2; one point transform t1
     assert calls.count(1) + calls.count(2) == 13 and calls.count(2) == 3
-    assert calls.count(3) == 6 and calls.count(4) == 1
+    assert calls.count(3) == 6 and calls.count(4) == 1 and calls.count(5) == 1
     monkeypatch.setattr(ndtnet, "_TRAIN_TORCH", True)
     f64_model = copy.deepcopy(ref_model).double()
     ref = ref_model(pts, cov)
-    assert len(calls) == 20
+    assert len(calls) == 21
     torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4)
     # and as close to a float64 evaluation as torch's own fp32 forward is
     f64 = f64_model(pts.double(), cov.double())
@@ -532,6 +545,8 @@ def test_float64_train_forward_backward_takes_torch_path(monkeypatch):
 
     monkeypatch.setattr(train_hip, "conv_bn_act", boom)
     monkeypatch.setattr(train_hip, "conv_bn_act_pool", boom)
+    monkeypatch.setattr(train_hip, "seg_conv1", boom)
+    monkeypatch.setattr(train_hip, "point_transform", boom)
     out = model(pts, cov)
     assert out.dtype == torch.float64
     out.sum().backward()
