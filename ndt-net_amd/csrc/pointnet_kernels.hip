@@ -70,6 +70,9 @@ constexpr int kDepth = NDNET_PN_DEPTH;  // weight k-groups in flight per wave
 #define NDNET_PN_DEPTH6 1
 #endif
 constexpr int kDepth6 = NDNET_PN_DEPTH6;  // the same for split-bf16 layers (3 fragment planes each)
+#ifndef NDNET_PN_PAIR_PFIRST
+#define NDNET_PN_PAIR_PFIRST 0
+#endif
 #ifndef NDNET_PN_CHUNK_ROT
 #define NDNET_PN_CHUNK_ROT 1
 #endif
@@ -759,6 +762,18 @@ __device__ __attribute__((always_inline)) inline void fused_pair_x6p(const Layer
   __syncthreads();
   for (int f = 0; f < nf; f++) {
     const __bf16* af6 = reinterpret_cast<const __bf16*>(g_smem + fbuf + (f & 1) * fbsz) + (qrow0 + cl) * fpb + 8 * kq;
+#if NDNET_PN_PAIR_PFIRST
+    // A/B: chunk f + 1's P (into the other buffer, free since the last
+    // barrier) before chunk f's Q, so its epilogue overlaps other waves' Q
+    // MFMAs and the barrier follows the uniform Q phase
+    if (f + 1 < nf) {
+      p_chunk(f + 1);
+      if (f + 2 < nf) load_p(f + 2);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; k++) mma_kgroup_x6<RB, 1>(acc2, af6 + 32 * k, kP * fpb, 16 * fpb, wq[k]);
+    if (f + 1 < nf) load_q(f + 1);
+#else
 #pragma unroll
     for (int k = 0; k < 2; k++) mma_kgroup_x6<RB, 1>(acc2, af6 + 32 * k, kP * fpb, 16 * fpb, wq[k]);
     if (f + 1 < nf) {
@@ -766,6 +781,7 @@ __device__ __attribute__((always_inline)) inline void fused_pair_x6p(const Layer
       p_chunk(f + 1);
       if (f + 2 < nf) load_p(f + 2);
     }
+#endif
     __syncthreads();
   }
   if (gmax) pool_cols<RB, 1>(acc2, Q.bias, 16 * qwc, Q.relu, qrow0, rows_valid, gmax);

@@ -628,9 +628,10 @@ def test_seg_conv1_matches_torch():
     out.backward(dz)
     ref.backward(dz)
     for a, b, what in ((x.grad, x2.grad, "x_t2"), (g.grad, g2.grad, "g"), (conv.weight.grad, conv2.weight.grad, "W"),
-                       (conv.bias.grad, conv2.bias.grad, "b"), (norm.weight.grad, norm2.weight.grad, "gamma"),
-                       (norm.bias.grad, norm2.bias.grad, "beta")):
+                       (norm.weight.grad, norm2.weight.grad, "gamma"), (norm.bias.grad, norm2.bias.grad, "beta")):
         _close(a, b, 1e-4, what)
+    # the conv bias gradient is sum(dy) ~ 0 under BN (both sides are rounding noise): absolute check
+    assert (conv.bias.grad - conv2.bias.grad).abs().max().item() <= 1e-3
 
 
 def test_nll_onehot_matches_torch():
