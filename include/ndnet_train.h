@@ -93,9 +93,12 @@ int ndnet_tr_row_sum(const float *x, float *out, int64_t rows, int N, void *stre
  * torch.argmax: the training step's accuracy (tools/train.py:84-87) without a
  * host sync; the caller zeroes count. */
 int ndnet_tr_argmax_match(const float *pred, const float *gt, int64_t rows, int cols, uint32_t *count, void *stream);
-/* The same with pred channel-major, [B][C][N] (gt [B][N][C]): the seg head's
- * log-probs as the model computes them, before their transposed view. */
-int ndnet_tr_argmax_match_cm(const float *pred, const float *gt, int B, int C, int N, uint32_t *count, void *stream);
+/* The same with pred channel-major, [B][C][N] (gt [B][N][C], C <= 32): the seg
+ * head's log-probs as the model computes them, before their transposed view.
+ * ctr[0] += the matches; ctr[1] counts workgroups, and the last writes
+ * acc[0] = ctr[0] / (B N) (acc may be NULL).  The caller zeroes ctr[0..1]. */
+int ndnet_tr_argmax_match_cm(const float *pred, const float *gt, int B, int C, int N, uint32_t *ctr, float *acc,
+                             void *stream);
 
 /* out[r] = the first argmax of row r of x [rows][cols] (NaN counting as a
  * maximum, as torch.argmax): the labelled NDT path's class of each point from
@@ -146,13 +149,15 @@ int ndnet_tr_nll_onehot_bwd(const float *gt, const float *dloss, float *dlogp, i
 
 /* The point transform t1 of the train forward (ndtnet.py:141-147, t . p and
  * t . C with the covariance multiplied on the left only): t [B][3][3], pts
- * [B][N][3], extra [B][N][9] (C row-major) -> x [B][12][N] (rows 0-2 t . p,
- * row 3 + 3 i + k (t . C)[i][k]); the backward gives dt [B][3][3] from dx
- * (the points and covariances are data, no gradient). */
-int ndnet_tr_point_transform(const float *t, const float *pts, const float *extra, float *x, int B, int N,
-                             void *stream);
-int ndnet_tr_point_transform_bwd(const float *dx, const float *pts, const float *extra, float *dt, int B, int N,
-                                 void *stream);
+ * [B][N][pld] (p in columns 0-2), extra [B][N][eld] (C row-major in columns
+ * 0-8) -- e.g. both views of ndt_preprocessing's [B][N][12] rows, pld = eld =
+ * 12 -- -> x [B][12][N] (rows 0-2 t . p, row 3 + 3 i + k (t . C)[i][k]); the
+ * backward gives dt [B][3][3] from dx (the points and covariances are data,
+ * no gradient). */
+int ndnet_tr_point_transform(const float *t, const float *pts, int pld, const float *extra, int eld, float *x, int B,
+                             int N, void *stream);
+int ndnet_tr_point_transform_bwd(const float *dx, const float *pts, int pld, const float *extra, int eld, float *dt,
+                                 int B, int N, void *stream);
 
 /* Adam, torch.optim.Adam's fused capturable form (tools/train.py's
  * optimizer): for each of the n tensors i, steps[i][0] += 1 (device float,

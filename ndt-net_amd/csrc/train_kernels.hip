@@ -678,20 +678,6 @@ __global__ __launch_bounds__(256) void k_tr_argmax_match(const float* __restrict
   if ((threadIdx.x & 63) == 0 && n) atomicAdd(count, n);
 }
 
-// the same with pred channel-major [B][C][N] (the seg head's log-probs before
-// their transposed view): a thread per point, the classes N apart
-__global__ __launch_bounds__(256) void k_tr_argmax_match_cm(const float* __restrict__ pred,
-                                                            const float* __restrict__ gt, int64_t rows, int C, int N,
-                                                            unsigned* __restrict__ count) {
-  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  unsigned n = 0;
-  if (r < rows)
-    n = row_argmax(pred + r / N * C * N + r % N, C, N) == row_argmax(gt + r * C, C);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
-  if ((threadIdx.x & 63) == 0 && n) atomicAdd(count, n);
-}
-
 // out[r] = first argmax of row r (NaN as the maximum): a thread per row
 __global__ __launch_bounds__(256) void k_row_argmax(const float* __restrict__ x, int64_t rows, int cols,
                                                     int* __restrict__ out) {
@@ -1093,6 +1079,52 @@ __global__ __launch_bounds__(kLsmT) void k_tr_nll_bwd(const float* __restrict__ 
     if (c < C) dlogp[base + (int64_t)c * N] = g[c] * s;
 }
 
+// The training step's accuracy (tools/train.py:84-87) on pred channel-major
+// [B][C][N] (the seg head's log-probs before their transposed view) and the
+// one-hot gt [B][N][C]: a point per thread with its <= kLsmC classes loaded
+// together (N apart, coalesced across the wave), gt staged in LDS as the loss
+// kernels do; first argmax with NaN as the maximum (torch.argmax).  The
+// matches go to ctr[0]; the last workgroup (ticket ctr[1]) writes acc =
+// ctr[0] / rows -- the caller zeroes ctr[0..1], no count-to-float launches.
+__global__ __launch_bounds__(kLsmT) void k_tr_argmax_match_cm(const float* __restrict__ pred,
+                                                              const float* __restrict__ gt, int Bn, int C, int N,
+                                                              unsigned* __restrict__ ctr, float* __restrict__ acc) {
+  __shared__ float s_gt[kLsmT * kLsmC];
+  const int64_t pts = (int64_t)Bn * N;
+  const int64_t t = (int64_t)blockIdx.x * kLsmT + threadIdx.x;
+  const int64_t tc = t < pts ? t : pts - 1;
+  const int64_t base = tc / N * C * N + tc % N;
+  float v[kLsmC];
+#pragma unroll
+  for (int c = 0; c < kLsmC; c++) v[c] = c < C ? pred[base + (int64_t)c * N] : 0.0f;
+  const float* g = nll_stage_gt(s_gt, gt, pts, C);
+  int bi = 0, gi = 0;
+  float bv = v[0], gv = g[0];
+#pragma unroll
+  for (int c = 1; c < kLsmC; c++) {
+    if (c < C) {
+      if (!(bv != bv) && (v[c] > bv || v[c] != v[c])) {
+        bv = v[c];
+        bi = c;
+      }
+      const float x = g[c];
+      if (!(gv != gv) && (x > gv || x != x)) {
+        gv = x;
+        gi = c;
+      }
+    }
+  }
+  unsigned n = t < pts && bi == gi ? 1u : 0u;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
+  if (threadIdx.x == 0) {
+    if (n) __hip_atomic_fetch_add(&ctr[0], n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the count has been added before the ticket
+    if (__hip_atomic_fetch_add(&ctr[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1 && acc)
+      acc[0] = (float)__hip_atomic_load(&ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) / (float)pts;
+  }
+}
+
 // ---- the point transform t1 (reference ndtnet.py:141-147: t . p and
 // t . C, left product only) of the train forward ----
 //
@@ -1105,17 +1137,17 @@ __global__ __launch_bounds__(kLsmT) void k_tr_nll_bwd(const float* __restrict__ 
 constexpr int kPtT = 256;
 constexpr int kPtBwdT = 1024;
 __global__ __launch_bounds__(kPtT) void k_tr_point_transform(const float* __restrict__ t,
-                                                             const float* __restrict__ pts,
-                                                             const float* __restrict__ extra, float* __restrict__ x,
-                                                             int N) {
+                                                             const float* __restrict__ pts, int pld,
+                                                             const float* __restrict__ extra, int eld,
+                                                             float* __restrict__ x, int N) {
   const int b = blockIdx.y;
   const int n = blockIdx.x * kPtT + threadIdx.x;
   if (n >= N) return;
   float tm[9], p[3], c[9];
 #pragma unroll
   for (int q = 0; q < 9; q++) tm[q] = t[9 * b + q];
-  const float* pp = pts + 3 * ((int64_t)b * N + n);
-  const float* cc = extra + 9 * ((int64_t)b * N + n);
+  const float* pp = pts + pld * ((int64_t)b * N + n);
+  const float* cc = extra + eld * ((int64_t)b * N + n);
 #pragma unroll
   for (int q = 0; q < 3; q++) p[q] = pp[q];
 #pragma unroll
@@ -1132,8 +1164,8 @@ __global__ __launch_bounds__(kPtT) void k_tr_point_transform(const float* __rest
 }
 
 __global__ __launch_bounds__(kPtBwdT) void k_tr_point_transform_bwd(const float* __restrict__ dx,
-                                                                    const float* __restrict__ pts,
-                                                                    const float* __restrict__ extra,
+                                                                    const float* __restrict__ pts, int pld,
+                                                                    const float* __restrict__ extra, int eld,
                                                                     float* __restrict__ dt, int N) {
   const int b = blockIdx.x;
   float acc[9];
@@ -1142,8 +1174,8 @@ __global__ __launch_bounds__(kPtBwdT) void k_tr_point_transform_bwd(const float*
   const float* d = dx + (int64_t)b * 12 * N;
   for (int n = threadIdx.x; n < N; n += kPtBwdT) {
     float p[3], c[9], g[12];
-    const float* pp = pts + 3 * ((int64_t)b * N + n);
-    const float* cc = extra + 9 * ((int64_t)b * N + n);
+    const float* pp = pts + pld * ((int64_t)b * N + n);
+    const float* cc = extra + eld * ((int64_t)b * N + n);
 #pragma unroll
     for (int q = 0; q < 3; q++) p[q] = pp[q];
 #pragma unroll
@@ -1434,11 +1466,13 @@ extern "C" int ndnet_tr_argmax_match(const float* pred, const float* gt, int64_t
   return launched();
 }
 
-extern "C" int ndnet_tr_argmax_match_cm(const float* pred, const float* gt, int B, int C, int N, uint32_t* count,
-                                        void* stream) {
+extern "C" int ndnet_tr_argmax_match_cm(const float* pred, const float* gt, int B, int C, int N, uint32_t* ctr,
+                                        float* acc, void* stream) {
   const int64_t rows = (int64_t)B * N;
-  if (!pred || !gt || !count || B <= 0 || C <= 0 || N <= 0 || (rows + 255) / 256 > (int64_t)INT32_MAX) return -20;
-  k_tr_argmax_match_cm<<<(unsigned)((rows + 255) / 256), 256, 0, (hipStream_t)stream>>>(pred, gt, rows, C, N, count);
+  if (!pred || !gt || !ctr || B <= 0 || C <= 0 || N <= 0 || C > kLsmC) return -20;
+  if ((rows + kLsmT - 1) / kLsmT > (int64_t)INT32_MAX) return -20;
+  k_tr_argmax_match_cm<<<(unsigned)((rows + kLsmT - 1) / kLsmT), kLsmT, 0, (hipStream_t)stream>>>(pred, gt, B, C, N,
+                                                                                                 ctr, acc);
   return launched();
 }
 
@@ -1519,18 +1553,18 @@ extern "C" int ndnet_tr_log_softmax_c_bwd(const float* y, const float* dy, float
   return launched();
 }
 
-extern "C" int ndnet_tr_point_transform(const float* t, const float* pts, const float* extra, float* x, int B, int N,
-                                        void* stream) {
-  if (!t || !pts || !extra || !x || B <= 0 || N <= 0) return -20;
+extern "C" int ndnet_tr_point_transform(const float* t, const float* pts, int pld, const float* extra, int eld,
+                                        float* x, int B, int N, void* stream) {
+  if (!t || !pts || !extra || !x || B <= 0 || N <= 0 || pld < 3 || eld < 9) return -20;
   k_tr_point_transform<<<dim3((unsigned)((N + kPtT - 1) / kPtT), (unsigned)B), kPtT, 0, (hipStream_t)stream>>>(
-      t, pts, extra, x, N);
+      t, pts, pld, extra, eld, x, N);
   return launched();
 }
 
-extern "C" int ndnet_tr_point_transform_bwd(const float* dx, const float* pts, const float* extra, float* dt, int B,
-                                            int N, void* stream) {
-  if (!dx || !pts || !extra || !dt || B <= 0 || N <= 0) return -20;
-  k_tr_point_transform_bwd<<<(unsigned)B, kPtBwdT, 0, (hipStream_t)stream>>>(dx, pts, extra, dt, N);
+extern "C" int ndnet_tr_point_transform_bwd(const float* dx, const float* pts, int pld, const float* extra, int eld,
+                                            float* dt, int B, int N, void* stream) {
+  if (!dx || !pts || !extra || !dt || B <= 0 || N <= 0 || pld < 3 || eld < 9) return -20;
+  k_tr_point_transform_bwd<<<(unsigned)B, kPtBwdT, 0, (hipStream_t)stream>>>(dx, pts, pld, extra, eld, dt, N);
   return launched();
 }
 

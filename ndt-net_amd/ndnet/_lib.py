@@ -143,14 +143,14 @@ TRAIN_EXPORTS: dict = {
     "ndnet_tr_chan_sum": (_I, [_P, _P, _I, _I, _I, _P]),
     "ndnet_tr_row_sum": (_I, [_P, _P, _I64, _I, _P]),
     "ndnet_tr_argmax_match": (_I, [_P, _P, _I64, _I, _P, _P]),
-    "ndnet_tr_argmax_match_cm": (_I, [_P, _P, _I, _I, _I, _P, _P]),
+    "ndnet_tr_argmax_match_cm": (_I, [_P, _P, _I, _I, _I, _P, _P, _P]),
     "ndnet_row_argmax": (_I, [_P, _I64, _I, _P, _P]),
     "ndnet_tr_fc_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, ctypes.c_float, ctypes.c_float,
                              _I, _I, _P, _P]),
     "ndnet_tr_fc_bwd_w": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "ndnet_tr_fc_bwd_x": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P]),
-    "ndnet_tr_point_transform": (_I, [_P, _P, _P, _P, _I, _I, _P]),
-    "ndnet_tr_point_transform_bwd": (_I, [_P, _P, _P, _P, _I, _I, _P]),
+    "ndnet_tr_point_transform": (_I, [_P, _P, _I, _P, _I, _P, _I, _I, _P]),
+    "ndnet_tr_point_transform_bwd": (_I, [_P, _P, _I, _P, _I, _P, _I, _I, _P]),
     "ndnet_tr_log_softmax_c": (_I, [_P, _P, _I, _I, _I, _P]),
     "ndnet_tr_log_softmax_c_bwd": (_I, [_P, _P, _P, _I, _I, _I, _P]),
     "ndnet_tr_nll_onehot": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),

@@ -287,7 +287,7 @@ class _SegConv1(torch.autograd.Function):
             dW[:, :c].copy_(conv_weight_grad(dy, x))
             torch.mm(dcb.t(), g, out=dW[:, c:])
             dW = dW.view(ctx.w_shape)
-        db = chan_sum(dcb.view(Bn, Cout, 1)) if need[3] else None
+        db = dbias if need[3] else None  # sum over clouds and points of dy (bn_bwd's conv-bias output)
         dg = torch.mm(dcb, W[:, c:]) if need[1] else None
         return (dx, dg, dW, db, dgamma if need[4] else None, dbeta if need[5] else None,
                 None, None, None, None, None)
@@ -511,12 +511,14 @@ class _PointTransform(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, t, points, extra):
-        t, points, extra = t.contiguous(), points.contiguous(), extra.contiguous()
-        _check_f32(t, points, extra)
+        t = t.contiguous()
+        points, extra = _rows(points), _rows(extra)  # views of the NDT's [B,N,12] rows are read in place
+        _check_f32(t)
         Bn, N, _ = points.shape
         x = torch.empty((Bn, 12, N), device=points.device, dtype=torch.float32)
-        _lib.check(_lib.lib().ndnet_tr_point_transform(t.data_ptr(), points.data_ptr(), extra.data_ptr(), x.data_ptr(),
-                                                       Bn, N, _stream()), "ndnet_tr_point_transform")
+        _lib.check(_lib.lib().ndnet_tr_point_transform(t.data_ptr(), points.data_ptr(), points.stride(1),
+                                                       extra.data_ptr(), extra.stride(1), x.data_ptr(), Bn, N,
+                                                       _stream()), "ndnet_tr_point_transform")
         ctx.save_for_backward(points, extra)
         return x
 
@@ -526,10 +528,22 @@ class _PointTransform(torch.autograd.Function):
         dx = dx.contiguous()
         Bn, N, _ = points.shape
         dt = torch.empty((Bn, 3, 3), device=points.device, dtype=torch.float32)
-        _lib.check(_lib.lib().ndnet_tr_point_transform_bwd(dx.data_ptr(), points.data_ptr(), extra.data_ptr(),
-                                                           dt.data_ptr(), Bn, N, _stream()),
-                   "ndnet_tr_point_transform_bwd")
+        _lib.check(_lib.lib().ndnet_tr_point_transform_bwd(dx.data_ptr(), points.data_ptr(), points.stride(1),
+                                                           extra.data_ptr(), extra.stride(1), dt.data_ptr(), Bn, N,
+                                                           _stream()), "ndnet_tr_point_transform_bwd")
         return dt, None, None
+
+
+def _rows(a: torch.Tensor) -> torch.Tensor:
+    """a [B,N,w] as the point-transform kernels read it: rows of stride
+    a.stride(1) >= w floats, clouds N rows apart, unit column stride (a column
+    slice of a contiguous [B,N,W] block qualifies); otherwise a contiguous copy."""
+    if not (a.dtype == torch.float32 and a.is_cuda):
+        raise ValueError("train kernels take float32 cuda tensors")
+    Bn, N, w = a.shape
+    if a.stride(2) == 1 and a.stride(1) >= w and a.stride(0) == N * a.stride(1):
+        return a
+    return a.contiguous()
 
 
 def point_transform(t: torch.Tensor, points: torch.Tensor, extra: torch.Tensor) -> torch.Tensor:

@@ -604,6 +604,13 @@ def test_point_transform_matches_torch():
     x.backward(g)
     x64.backward(g.double())
     _close(t.grad, t64.grad, 1e-5, "point transform backward")
+    # ndt_preprocessing's views of one [B,N,12] block, read in place: the same bits
+    rows = torch.cat((p, c), dim=2)
+    t2 = t.detach().clone().requires_grad_()
+    xv = train_hip.point_transform(t2, rows[:, :, :3], rows[:, :, 3:])
+    assert torch.equal(xv, x)
+    xv.backward(g)
+    assert torch.equal(t2.grad, t.grad)
 
 
 def test_seg_conv1_matches_torch():
