@@ -144,7 +144,7 @@ __device__ inline int pn_tid() {
 
 // Timing build only (-DNDNET_PN_STAMPS, tools/pn_stamps.py): s_memrealtime
 // (100 MHz) of every workgroup at its start (0), after chain B's head
-// prologue (1), after the input tile (2), after each layer's closing barrier
+// prologue or chain C's t2 fold (1), after the input tile (2), after each layer's closing barrier
 // (3 + layer) and at its end (15), read back by ndnet_pn_debug_stamps.  The
 // product build compiles none of it.
 #ifdef NDNET_PN_STAMPS
@@ -1030,6 +1030,7 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
         }
       }
     }
+    PN_STAMP(1);  // (timing builds) chains C / D: t2 staged and folded into layer 0
   }
   __syncthreads();
   if (v0) {

@@ -67,7 +67,7 @@ for i, name in enumerate(ph.CHAIN_NAMES):
     print(f"chain {name}: launch span median {np.median(spans):.2f} us (first start -> last end, reps {a.reps})")
     st = rel[:, 0] * 10e-3
     print(f"  start skew: median {np.median(st):.2f} us, max {st.max():.2f} us")
-    labels = {0: "start", 1: "head prologue", 2: "input tile", 15: "end"}
+    labels = {0: "start", 1: "t2 fold" if name.startswith("C") else "head prologue", 2: "input tile", 15: "end"}
     for p, q in zip(idx, idx[1:]):
         d = (rel[:, idx.index(q)] - rel[:, idx.index(p)]) * 10e-3
         lab = labels.get(q, f"layer {q - 3}")
