@@ -3167,6 +3167,38 @@ __device__ inline uint32_t count_composite(KP K, SP S, uint32_t n, unsigned long
   return lo;
 }
 
+// #keys of Q sorted runs K[base[q], base[q] + len[q]) ahead of x (keys <= x
+// where le[q], else keys < x), searched together: the halving of count_nan3
+// with each run's own length (the runs a wave searches are the same for
+// every lane, so the loop's trip count is uniform).
+template <int Q, typename KP>
+__device__ inline void count_runs_q(KP K, const uint32_t (&base)[Q], const uint32_t (&len)[Q], unsigned long long x,
+                                    const bool (&le)[Q], uint32_t (&cnt)[Q]) {
+  uint32_t bq[Q], nq[Q];
+  unsigned long long xq[Q];
+#pragma unroll
+  for (int q = 0; q < Q; q++) {
+    bq[q] = base[q];
+    nq[q] = len[q];
+    xq[q] = le[q] && x != ~0ull ? x + 1 : x;
+  }
+  for (;;) {
+    bool any = false;
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+      if (nq[q] > 1) {
+        const uint32_t h = nq[q] >> 1;
+        bq[q] += K[bq[q] + h] < xq[q] ? h : 0u;
+        nq[q] -= h;
+        any = true;
+      }
+    }
+    if (!any) break;
+  }
+#pragma unroll
+  for (int q = 0; q < Q; q++) cnt[q] = nq[q] ? bq[q] - base[q] + (K[bq[q]] < xq[q] ? 1u : 0u) : 0u;
+}
+
 #ifndef NDNET_MERGE_Q
 #define NDNET_MERGE_Q 8
 #endif
@@ -3181,7 +3213,10 @@ constexpr int kMergeRuns = 2;  // chunks merged per k_kl_merge workgroup (512 th
 constexpr int kMergeRuns1 = NDNET_MERGE_RUNS1;
 
 // kMode 2: score runs and NaN keys in LDS, the NaN keys computed here (up to
-// kMergeLdsChunks chunks); 1: score runs in LDS, NaN keys from k_kl_nan_keys
+// kMergeLdsChunks chunks); the runs are stored compacted (each chunk's scores
+// only, at the prefix of the score counts; the NaN keys after them): at most
+// 6 ndcap keys, half the padded runs' LDS (round 5), and each run searched
+// over its own length.  1: score runs in LDS, NaN keys from k_kl_nan_keys
 // (up to kMergeScoreChunks); 0: everything from global memory.
 // kCoh: the list entries are stored write-through (sc1) for a last
 // workgroup on another XCD to read in the same launch (k_kl_merge's tail).
@@ -3251,6 +3286,7 @@ __device__ inline void merge_runs(const KLArgs& A, const int b) {
   __shared__ uint32_t s_own_num_slot[kMergeRuns][kChunk];
   __shared__ uint32_t s_own_nan_slot[kMergeRuns][kChunk];
   __shared__ double s_pre_min[kLds ? kChunk * kMergeRuns : 1];
+  __shared__ uint32_t s_sb[kLds ? kMergeLdsChunks + 1 : 1];  // mode 2: compacted run bases (+ the score total)
   if (kLds && tid < nch * kNanPre) s_pre_min[tid] = pre_min;
   for (uint32_t c2 = tid; c2 < nch; c2 += blockDim.x) {
     s_cnt[c2] = A.chunk_cnt[cb + c2];
@@ -3260,43 +3296,52 @@ __device__ inline void merge_runs(const KLArgs& A, const int b) {
   if (!kLds && tid == 0) s_nb[nch] = A.chunk_nanbase[cb + nch - 1] + (A.chunk_cnt[cb + nch - 1] & 0xffffu);  // NaN total
   const unsigned long long* gN = A.nan_key_all + eb;
   if (ch < nch) s_own_num_slot[lc][t] = A.sort_idx_all[kb + ch * kChunk + t];
-  if (kLds) {
-    ulonglong2* dst = reinterpret_cast<ulonglong2*>(lK);
-#pragma unroll
-    for (int u = 0; u < kStageU; u++) {
-      const uint32_t i = u * blockDim.x + tid;
-      if (i < nv) dst[i] = sv[u];
-    }
-  }
   __syncthreads();
   MERGE_MARK(16);
   if (kLds) {
-    // the NaN bases and the min over earlier chunks (k_kl_nan_keys' scans),
-    // one lane per chunk (nch <= kMergeLdsChunks < 64)
+    // the NaN bases, the score bases and the min over earlier chunks
+    // (k_kl_nan_keys' scans), one lane per chunk (nch <= kMergeLdsChunks < 64)
     if (tid < 64) {
-      uint32_t nn = tid < nch ? (s_cnt[tid] & 0xffffu) : 0u;
+      uint32_t nn = tid < nch ? (s_cnt[tid] & 0xffffu) : 0u, ns = tid < nch ? (s_cnt[tid] >> 16) : 0u;
       double cm = tid < nch ? s_pm[tid] : __builtin_inf();
       for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t o = __shfl_up(nn, off, 64);
+        const uint32_t o = __shfl_up(nn, off, 64), os = __shfl_up(ns, off, 64);
         const double om = __shfl_up(cm, off, 64);
         if ((int)tid >= off) {
           nn += o;
+          ns += os;
           cm = MinF64()(cm, om);
         }
       }
-      uint32_t ex = __shfl_up(nn, 1, 64);
+      uint32_t ex = __shfl_up(nn, 1, 64), exs = __shfl_up(ns, 1, 64);
       double exm = __shfl_up(cm, 1, 64);
       if (tid == 0) {
-        ex = 0;
+        ex = exs = 0;
         exm = __builtin_inf();
       }
       if (tid < nch) {
         s_nb[tid] = ex;
+        s_sb[tid] = exs;
         s_pm[tid] = exm;
       }
-      if (tid + 1 == nch) s_nb[nch] = nn;
+      if (tid + 1 == nch) {
+        s_nb[nch] = nn;
+        s_sb[nch] = ns;
+      }
     }
     __syncthreads();
+    // the staged runs into LDS, compacted: chunk c's scores at s_sb[c]
+#pragma unroll
+    for (int u = 0; u < kStageU; u++) {
+      const uint32_t i = u * blockDim.x + tid;
+      if (i < nv) {
+        const uint32_t e = 2 * i, c2 = e / kChunk, pp = e % kChunk;  // a pair never straddles chunks
+        const uint32_t ns = s_cnt[c2] >> 16, sb = s_sb[c2];
+        if (pp < ns) lK[sb + pp] = sv[u].x;
+        if (pp + 1 < ns) lK[sb + pp + 1] = sv[u].y;
+      }
+    }
+    lN = lK + s_sb[nch];
     MERGE_MARK(17);
   }
   const uint32_t nnan_tot = s_nb[nch];
@@ -3330,12 +3375,14 @@ __device__ inline void merge_runs(const KLArgs& A, const int b) {
   if (!is_num && t >= nnum + nnan) return;
   const uint32_t* own_num_slot = s_own_num_slot[lc];
   const uint32_t* own_nan_slot = s_own_nan_slot[lc];
+  // a run's first key: compacted (mode 2) or kChunk-padded
+  const uint32_t own_base = kLds ? s_sb[ch] : ch * kChunk;
   auto body = [&](auto K, auto N) {
     uint32_t sl;
     unsigned long long x;
     uint32_t pos;
     if (is_num) {
-      x = K[ch * kChunk + t];
+      x = K[own_base + t];
       sl = own_num_slot[t];
       pos = t;
       // NaN events ahead: earlier chunks (key <= x), this chunk (composite), later chunks (key < x)
@@ -3347,7 +3394,7 @@ __device__ inline void merge_runs(const KLArgs& A, const int b) {
       x = N[nb0 + j];
       sl = own_nan_slot[j];
       // scores of its own chunk ahead of it, then every earlier NaN
-      pos = count_composite(K + ch * kChunk, own_num_slot, nnum, x, sl) + nb0 + j;
+      pos = count_composite(K + own_base, own_num_slot, nnum, x, sl) + nb0 + j;
     }
     // scores of the other chunks ahead of it, kMergeQ runs per pass
     for (uint32_t c0 = 0; c0 < nch; c0 += kMergeQ) {
@@ -3359,7 +3406,17 @@ __device__ inline void merge_runs(const KLArgs& A, const int b) {
         run[q] = (c2 < nch && c2 != ch) ? c2 : ch;  // own run: masked below
         le[q] = c2 < ch;
       }
-      count_before_q<kMergeQ>(K, run, x, le, add);
+      if constexpr (kLds) {
+        uint32_t rb[kMergeQ], rl[kMergeQ];
+#pragma unroll
+        for (int q = 0; q < kMergeQ; q++) {
+          rb[q] = s_sb[run[q]];
+          rl[q] = s_cnt[run[q]] >> 16;
+        }
+        count_runs_q<kMergeQ>(K, rb, rl, x, le, add);
+      } else {
+        count_before_q<kMergeQ>(K, run, x, le, add);
+      }
 #pragma unroll
       for (int q = 0; q < kMergeQ; q++)
         if (c0 + q < nch && c0 + q != ch) pos += add[q];
@@ -3723,7 +3780,8 @@ static int build_deferred_lists(Plan* P, hipStream_t st) {
   return NDNET_OK;
 }
 
-static size_t merge_lds_bytes(const Plan* P) { return 2 * (size_t)P->nchunk * kChunk * sizeof(unsigned long long); }
+// mode 2's dynamic LDS: every event's key once (compacted score runs + NaN keys)
+static size_t merge_lds_bytes(const Plan* P) { return (size_t)P->ecap * sizeof(unsigned long long); }
 
 // ---- k_front admission: the device's front lanes ----
 //
