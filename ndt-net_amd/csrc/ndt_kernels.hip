@@ -50,7 +50,10 @@ constexpr int kBitsWords = kBitsCap / 32;
 constexpr int kKLThreads = 1024;
 constexpr int kChunk = 256;          // slots per chunk of the chip-wide event sort
 constexpr int kKLMarks = 32;  // phase stamps per cloud of the KL kernels (timing level 2)
-constexpr int kMergeLdsChunks = 34;  // k_kl_merge stages score + NaN keys in LDS up to this many chunks (136 KB)
+// k_kl_merge stages the score runs (compacted) + NaN keys in LDS up to this
+// many chunks (ecap keys <= 128 KB; round 4's padded runs took 2 x 34 chunks'
+// worth, so C5's 2000-ND level ran mode 1 with its extra k_kl_nan_keys launch)
+constexpr int kMergeLdsChunks = 64;
 constexpr int kMergeScoreChunks = 72; // ... and the score runs alone up to this many (144 KB; k <= 2440)
 constexpr int kMaxChunks = 6 * 16384 / kChunk;  // ndcap <= 16384
 // NDs with at least this many samples get a whole wave each in k_welford_q
@@ -3300,7 +3303,7 @@ __device__ inline void merge_runs(const KLArgs& A, const int b) {
   MERGE_MARK(16);
   if (kLds) {
     // the NaN bases, the score bases and the min over earlier chunks
-    // (k_kl_nan_keys' scans), one lane per chunk (nch <= kMergeLdsChunks < 64)
+    // (k_kl_nan_keys' scans), one lane per chunk (nch <= kMergeLdsChunks <= 64)
     if (tid < 64) {
       uint32_t nn = tid < nch ? (s_cnt[tid] & 0xffffu) : 0u, ns = tid < nch ? (s_cnt[tid] >> 16) : 0u;
       double cm = tid < nch ? s_pm[tid] : __builtin_inf();
@@ -4257,7 +4260,7 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
                             (int)(kWqRt * kWqRtBytes + 8 * ((batch + 1 + 3) & ~3) + kWqHistMax));
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_kl_merge<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(2 * kMergeLdsChunks * kChunk * sizeof(unsigned long long)));
+                            (int)(kMergeLdsChunks * kChunk * sizeof(unsigned long long)));
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_kl_merge<1, kMergeRuns1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(kMergeScoreChunks * kChunk * sizeof(unsigned long long)));
