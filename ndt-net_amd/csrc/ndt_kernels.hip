@@ -54,6 +54,10 @@ constexpr int kKLMarks = 32;  // phase stamps per cloud of the KL kernels (timin
 // many chunks (ecap keys <= 128 KB; round 4's padded runs took 2 x 34 chunks'
 // worth, so C5's 2000-ND level ran mode 1 with its extra k_kl_nan_keys launch)
 constexpr int kMergeLdsChunks = 64;
+// ... two runs per 512-thread workgroup up to this many chunks, then four per
+// 1024-thread workgroup (a 57-chunk C5 level in one round of workgroups: the
+// LDS allows one per CU)
+constexpr int kMergeLds2Chunks = 34;
 constexpr int kMergeScoreChunks = 72; // ... and the score runs alone up to this many (144 KB; k <= 2440)
 constexpr int kMaxChunks = 6 * 16384 / kChunk;  // ndcap <= 16384
 // NDs with at least this many samples get a whole wave each in k_welford_q
@@ -3172,31 +3176,36 @@ __device__ inline uint32_t count_composite(KP K, SP S, uint32_t n, unsigned long
 
 // #keys of Q sorted runs K[base[q], base[q] + len[q]) ahead of x (keys <= x
 // where le[q], else keys < x), searched together: the halving of count_nan3
-// with each run's own length (the runs a wave searches are the same for
-// every lane, so the loop's trip count is uniform).
+// with each run's own length.  The runs a wave searches are the same for
+// every lane, so the round count (that of the longest run) is uniform, and
+// every round issues all Q probes unconditionally (a run already down to one
+// key re-reads it, h = 0), so the Q reads of a round are in flight together.
 template <int Q, typename KP>
 __device__ inline void count_runs_q(KP K, const uint32_t (&base)[Q], const uint32_t (&len)[Q], unsigned long long x,
                                     const bool (&le)[Q], uint32_t (&cnt)[Q]) {
-  uint32_t bq[Q], nq[Q];
+  uint32_t bq[Q], nq[Q], rounds = 0;
   unsigned long long xq[Q];
 #pragma unroll
   for (int q = 0; q < Q; q++) {
-    bq[q] = base[q];
+    bq[q] = len[q] ? base[q] : 0u;  // an empty run probes key 0 (any valid index), counted as 0
     nq[q] = len[q];
     xq[q] = le[q] && x != ~0ull ? x + 1 : x;
+    const uint32_t r = len[q] > 1 ? 32u - (uint32_t)__clz((int)(len[q] - 1)) : 0u;
+    rounds = r > rounds ? r : rounds;
   }
-  for (;;) {
-    bool any = false;
+  for (uint32_t r = 0; r < rounds; r++) {
+    uint32_t h[Q];
+    unsigned long long kv[Q];
 #pragma unroll
     for (int q = 0; q < Q; q++) {
-      if (nq[q] > 1) {
-        const uint32_t h = nq[q] >> 1;
-        bq[q] += K[bq[q] + h] < xq[q] ? h : 0u;
-        nq[q] -= h;
-        any = true;
-      }
+      h[q] = nq[q] >> 1;
+      kv[q] = K[bq[q] + h[q]];
     }
-    if (!any) break;
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+      bq[q] += kv[q] < xq[q] ? h[q] : 0u;
+      nq[q] -= h[q];
+    }
   }
 #pragma unroll
   for (int q = 0; q < Q; q++) cnt[q] = nq[q] ? bq[q] - base[q] + (K[bq[q]] < xq[q] ? 1u : 0u) : 0u;
@@ -3731,7 +3740,10 @@ __global__ void __launch_bounds__(256) k_kl_chains(KLArgs A) {
 
 // The dynamic LDS of the fused merge + prune launches (k_kl_merge<.., true>):
 // the larger of the merge's and the LDS-resident prune's (kl_lds_bytes).
-constexpr size_t kKLFusedLds = kMergeScoreChunks * kChunk * sizeof(unsigned long long);  // 144 KB
+// 136 KB: with the four-run merge's ~20 KB of static LDS it stays within the
+// CU's 160 KB (a C5 2000-ND level's prune needs 127 KB; mode 1 and 0 plans,
+// k > 2270, exceed it and keep k_kl)
+constexpr size_t kKLFusedLds = 136 * 1024;
 static size_t kl_lds_bytes(const Plan* P);
 
 // tail: the merge's last workgroup per cloud also prunes and emits the rows
@@ -3742,9 +3754,15 @@ static void launch_list_sort(Plan* P, const KLArgs& A, hipStream_t st, bool tail
   const uint32_t mg = (P->nchunk + kMergeRuns - 1) / kMergeRuns;
   const size_t kl = tail ? kl_lds_bytes(P) : 0;
   auto dyn = [&](size_t m) { return m > kl ? m : kl; };
-  if (P->nchunk <= (uint32_t)kMergeLdsChunks) {  // the merge computes the NaN keys itself
+  if (P->nchunk <= (uint32_t)kMergeLds2Chunks) {  // the merge computes the NaN keys itself
     if (tail) k_kl_merge<2, kMergeRuns, true><<<dim3(mg, B), kChunk * kMergeRuns, dyn(merge_lds_bytes(P)), st>>>(A);
     else k_kl_merge<2><<<dim3(mg, B), kChunk * kMergeRuns, merge_lds_bytes(P), st>>>(A);
+  } else if (P->nchunk <= (uint32_t)kMergeLdsChunks) {  // the same, four runs per 1024-thread workgroup
+    const uint32_t mg1 = (P->nchunk + kMergeRuns1 - 1) / kMergeRuns1;
+    if (tail)
+      k_kl_merge<2, kMergeRuns1, true><<<dim3(mg1, B), kChunk * kMergeRuns1, dyn(merge_lds_bytes(P)), st>>>(A);
+    else
+      k_kl_merge<2, kMergeRuns1><<<dim3(mg1, B), kChunk * kMergeRuns1, merge_lds_bytes(P), st>>>(A);
   } else if (P->nchunk <= (uint32_t)kMergeScoreChunks) {
     k_kl_nan_keys<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
     KLArgs A1 = A;
@@ -3764,7 +3782,7 @@ static void launch_list_sort(Plan* P, const KLArgs& A, hipStream_t st, bool tail
 }
 
 // The run's prune can ride on the merge launch: the prune's arrays fit the
-// fused launch's LDS (the LDS-resident prune) and NDNET_KL_FUSE is not 0.
+// fused launch's LDS (kKLFusedLds) (the LDS-resident prune) and NDNET_KL_FUSE is not 0.
 static bool kl_fusable(const Plan* P, const KLArgs& A) {
   return P->kl_fuse && A.kl_lds && kl_lds_bytes(P) <= kKLFusedLds;
 }
@@ -4261,6 +4279,12 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_kl_merge<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(kMergeLdsChunks * kChunk * sizeof(unsigned long long)));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_kl_merge<2, kMergeRuns1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(kMergeLdsChunks * kChunk * sizeof(unsigned long long)));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_kl_merge<2, kMergeRuns1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)kKLFusedLds);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_kl_merge<1, kMergeRuns1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(kMergeScoreChunks * kChunk * sizeof(unsigned long long)));
