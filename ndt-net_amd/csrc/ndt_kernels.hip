@@ -50,14 +50,7 @@ constexpr int kBitsWords = kBitsCap / 32;
 constexpr int kKLThreads = 1024;
 constexpr int kChunk = 256;          // slots per chunk of the chip-wide event sort
 constexpr int kKLMarks = 32;  // phase stamps per cloud of the KL kernels (timing level 2)
-// k_kl_merge stages the score runs (compacted) + NaN keys in LDS up to this
-// many chunks (ecap keys <= 128 KB; round 4's padded runs took 2 x 34 chunks'
-// worth, so C5's 2000-ND level ran mode 1 with its extra k_kl_nan_keys launch)
-constexpr int kMergeLdsChunks = 64;
-// ... two runs per 512-thread workgroup up to this many chunks, then four per
-// 1024-thread workgroup (a 57-chunk C5 level in one round of workgroups: the
-// LDS allows one per CU)
-constexpr int kMergeLds2Chunks = 34;
+constexpr int kMergeLdsChunks = 34;  // k_kl_merge stages score + NaN keys in LDS up to this many chunks (136 KB)
 constexpr int kMergeScoreChunks = 72; // ... and the score runs alone up to this many (144 KB; k <= 2440)
 constexpr int kMaxChunks = 6 * 16384 / kChunk;  // ndcap <= 16384
 // NDs with at least this many samples get a whole wave each in k_welford_q
@@ -3174,43 +3167,6 @@ __device__ inline uint32_t count_composite(KP K, SP S, uint32_t n, unsigned long
   return lo;
 }
 
-// #keys of Q sorted runs K[base[q], base[q] + len[q]) ahead of x (keys <= x
-// where le[q], else keys < x), searched together: the halving of count_nan3
-// with each run's own length.  The runs a wave searches are the same for
-// every lane, so the round count (that of the longest run) is uniform, and
-// every round issues all Q probes unconditionally (a run already down to one
-// key re-reads it, h = 0), so the Q reads of a round are in flight together.
-template <int Q, typename KP>
-__device__ inline void count_runs_q(KP K, const uint32_t (&base)[Q], const uint32_t (&len)[Q], unsigned long long x,
-                                    const bool (&le)[Q], uint32_t (&cnt)[Q]) {
-  uint32_t bq[Q], nq[Q], rounds = 0;
-  unsigned long long xq[Q];
-#pragma unroll
-  for (int q = 0; q < Q; q++) {
-    bq[q] = len[q] ? base[q] : 0u;  // an empty run probes key 0 (any valid index), counted as 0
-    nq[q] = len[q];
-    xq[q] = le[q] && x != ~0ull ? x + 1 : x;
-    const uint32_t r = len[q] > 1 ? 32u - (uint32_t)__clz((int)(len[q] - 1)) : 0u;
-    rounds = r > rounds ? r : rounds;
-  }
-  for (uint32_t r = 0; r < rounds; r++) {
-    uint32_t h[Q];
-    unsigned long long kv[Q];
-#pragma unroll
-    for (int q = 0; q < Q; q++) {
-      h[q] = nq[q] >> 1;
-      kv[q] = K[bq[q] + h[q]];
-    }
-#pragma unroll
-    for (int q = 0; q < Q; q++) {
-      bq[q] += kv[q] < xq[q] ? h[q] : 0u;
-      nq[q] -= h[q];
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < Q; q++) cnt[q] = nq[q] ? bq[q] - base[q] + (K[bq[q]] < xq[q] ? 1u : 0u) : 0u;
-}
-
 #ifndef NDNET_MERGE_Q
 #define NDNET_MERGE_Q 8
 #endif
@@ -3225,10 +3181,7 @@ constexpr int kMergeRuns = 2;  // chunks merged per k_kl_merge workgroup (512 th
 constexpr int kMergeRuns1 = NDNET_MERGE_RUNS1;
 
 // kMode 2: score runs and NaN keys in LDS, the NaN keys computed here (up to
-// kMergeLdsChunks chunks); the runs are stored compacted (each chunk's scores
-// only, at the prefix of the score counts; the NaN keys after them): at most
-// 6 ndcap keys, half the padded runs' LDS (round 5), and each run searched
-// over its own length.  1: score runs in LDS, NaN keys from k_kl_nan_keys
+// kMergeLdsChunks chunks); 1: score runs in LDS, NaN keys from k_kl_nan_keys
 // (up to kMergeScoreChunks); 0: everything from global memory.
 // kCoh: the list entries are stored write-through (sc1) for a last
 // workgroup on another XCD to read in the same launch (k_kl_merge's tail).
@@ -3298,7 +3251,6 @@ __device__ inline void merge_runs(const KLArgs& A, const int b) {
   __shared__ uint32_t s_own_num_slot[kMergeRuns][kChunk];
   __shared__ uint32_t s_own_nan_slot[kMergeRuns][kChunk];
   __shared__ double s_pre_min[kLds ? kChunk * kMergeRuns : 1];
-  __shared__ uint32_t s_sb[kLds ? kMergeLdsChunks + 1 : 1];  // mode 2: compacted run bases (+ the score total)
   if (kLds && tid < nch * kNanPre) s_pre_min[tid] = pre_min;
   for (uint32_t c2 = tid; c2 < nch; c2 += blockDim.x) {
     s_cnt[c2] = A.chunk_cnt[cb + c2];
@@ -3308,52 +3260,43 @@ __device__ inline void merge_runs(const KLArgs& A, const int b) {
   if (!kLds && tid == 0) s_nb[nch] = A.chunk_nanbase[cb + nch - 1] + (A.chunk_cnt[cb + nch - 1] & 0xffffu);  // NaN total
   const unsigned long long* gN = A.nan_key_all + eb;
   if (ch < nch) s_own_num_slot[lc][t] = A.sort_idx_all[kb + ch * kChunk + t];
+  if (kLds) {
+    ulonglong2* dst = reinterpret_cast<ulonglong2*>(lK);
+#pragma unroll
+    for (int u = 0; u < kStageU; u++) {
+      const uint32_t i = u * blockDim.x + tid;
+      if (i < nv) dst[i] = sv[u];
+    }
+  }
   __syncthreads();
   MERGE_MARK(16);
   if (kLds) {
-    // the NaN bases, the score bases and the min over earlier chunks
-    // (k_kl_nan_keys' scans), one lane per chunk (nch <= kMergeLdsChunks <= 64)
+    // the NaN bases and the min over earlier chunks (k_kl_nan_keys' scans),
+    // one lane per chunk (nch <= kMergeLdsChunks < 64)
     if (tid < 64) {
-      uint32_t nn = tid < nch ? (s_cnt[tid] & 0xffffu) : 0u, ns = tid < nch ? (s_cnt[tid] >> 16) : 0u;
+      uint32_t nn = tid < nch ? (s_cnt[tid] & 0xffffu) : 0u;
       double cm = tid < nch ? s_pm[tid] : __builtin_inf();
       for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t o = __shfl_up(nn, off, 64), os = __shfl_up(ns, off, 64);
+        const uint32_t o = __shfl_up(nn, off, 64);
         const double om = __shfl_up(cm, off, 64);
         if ((int)tid >= off) {
           nn += o;
-          ns += os;
           cm = MinF64()(cm, om);
         }
       }
-      uint32_t ex = __shfl_up(nn, 1, 64), exs = __shfl_up(ns, 1, 64);
+      uint32_t ex = __shfl_up(nn, 1, 64);
       double exm = __shfl_up(cm, 1, 64);
       if (tid == 0) {
-        ex = exs = 0;
+        ex = 0;
         exm = __builtin_inf();
       }
       if (tid < nch) {
         s_nb[tid] = ex;
-        s_sb[tid] = exs;
         s_pm[tid] = exm;
       }
-      if (tid + 1 == nch) {
-        s_nb[nch] = nn;
-        s_sb[nch] = ns;
-      }
+      if (tid + 1 == nch) s_nb[nch] = nn;
     }
     __syncthreads();
-    // the staged runs into LDS, compacted: chunk c's scores at s_sb[c]
-#pragma unroll
-    for (int u = 0; u < kStageU; u++) {
-      const uint32_t i = u * blockDim.x + tid;
-      if (i < nv) {
-        const uint32_t e = 2 * i, c2 = e / kChunk, pp = e % kChunk;  // a pair never straddles chunks
-        const uint32_t ns = s_cnt[c2] >> 16, sb = s_sb[c2];
-        if (pp < ns) lK[sb + pp] = sv[u].x;
-        if (pp + 1 < ns) lK[sb + pp + 1] = sv[u].y;
-      }
-    }
-    lN = lK + s_sb[nch];
     MERGE_MARK(17);
   }
   const uint32_t nnan_tot = s_nb[nch];
@@ -3387,14 +3330,12 @@ __device__ inline void merge_runs(const KLArgs& A, const int b) {
   if (!is_num && t >= nnum + nnan) return;
   const uint32_t* own_num_slot = s_own_num_slot[lc];
   const uint32_t* own_nan_slot = s_own_nan_slot[lc];
-  // a run's first key: compacted (mode 2) or kChunk-padded
-  const uint32_t own_base = kLds ? s_sb[ch] : ch * kChunk;
   auto body = [&](auto K, auto N) {
     uint32_t sl;
     unsigned long long x;
     uint32_t pos;
     if (is_num) {
-      x = K[own_base + t];
+      x = K[ch * kChunk + t];
       sl = own_num_slot[t];
       pos = t;
       // NaN events ahead: earlier chunks (key <= x), this chunk (composite), later chunks (key < x)
@@ -3406,7 +3347,7 @@ __device__ inline void merge_runs(const KLArgs& A, const int b) {
       x = N[nb0 + j];
       sl = own_nan_slot[j];
       // scores of its own chunk ahead of it, then every earlier NaN
-      pos = count_composite(K + own_base, own_num_slot, nnum, x, sl) + nb0 + j;
+      pos = count_composite(K + ch * kChunk, own_num_slot, nnum, x, sl) + nb0 + j;
     }
     // scores of the other chunks ahead of it, kMergeQ runs per pass
     for (uint32_t c0 = 0; c0 < nch; c0 += kMergeQ) {
@@ -3418,17 +3359,7 @@ __device__ inline void merge_runs(const KLArgs& A, const int b) {
         run[q] = (c2 < nch && c2 != ch) ? c2 : ch;  // own run: masked below
         le[q] = c2 < ch;
       }
-      if constexpr (kLds) {
-        uint32_t rb[kMergeQ], rl[kMergeQ];
-#pragma unroll
-        for (int q = 0; q < kMergeQ; q++) {
-          rb[q] = s_sb[run[q]];
-          rl[q] = s_cnt[run[q]] >> 16;
-        }
-        count_runs_q<kMergeQ>(K, rb, rl, x, le, add);
-      } else {
-        count_before_q<kMergeQ>(K, run, x, le, add);
-      }
+      count_before_q<kMergeQ>(K, run, x, le, add);
 #pragma unroll
       for (int q = 0; q < kMergeQ; q++)
         if (c0 + q < nch && c0 + q != ch) pos += add[q];
@@ -3740,10 +3671,7 @@ __global__ void __launch_bounds__(256) k_kl_chains(KLArgs A) {
 
 // The dynamic LDS of the fused merge + prune launches (k_kl_merge<.., true>):
 // the larger of the merge's and the LDS-resident prune's (kl_lds_bytes).
-// 136 KB: with the four-run merge's ~20 KB of static LDS it stays within the
-// CU's 160 KB (a C5 2000-ND level's prune needs 127 KB; mode 1 and 0 plans,
-// k > 2270, exceed it and keep k_kl)
-constexpr size_t kKLFusedLds = 136 * 1024;
+constexpr size_t kKLFusedLds = kMergeScoreChunks * kChunk * sizeof(unsigned long long);  // 144 KB
 static size_t kl_lds_bytes(const Plan* P);
 
 // tail: the merge's last workgroup per cloud also prunes and emits the rows
@@ -3754,15 +3682,9 @@ static void launch_list_sort(Plan* P, const KLArgs& A, hipStream_t st, bool tail
   const uint32_t mg = (P->nchunk + kMergeRuns - 1) / kMergeRuns;
   const size_t kl = tail ? kl_lds_bytes(P) : 0;
   auto dyn = [&](size_t m) { return m > kl ? m : kl; };
-  if (P->nchunk <= (uint32_t)kMergeLds2Chunks) {  // the merge computes the NaN keys itself
+  if (P->nchunk <= (uint32_t)kMergeLdsChunks) {  // the merge computes the NaN keys itself
     if (tail) k_kl_merge<2, kMergeRuns, true><<<dim3(mg, B), kChunk * kMergeRuns, dyn(merge_lds_bytes(P)), st>>>(A);
     else k_kl_merge<2><<<dim3(mg, B), kChunk * kMergeRuns, merge_lds_bytes(P), st>>>(A);
-  } else if (P->nchunk <= (uint32_t)kMergeLdsChunks) {  // the same, four runs per 1024-thread workgroup
-    const uint32_t mg1 = (P->nchunk + kMergeRuns1 - 1) / kMergeRuns1;
-    if (tail)
-      k_kl_merge<2, kMergeRuns1, true><<<dim3(mg1, B), kChunk * kMergeRuns1, dyn(merge_lds_bytes(P)), st>>>(A);
-    else
-      k_kl_merge<2, kMergeRuns1><<<dim3(mg1, B), kChunk * kMergeRuns1, merge_lds_bytes(P), st>>>(A);
   } else if (P->nchunk <= (uint32_t)kMergeScoreChunks) {
     k_kl_nan_keys<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
     KLArgs A1 = A;
@@ -3782,7 +3704,7 @@ static void launch_list_sort(Plan* P, const KLArgs& A, hipStream_t st, bool tail
 }
 
 // The run's prune can ride on the merge launch: the prune's arrays fit the
-// fused launch's LDS (kKLFusedLds) (the LDS-resident prune) and NDNET_KL_FUSE is not 0.
+// fused launch's LDS (the LDS-resident prune) and NDNET_KL_FUSE is not 0.
 static bool kl_fusable(const Plan* P, const KLArgs& A) {
   return P->kl_fuse && A.kl_lds && kl_lds_bytes(P) <= kKLFusedLds;
 }
@@ -3801,8 +3723,7 @@ static int build_deferred_lists(Plan* P, hipStream_t st) {
   return NDNET_OK;
 }
 
-// mode 2's dynamic LDS: every event's key once (compacted score runs + NaN keys)
-static size_t merge_lds_bytes(const Plan* P) { return (size_t)P->ecap * sizeof(unsigned long long); }
+static size_t merge_lds_bytes(const Plan* P) { return 2 * (size_t)P->nchunk * kChunk * sizeof(unsigned long long); }
 
 // ---- k_front admission: the device's front lanes ----
 //
@@ -4278,13 +4199,7 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
                             (int)(kWqRt * kWqRtBytes + 8 * ((batch + 1 + 3) & ~3) + kWqHistMax));
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_kl_merge<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(kMergeLdsChunks * kChunk * sizeof(unsigned long long)));
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_kl_merge<2, kMergeRuns1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(kMergeLdsChunks * kChunk * sizeof(unsigned long long)));
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_kl_merge<2, kMergeRuns1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)kKLFusedLds);
+                            (int)(2 * kMergeLdsChunks * kChunk * sizeof(unsigned long long)));
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_kl_merge<1, kMergeRuns1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(kMergeScoreChunks * kChunk * sizeof(unsigned long long)));

@@ -581,13 +581,12 @@ def test_front_barrier_timeout_fails_clouds_cleanly():
 
 @pytest.mark.parametrize("k", [1300, 2000, 2400, 2600])
 def test_merge_paths_match_oracle(k):
-    """The three k_kl_merge forms by list size: the all-LDS merge (compacted
-    score runs + NaN keys computed in place) up to 64 chunks -- k = 1000 in
-    every other test, 1300 and 2000 (C5's first level) past round 4's 34-chunk
-    limit --, k = 2400 the score-runs-in-LDS form with k_kl_nan_keys (65-72
-    chunks), k = 2600 the global-memory form (> 72 chunks; its prune also takes
-    the global-memory walk).  Rows, event counts and the level-1 list against
-    the oracle, on clouds whose prune removes NDs."""
+    """The three k_kl_merge forms by list size: k = 1000 runs the all-LDS merge
+    (every other test), k = 1300, 2000 (C5's first level) and 2400 the
+    score-runs-in-LDS form with k_kl_nan_keys (35-72 chunks), k = 2600 the
+    global-memory form (> 72 chunks; its prune also takes the global-memory
+    walk).  Rows, event counts and the level-1 list against the oracle, on
+    clouds whose prune removes NDs."""
     import torch
     import oracle as O
     from ndnet.preprocessing.ndtnet_preprocessing import ndt_preprocessing, last_stats
