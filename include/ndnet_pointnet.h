@@ -177,6 +177,15 @@ int ndnet_pn_fold_run(const ndnet_pn_fold_job *device_jobs, int num_jobs, int64_
 int ndnet_pn_head3_run(const float *h2, int ld_h, const float *W3, const float *b3, const float *basis,
                        float *t1, float *w1f, int batch, int K, int kin, int nout, void *stream);
 
+/* TNet(64)'s transform through conv1 (ndtnet.py:152-155), once per cloud, for
+ * chains C and D's layer 0 (round 5; chain C's fold_t2 prologue did it per
+ * workgroup): outf[b] = (w1f[b] as W1'^T, 12 of its 16 rows) @ t2[b] in the
+ * fragment-major K = 16 layout (rows 12..15 untouched), outb[b] = b1^T t2[b].
+ * w1f [batch][w1_stride >= 1024], b1 [64], t2 [batch][t2_ld >= 4096] (16-byte
+ * aligned), outf [batch][1024], outb [batch][64]. */
+int ndnet_pn_fold_t2_run(const float *w1f, int w1_stride, const float *b1, const float *t2, int t2_ld, float *outf,
+                         float *outb, int batch, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1364,6 +1364,41 @@ __global__ void __launch_bounds__(256) k_pn_fc_split(const float* __restrict__ i
   }
 }
 
+// TNet(64)'s transform through conv1 for chains C and D (ndtnet.py:152-155,
+// x_t2 = t2^T (W1' x + b1)): W1''[b] = W1'[b]^T t2[b] (12 x 64) and b1''[b] =
+// b1^T t2[b], once per cloud, written as chains C / D read their layer 0
+// (fragment-major, K padded to 16, rows 12..15 left as they are: zero) and
+// the per-cloud bias.  fp32 FMAs in i order.  (Before round 5 every chain-C
+// workgroup computed it in its prologue on the fp32 MFMA: 16 workgroups per
+// cloud doing the same 16 x 64 x 64 product, ~2 us of each one's time.)
+__global__ void __launch_bounds__(1024) k_pn_fold_t2(const float* __restrict__ w1f, int w1_stride,
+                                                     const float* __restrict__ b1, const float* __restrict__ t2,
+                                                     int t2_ld, float* __restrict__ outf, float* __restrict__ outb) {
+  const int b = blockIdx.x, e = threadIdx.x;
+  __shared__ float s_w[13 * 64];  // rows 0..11 W1'^T (row-major [k][n]), row 12 the bias
+  __shared__ float s_t[64 * 64];
+  {
+    const float* wb = w1f + (int64_t)b * w1_stride;
+    if (e < 16 * 64) {  // fragment-major element e -> (k, n)
+      const int cb = e >> 8, ln = (e >> 2) & 63, k = 4 * (ln >> 4) + (e & 3), n = 16 * cb + (ln & 15);
+      const float v = wb[e];
+      if (k < 12) s_w[k * 64 + n] = v;
+    }
+    if (e < 64) s_w[12 * 64 + e] = b1[e];
+    const f32x4* tb = reinterpret_cast<const f32x4*>(t2 + (int64_t)b * t2_ld);
+    reinterpret_cast<f32x4*>(s_t)[e] = tb[e];  // 1024 threads x 4 = the 64 x 64 matrix
+  }
+  __syncthreads();
+  if (e < 13 * 64) {
+    const int r = e >> 6, n = e & 63;
+    float acc = 0.0f;
+#pragma unroll 16
+    for (int i = 0; i < 64; i++) acc = fmaf(s_w[r * 64 + i], s_t[i * 64 + n], acc);
+    if (r < 12) outf[(int64_t)b * 1024 + ((((n >> 4) * 64 + ((r >> 2) & 3) * 16 + (n & 15)) << 2) + (r & 3))] = acc;
+    else outb[(int64_t)b * 64 + n] = acc;
+  }
+}
+
 // TNet(3) tail: t1[b] = fc3(h2[b]) (+ I, folded into the bias) and the t1
 // fold of conv1, W1'^T[b] = t1[b] (1 x 9) @ basis (9 x kin*nout), written
 // fragment-major with K padded to 16 (rows kin..15 zero).  One workgroup per cloud.
@@ -1572,6 +1607,15 @@ int ndnet_pn_head3_run(const float* h2, int ld_h, const float* W3, const float* 
       nout % 16)
     return -20;
   k_pn_head3<<<batch, 256, 0, (hipStream_t)stream>>>(h2, ld_h, W3, b3, basis, t1, w1f, K, kin, nout);
+  return hipGetLastError() == hipSuccess ? 0 : -21;
+}
+
+int ndnet_pn_fold_t2_run(const float* w1f, int w1_stride, const float* b1, const float* t2, int t2_ld, float* outf,
+                         float* outb, int batch, void* stream) {
+  if (!w1f || !b1 || !t2 || !outf || !outb || batch <= 0 || w1_stride < 1024 || t2_ld < 4096 || t2_ld % 4 ||
+      (uintptr_t)t2 % 16)
+    return -20;
+  k_pn_fold_t2<<<batch, 1024, 0, (hipStream_t)stream>>>(w1f, w1_stride, b1, t2, t2_ld, outf, outb);
   return hipGetLastError() == hipSuccess ? 0 : -21;
 }
 

@@ -125,6 +125,7 @@ POINTNET_EXPORTS: dict = {
     "ndnet_pn_fc_run": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "ndnet_pn_fc_mfma_run": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "ndnet_pn_head3_run": (_I, [_P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "ndnet_pn_fold_t2_run": (_I, [_P, _I, _P, _P, _I, _P, _P, _I, _P]),
     "ndnet_pn_fold_prepare": (_I, [_P, _I, ctypes.POINTER(ctypes.c_int64)]),
     "ndnet_pn_fold_run": (_I, [_P, _I, ctypes.c_int64, _P]),
 }

@@ -486,10 +486,13 @@ class _Workspace:
             return (W.frag[id(w)], 0, b, w.shape[0], w.shape[1])
 
         L1 = (self.w1f, self.w1f.stride(0), W.c1b, 16, 64)
+        # chain C's layer 0: conv1 with t1 and t2 folded (ndnet_pn_fold_t2_run), or
+        # with t1 only and t2 folded in its prologue (NDNET_PN_FOLD_T2=chain)
+        LC = (self.w1t2f, self.w1t2f.stride(0), self.b1t2, 16, 64) if FOLD_T2_KERNEL else L1
         self.hip_layers = [
             [shared(x) for x in W.A],
             [L1] + [shared(x) for x in W.B_tail],
-            [L1, shared(W.C_mid), shared(W.C_tail)],
+            [LC, shared(W.C_mid), shared(W.C_tail)],
             [(self.w1t2f, self.w1t2f.stride(0), self.b1t2, 16, 64), shared((W.s1aT, self.cvec))] +
             [shared(x) for x in W.D_tail],
         ]
@@ -516,10 +519,10 @@ class _Workspace:
                 cb.head_w3, cb.head_b3 = W.t1["f3"].data_ptr(), W.t1["c3"].data_ptr()
                 cb.head_basis, cb.head_kin, cb.head_nout = W.t1_basis.data_ptr(), 12, 64
                 cb.head_t1 = self.t1.data_ptr()
-            # chain C: t2 through layer 0 (prologue fold), published for chain D's layer 0
-            cc = self.structs[2]
-            cc.fold_t2, cc.fold_ld = self.t2.data_ptr(), self.t2.stride(0)
-            cc.fold_out_w, cc.fold_out_b = self.w1t2f.data_ptr(), self.b1t2.data_ptr()
+            if not FOLD_T2_KERNEL:  # chain C: t2 through layer 0 (prologue fold), published for chain D
+                cc = self.structs[2]
+                cc.fold_t2, cc.fold_ld = self.t2.data_ptr(), self.t2.stride(0)
+                cc.fold_out_w, cc.fold_out_b = self.w1t2f.data_ptr(), self.b1t2.data_ptr()
         if chain_timing is not None:  # torch events on the launch stream (bench.py)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -553,6 +556,10 @@ def _folded(model):
     return cache
 
 
+# TNet(64)'s transform through conv1 (layer 0 of chains C and D): "kernel"
+# (default, round 5) once per cloud by ndnet_pn_fold_t2_run after fc3; "chain"
+# in chain C's prologue, every workgroup (fold_t2), published for chain D
+FOLD_T2_KERNEL = os.environ.get("NDNET_PN_FOLD_T2", "kernel") == "kernel"
 # TNet(3)'s tail (fc3 + the t1 fold of conv1): "chain" (default) computes it in
 # chain B's prologue, per workgroup (ndnet_pn_chain.head_*: one launch and one
 # boundary fewer); "kernel" runs ndnet_pn_head3_run before chain B
@@ -611,7 +618,12 @@ def _glue_hip(W, ws, B: int):
         t = W.t2
         fc(ws.g2, t["f1"], t["c1"], ws.h1, True)
         fc(ws.h1, t["f2"], t["c2"], ws.h2, True)
-        fc(ws.h2, t["f3"], t["c3"], ws.t2, False)  # t2: folded into chains C / D's layer 0 by chain C's prologue
+        fc(ws.h2, t["f3"], t["c3"], ws.t2, False)  # t2
+        if FOLD_T2_KERNEL:  # t2 through conv1: chains C / D's layer 0, once per cloud
+            rc = _lib.lib().ndnet_pn_fold_t2_run(ws.w1f.data_ptr(), ws.w1f.stride(0), W.c1b.data_ptr(),
+                                                 ws.t2.data_ptr(), ws.t2.stride(0), ws.w1t2f.data_ptr(),
+                                                 ws.b1t2.data_ptr(), B, st())
+            _lib.check(rc, "ndnet_pn_fold_t2_run")
 
     def seg_bias():
         fc(ws.g3[:, : W.F], W.s1g, W.s1b, ws.cvec, False)
