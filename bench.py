@@ -184,6 +184,14 @@ def main() -> None:
     shard0, shard_n = D.shard(B * world, world, rank)
     assert shard_n == B
     pts = torch.from_numpy(make_batch(args.kind, B, n, seed0=shard0)).to(dev)
+    per_dev = -(-world // ndev)
+    if per_dev > 1:
+        # ranks sharing one card (the one-card rehearsal): the library's front
+        # lanes admit k_front launches within a process only, so each rank's
+        # k_front takes at most CUs / ranks-per-card, or two processes' share-1
+        # grids can each hold part of the chip and wait on each other at their
+        # cloud barriers (NDNET_ERR_SYNC).  The pipelines' share 2 fits two ranks.
+        get_plan(B, n, k, -1, dev).set_cu_share(per_dev)
     torch.manual_seed(1234)
     model = NDTNetSegmentation(3, C, F).to(dev).eval()
     with torch.no_grad():
