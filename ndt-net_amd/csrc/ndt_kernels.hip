@@ -3325,21 +3325,15 @@ __device__ inline void merge_runs(const KLArgs& A, const int b) {
   }
   __syncthreads();
   MERGE_MARK(13);
-  // every thread runs the body (it holds a barrier); lanes without an event idle
-  const bool live = ch < nch;
-  const bool is_num = live && t < nnum;
-  const bool is_nan = live && !is_num && t < nnum + nnan;
+  if (ch >= nch) return;
+  const bool is_num = t < nnum;
+  if (!is_num && t >= nnum + nnan) return;
   const uint32_t* own_num_slot = s_own_num_slot[lc];
   const uint32_t* own_nan_slot = s_own_nan_slot[lc];
-  // A chunk's NaN events mostly share one key (the prefix minimum of the
-  // scores before them changes only at a new minimum; half of an L cloud's
-  // events are NaN): only the first event of each run of equal keys searches
-  // the other chunks, the others take its count from here
-  __shared__ uint32_t s_nan_other[kMergeRuns][kChunk];
   auto body = [&](auto K, auto N) {
-    uint32_t sl = 0, pos = 0, lead = 0;
-    unsigned long long x = 0;
-    bool search = is_num;
+    uint32_t sl;
+    unsigned long long x;
+    uint32_t pos;
     if (is_num) {
       x = K[ch * kChunk + t];
       sl = own_num_slot[t];
@@ -3348,26 +3342,15 @@ __device__ inline void merge_runs(const KLArgs& A, const int b) {
       if (nnan_tot) {
         pos += count_nan3(N, own_nan_slot, nb0, nnan, nnan_tot, x, sl);
       }
-    } else if (is_nan) {
+    } else {
       const uint32_t j = t - nnum;
       x = N[nb0 + j];
       sl = own_nan_slot[j];
       // scores of its own chunk ahead of it, then every earlier NaN
       pos = count_composite(K + ch * kChunk, own_num_slot, nnum, x, sl) + nb0 + j;
-      search = j == 0 || N[nb0 + j - 1] != x;
-      if (!search) {  // the first of the chunk's NaN keys equal to x (keys ascend with j)
-        uint32_t lo = 0, hi = j;
-        while (lo < hi) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (N[nb0 + mid] < x) lo = mid + 1;
-          else hi = mid;
-        }
-        lead = lo;
-      }
     }
-    uint32_t other = 0;
     // scores of the other chunks ahead of it, kMergeQ runs per pass
-    for (uint32_t c0 = 0; search && c0 < nch; c0 += kMergeQ) {
+    for (uint32_t c0 = 0; c0 < nch; c0 += kMergeQ) {
       uint32_t run[kMergeQ], add[kMergeQ];
       bool le[kMergeQ];
 #pragma unroll
@@ -3379,13 +3362,8 @@ __device__ inline void merge_runs(const KLArgs& A, const int b) {
       count_before_q<kMergeQ>(K, run, x, le, add);
 #pragma unroll
       for (int q = 0; q < kMergeQ; q++)
-        if (c0 + q < nch && c0 + q != ch) other += add[q];
+        if (c0 + q < nch && c0 + q != ch) pos += add[q];
     }
-    if (is_nan && search) s_nan_other[lc][t - nnum] = other;
-    __syncthreads();
-    if (is_nan && !search) other = s_nan_other[lc][lead];
-    pos += other;
-    if (!is_num && !is_nan) return;
     const double ov = A.slot_val_all[eb + sl];
     const uint32_t oq = (uint32_t)A.nb_all[6 * (uint64_t)b * A.ndcap + sl];
     if constexpr (kCoh) {
