@@ -1944,7 +1944,11 @@ __global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const Cl
     return __builtin_amdgcn_readfirstlane(v);
   };
   for (uint32_t item = blockIdx.x * (kWqThreads / 64) + wave; item < total; item = next_item()) {
+#ifdef NDNET_WQ_EXP_LIGHTONLY  // register probe only (wrong results): the light path alone
+  const bool hv = false;
+#else
   const bool hv = item < H;  // a heavy ND (wave-uniform)
+#endif
 #ifdef NDNET_WQ_EXP_HEAVYONLY  // timing experiment only (wrong results): light items skipped
   if (!hv) continue;
 #endif
