@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Full-size parity fixtures (build container; oracle only, no reference code).
 
-For configs C2 (16 x 100k -> 1000) and C5 (16 x 100k -> 2000 -> 1000 -> 500),
-U and L clouds (SURVEY §8d generators, seeds 0..15), the CPU oracle is run
+For configs C2 (16 x 100k -> 1000), C5 (16 x 100k -> 2000 -> 1000 -> 500)
+and C4 (128 x 100k -> 1000: the 8 rank shards of 16 clouds bench.py --gpus 8
+runs, seeds 0..127), U and L clouds (SURVEY §8d generators, cloud i = seed i),
+the CPU oracle is run
 through the reference ABI sequence NDT_Sampler drives (ndt_legacy.py:111-240)
 in three arithmetic variants:
 
@@ -38,9 +40,10 @@ sys.path.insert(0, os.path.join(REPO, "ndt-net_amd"))
 import oracle as O  # noqa: E402
 from ndnet.synthetic import make_batch  # noqa: E402
 
-CONFIGS = {"C2": (1000,), "C5": (2000, 1000, 500)}
+# config -> (NDs per level, clouds)
+CONFIGS = {"C2": ((1000,), 16), "C5": ((2000, 1000, 500), 16), "C4": ((1000,), 128)}
 VARIANTS = {"canonical": (True, True), "glibc": (False, True), "columns": (True, False)}
-B, N = 16, 100_000
+N = 100_000
 
 
 def rows_f32(pc, cov):
@@ -64,7 +67,7 @@ def chain(pts, levels, portable, gsl):
 
 def main():
     data = {}
-    for cfg, levels in CONFIGS.items():
+    for cfg, (levels, B) in CONFIGS.items():
         for kind in ("U", "L"):
             pts = make_batch(kind, B, N)
             sha = np.zeros((B, len(levels), 32), np.uint8)
@@ -85,8 +88,9 @@ def main():
                       f"{[int((a[:, lv] > 0).sum()) for lv in range(len(levels))]}, "
                       f"NDs differing per level {[int(a[:, lv].sum()) for lv in range(len(levels))]} "
                       f"of {[B * k for k in levels]}")
-    np.savez_compressed(os.path.join(HERE, "fullsize_rows.npz"), **data, batch=B, points=N,
-                        levels_C2=np.array(CONFIGS["C2"]), levels_C5=np.array(CONFIGS["C5"]))
+    np.savez_compressed(os.path.join(HERE, "fullsize_rows.npz"), **data, batch=CONFIGS["C2"][1], points=N,
+                        batch_C4=CONFIGS["C4"][1],
+                        **{f"levels_{c}": np.array(lv) for c, (lv, _) in CONFIGS.items()})
     print("wrote fullsize_rows.npz")
 
 

@@ -114,6 +114,31 @@ def test_hip_forward_on_ndt_rows():
     assert (out - ref).abs().max().item() < TOL
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["U", "L"])
+def test_hip_forward_on_c2_rows(kind):
+    """Config C3 on the rows the NDT stage actually emits: the C2 batch (16 x
+    100k -> 1000, seeds 0..15) through ndt_preprocessing, its rows (means and
+    the post-KL covariances: asymmetric LU iterates with negative diagonals,
+    magnitudes up to ~65) into the model.  Log-probs within
+    1e-4 of torch fp32, the predicted class equal wherever the reference's top
+    two are further apart than 2e-4."""
+    from ndnet.preprocessing.ndtnet_preprocessing import ndt_preprocessing
+    from ndnet.synthetic import make_batch
+    m = _model(768, 28, "cuda")
+    pts = torch.from_numpy(make_batch(kind, 16, 100_000)).cuda()
+    p, c, _ = ndt_preprocessing(1000, pts, check=True)
+    assert c.abs().max().item() > 1.0  # the LU-mutated covariances, not unit-scale noise
+    with torch.no_grad():
+        out = m(p, c)
+        ref = m.forward_torch(p.contiguous(), c.contiguous())
+    assert out.shape == (16, 1000, 29)
+    assert (out - ref).abs().max().item() < TOL
+    top2 = ref.topk(2, dim=-1).values
+    clear = (top2[..., 0] - top2[..., 1]) > 2 * TOL
+    assert torch.equal(out.argmax(-1)[clear], ref.argmax(-1)[clear])
+
+
 @pytest.mark.parametrize("F,C", [(768, 28), (64, 5)])
 def test_fold_jobs_cover_every_folded_tensor(F, C):
     """The re-fold's job list (ndnet_pn_fold_job per output, the kernel's

@@ -188,10 +188,10 @@ def test_fullsize_fixture_pins_oracle():
     import hashlib
     from ndnet.synthetic import make_batch
     z = golden("fullsize_rows.npz")
-    for cfg in ("C2", "C5"):
+    for cfg, clouds in (("C2", (("U", 3), ("L", 5))), ("C5", (("U", 3), ("L", 5))), ("C4", (("U", 101), ("L", 77)))):
         levels = [int(v) for v in z[f"levels_{cfg}"]]
-        for kind, b in (("U", 3), ("L", 5)):
-            pts = make_batch(kind, b + 1, int(z["points"]))[b].astype(np.float64)
+        for kind, b in clouds:
+            pts = make_batch(kind, 1, int(z["points"]), seed0=b)[0].astype(np.float64)
             ch = O.LegacyChain(pts)
             res = [ch.downsample(levels[0])] + [ch.prune(k) for k in levels[1:]]
             ch.cleanup()
