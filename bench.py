@@ -185,12 +185,17 @@ def main() -> None:
     assert shard_n == B
     pts = torch.from_numpy(make_batch(args.kind, B, n, seed0=shard0)).to(dev)
     per_dev = -(-world // ndev)
+    # ranks sharing one card (the one-card rehearsal): k_front's cloud-major
+    # deal keeps any two launches at once deadlock-free (csrc/ndt_front.h), but
+    # more ranks per card than that, each with pipelines of its own, could
+    # want more k_front workgroups than the chip holds.  Each rank's k_front
+    # then takes CUs / (ranks per card x its NDT streams) (pipe_share); the
+    # cached plan of the stage lines takes CUs / ranks per card.
+    from ndnet.pipeline import PIPE_CU_SHARE
+
+    def pipe_share(ndt_streams: int = 1):
+        return None if per_dev == 1 else max(PIPE_CU_SHARE, ndt_streams) * per_dev
     if per_dev > 1:
-        # ranks sharing one card (the one-card rehearsal): the library's front
-        # lanes admit k_front launches within a process only, so each rank's
-        # k_front takes at most CUs / ranks-per-card, or two processes' share-1
-        # grids can each hold part of the chip and wait on each other at their
-        # cloud barriers (NDNET_ERR_SYNC).  The pipelines' share 2 fits two ranks.
         get_plan(B, n, k, -1, dev).set_cu_share(per_dev)
     torch.manual_seed(1234)
     model = NDTNetSegmentation(3, C, F).to(dev).eval()
@@ -217,7 +222,7 @@ def main() -> None:
         else:
             # step i: NDT of batch i on one stream || forward(s) of batch i - 1 on another
             from ndnet.pipeline import PipelinedSegmentation
-            graphed = PipelinedSegmentation(model, k, B, n, device=dev, levels=levels)
+            graphed = PipelinedSegmentation(model, k, B, n, device=dev, levels=levels, cu_share=pipe_share())
         if hasattr(graphed, "load_resident"):
             graphed.load_resident(pts)
         else:
@@ -286,7 +291,8 @@ def main() -> None:
                 and "NDNET_PIPE_NDT_STREAMS" not in os.environ):
             from ndnet.pipeline import PipelinedSegmentation
             o_ndt_streams = 2
-            o_graphed = PipelinedSegmentation(model, k, B, n, device=dev, ndt_streams=o_ndt_streams)
+            o_graphed = PipelinedSegmentation(model, k, B, n, device=dev, ndt_streams=o_ndt_streams,
+                                              cu_share=pipe_share(o_ndt_streams))
         if hasattr(o_graphed, "load_resident"):
             o_graphed.load_resident(opts)
         else:
@@ -415,7 +421,7 @@ def main() -> None:
         # forward per level -- through the same stream pipeline ----
         c5 = (2000, 1000, 500)
         from ndnet.pipeline import PipelinedSegmentation
-        p5 = PipelinedSegmentation(model, c5[0], B, n, device=dev, levels=c5)
+        p5 = PipelinedSegmentation(model, c5[0], B, n, device=dev, levels=c5, cu_share=pipe_share())
         p5.load_resident(pts)
         with torch.no_grad():
             t5 = time.perf_counter()

@@ -123,19 +123,23 @@ void ndnet_ndt_plan_destroy(void *plan);
  * allowed, else 1 (the default).  Both paths give identical results.
  * ndnet_ndt_get_path returns the path in use.
  * Concurrency: path 2's cloud barriers need every workgroup of a cloud
- * resident at once, and two k_front grids that together want more workgroups
- * than the chip holds could each hold part of the chip and wait on the other
- * (until the ~2 s barrier timeout failed their clouds).  The library admits
- * k_front launches itself: the chip is split into 4 front lanes, a plan's
- * k_front occupies ceil(4 * workgroups / CUs) of them (4 at CU share 1, 2 at
- * share 2), waits for the previous k_front of each of its lanes and records
- * itself on them (HIP events; external event nodes when the stream is being
- * captured, so graph replays are admitted the same way).  Any number of plans
- * on any number of streams (or in graphs) on one device can therefore run
- * concurrently; k_fronts whose lanes are disjoint (e.g. two share-2 plans) run
- * side by side, the others in launch order.  (Processes sharing one GPU do not
- * see each other's lanes.)  ndnet_ndt_get_front_lanes reports a plan's lanes
- * (nlanes 0 on path 1). */
+ * resident at once.  k_front deals each launch's clouds cloud-major within an
+ * XCD (workgroups start in id order), so a launch has at most one partially
+ * resident cloud per XCD, and ANY TWO k_front launches at once -- two plans,
+ * two streams, two graphs, two processes on one GPU -- always complete.  On
+ * top of that the library keeps one process's k_front launches to one chip's
+ * worth: the chip is split into 4 front lanes, a plan's k_front occupies
+ * ceil(4 * workgroups / CUs) of them (4 at CU share 1, 2 at share 2), waits
+ * for the previous k_front of each of its lanes and records itself on them
+ * (HIP events; explicit event nodes when the stream is being captured, so the
+ * replays of a graph wait for the launches its capture saw on its lanes).  A
+ * plan that is its device's only plan skips the admission.  k_fronts whose
+ * lanes are disjoint (two share-2 plans) run side by side.  What the lanes
+ * cannot order -- launches of other processes, a graph replayed beside a plan
+ * created after its capture -- overlaps at most pairwise in practice; three
+ * or more share-1 launches at once can still time out (NDNET_ERR_SYNC, never
+ * a hang).  ndnet_ndt_get_front_lanes reports a plan's lanes (nlanes 0 on
+ * path 1). */
 int ndnet_ndt_set_path(void *plan, int path);
 int ndnet_ndt_get_path(void *plan);
 int ndnet_ndt_get_front_lanes(void *plan, int *lane0, int *nlanes);
@@ -182,6 +186,16 @@ int ndnet_ndt_get_front_staged(void *plan);
  * operations in the reference's order, normal_distributions.c:75-103); the
  * threshold only moves work.  Default 256; min_samples >= 1. */
 int ndnet_ndt_set_heavy_threshold(void *plan, uint32_t min_samples);
+
+/* k_welford_q's form for the NDs below the heavy threshold: 1 = one ND per
+ * lane (64 NDs per wave: a quarter of the CUs on C2, for a plan whose k_front
+ * leaves the chip to other streams), 2 = a lane quad per ND (16 NDs per wave:
+ * every CU, the faster form alone), 0 = by the CU share: 2 at share 1, 1 above
+ * (the default; NDNET_WQ_FORM=light64|quad overrides it for every plan).
+ * Identical results either way.  ndnet_ndt_get_welford_form returns the form
+ * in use (1 or 2). */
+int ndnet_ndt_set_welford_form(void *plan, int form);
+int ndnet_ndt_get_welford_form(void *plan);
 
 /* Split ndnet_ndt_run in two stream-ordered calls (a caller that overlaps the
  * run with other work on another stream, e.g. ndnet.pipeline): part 1 runs the

@@ -305,13 +305,24 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
   // output stay in one XCD's L2, whose partial 12-byte writes then merge
   // into whole lines before write-back instead of leaving partial lines dirty
   // in several XCDs.
+  // Within an XCD the clouds are dealt cloud-major (slot s: cloud s / G,
+  // workgroup s % G): workgroups start in linear-id order, so at any moment
+  // a launch has at most ONE cloud per XCD with only part of its workgroups
+  // resident -- the last one dispatched -- and every earlier cloud complete.
+  // Two k_front launches that share the chip (two processes, or graphs whose
+  // admission the front lanes could not order) then leave at most 2 (G - 1)
+  // of an XCD's 32 CUs waiting on workgroups not yet dispatched, so one of
+  // them always completes a cloud and frees its CUs: no cross-launch deadlock
+  // at the cloud barriers.  (Rounds 2-5 dealt them slot-minor, s % (B / 8):
+  // with two launches interleaved every cloud of both could be partial, and
+  // the one-card two-process rehearsal timed out, gpurun_out/r05g.)
   const uint32_t L = blockIdx.x, G = A.G, bpw = A.bpw, rbs = A.rbs, nrb = bpw * (1024 / A.rbs);
   uint32_t g;
   int b;
   if (A.xcd_local) {
-    const uint32_t cpx = A.B / 8u, slot = L / 8u;  // clouds per XCD, slot within the XCD
-    b = (int)((slot % cpx) * 8u + L % 8u);
-    g = slot / cpx;
+    const uint32_t slot = L / 8u;  // slot within the XCD
+    b = (int)((slot / G) * 8u + L % 8u);
+    g = slot % G;
   } else {
     b = (int)(L / G);
     g = L % G;

@@ -180,7 +180,8 @@ struct Plan {
   uint32_t* fbar;            // [B][kBarStride]
   unsigned long long* fmarks; // [B][kFrontMarkStride]: k_front phase stamps of WG 0 + start/end of every WG (timing level 2)
   int exact_counts;           // k_front counts every bisection grid (ndnet_ndt_set_exact_counts)
-  size_t wq_lds;              // k_welford_q dynamic LDS (labelled runs: class histograms)
+  int wq_l64;                 // k_welford_q light form: 1 light64 (one ND per lane), 0 lane quads
+  int wq_form;                // 0 auto (quads at CU share 1, light64 above), 1 light64, 2 quads
   uint32_t wq_grid;           // k_welford_q workgroups: one per CU (of the plan's CU share)
   int cus;                    // the device's CUs
   int cu_share;               // k_front / k_welford_q use CUs / cu_share (ndnet_ndt_set_cu_share)
@@ -1454,17 +1455,18 @@ __global__ void __launch_bounds__(64) k_debug_lu_chain(const double* A, uint32_t
 // never being -0).  A lane whose coordinates leave the fast range (non-finite
 // floats; doubles outside [2^-300, 2^300]) refolds its ND with IEEE divisions
 // and the reference's per-step NaN -> 0 of the off-diagonal sums.
-#ifndef NDNET_WQ_LIGHT64
-#define NDNET_WQ_LIGHT64 1
-#endif
-constexpr uint32_t kWqLightNDs = NDNET_WQ_LIGHT64 ? 64u : 16u;  // NDs per light item (one wave)
+// Both light forms are built; a plan picks one by its CU share (Plan::wq_l64,
+// ndnet_ndt_set_welford_form): the lane quads for a plan that has the whole
+// chip (isolated U 30.5 us against light64's 37: profiles/r05final_*), light64
+// where the pipeline runs the forward beside it (a quarter of the CUs).
+constexpr uint32_t wq_light_nds(bool l64) { return l64 ? 64u : 16u; }  // NDs per light item (one wave)
 constexpr int kL64B = 8;                                      // samples per register block
 static_assert(4 * kL64B <= 32, "wq_rt_entries' margin covers a light64 group's last round (ring <= 4)");
 #ifndef NDNET_WQ_L64_COALESCE
 #define NDNET_WQ_L64_COALESCE 1
 #endif
-constexpr size_t kWqRtBytes = NDNET_WQ_LIGHT64 ? sizeof(double2) : sizeof(double);  // LDS table entry
-constexpr uint32_t kWqHistNDs = NDNET_WQ_LIGHT64 ? kWqThreads : kWqNDs;            // NDs of a workgroup at once
+constexpr size_t wq_rt_bytes(bool l64) { return l64 ? sizeof(double2) : sizeof(double); }  // LDS table entry
+constexpr uint32_t wq_hist_nds(bool l64) { return l64 ? kWqThreads : kWqNDs; }          // NDs of a workgroup at once
 
 template <typename T>
 struct L64Blk {
@@ -1864,7 +1866,7 @@ __device__ __attribute__((always_inline)) inline void wq_light64(const CloudCtl*
   }
 }
 
-template <typename T>
+template <typename T, bool L64>
 __global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const CloudCtl* ctl, int B, const T* __restrict__ nd_pts,
                                                           const uint16_t* __restrict__ nd_lbl,
                                                           const uint32_t* __restrict__ nd_n,
@@ -1884,10 +1886,12 @@ __global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const Cl
   double* lrt = (double*)wq_smem;                                // quads: [rtn] refined reciprocals of 1..rtn
   double2* lrt2 = (double2*)wq_smem;                             // light64: [rtn] (rc, rl) of counts 0..rtn - 1
   const uint32_t bw = (uint32_t)((B + 1 + 3) & ~3);
-  uint32_t* pre = (uint32_t*)(wq_smem + rtn * kWqRtBytes);       // [B + 1] first light item of each cloud
+  constexpr uint32_t kWqLightNDs = wq_light_nds(L64);
+  constexpr uint32_t kWqHistNDs = wq_hist_nds(L64);
+  uint32_t* pre = (uint32_t*)(wq_smem + rtn * wq_rt_bytes(L64)); // [B + 1] first light item of each cloud
   uint32_t* hpre = pre + bw;                                      // [B + 1] first heavy item of each cloud
   uint32_t* wq_hist = hpre + bw;                                  // labelled runs: [kWqHistNDs][ncls + 1]
-  if constexpr (NDNET_WQ_LIGHT64) {
+  if constexpr (L64) {
     // every entry finite: a masked step past a lane's count reads one (x = mean
     // makes t = +0, and 0 * rl must not be 0 * inf); rtab holds counts 0..n
     for (uint32_t i = threadIdx.x; i < rtn; i += kWqThreads) lrt2[i] = rtab[i <= n ? i : n];
@@ -1966,7 +1970,7 @@ __global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const Cl
     else hi = mid - 1;
   }
   const int b = lo;
-  if (NDNET_WQ_LIGHT64 && !hv) {  // 64 NDs, one per lane
+  if (L64 && !hv) {  // 64 NDs, one per lane
     unsigned long long t_mom = 0, t_loop = 0, t_lbl = 0;
     uint32_t lmx = 0;
     wq_light64<T>(ctl, b, (li - pre[b]) * kWqLightNDs, nd_pts, nd_lbl, nd_n, nd_base, nd_mean, nd_cov, nd_cls,
@@ -2238,7 +2242,7 @@ __global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const Cl
     double* hl = reinterpret_cast<double*>(&wq_stage[wave * 16][0]);
     if (wq_marks) wq_heavy<T, true>(rec, hc, rtab, hl, wq_hr[wave], lane, mean, m2, off, bad, ph);
     else wq_heavy<T>(rec, hc, rtab, hl, wq_hr[wave], lane, mean, m2, off, bad);
-  } else if constexpr (!NDNET_WQ_LIGHT64) {  // (light64: light items never reach this point)
+  } else if constexpr (!L64) {  // (light64: light items never reach this point)
     run(mx, true, std::false_type{});
   }
   if (wq_marks) mk_t1 = __builtin_amdgcn_s_memtime();
@@ -2299,7 +2303,7 @@ __global__ void __launch_bounds__(kWqThreads) NDNET_WQ_ATTR k_welford_q(const Cl
     // light64: a lane per slot, [wave * 64, wave * 64 + 64) per wave, so a heavy
     // wave's quad 0 takes its own wave's first slot (a quad index would land
     // in another wave's range while that wave's light64 item counts into it)
-    uint32_t* hist = wq_hist + (NDNET_WQ_LIGHT64 ? (threadIdx.x & ~3u) : (threadIdx.x >> 2)) * nbins;
+    uint32_t* hist = wq_hist + (L64 ? (threadIdx.x & ~3u) : (threadIdx.x >> 2)) * nbins;
     for (uint32_t k = j; k < nbins; k += 4) hist[k] = 0;
     __builtin_amdgcn_wave_barrier();
     const uint16_t* l = nd_lbl + (uint64_t)b * n + beg;
@@ -3561,11 +3565,8 @@ static void plan_free(Plan* P) {
   if (P->sync_fail_h) (void)hipHostFree(P->sync_fail_h);
   if (P->front_ev) {
     (void)hipEventSynchronize(P->front_ev);
-    {
-      std::lock_guard<std::mutex> lk(g_lane_mu);
-      front_lanes_forget(P);
-    }
-    (void)hipEventDestroy(P->front_ev);
+    std::lock_guard<std::mutex> lk(g_lane_mu);
+    front_lanes_forget(P);  // the event goes back to the device's pool, not destroyed (graphs may wait on it)
   }
   void* bufs[]= {P->flims, P->frec, P->fwgcnt, P->fbar, P->ctl, P->stamps, P->dense_of, P->vox, P->gbits, P->pkeys, P->did, P->bin_cnt, P->nd_base,
                   P->nd_pts, P->nd_lbl, P->nd_n,
@@ -3757,19 +3758,28 @@ constexpr int kFrontLanes = 4;
 constexpr int kMaxDevices = 64;
 struct FrontLaneSet {
   int next;                          // the lane the next plan's lanes start at (round robin)
+  int plans;                         // live plans holding a lane event on this device
   hipEvent_t ev[kFrontLanes];        // the event of the lane's last k_front launch (null: none yet)
   hipStream_t st[kFrontLanes];       // the stream it was launched on
   unsigned long long cap[kFrontLanes];  // the capture it was launched in (0: eager)
+  std::vector<hipEvent_t> pool;      // events of freed plans, reused by later plans
 };
 static FrontLaneSet g_lanes[kMaxDevices];
 
 // Drops a freed plan's event from the lanes (caller holds g_lane_mu; the
-// event has completed, so nothing left to wait for).
+// event has completed, so nothing left to wait for).  The event itself is
+// kept in the device's pool and handed to the next plan: a graph captured
+// while this plan held a lane may still hold a wait node on it,
+// and waiting on a pooled event only ever waits for a completed or a later
+// k_front launch.
 static void front_lanes_forget(Plan* P) {
   if (P->dev < 0 || P->dev >= kMaxDevices || !P->front_ev) return;
   FrontLaneSet& L = g_lanes[P->dev];
   for (int i = 0; i < kFrontLanes; i++)
     if (L.ev[i] == P->front_ev) L.ev[i] = nullptr;
+  L.pool.push_back(P->front_ev);
+  L.plans--;
+  P->front_ev = nullptr;
 }
 
 // Assigns the plan's lanes for its current k_front geometry (caller holds g_lane_mu).
@@ -3777,8 +3787,14 @@ static hipError_t front_lanes_assign(Plan* P) {
   if (P->dev < 0 || P->dev >= kMaxDevices) return hipErrorInvalidDevice;
   FrontLaneSet& L = g_lanes[P->dev];
   if (!P->front_ev) {
-    const hipError_t e = hipEventCreateWithFlags(&P->front_ev, hipEventDisableTiming);
-    if (e != hipSuccess) return e;
+    if (!L.pool.empty()) {
+      P->front_ev = L.pool.back();
+      L.pool.pop_back();
+    } else {
+      const hipError_t e = hipEventCreateWithFlags(&P->front_ev, hipEventDisableTiming);
+      if (e != hipSuccess) return e;
+    }
+    L.plans++;
   }
   const uint64_t wgs = (uint64_t)P->fG * (uint64_t)P->B;
   const int cus = P->cus > 0 ? P->cus : 1;
@@ -3791,19 +3807,33 @@ static hipError_t front_lanes_assign(Plan* P) {
 }
 
 // Launches k_front between the lane waits and records (front_lanes_assign).
-// How a stream being captured is admitted (NDNET_LANE_CAPTURE, read once;
-// tools/capture_lane_probe.py tries each form): 0 no lane nodes in the graph,
-// 1 external wait nodes only, 2 external record nodes only, 3 both, 4 both as
-// explicit graph nodes (hipGraphAddEventWaitNode / hipGraphAddEventRecordNode
-// on the capture's graph, then the capture's dependencies moved past them).
-// On ROCm 7.2 only 4 works: hipStreamWaitEvent(hipEventWaitExternal) in a
-// capture throws std::bad_alloc inside HIP (modes 1, 3) and
-// hipEventRecordWithFlags(hipEventRecordExternal) fails (mode 2, -21)
-// (profiles/r05_capture_lane_probe.txt).  4 is the default.
-static int lane_capture_mode() {
-  static const int v = [] {
+// A stream being captured is admitted with explicit graph nodes
+// (hipGraphAddEventWaitNode / hipGraphAddEventRecordNode on the capture's
+// graph, then the capture's dependencies moved past them).  The capture forms
+// hipStreamWaitEvent(hipEventWaitExternal) and
+// hipEventRecordWithFlags(hipEventRecordExternal) abort inside HIP on ROCm 7.2
+// (std::bad_alloc; error -21: profiles/r05_capture_lane_probe.txt) and are not
+// used.  NDNET_LANE_CAPTURE=0 (A/B only, read once) puts no lane nodes in a
+// captured graph.
+static bool lane_capture_nodes() {
+  static const bool v = [] {
     const char* e = getenv("NDNET_LANE_CAPTURE");
-    return e ? atoi(e) : 4;
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+// A plan that is the only one on its device with a lane event skips the
+// admission (no waits: nothing else to order against; no record: the event
+// would order nothing), NDNET_FRONT_SOLO=0 (A/B) keeps it.  When a second
+// plan appears, its first k_front may overlap the solo plan's last one: two
+// launches at once are safe by k_front's cloud-major deal (ndt_front.h), and
+// from then on both record.  (Round 5's one record per run cost the isolated
+// C2 NDT stage ~4 us: profiles/r05_lanes_ab.txt.)
+static bool solo_skip() {
+  static const bool v = [] {
+    const char* e = getenv("NDNET_FRONT_SOLO");
+    return !(e && e[0] == '0');
   }();
   return v;
 }
@@ -3845,12 +3875,17 @@ static int front_launch(Plan* P, hipStream_t st, const T* pts, const FrontArgs& 
   }
   std::lock_guard<std::mutex> lk(g_lane_mu);  // waits, launch and records in one host order
   FrontLaneSet& L = g_lanes[P->dev];
+  if (L.plans <= 1 && solo_skip()) {
+    k_front<T><<<P->fG * P->B, kFrontThreads, P->flds, st>>>(pts, F);
+    HIPCHK(hipGetLastError());
+    return NDNET_OK;
+  }
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   unsigned long long cap_id = 0;
   HIPCHK(hipStreamGetCaptureInfo(st, &cs, &cap_id));
   const bool cap = cs == hipStreamCaptureStatusActive;
   if (!cap) cap_id = 0;
-  const int mode = cap ? lane_capture_mode() : 3;
+  const bool nodes = !cap || lane_capture_nodes();
   hipEvent_t waited[kFrontLanes];
   int nw = 0;
   for (int i = 0; i < P->nlanes; i++) {
@@ -3862,15 +3897,13 @@ static int front_launch(Plan* P, hipStream_t st, const T* pts, const FrontArgs& 
     if (dup) continue;
     waited[nw++] = ev;
     if (!cap) HIPCHK(hipStreamWaitEvent(st, ev, 0));
-    else if (mode == 1 || mode == 3) HIPCHK(hipStreamWaitEvent(st, ev, hipEventWaitExternal));
-    else if (mode == 4) HIPCHK(capture_event_node(st, ev, true));
+    else if (nodes) HIPCHK(capture_event_node(st, ev, true));
   }
   k_front<T><<<P->fG * P->B, kFrontThreads, P->flds, st>>>(pts, F);
   HIPCHK(hipGetLastError());
   if (!cap) HIPCHK(hipEventRecord(P->front_ev, st));
-  else if (mode == 2 || mode == 3) HIPCHK(hipEventRecordWithFlags(P->front_ev, st, hipEventRecordExternal));
-  else if (mode == 4) HIPCHK(capture_event_node(st, P->front_ev, false));
-  if (!cap || mode == 2 || mode == 3 || mode == 4) {  // mode 0/1 captures record nothing: the lanes keep their last launch
+  else if (nodes) HIPCHK(capture_event_node(st, P->front_ev, false));
+  if (nodes) {  // a capture without lane nodes records nothing: the lanes keep their last launch
     for (int i = 0; i < P->nlanes; i++) {
       const int l = (P->lane0 + i) % kFrontLanes;
       L.ev[l] = P->front_ev;
@@ -3880,6 +3913,16 @@ static int front_launch(Plan* P, hipStream_t st, const T* pts, const FrontArgs& 
   }
   return NDNET_OK;
 }
+
+// k_welford_q's class-histogram LDS of a labelled run (0: the global histograms)
+static size_t wq_hist_lds(const Plan* P, bool l64) {
+  if (P->ncls < 0) return 0;
+  const size_t hb = (size_t)wq_hist_nds(l64) * (size_t)(P->ncls + 1) * sizeof(uint32_t);
+  return hb <= (size_t)kWqHistMax ? hb : 0;
+}
+
+// The light form for the plan's CU share (Plan::wq_form; ndnet_ndt_set_welford_form)
+static void wq_pick_form(Plan* P) { P->wq_l64 = P->wq_form == 1 ? 1 : P->wq_form == 2 ? 0 : (P->cu_share > 1); }
 
 template <typename T>
 static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, float* out, float* out_cls,
@@ -3964,14 +4007,19 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
   }
 welford:
   P->lists_built = 0;
-  k_welford_q<T><<<P->wq_grid, kWqThreads,
-                    wq_rt_entries(P->heavy_t) * kWqRtBytes + 8 * ((B + 1 + 3) & ~3) + (lbl ? P->wq_lds : 0),
-                    st>>>(
-      P->ctl, B, (const T*)P->nd_pts, lbl ? P->nd_lbl : nullptr, P->nd_n, P->nd_base, P->nd_mean, P->nd_cov,
-      P->nd_cls, P->hist, P->ncls, n, P->ndcap, P->wq_ctr, P->heavy, P->heavy_t, (const double2*)P->rtab,
-      P->timing >= 2 ? P->wq_marks : nullptr,
-      WqChainArgs{P->vox, P->dense_of, P->nb, P->nkeys, P->nd_cov, P->chain, P->chain_ps, P->nd_cov_post, P->vcap,
-                  P->eager_list ? 0ull : (uint64_t)P->k, P->chain_ok, P->lu_done});
+  auto wq = [&](auto l64_tag) {
+    constexpr bool L64 = decltype(l64_tag)::value;
+    k_welford_q<T, L64><<<P->wq_grid, kWqThreads,
+                      wq_rt_entries(P->heavy_t) * wq_rt_bytes(L64) + 8 * ((B + 1 + 3) & ~3) + (lbl ? wq_hist_lds(P, L64) : 0),
+                      st>>>(
+        P->ctl, B, (const T*)P->nd_pts, lbl ? P->nd_lbl : nullptr, P->nd_n, P->nd_base, P->nd_mean, P->nd_cov,
+        P->nd_cls, P->hist, P->ncls, n, P->ndcap, P->wq_ctr, P->heavy, P->heavy_t, (const double2*)P->rtab,
+        P->timing >= 2 ? P->wq_marks : nullptr,
+        WqChainArgs{P->vox, P->dense_of, P->nb, P->nkeys, P->nd_cov, P->chain, P->chain_ps, P->nd_cov_post, P->vcap,
+                    P->eager_list ? 0ull : (uint64_t)P->k, P->chain_ok, P->lu_done});
+  };
+  if (P->wq_l64) wq(std::true_type{});
+  else wq(std::false_type{});
   if (P->timing) HIPCHK(hipEventRecord(P->ev[5], st));
   KLArgs A = kl_args(P, P->k, out, out_cls, pc64, cov64, cls16);
   A.stats_out = stats_dst;
@@ -4044,6 +4092,7 @@ hipError_t front_config(Plan* P, int share) {
   P->flds = lds;
   P->front_ok = e == hipSuccess && ok;
   P->cu_share = share;
+  wq_pick_form(P);
   if (e == hipSuccess && P->front_ok) {
     std::lock_guard<std::mutex> lk(g_lane_mu);
     e = front_lanes_assign(P);
@@ -4076,6 +4125,8 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   }
   P->kl_fuse = 1;
   if (const char* e = getenv("NDNET_KL_FUSE")) P->kl_fuse = atoi(e) != 0;  // A/B: 0 launches k_kl
+  if (const char* e = getenv("NDNET_WQ_FORM"))  // A/B: "light64" / "quad" for every plan (default: by CU share)
+    P->wq_form = !strcmp(e, "light64") ? 1 : !strcmp(e, "quad") ? 2 : 0;
   const double upper = (double)num_desired * (1 + 0.2);
   P->ndcap = (uint32_t)upper + 1;
   P->ecap = 6 * P->ndcap;
@@ -4182,8 +4233,6 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
     e = hipMemcpy(P->rtab, rt.data(), rt.size() * sizeof(double), hipMemcpyHostToDevice);
   }
   {
-    const size_t hb = (size_t)kWqHistNDs * (size_t)nb * sizeof(uint32_t);
-    P->wq_lds = num_classes >= 0 && hb <= (size_t)kWqHistMax ? hb : 0;
     int dv = 0, ncu = 0;
     if (e == hipSuccess) e = hipGetDevice(&dv);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dv);
@@ -4195,12 +4244,13 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
     // latency-bound, so a second wave per SIMD shares the same issue slots)
     P->wq_grid = ncu > 0 ? (uint32_t)ncu * NDNET_WQ_WPC : 1u;
   }
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_welford_q<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(kWqRt * kWqRtBytes + 8 * ((batch + 1 + 3) & ~3) + kWqHistMax));
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_welford_q<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(kWqRt * kWqRtBytes + 8 * ((batch + 1 + 3) & ~3) + kWqHistMax));
+  {
+    const int wq_dyn = (int)(kWqRt * wq_rt_bytes(true) + 8 * ((batch + 1 + 3) & ~3) + kWqHistMax);
+    const void* wqk[] = {(const void*)k_welford_q<float, true>, (const void*)k_welford_q<double, true>,
+                         (const void*)k_welford_q<float, false>, (const void*)k_welford_q<double, false>};
+    for (const void* f : wqk)
+      if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, wq_dyn);
+  }
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_kl_merge<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(2 * kMergeLdsChunks * kChunk * sizeof(unsigned long long)));
@@ -4254,6 +4304,20 @@ int ndnet_ndt_set_cu_share(void* plan, int front_share, int welford_share) {
   P->front = on_front ? 1 : 0;
   P->wq_grid = (uint32_t)(P->cus / welford_share > 0 ? P->cus / welford_share : 1) * NDNET_WQ_WPC;
   return NDNET_OK;
+}
+
+int ndnet_ndt_set_welford_form(void* plan, int form) {
+  Plan* P = (Plan*)plan;
+  if (!P || form < 0 || form > 2) return NDNET_ERR_ARG;
+  P->wq_form = form;
+  wq_pick_form(P);
+  return NDNET_OK;
+}
+
+int ndnet_ndt_get_welford_form(void* plan) {
+  Plan* P = (Plan*)plan;
+  if (!P) return NDNET_ERR_ARG;
+  return P->wq_l64 ? 1 : 2;
 }
 
 int ndnet_ndt_set_exact_counts(void* plan, int on) {

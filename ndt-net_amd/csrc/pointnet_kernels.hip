@@ -62,6 +62,26 @@ constexpr int kFuseNC = 64;     // columns per chunk of a fused layer
 // for the input tile), so width + kPadF floats / width + kPadB bf16 give it.
 constexpr int kPadF = 8;        // fp32 regions: pitch = width + 8 floats
 constexpr int kPadB = 16;       // bf16 planes: pitch = width + 16 bf16
+// bf16 planes, round 6: the epilogues store a lane's 4 channels of one point
+// as one ds_write_b64 per plane, and a write's 16-lane group (one kq, points
+// cl = 0..15) lands on 16 rows of the same columns.  Writes bank on (a/4) mod
+// 32 (MI355X_MICROARCH.md §LDS): with these pitches (32 B + a multiple of
+// 128 B: 8 dwords mod 32) rows r and r + 4 share banks -- 4-way, the chain
+// D conflicts (25.7% of its LDS cycles, profiles/r05_pmc_summary.txt).  So the
+// 16-byte slots of row r are XOR-swizzled by bit 2 of r (slot s at s ^
+// ((r >> 2) & 1)): the writes become 2-way, the least 16 rows x 8 bytes at
+// 16-byte granularity allow (8 distinct slots mod 128 B), and the
+// ds_read_b128 A-fragment reads stay conflict-free (every lane group on 16
+// distinct 16-byte slots; checked exhaustively for the pitches used).  A read
+// keeps its 16 bytes whole: only which slot of its row it reads moves.
+#ifndef NDNET_PN_PLANE_SWZ
+#define NDNET_PN_PLANE_SWZ 1
+#endif
+// the bf16 column where element (row, col) of a plane is stored (bit 3 of the
+// column, slot bit 0, flipped on rows 4..7 mod 8)
+__device__ inline int plane_col(int row, int col) {
+  return NDNET_PN_PLANE_SWZ ? col ^ (((row >> 2) & 1) << 3) : col;
+}
 #ifndef NDNET_PN_DEPTH
 #define NDNET_PN_DEPTH 2
 #endif
@@ -458,7 +478,8 @@ __device__ __attribute__((always_inline)) inline void store_cols_planes(const f3
         m4[r] = m;
         l4[r] = l;
       }
-      const int e = (row0 + 16 * rb + cl) * pitchb + oc0 + 16 * j + 4 * kq;  // 4 channels: 8 bytes
+      const int row = row0 + 16 * rb + cl;
+      const int e = row * pitchb + plane_col(row, oc0 + 16 * j + 4 * kq);  // 4 channels: 8 bytes
       *reinterpret_cast<bf16x4*>(base + e) = h4;
       *reinterpret_cast<bf16x4*>(base + plane + e) = m4;
       *reinterpret_cast<bf16x4*>(base + 2 * plane + e) = l4;
@@ -476,7 +497,8 @@ __device__ __attribute__((always_inline)) inline void store_cols_planes(const f3
         if (relu) v = fmaxf(v, 0.0f);
         __bf16 h, m, l;
         split3(v, h, m, l);
-        const int e = (row0 + 16 * rb + 4 * kq + r) * pitchb + oc0 + 16 * j + cl;
+        const int row = row0 + 16 * rb + 4 * kq + r;
+        const int e = row * pitchb + plane_col(row, oc0 + 16 * j + cl);
         base[e] = h;
         base[plane + e] = m;
         base[2 * plane + e] = l;
@@ -622,7 +644,7 @@ __device__ __attribute__((always_inline)) inline void plain_layer(const LayerCtx
   const int nchunk = C.N < CB * 16 ? 1 : C.N / (CB * 16);
   if (C.prec) {  // input: three bf16 planes of pitch K + kPadB (the producer's N + kPadB)
     const int pb = 32 * C.KG + kPadB;
-    const __bf16* abase6 = reinterpret_cast<const __bf16*>(g_smem + in) + (row0 + cl) * pb + 8 * kq;
+    const __bf16* abase6 = reinterpret_cast<const __bf16*>(g_smem + in) + (row0 + cl) * pb + plane_col(cl, 8 * kq);
 #ifndef NDNET_PN_SHORT_D2
 #define NDNET_PN_SHORT_D2 1
 #endif
@@ -661,7 +683,8 @@ __device__ __attribute__((always_inline)) inline void fused_pair(const LayerCtx&
   constexpr int PWC = kWaves / kRowBlocks, PNB = 4 / PWC;
   const int prow0 = (wave / PWC) * 16, pwc = (wave % PWC) * PNB;
   const float* ain = g_smem + in + (prow0 + cl) * pin + 4 * kq;
-  const __bf16* ain6 = reinterpret_cast<const __bf16*>(g_smem + in) + (prow0 + cl) * (32 * P.KG + kPadB) + 8 * kq;
+  const __bf16* ain6 = reinterpret_cast<const __bf16*>(g_smem + in) + (prow0 + cl) * (32 * P.KG + kPadB) +
+                       plane_col(cl, 8 * kq);
   // Q: row group wave / WC, column group wave % WC
   const int qrow0 = (wave / WC) * RB * 16, qwc = wave % WC;
   const bool qidle = qwc * NB * 16 >= Q.N;
@@ -689,7 +712,7 @@ __device__ __attribute__((always_inline)) inline void fused_pair(const LayerCtx&
     if (!qidle) {
       if (Q.prec) {
         const __bf16* af6 = reinterpret_cast<const __bf16*>(g_smem + fbuf + (f & 1) * fbsz) +
-                            (qrow0 + cl) * (kFuseNC + kPadB) + 8 * kq;
+                            (qrow0 + cl) * (kFuseNC + kPadB) + plane_col(cl, 8 * kq);
         run_tiles_x6<RB, NB>(acc2, Q.w6, Q.KG, 2 * f, 2, qwc * NB, 0, 1, af6, kFuseNC + kPadB,
                              [](f32x4 (&)[RB][NB], int) {});
       } else {
@@ -727,7 +750,7 @@ __device__ __attribute__((always_inline)) inline void fused_pair_x6p(const Layer
   const int kq = lane >> 4, cl = lane & 15;
   const int prow0 = (wave / PWC) * 16, pwc = wave % PWC;
   const int pinb = 32 * P.KG + kPadB;  // P.KG == 2
-  const __bf16* ain6 = reinterpret_cast<const __bf16*>(g_smem + in) + (prow0 + cl) * pinb + 8 * kq;
+  const __bf16* ain6 = reinterpret_cast<const __bf16*>(g_smem + in) + (prow0 + cl) * pinb + plane_col(cl, 8 * kq);
   const int qrow0 = (wave / WC) * RB * 16, qwc = wave % WC;
   const int nf = P.N / kFuseNC;
   const int fbsz = fbuf_floats(1) / 2;
@@ -763,7 +786,8 @@ __device__ __attribute__((always_inline)) inline void fused_pair_x6p(const Layer
   if (nf > 1) load_p(1);
   __syncthreads();
   for (int f = 0; f < nf; f++) {
-    const __bf16* af6 = reinterpret_cast<const __bf16*>(g_smem + fbuf + (f & 1) * fbsz) + (qrow0 + cl) * fpb + 8 * kq;
+    const __bf16* af6 =
+        reinterpret_cast<const __bf16*>(g_smem + fbuf + (f & 1) * fbsz) + (qrow0 + cl) * fpb + plane_col(cl, 8 * kq);
 #if NDNET_PN_PAIR_PFIRST
     // A/B: chunk f + 1's P (into the other buffer, free since the last
     // barrier) before chunk f's Q, so its epilogue overlaps other waves' Q
@@ -1060,7 +1084,7 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
       if (A.L[1].prec) {  // three bf16 planes, pitch 64 + kPadB
         typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
         const int pb = 64 + kPadB;
-        __bf16* const base = reinterpret_cast<__bf16*>(g_smem + out) + vr * pb + 4 * vq;
+        __bf16* const base = reinterpret_cast<__bf16*>(g_smem + out) + vr * pb + plane_col(vr, 4 * vq);
         bf16x4 h4, m4, l4;
 #pragma unroll
         for (int j = 0; j < 4; j++) {

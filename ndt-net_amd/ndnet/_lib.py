@@ -76,6 +76,8 @@ EXPORTS = {
     "ndnet_ndt_set_run_part": (_I, [_P, _I]),
     "ndnet_ndt_set_lazy_list": (_I, [_P, _I]),
     "ndnet_ndt_set_heavy_threshold": (_I, [_P, ctypes.c_uint32]),
+    "ndnet_ndt_set_welford_form": (_I, [_P, _I]),
+    "ndnet_ndt_get_welford_form": (_I, [_P]),
     "ndnet_ndt_debug_set_sync_timeout": (_I, [_P, ctypes.c_uint64]),
     "ndnet_ndt_run": (_I, [_P, _P, _P, _P, _P, _P, _P]),
     "ndnet_ndt_run_f64": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),

@@ -246,12 +246,14 @@ class PipelinedSegmentation:
         # barrier timeout fails the clouds (measured: 640 ms per step with two
         # streams at share 1).  So the share is at least N, the largest that
         # fits from the requested one down to N; a shape that fits none of them
-        # takes the one-launch-per-stage path (no cloud barriers).
+        # takes the one-launch-per-stage path (no cloud barriers).  With one
+        # NDT stream a share the shape does not fit falls back to the largest
+        # smaller one that does (at worst share 1: the whole chip).
         self.front_share = []
         for plan in self.plans:
             applied = 1
             if plan.path == 2:
-                want = [cu_share] if N == 1 else list(range(max(cu_share, N), N - 1, -1))
+                want = list(range(cu_share, 1, -1)) if N == 1 else list(range(max(cu_share, N), N - 1, -1))
                 for sh in want:
                     if sh <= 1:
                         break

@@ -101,6 +101,17 @@ class NdtPlan:
         include/ndnet_amd.h ndnet_ndt_set_lazy_list)."""
         _lib.check(_lib.lib().ndnet_ndt_set_lazy_list(self.handle, 1 if on else 0), "ndnet_ndt_set_lazy_list")
 
+    def set_welford_form(self, form: str) -> None:
+        """k_welford_q's light form: "light64" (one ND per lane), "quad" (a lane
+        quad per ND) or "auto" (quad at CU share 1, light64 above: the default);
+        identical results (include/ndnet_amd.h ndnet_ndt_set_welford_form)."""
+        code = {"auto": 0, "light64": 1, "quad": 2}[form]
+        _lib.check(_lib.lib().ndnet_ndt_set_welford_form(self.handle, code), "ndnet_ndt_set_welford_form")
+
+    @property
+    def welford_form(self) -> str:
+        return {1: "light64", 2: "quad"}[_lib.lib().ndnet_ndt_get_welford_form(self.handle)]
+
     def set_heavy_threshold(self, min_samples: int) -> None:
         """NDs with at least ``min_samples`` points get a whole wave in
         k_welford_q (include/ndnet_amd.h ndnet_ndt_set_heavy_threshold;

@@ -81,7 +81,7 @@ def _kernel_meta(cos):
 def test_welford_kernels_have_no_scratch_or_spills(tmp_path):
     meta = _kernel_meta(_code_objects(tmp_path))
     wq = {k: v for k, v in meta.items() if "k_welford_q" in k}
-    assert len(wq) == 2, sorted(meta)  # float and double inputs
+    assert len(wq) == 4, sorted(meta)  # float and double inputs x the two light forms
     for name, m in wq.items():
         assert m["private_segment_fixed_size"] == 0, (name, m)
         # (SGPR spills go to VGPR lanes, v_writelane / v_readlane: no memory, and
@@ -163,7 +163,7 @@ def test_welford_lds_loads_are_not_touched_before_their_wait(tmp_path):
             hz = _lds_hazards(lines)
             assert not hz, f"{head}: registers of an outstanding LDS load touched: {hz[:5]}"
             checked += 1
-    assert checked == 2
+    assert checked == 4
 
 
 def test_hazard_scan_flags_an_early_use():

@@ -797,19 +797,20 @@ def test_cu_share_results_identical(share, k):
         assert np.array_equal(res[0][0], res[1][0]) and res[0][1] == res[1][1], kind
 
 
-def _run_thresholds(pts, k, thresholds, path=2, labels=None, num_classes=-1):
-    """One plan per heavy threshold over the same batch: rows, one-hot
-    classes, stats and every dumped intermediate (counts, means, pre- and
-    post-KL covariances, list, kept set)."""
+def _run_thresholds(pts, k, thresholds, path=2, labels=None, num_classes=-1, forms=("auto",)):
+    """One plan per heavy threshold (and k_welford_q light form) over the
+    same batch: rows, one-hot classes, stats and every dumped intermediate
+    (counts, means, pre- and post-KL covariances, list, kept set)."""
     import torch
     from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
     B, n, _ = pts.shape
     res = []
-    for t in thresholds:
+    for t, form in ((t, f) for t in thresholds for f in forms):
         plan = NdtPlan(B, n, k, num_classes)
         plan.set_path(path)
         plan.set_lazy_list(False)
         plan.set_heavy_threshold(t)
+        plan.set_welford_form(form)
         out = torch.empty((B, k, 12), dtype=torch.float32, device="cuda")
         lbl = None if labels is None else torch.from_numpy(labels.astype(np.int32)).cuda()
         oc = None if labels is None else torch.empty((B, k, num_classes + 1), dtype=torch.float32, device="cuda")
@@ -874,6 +875,32 @@ def test_heavy_nds_labelled_and_full_size():
     lbl = rng.integers(0, 29, (3, 20_000))
     _same(_run_thresholds(pts, 30, (1, 256, 1 << 31), labels=lbl, num_classes=28))
     _same(_run_thresholds(make_batch("L", 16, 100_000), 1000, (256, 1 << 31)))
+
+
+@pytest.mark.parametrize("labelled", [False, True])
+def test_welford_forms_equal(labelled):
+    """k_welford_q's two light forms (light64: one ND per lane; quad: a lane
+    quad per ND -- a plan picks by its CU share, include/ndnet_amd.h
+    ndnet_ndt_set_welford_form) with the heavy threshold at 256 and at 2^31
+    (every ND light): identical rows, classes, stats and intermediates, on U
+    and L clouds at full size and on a labelled L batch; the default form is
+    quad at CU share 1 and light64 at share 2."""
+    from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
+    from ndnet.synthetic import make_batch
+    if labelled:
+        rng = np.random.default_rng(13)
+        pts = make_batch("L", 3, 20_000, seed0=9)
+        lbl = rng.integers(0, 29, (3, 20_000))
+        _same(_run_thresholds(pts, 30, (256, 1 << 31), labels=lbl, num_classes=28, forms=("light64", "quad")))
+        return
+    for kind in ("U", "L"):
+        _same(_run_thresholds(make_batch(kind, 16, 100_000), 1000, (256, 1 << 31), forms=("light64", "quad")))
+    plan = NdtPlan(16, 100_000, 1000, -1)
+    assert plan.welford_form == "quad"
+    plan.set_cu_share(2)
+    assert plan.welford_form == "light64"
+    plan.set_welford_form("quad")
+    assert plan.welford_form == "quad"
 
 
 def test_heavy_nds_float64_and_out_of_range():

@@ -12,7 +12,8 @@
 #   bash tools/gpu.sh ab      TAG NAME[:VAR=VAL,VAR=VAL] ...   env A/B on the bench (AB_ARGS: bench args)
 #   bash tools/gpu.sh variants TAG base NAME ...  library-variant A/B (tools/build_variant.sh NAME)
 #   bash tools/gpu.sh trace   TAG [bench args]    isolated-step kernel trace (one graph per step) + summary
-#   bash tools/gpu.sh pmc     TAG ndt|pn|chain|cache|issue    PMC passes, one counter group per run
+#   bash tools/gpu.sh pmc     TAG ndt|pn|chain|cache|issue|lds  PMC passes, one counter group per run
+#                                                 (NDNET_AMD_LIB=<variant .so> runs a library variant)
 #   bash tools/gpu.sh train   TAG                 train-path tests + the eager / graphed train step
 #   bash tools/gpu.sh stamps  TAG                 per-layer chain stamps (variant "stamps")
 #   bash tools/gpu.sh py      TAG tool.py [args]  a python tool under a time limit (output kept)
@@ -136,6 +137,8 @@ pmc)
       pmc_passes $OUT/$K "python3 $R/bench.py --eager --kind $K --steps 3 --warmup 1 --no-cpu-baseline --no-other" \
         "SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_SCA,SQ_ACTIVE_INST_LDS,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES"
     done ;;
+  lds)  # the chains' LDS instruction mix and bank conflicts only (one pass)
+    pmc_passes $OUT "python3 $R/tools/pn_forward.py --reps 3" $SQ_MIX ;;
   *) echo "unknown pmc kind $KIND"; exit 2 ;;
   esac
   ;;
