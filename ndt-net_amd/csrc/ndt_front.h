@@ -321,8 +321,14 @@ __global__ void __launch_bounds__(kFrontThreads) k_front(const T* __restrict__ p
   int b;
   if (A.xcd_local) {
     const uint32_t slot = L / 8u;  // slot within the XCD
+#ifdef NDNET_FRONT_DEAL_MINOR  // A/B only: the round 2-5 deal (deadlocks two concurrent launches)
+    const uint32_t cpx = A.B / 8u;
+    b = (int)((slot % cpx) * 8u + L % 8u);
+    g = slot / cpx;
+#else
     b = (int)((slot / G) * 8u + L % 8u);
     g = slot % G;
+#endif
   } else {
     b = (int)(L / G);
     g = L % G;

@@ -192,6 +192,7 @@ struct Plan {
   int lists_built;            // the deferred lists of the last run are built (no further build launches)
   int front_staged;           // k_front's scatter through LDS records (ndnet_ndt_set_front_staged; default 1)
   int run_part;               // ndnet_ndt_set_run_part: 0 whole run, 1 front only, 2 from k_welford_q on
+  int lane_rec;               // this run's k_front still to be recorded on its lanes (front_lanes_finish)
   uint32_t* heavy;            // [B][ndcap] the heavy NDs of each cloud (CloudCtl::heavy_n of them)
   double* rtab;               // [n + 1][2] (rc, rl) per count for wq_heavy's divisions
   uint32_t* lu_done;          // [B][ceil(ndcap / 64)] k_welford_q's per-group completion counters (re-armed to 0)
@@ -3866,14 +3867,58 @@ static bool lanes_enabled() {
   return v;
 }
 
+// Where a plan's k_front is recorded on its lanes: at the end of its run (the
+// default: a record node between k_front and k_welford_q held the next launch
+// back -- the isolated C2 k_front stage 51 -> 55 us, profiles/r05_lanes_ab.txt;
+// at the run's end it follows the last KL launch, where the pipeline records
+// its own stage event anyway), or right after k_front (NDNET_FRONT_REC_END=0,
+// A/B).  A later k_front on those lanes then waits for the whole run instead
+// of its k_front only: stricter, and still one chip's worth at a time.
+static bool rec_at_end() {
+  static const bool v = [] {
+    const char* e = getenv("NDNET_FRONT_REC_END");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+// Records the plan's last k_front launch on its lanes (caller holds g_lane_mu).
+static int front_lanes_record(Plan* P, hipStream_t st) {
+  FrontLaneSet& L = g_lanes[P->dev];
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  unsigned long long cap_id = 0;
+  HIPCHK(hipStreamGetCaptureInfo(st, &cs, &cap_id));
+  const bool cap = cs == hipStreamCaptureStatusActive;
+  if (!cap) cap_id = 0;
+  if (cap && !lane_capture_nodes()) return NDNET_OK;  // the lanes keep their last launch
+  if (!cap) HIPCHK(hipEventRecord(P->front_ev, st));
+  else HIPCHK(capture_event_node(st, P->front_ev, false));
+  for (int i = 0; i < P->nlanes; i++) {
+    const int l = (P->lane0 + i) % kFrontLanes;
+    L.ev[l] = P->front_ev;
+    L.st[l] = st;
+    L.cap[l] = cap_id;
+  }
+  return NDNET_OK;
+}
+
+// The record a run deferred to its end (rec_at_end): after its last launch.
+static int front_lanes_finish(Plan* P, hipStream_t st) {
+  if (!P->lane_rec) return NDNET_OK;
+  P->lane_rec = 0;
+  std::lock_guard<std::mutex> lk(g_lane_mu);
+  return front_lanes_record(P, st);
+}
+
 template <typename T>
 static int front_launch(Plan* P, hipStream_t st, const T* pts, const FrontArgs& F) {
+  P->lane_rec = 0;
   if (!lanes_enabled()) {
     k_front<T><<<P->fG * P->B, kFrontThreads, P->flds, st>>>(pts, F);
     HIPCHK(hipGetLastError());
     return NDNET_OK;
   }
-  std::lock_guard<std::mutex> lk(g_lane_mu);  // waits, launch and records in one host order
+  std::lock_guard<std::mutex> lk(g_lane_mu);  // waits and launch in one host order
   FrontLaneSet& L = g_lanes[P->dev];
   if (L.plans <= 1 && solo_skip()) {
     k_front<T><<<P->fG * P->B, kFrontThreads, P->flds, st>>>(pts, F);
@@ -3901,17 +3946,11 @@ static int front_launch(Plan* P, hipStream_t st, const T* pts, const FrontArgs& 
   }
   k_front<T><<<P->fG * P->B, kFrontThreads, P->flds, st>>>(pts, F);
   HIPCHK(hipGetLastError());
-  if (!cap) HIPCHK(hipEventRecord(P->front_ev, st));
-  else if (nodes) HIPCHK(capture_event_node(st, P->front_ev, false));
-  if (nodes) {  // a capture without lane nodes records nothing: the lanes keep their last launch
-    for (int i = 0; i < P->nlanes; i++) {
-      const int l = (P->lane0 + i) % kFrontLanes;
-      L.ev[l] = P->front_ev;
-      L.st[l] = st;
-      L.cap[l] = cap_id;
-    }
+  if (rec_at_end()) {
+    P->lane_rec = 1;
+    return NDNET_OK;
   }
-  return NDNET_OK;
+  return front_lanes_record(P, st);
 }
 
 // k_welford_q's class-histogram LDS of a labelled run (0: the global histograms)
@@ -4003,7 +4042,7 @@ static int run_impl(Plan* P, hipStream_t st, const T* pts, const int32_t* lbl, f
   }
   if (P->run_part == 1) {
     HIPCHK(hipGetLastError());
-    return NDNET_OK;
+    return front_lanes_finish(P, st);
   }
 welford:
   P->lists_built = 0;
@@ -4031,7 +4070,7 @@ welford:
   }
   if (P->timing) HIPCHK(hipEventRecord(P->ev[6], st));
   HIPCHK(hipGetLastError());
-  return NDNET_OK;
+  return front_lanes_finish(P, st);
 }
 
 __global__ void k_set_epoch(CloudCtl* ctl, int B, uint32_t epoch) {
