@@ -327,8 +327,14 @@ def main() -> None:
                  "pruned_per_cloud": round(float(np.mean([st.num_nds - k for st in ost])), 1)}
         if o_ndt_streams:
             other["ndt_streams"] = o_ndt_streams
+        # free the L pipeline's plans: the stage lines below time the plans a
+        # standalone caller has (include/ndnet_amd.h: with fewer live k_front
+        # plans than the cloud-major deal's bound, no lane admission)
+        del o_plans, o_stats
         if o_graphed is not graphed:
             del o_graphed
+            import gc
+            gc.collect()
         if hasattr(graphed, "load_resident"):
             graphed.load_resident(pts)
         else:

