@@ -722,6 +722,14 @@ def main() -> None:
                       " per-point layers, fp32 MFMA on the K=16 first layers and the TNet / seg-bias FC layers"
                       if pointnet_hip.SPLIT_BF16 else "f64 NDT; PointNet fp32 MFMA"),
             "data": f"synthetic {args.kind} clouds (SURVEY 8d), random-init weights",
+            "measurement_notes": [
+                "U clouds reach exactly k occupied voxels at the accepted size, so their level-1 prune removes "
+                "nothing: the run counts the KL events (stats num_events / num_kl) and builds the sorted list only "
+                "on demand (ndnet_ndt_set_lazy_list; bit-equal to the eager build by test_lazy_list_equals_eager). "
+                "The L line (other_distribution) times the KL scoring, sort and prune of ~121 pruned NDs per cloud.",
+                "Every ring slot replays one resident batch (bench inputs already in HBM, as the contract asks; "
+                "the slots' inputs total ~115 MB, within the 256 MB Infinity Cache); pcie_inclusive streams the "
+                "batch from pinned host memory instead."] if not levels else None,
             "config": {"workload": (f"batch {B} x {n} pts -> {k} NDs, NDTNetSegmentation F={F} C={C} eval"
                                     if not levels and world == 1 else
                                     f"C4: {B * world} clouds end to end ({n} pts -> {k} NDs -> NDTNetSegmentation "

@@ -52,6 +52,10 @@ int ndnet_tr_gemm(const float *A, const float *B, float *C, const float *bias, i
 
 /* out[i] = sum_{p < nparts} part[p * count + i], in p order (deterministic). */
 int ndnet_tr_sum_parts(const float *part, float *out, int64_t count, int nparts, void *stream);
+/* The same over a [rows][cols] block written into rows of stride ldo >= cols
+ * (a column slice of a wider matrix). */
+int ndnet_tr_sum_parts_2d(const float *part, float *out, int64_t rows, int64_t cols, int64_t ldo, int nparts,
+                          void *stream);
 
 /* BatchNorm1d forward with batch statistics (torch's training mode) over
  * y [B][C][N], one workgroup per channel: mean and biased variance over the
@@ -123,16 +127,20 @@ int ndnet_row_argmax(const float *x, int64_t rows, int cols, int32_t *out, void 
  * gradient dW[n][k] = sum_b dpre[b][n] x[b][k] (any output may be NULL);
  * ndnet_tr_fc_bwd_x -- dx[b][k] = sum_n dpre[b][n] W[n][k], over `nsplit`
  * channel ranges of at most 256 (partials part [nsplit][B][K], summed in split
- * order into dx; part may be NULL with nsplit == 1). */
+ * order into dx; part may be NULL with nsplit == 1).
+ * ldw: the row stride of W (forward, input gradient) and of dW (weight
+ * gradient) in floats, >= K (a multiple of 4 where rows are read or written
+ * as float4); 0 = K.  A column slice W[:, c:] of a wider weight runs in place:
+ * the seg head's per-cloud bias b + W[:, 64:] g (ndtnet.py:230-234). */
 int ndnet_tr_fc_fwd(const float *x, const float *W, const float *bias, float *y, float *z, float *mean,
                     float *invstd, float *running_mean, float *running_var, const float *gamma, const float *beta,
-                    int B, int K, int N, float eps, float momentum, int relu, int eye, int64_t *batches_tracked,
-                    void *stream);
+                    int B, int K, int N, int64_t ldw, float eps, float momentum, int relu, int eye,
+                    int64_t *batches_tracked, void *stream);
 int ndnet_tr_fc_bwd_w(const float *dz, const float *x, const float *y, const float *mean, const float *invstd,
                       const float *gamma, const float *beta, float *dpre, float *dW, float *db, float *dgamma,
-                      float *dbeta, int B, int K, int N, int relu, void *stream);
-int ndnet_tr_fc_bwd_x(const float *dpre, const float *W, float *dx, float *part, int B, int K, int N, int nsplit,
-                      void *stream);
+                      float *dbeta, int B, int K, int N, int64_t ldw, int relu, void *stream);
+int ndnet_tr_fc_bwd_x(const float *dpre, const float *W, float *dx, float *part, int B, int K, int N, int64_t ldw,
+                      int nsplit, void *stream);
 
 /* The seg head's log_softmax over the class dim (ndtnet.py:241; x, out
  * [B][C][N]) and its backward (dx = dy - exp(y) sum_c dy, y the forward's

@@ -367,8 +367,11 @@ __global__ __launch_bounds__(256) void k_tr_gemm_x6(const float* __restrict__ A,
 // parts per round left the small layers' launches at 4 workgroups and 4
 // dependent rounds, 178 us a step over 19 launches, r05k)
 constexpr int kSumParts = 32;
+// out[r * ldo + c] = the sum of part[p][r * cols + c] over p in part order
+// (ldo == cols: a contiguous output; the seg head's conv1 writes the first
+// columns of its [Cout][c + F] weight gradient in place)
 __global__ __launch_bounds__(256) void k_tr_sum_parts(const float* __restrict__ part, float* __restrict__ out,
-                                                      int64_t count, int nparts) {
+                                                      int64_t count, int nparts, int64_t cols, int64_t ldo) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= count) return;
   float s = 0.0f;
@@ -380,7 +383,7 @@ __global__ __launch_bounds__(256) void k_tr_sum_parts(const float* __restrict__ 
     for (int u = 0; u < kSumParts; u++)
       if (p0 + u < nparts) s = (p0 + u == 0) ? v[u] : s + v[u];
   }
-  out[i] = s;
+  out[cols == ldo ? i : i / cols * ldo + i % cols] = s;
 }
 
 // sum over the workgroup in a fixed order (wave shuffles, then the waves in order)
@@ -805,14 +808,14 @@ __global__ __launch_bounds__(kFcWaves * 64) void k_tr_fc_fwd(const float* __rest
                                                    float* __restrict__ rvar, const float* __restrict__ gamma,
                                                    const float* __restrict__ beta, int Bn, int K, int N, float eps,
                                                    float momentum, int relu, int eye,
-                                                   long long* __restrict__ batches_tracked) {
+                                                   long long* __restrict__ batches_tracked, int64_t ldw) {
   extern __shared__ f32x4 s_x[];  // [Bn][K / 4]
   const int lane = threadIdx.x & 63;
   const int K4 = K / 4;
   if (batches_tracked && blockIdx.x == 0 && threadIdx.x == 0) batches_tracked[0] += 1;
   fc_stage_x(s_x, x, Bn, K4);
   for (int n = blockIdx.x * kFcWaves + (threadIdx.x >> 6); n < N; n += gridDim.x * kFcWaves) {
-    const f32x4* w = reinterpret_cast<const f32x4*>(W + (int64_t)n * K);
+    const f32x4* w = reinterpret_cast<const f32x4*>(W + (int64_t)n * ldw);
     float acc[kFcB];
 #pragma unroll
     for (int b = 0; b < kFcB; b++) acc[b] = 0.0f;
@@ -875,7 +878,8 @@ __global__ __launch_bounds__(kFcWaves * 64) void k_tr_fc_bwd_w(const float* __re
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      float* __restrict__ dpre, float* __restrict__ dW,
                                                      float* __restrict__ db, float* __restrict__ dgamma,
-                                                     float* __restrict__ dbeta, int Bn, int K, int N, int relu) {
+                                                     float* __restrict__ dbeta, int Bn, int K, int N, int relu,
+                                                     int64_t ldw) {
   extern __shared__ f32x4 s_x[];  // [Bn][K / 4] (dW only)
   const int lane = threadIdx.x & 63;
   const int K4 = K / 4;
@@ -909,7 +913,7 @@ __global__ __launch_bounds__(kFcWaves * 64) void k_tr_fc_bwd_w(const float* __re
     float dv[kFcB];
 #pragma unroll
     for (int b = 0; b < kFcB; b++) dv[b] = __shfl(d, b);  // 0 past the rows
-    f32x4* wrow = reinterpret_cast<f32x4*>(dW + (int64_t)n * K);
+    f32x4* wrow = reinterpret_cast<f32x4*>(dW + (int64_t)n * ldw);
     for (int f = lane; f < K4; f += 64) {
       f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -924,7 +928,8 @@ __global__ __launch_bounds__(kFcWaves * 64) void k_tr_fc_bwd_w(const float* __re
 // split s); part[s][b][k] (or dx itself with one split), summed in split order.
 constexpr int kFcXMaxN = 256;  // channels of a split staged in LDS
 __global__ __launch_bounds__(256) void k_tr_fc_bwd_x(const float* __restrict__ dpre, const float* __restrict__ W,
-                                                     float* __restrict__ out, int Bn, int K, int N, int nsplit) {
+                                                     float* __restrict__ out, int Bn, int K, int N, int nsplit,
+                                                     int64_t ldw) {
   __shared__ float s_d[kFcXMaxN][kFcB];
   const int s = blockIdx.y;
   const int n0 = (int)((int64_t)N * s / nsplit), n1 = (int)((int64_t)N * (s + 1) / nsplit);
@@ -942,14 +947,14 @@ __global__ __launch_bounds__(256) void k_tr_fc_bwd_x(const float* __restrict__ d
   for (; nn + 8 <= n1; nn += 8) {  // 8 weight loads in flight, summed in channel order
     float wv[8];
 #pragma unroll
-    for (int j = 0; j < 8; j++) wv[j] = W[(int64_t)(nn + j) * K + k];
+    for (int j = 0; j < 8; j++) wv[j] = W[(int64_t)(nn + j) * ldw + k];
 #pragma unroll
     for (int j = 0; j < 8; j++)
 #pragma unroll
       for (int b = 0; b < kFcB; b++) acc[b] = fmaf(s_d[nn + j - n0][b], wv[j], acc[b]);
   }
   for (; nn < n1; nn++) {
-    const float wv = W[(int64_t)nn * K + k];
+    const float wv = W[(int64_t)nn * ldw + k];
 #pragma unroll
     for (int b = 0; b < kFcB; b++) acc[b] = fmaf(s_d[nn - n0][b], wv, acc[b]);
   }
@@ -1413,7 +1418,16 @@ extern "C" int ndnet_tr_sum_parts(const float* part, float* out, int64_t count, 
   if (!part || !out || count <= 0 || nparts <= 0) return -20;
   const int64_t blocks = (count + 255) / 256;
   if (blocks > (int64_t)INT32_MAX) return -20;
-  k_tr_sum_parts<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(part, out, count, nparts);
+  k_tr_sum_parts<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(part, out, count, nparts, count, count);
+  return launched();
+}
+
+extern "C" int ndnet_tr_sum_parts_2d(const float* part, float* out, int64_t rows, int64_t cols, int64_t ldo,
+                                     int nparts, void* stream) {
+  if (!part || !out || rows <= 0 || cols <= 0 || ldo < cols || nparts <= 0) return -20;
+  const int64_t count = rows * cols, blocks = (count + 255) / 256;
+  if (blocks > (int64_t)INT32_MAX) return -20;
+  k_tr_sum_parts<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(part, out, count, nparts, cols, ldo);
   return launched();
 }
 
@@ -1495,9 +1509,10 @@ static unsigned fc_grid(int N) {
 
 extern "C" int ndnet_tr_fc_fwd(const float* x, const float* W, const float* bias, float* y, float* z, float* mean,
                                float* invstd, float* running_mean, float* running_var, const float* gamma,
-                               const float* beta, int B, int K, int N, float eps, float momentum, int relu, int eye,
-                               int64_t* batches_tracked, void* stream) {
-  if (!x || !W || !bias || !z || B <= 0 || B > kFcB || K <= 0 || K % 4 || N <= 0) return -20;
+                               const float* beta, int B, int K, int N, int64_t ldw, float eps, float momentum, int relu,
+                               int eye, int64_t* batches_tracked, void* stream) {
+  if (ldw == 0) ldw = K;
+  if (!x || !W || !bias || !z || B <= 0 || B > kFcB || K <= 0 || K % 4 || N <= 0 || ldw < K || ldw % 4) return -20;
   if (gamma && (!y || !mean || !invstd || !beta)) return -20;
   if (!gamma && (relu || batches_tracked)) return -20;
   if ((((uintptr_t)x | (uintptr_t)W) & 15) != 0) return -20;  // float4 rows
@@ -1505,33 +1520,38 @@ extern "C" int ndnet_tr_fc_fwd(const float* x, const float* W, const float* bias
   if (lds > (size_t)kFcMaxLds) return -20;  // x staged whole (K <= 1024 at 16 rows)
   k_tr_fc_fwd<<<fc_grid(N), kFcWaves * 64, lds, (hipStream_t)stream>>>(x, W, bias, y, z, mean, invstd, running_mean,
                                                               running_var, gamma, beta, B, K, N, eps, momentum, relu,
-                                                              eye, reinterpret_cast<long long*>(batches_tracked));
+                                                              eye, reinterpret_cast<long long*>(batches_tracked), ldw);
   return launched();
 }
 
 extern "C" int ndnet_tr_fc_bwd_w(const float* dz, const float* x, const float* y, const float* mean,
                                  const float* invstd, const float* gamma, const float* beta, float* dpre, float* dW,
-                                 float* db, float* dgamma, float* dbeta, int B, int K, int N, int relu, void* stream) {
-  if (!dz || !x || B <= 0 || B > kFcB || K <= 0 || K % 4 || N <= 0) return -20;
+                                 float* db, float* dgamma, float* dbeta, int B, int K, int N, int64_t ldw, int relu,
+                                 void* stream) {
+  if (ldw == 0) ldw = K;
+  if (!dz || !x || B <= 0 || B > kFcB || K <= 0 || K % 4 || N <= 0 || ldw < K || ldw % 4) return -20;
   if (gamma && (!y || !mean || !invstd || !beta)) return -20;
   if (!gamma && relu) return -20;
   if ((((uintptr_t)x | (uintptr_t)dW) & 15) != 0) return -20;
   const size_t lds = dW ? (size_t)B * K * sizeof(float) : 0;
   if (lds > (size_t)kFcMaxLds) return -20;
   k_tr_fc_bwd_w<<<fc_grid(N), kFcWaves * 64, lds, (hipStream_t)stream>>>(dz, x, y, mean, invstd, gamma, beta, dpre, dW, db,
-                                                                dgamma, dbeta, B, K, N, relu);
+                                                                dgamma, dbeta, B, K, N, relu, ldw);
   return launched();
 }
 
 extern "C" int ndnet_tr_fc_bwd_x(const float* dpre, const float* W, float* dx, float* part, int B, int K, int N,
-                                 int nsplit, void* stream) {
-  if (!dpre || !W || !dx || B <= 0 || B > kFcB || K <= 0 || N <= 0 || nsplit <= 0 || nsplit > N) return -20;
+                                 int64_t ldw, int nsplit, void* stream) {
+  if (ldw == 0) ldw = K;
+  if (!dpre || !W || !dx || B <= 0 || B > kFcB || K <= 0 || N <= 0 || nsplit <= 0 || nsplit > N || ldw < K)
+    return -20;
   if ((N + nsplit - 1) / nsplit > kFcXMaxN || (nsplit > 1 && !part)) return -20;
   float* out = nsplit > 1 ? part : dx;
-  k_tr_fc_bwd_x<<<dim3((K + 255) / 256, nsplit), 256, 0, (hipStream_t)stream>>>(dpre, W, out, B, K, N, nsplit);
+  k_tr_fc_bwd_x<<<dim3((K + 255) / 256, nsplit), 256, 0, (hipStream_t)stream>>>(dpre, W, out, B, K, N, nsplit, ldw);
   if (nsplit > 1) {
     const int64_t count = (int64_t)B * K;
-    k_tr_sum_parts<<<(unsigned)((count + 255) / 256), 256, 0, (hipStream_t)stream>>>(part, dx, count, nsplit);
+    k_tr_sum_parts<<<(unsigned)((count + 255) / 256), 256, 0, (hipStream_t)stream>>>(part, dx, count, nsplit, count,
+                                                                                     count);
   }
   return launched();
 }

@@ -140,6 +140,7 @@ TRAIN_EXPORTS: dict = {
     "ndnet_tr_gemm": (_I, [_P, _P, _P, _P, _I64, _I, _I, _I, _I64, _I64, _I64, _I64, _I64, _I64, _I, _I, _I, _I, _I,
                            _I, _P]),
     "ndnet_tr_sum_parts": (_I, [_P, _P, _I64, _I, _P]),
+    "ndnet_tr_sum_parts_2d": (_I, [_P, _P, _I64, _I64, _I64, _I, _P]),
     "ndnet_tr_bn_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, ctypes.c_float, ctypes.c_float, _I, _P, _P,
                              _P, _P]),
     "ndnet_tr_bn_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P]),
@@ -148,10 +149,10 @@ TRAIN_EXPORTS: dict = {
     "ndnet_tr_argmax_match": (_I, [_P, _P, _I64, _I, _P, _P]),
     "ndnet_tr_argmax_match_cm": (_I, [_P, _P, _I, _I, _I, _P, _P, _P]),
     "ndnet_row_argmax": (_I, [_P, _I64, _I, _P, _P]),
-    "ndnet_tr_fc_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, ctypes.c_float, ctypes.c_float,
-                             _I, _I, _P, _P]),
-    "ndnet_tr_fc_bwd_w": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
-    "ndnet_tr_fc_bwd_x": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "ndnet_tr_fc_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I64, ctypes.c_float,
+                             ctypes.c_float, _I, _I, _P, _P]),
+    "ndnet_tr_fc_bwd_w": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I64, _I, _P]),
+    "ndnet_tr_fc_bwd_x": (_I, [_P, _P, _P, _P, _I, _I, _I, _I64, _I, _P]),
     "ndnet_tr_point_transform": (_I, [_P, _P, _I, _P, _I, _P, _I, _I, _P]),
     "ndnet_tr_point_transform_bwd": (_I, [_P, _P, _I, _P, _I, _P, _I, _I, _P]),
     "ndnet_tr_log_softmax_c": (_I, [_P, _P, _I, _I, _I, _P]),

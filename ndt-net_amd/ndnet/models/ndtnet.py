@@ -18,9 +18,10 @@ Two forward paths:
   * train mode on the GPU -> every Conv1d(k=1) + BatchNorm1d (batch
     statistics) [+ ReLU] block forward and backward on the train kernels of
     lib/libndnet_amd.so (``ndnet.models.train_hip``, include/ndnet_train.h);
-    the TNet FC heads (Linear + BatchNorm1d + ReLU fused per layer) and the
-    x^T t2 product also run on HIP kernels; the point transform t1 (one bmm)
-    and log-softmax stay torch ops.
+    the TNet FC heads (Linear + BatchNorm1d + ReLU fused per layer), the
+    point transform t1, x^T t2, the seg head's conv1 over cat(x_t2, g), the
+    log-softmax over the class dim and the loss also run on HIP kernels
+    (round 5); what torch still runs per step is listed in DESIGN.md §3.
     ``NDNET_TRAIN_PATH=torch`` selects the torch composition instead (A/B).
   * anything else (eval-mode autograd, CPU) -> the PyTorch composition below,
     which is also the fp32 reference the kernels are tested against.
@@ -52,11 +53,19 @@ def _hip_train(conv: nn.Conv1d, bn, x: torch.Tensor) -> bool:
 def _hip_fc(t: "TNet", g: torch.Tensor) -> bool:
     """The TNet head on the HIP FC kernels: train mode, fp32 on the GPU, at most
     16 clouds (train_hip.FC_MAX_ROWS), every layer's input width a multiple of
-    4 and its rows small enough for the kernels' LDS stage (B * K <= 16384)."""
+    4 and its rows small enough for the kernels' LDS stage (B * K <= 16384),
+    and what ndnet_tr_fc_fwd / _bwd_w read with 16-byte loads 16-byte aligned
+    and contiguous (a weight viewed at an odd offset into a flat buffer, or a
+    layer without a bias, takes the torch path)."""
+    def aligned(x):
+        return x is not None and x.is_contiguous() and x.data_ptr() % 16 == 0
     return (_hip_train(t.conv1, t.bn1, g) and t.fc1.training and t.bn4.training and t.bn5.training
-            and 2 <= g.shape[0] <= 16 and g.dim() == 2
+            and 2 <= g.shape[0] <= 16 and g.dim() == 2 and g.is_contiguous() and g.data_ptr() % 16 == 0
             and all(fc.weight.dtype == torch.float32 and fc.in_features % 4 == 0
-                    and g.shape[0] * fc.in_features <= 16384 for fc in (t.fc1, t.fc2, t.fc3)))
+                    and g.shape[0] * fc.in_features <= 16384 and fc.bias is not None
+                    and aligned(fc.weight) and aligned(fc.bias)
+                    and (fc.weight.grad is None or aligned(fc.weight.grad))
+                    for fc in (t.fc1, t.fc2, t.fc3)))
 
 
 def _block_pool(conv: nn.Conv1d, bn, x: torch.Tensor, relu: bool) -> torch.Tensor:

@@ -105,19 +105,27 @@ def dw_split(Bn: int, Cout: int, Cin: int, N: int):
     return 1, -(-N // kchunk), kchunk
 
 
-def conv_weight_grad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
-    """dW = sum over clouds and points of dy x^T: [Cout,Cin]."""
+def conv_weight_grad(dy: torch.Tensor, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dW = sum over clouds and points of dy x^T: [Cout,Cin], into ``out``
+    when given (a [Cout,Cin] view with unit column stride: rows of any stride,
+    e.g. the first columns of a wider weight's gradient)."""
     Bn, Cout, N = dy.shape
     Cin = x.shape[1]
     cpz, nch, kchunk = dw_split(Bn, Cout, Cin, N)
     parts = -(-Bn // cpz) * nch
-    dw = torch.empty(Cout, Cin, device=dy.device, dtype=torch.float32)
-    out = dw if parts == 1 else torch.empty(parts, Cout, Cin, device=dy.device, dtype=torch.float32)
-    gemm(dy, x, out, None, Cout, Cin, N, N, N, Cin, Cout * N, Cin * N, Cout * Cin, Bn, True, True, nch, kchunk,
+    dw = torch.empty(Cout, Cin, device=dy.device, dtype=torch.float32) if out is None else out
+    if dw.shape != (Cout, Cin) or dw.stride(1) != 1:
+        raise ValueError("conv_weight_grad: out must be [Cout, Cin] with unit column stride")
+    ldo = dw.stride(0)
+    if parts == 1:
+        gemm(dy, x, dw, None, Cout, Cin, N, N, N, ldo, Cout * N, Cin * N, Cout * ldo, Bn, True, True, nch, kchunk,
+             clouds_per_part=cpz)
+        return dw
+    tmp = torch.empty(parts, Cout, Cin, device=dy.device, dtype=torch.float32)
+    gemm(dy, x, tmp, None, Cout, Cin, N, N, N, Cin, Cout * N, Cin * N, Cout * Cin, Bn, True, True, nch, kchunk,
          clouds_per_part=cpz)
-    if parts > 1:
-        _lib.check(_lib.lib().ndnet_tr_sum_parts(out.data_ptr(), dw.data_ptr(), Cout * Cin, parts, _stream()),
-                   "ndnet_tr_sum_parts")
+    _lib.check(_lib.lib().ndnet_tr_sum_parts_2d(tmp.data_ptr(), dw.data_ptr(), Cout, Cin, ldo, parts, _stream()),
+               "ndnet_tr_sum_parts_2d")
     return dw
 
 
@@ -230,6 +238,32 @@ def conv_bn_act(conv: torch.nn.Conv1d, bn: Optional[torch.nn.BatchNorm1d], x: to
     return out
 
 
+def _seg_fc_ok(g: torch.Tensor, W: torch.Tensor, c: int) -> bool:
+    """The seg head's per-cloud bias GEMMs fit the FC kernels (ndnet_tr_fc_*,
+    include/ndnet_train.h): <= 16 clouds, F % 4 == 0, g staged whole in LDS,
+    16-byte aligned rows of W[:, c:] (row stride Ct) and g."""
+    Bn, F = g.shape
+    Ct = W.shape[1]
+    return (Bn <= FC_MAX_ROWS and F % 4 == 0 and Bn * F <= 16384 and Ct % 4 == 0 and c % 4 == 0
+            and W.stride(1) == 1 and W.stride(0) == Ct and W.data_ptr() % 16 == 0
+            and g.is_contiguous() and g.data_ptr() % 16 == 0)
+
+
+def _seg_bias(g: torch.Tensor, W: torch.Tensor, b: torch.Tensor, c: int) -> torch.Tensor:
+    """cb = b + g W[:, c:]^T [B,Cout]: one FC-kernel launch reading the weight's
+    columns c.. in place (torch's addmm on the strided slice: ~8 us)."""
+    if not _seg_fc_ok(g, W, c):
+        return torch.addmm(b, g, W[:, c:].t())
+    Bn, F = g.shape
+    Cout, Ct = W.shape
+    cb = torch.empty(Bn, Cout, device=g.device, dtype=torch.float32)
+    b = b.contiguous()
+    rc = _lib.lib().ndnet_tr_fc_fwd(g.data_ptr(), W[:, c:].data_ptr(), b.data_ptr(), None, cb.data_ptr(), None, None,
+                                    None, None, None, None, Bn, F, Cout, Ct, 0.0, 0.0, 0, 0, None, _stream())
+    _lib.check(rc, "ndnet_tr_fc_fwd (seg bias)")
+    return cb
+
+
 class _SegConv1(torch.autograd.Function):
     """The segmentation head's first block (ndtnet.py:230-234): relu(bn(conv1(
     cat(x_t2, g broadcast over the points)))) as a conv over x_t2's c channels
@@ -247,7 +281,7 @@ class _SegConv1(torch.autograd.Function):
         Cout, Ct = W.shape
         if Ct != c + g.shape[1]:
             raise ValueError(f"conv1 expects {Ct} input channels, got {c} + {g.shape[1]}")
-        cb = torch.addmm(b.detach(), g.detach(), W[:, c:].t())     # [B,Cout]
+        cb = _seg_bias(g, W, b.detach(), c)                         # [B,Cout]: b + W[:, c:] g
         y = torch.empty(Bn, Cout, N, device=x.device, dtype=torch.float32)
         gemm(W, x, y, cb, Cout, N, c, Ct, N, N, 0, c * N, Cout * N, Bn, True, False, sbias=Cout)
         z = torch.empty_like(y)
@@ -282,13 +316,31 @@ class _SegConv1(torch.autograd.Function):
             gemm(W, dy, dx, None, c, N, Cout, Ct, N, N, 0, Cout * N, c * N, Bn, False, False)
         dcb = row_sum(dy)                                            # [B,Cout]: the per-cloud bias gradient
         dW = None
+        fc = _seg_fc_ok(g, W, c)
         if need[2]:
             dW = torch.empty(Cout, Ct, device=dy.device, dtype=torch.float32)
-            dW[:, :c].copy_(conv_weight_grad(dy, x))
-            torch.mm(dcb.t(), g, out=dW[:, c:])
+            conv_weight_grad(dy, x, out=dW[:, :c])
+            if fc:  # dW[:, c:] = dcb^T g on the FC kernel, rows of stride Ct written in place
+                rc = _lib.lib().ndnet_tr_fc_bwd_w(dcb.data_ptr(), g.data_ptr(), None, None, None, None, None, None,
+                                                  dW[:, c:].data_ptr(), None, None, None, Bn, Ct - c, Cout, Ct, 0,
+                                                  _stream())
+                _lib.check(rc, "ndnet_tr_fc_bwd_w (seg bias)")
+            else:
+                torch.mm(dcb.t(), g, out=dW[:, c:])
             dW = dW.view(ctx.w_shape)
         db = dbias if need[3] else None  # sum over clouds and points of dy (bn_bwd's conv-bias output)
-        dg = torch.mm(dcb, W[:, c:]) if need[1] else None
+        dg = None
+        if need[1]:
+            if fc:  # dg = dcb W[:, c:], the weight read in place
+                F = Ct - c
+                dg = torch.empty(Bn, F, device=dy.device, dtype=torch.float32)
+                ns = _fc_splits(Cout)
+                part = torch.empty(ns, Bn, F, device=dy.device, dtype=torch.float32) if ns > 1 else None
+                rc = _lib.lib().ndnet_tr_fc_bwd_x(dcb.data_ptr(), W[:, c:].data_ptr(), dg.data_ptr(), _ptr(part), Bn,
+                                                  F, Cout, Ct, ns, _stream())
+                _lib.check(rc, "ndnet_tr_fc_bwd_x (seg bias)")
+            else:
+                dg = torch.mm(dcb, W[:, c:])
         return (dx, dg, dW, db, dgamma if need[4] else None, dbeta if need[5] else None,
                 None, None, None, None, None)
 
@@ -414,8 +466,8 @@ class _FcBNAct(torch.autograd.Function):
         bt = beta.detach().contiguous() if bn else None
         rc = _lib.lib().ndnet_tr_fc_fwd(x.data_ptr(), w2.data_ptr(), b.detach().contiguous().data_ptr(), _ptr(y),
                                         z.data_ptr(), _ptr(mean), _ptr(invstd), _ptr(run_mean), _ptr(run_var),
-                                        _ptr(g), _ptr(bt), Bn, K, N, float(eps), float(momentum), int(relu), int(eye),
-                                        _ptr(nbt), _stream())
+                                        _ptr(g), _ptr(bt), Bn, K, N, 0, float(eps), float(momentum), int(relu),
+                                        int(eye), _ptr(nbt), _stream())
         _lib.check(rc, "ndnet_tr_fc_fwd")
         ctx.relu, ctx.bn = bool(relu), bn
         ctx.save_for_backward(x, w2, y, mean, invstd, g, bt)
@@ -436,15 +488,15 @@ class _FcBNAct(torch.autograd.Function):
         dbeta = torch.empty(N, device=dev, dtype=torch.float32) if ctx.bn and need[4] else None
         rc = _lib.lib().ndnet_tr_fc_bwd_w(dz.data_ptr(), x.data_ptr(), _ptr(y), _ptr(mean), _ptr(invstd), _ptr(g),
                                           _ptr(bt), dpre.data_ptr(), _ptr(dw), _ptr(db), _ptr(dgamma), _ptr(dbeta),
-                                          Bn, K, N, int(ctx.relu), _stream())
+                                          Bn, K, N, 0, int(ctx.relu), _stream())
         _lib.check(rc, "ndnet_tr_fc_bwd_w")
         dx = None
         if need[0]:
             dx = torch.empty(Bn, K, device=dev, dtype=torch.float32)
             ns = _fc_splits(N)
             part = torch.empty(ns, Bn, K, device=dev, dtype=torch.float32) if ns > 1 else None
-            rc = _lib.lib().ndnet_tr_fc_bwd_x(dpre.data_ptr(), w2.data_ptr(), dx.data_ptr(), _ptr(part), Bn, K, N, ns,
-                                              _stream())
+            rc = _lib.lib().ndnet_tr_fc_bwd_x(dpre.data_ptr(), w2.data_ptr(), dx.data_ptr(), _ptr(part), Bn, K, N, 0,
+                                              ns, _stream())
             _lib.check(rc, "ndnet_tr_fc_bwd_x")
         return dx, dw, db, dgamma, dbeta, None, None, None, None, None, None, None
 

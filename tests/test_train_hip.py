@@ -232,6 +232,38 @@ def test_fc_head_matches_torch(K, N, bn, relu, eye, B):
         _close(fc.bias.grad, fc2.bias.grad, tol, "db")
 
 
+def test_fc_head_unsupported_layouts_take_torch_path():
+    """a TNet FC layer without a bias, or a weight viewed at an
+    8-byte offset into a flat buffer, is not what ndnet_tr_fc_fwd / _bwd_w
+    read (16-byte loads, a bias row): the head takes the torch path and
+    trains like the torch module, instead of failing."""
+    from ndnet.models import ndtnet
+    for case in ("nobias", "offset"):
+        torch.manual_seed(3)
+        t = ndtnet.TNet(3).cuda().train()
+        if case == "nobias":
+            t.fc2.bias = None
+        else:
+            flat = torch.empty(t.fc1.weight.numel() + 2, device="cuda")
+            w = flat[2:].view_as(t.fc1.weight)
+            w.copy_(t.fc1.weight.detach())
+            t.fc1.weight = torch.nn.Parameter(w)
+            assert t.fc1.weight.data_ptr() % 16 == 8
+        g = torch.randn(8, 1024, device="cuda")
+        assert not ndtnet._hip_fc(t, g), case
+        x = torch.randn(8, 3, 200, device="cuda")
+        ref = copy.deepcopy(t)
+        out = t(x)
+        out.sum().backward()
+        with torch.no_grad():
+            h = ref.relu(ref.bn4(ref.fc1(ndtnet._block_pool(ref.conv3, ref.bn3, ndtnet._block(
+                ref.conv2, ref.bn2, ndtnet._block(ref.conv1, ref.bn1, x, True), True), True))))
+            h = ref.relu(ref.bn5(ref.fc2(h)))
+            expect = (ref.fc3(h) + torch.eye(3, device="cuda").reshape(1, -1)).view(-1, 3, 3)
+        torch.testing.assert_close(out, expect, rtol=0, atol=1e-4)
+        assert t.fc1.weight.grad is not None and torch.isfinite(t.fc1.weight.grad).all()
+
+
 def test_transform_t_matches_bmm():
     """x^T t2 (ndtnet.py:153-155) on the HIP GEMM against torch's bmm, forward
     and both gradients."""
