@@ -3181,7 +3181,10 @@ __device__ inline uint32_t count_composite(KP K, SP S, uint32_t n, unsigned long
 #define NDNET_MERGE_Q 8
 #endif
 constexpr int kMergeQ = NDNET_MERGE_Q;  // other runs searched together per probe round
-constexpr int kMergeRuns = 2;  // chunks merged per k_kl_merge workgroup (512 threads; ~one workgroup per CU at B = 16)
+#ifndef NDNET_MERGE_RUNS
+#define NDNET_MERGE_RUNS 2
+#endif
+constexpr int kMergeRuns = NDNET_MERGE_RUNS;  // chunks merged per k_kl_merge workgroup (512 threads; ~one workgroup per CU at B = 16)
 // mode 1 (score runs staged whole per workgroup, 144 KB: one workgroup per
 // CU) merges 4 chunks per workgroup: C5's 57-chunk clouds then fit one round
 // of workgroups on the chip instead of two, and stage the runs half as often

@@ -1186,6 +1186,9 @@ __global__ void __launch_bounds__(kThreads) k_pn_chain(ndnet_pn_chain A, int pla
     } else {
       __syncthreads();
     }
+#elif defined(NDNET_PN_LBAR)  // A/B: the layer barrier without the vmcnt drain, no prefetch
+    if (l + 1 < A.num_layers) layer_barrier();
+    else __syncthreads();
 #else
     __syncthreads();
 #endif
