@@ -50,6 +50,9 @@ PIPE_FWD_STREAMS = int(os.environ.get("NDNET_PIPE_FWD_STREAMS", "3"))
 # 53.2k clouds/s, but U 83k -> 79k and C5 26.0k -> 25.7k, so 1 by default
 # (profiles/r03ah_ndt_streams.txt)
 PIPE_NDT_STREAMS = int(os.environ.get("NDNET_PIPE_NDT_STREAMS", "1"))
+# k_welford_q's light form for the plans of a pipeline with more than one NDT
+# stream ("quad", "light64" or "auto": by the CU share, light64 here)
+PIPE_WQ_FORM_MULTI = os.environ.get("NDNET_PIPE_WQ_FORM_MULTI", "quad")
 # Stream priorities: "none" (default), "fwd" (the forward streams high, so the
 # TNet heads' few workgroups are dispatched ahead of k_front / chain
 # workgroups queued on the other streams) or "ndt".  Measured
@@ -267,6 +270,12 @@ class PipelinedSegmentation:
                     plan.set_path(1)
                     applied = 0
             self.front_share.append(applied)  # 0: the one-launch-per-stage path
+            if N > 1 and PIPE_WQ_FORM_MULTI != "auto":
+                # two NDT streams (the L clouds' pipeline): k_welford_q's lane-quad
+                # form, not light64 -- L 66.0k vs 65.1k clouds/s, while one NDT
+                # stream keeps light64 (U 89.2k vs 87.3k with quads):
+                # profiles/r06j_welford_form_ab.txt
+                plan.set_welford_form(PIPE_WQ_FORM_MULTI)
         # stream priorities (NDNET_PIPE_PRIORITY): none by default, see PIPE_PRIORITY
         hi = torch.cuda.Stream.priority_range()[1] if PIPE_PRIORITY != "none" else 0
         self.s_ndts = [torch.cuda.Stream(device=dev, priority=hi if PIPE_PRIORITY == "ndt" else 0) for _ in range(N)]
