@@ -268,6 +268,7 @@ def main() -> None:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         out = run_steps(args.steps)
+        t_enq = time.perf_counter() - t0  # host time to enqueue the K steps (diagnostic)
         torch.cuda.synchronize()
         D.barrier()
         torch.cuda.synchronize()
@@ -715,6 +716,7 @@ def main() -> None:
             "warmup": args.warmup,
             "settle": {"ms": args.settle_ms, "steps": n_settle},
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

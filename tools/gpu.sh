@@ -69,7 +69,7 @@ suite)
   step bench 300 $OUT/bench.log python -u bench.py
   line bench $OUT/bench.log
   step bench2 400 $OUT/bench_2ranks.log python -u bench.py --gpus 2 --dist-backend gloo --steps 20 --warmup 5 \
-    --no-cpu-baseline --no-other
+    --no-cpu-baseline
   tail -1 $OUT/bench_2ranks.log | cut -c1-300
   ;;
 tests)
