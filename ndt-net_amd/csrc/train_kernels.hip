@@ -419,6 +419,33 @@ struct ChanWalk {
   __device__ int64_t off(int C, int N, int c) const { return ((int64_t)b * C + c) * N + n; }
 };
 
+// Round 6: the channel walked four points at a time (N % 4 == 0, 16-byte aligned
+// rows: every [B][C][N] activation of the model at N = 1000), one 16-byte load
+// or store per thread and step instead of four 4-byte ones.  Element (b, n4 * 4 + k)
+// of the float4 index q = tid + T i.  NDNET_TR_BN_VEC=0 keeps the scalar walk (A/B).
+template <int T>
+struct ChanWalk4 {
+  int b, n4;  // cloud, float4 index in the cloud's row of N / 4
+  __device__ explicit ChanWalk4(int N4) : b(0), n4(threadIdx.x) { fold(N4); }
+  __device__ void fold(int N4) {
+    while (n4 >= N4) {
+      n4 -= N4;
+      b++;
+    }
+  }
+  __device__ void next(int N4) {
+    n4 += T;
+    fold(N4);
+  }
+  __device__ int64_t off(int C, int N, int c) const { return ((int64_t)b * C + c) * N + 4 * (int64_t)n4; }
+};
+#ifndef NDNET_TR_BN_VEC
+#define NDNET_TR_BN_VEC 1
+#endif
+__device__ inline bool bn_vec_ok(int N, const void* a, const void* b2) {
+  return NDNET_TR_BN_VEC && N % 4 == 0 && ((((uintptr_t)a) | ((uintptr_t)b2)) & 15u) == 0;
+}
+
 // the normalised, affine value: one rounding per operation (no contraction), so
 // the backward's ReLU mask recomputed from y equals the forward's output sign
 __device__ __forceinline__ float bn_apply(float v, float fm, float inv, float g, float bt) {
@@ -443,6 +470,81 @@ __global__ __launch_bounds__(T) void k_tr_bn_fwd(const float* __restrict__ y, fl
   const int64_t M = (int64_t)Bn * N;
   const bool cached = M <= (int64_t)kBnValues;
   if (pool && threadIdx.x < Bn) pk[threadIdx.x] = 0ull;  // ordered before use by block_sum's barriers
+  if (cached && bn_vec_ok(N, y, pool ? (const void*)y : (const void*)z)) {
+    constexpr int kC4 = kCache / 4;
+    const int N4 = N / 4;
+    f32x4 v4[kC4];
+    double s = 0.0;
+    {
+      ChanWalk4<T> w(N4);
+#pragma unroll
+      for (int i = 0; i < kC4; i++, w.next(N4)) v4[i] = w.b < Bn ? *reinterpret_cast<const f32x4*>(y + w.off(C, N, c))
+                                                              : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < kC4; i++) s += ((double)v4[i][0] + (double)v4[i][1]) + ((double)v4[i][2] + (double)v4[i][3]);
+    const double mu = block_sum<T>(s, red) / (double)M;
+    double s2 = 0.0;
+    {
+      ChanWalk4<T> w(N4);
+#pragma unroll
+      for (int i = 0; i < kC4; i++, w.next(N4)) {
+        if (w.b < Bn) {
+          const double d0 = (double)v4[i][0] - mu, d1 = (double)v4[i][1] - mu;
+          const double d2 = (double)v4[i][2] - mu, d3 = (double)v4[i][3] - mu;
+          s2 += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+        }
+      }
+    }
+    const double var = block_sum<T>(s2, red) / (double)M;
+    const float inv = (float)(1.0 / sqrt(var + (double)eps));
+    if (threadIdx.x == 0) {
+      mean[c] = (float)mu;
+      invstd[c] = inv;
+      if (rmean) rmean[c] = (1.0f - momentum) * rmean[c] + momentum * (float)mu;
+      if (rvar) {
+        const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+        rvar[c] = (1.0f - momentum) * rvar[c] + momentum * (float)unb;
+      }
+    }
+    const float fm = (float)mu, g = gamma[c], bt = beta[c];
+    ChanWalk4<T> w(N4);
+#pragma unroll
+    for (int i = 0; i < kC4; i++, w.next(N4)) {
+      if (w.b >= Bn) continue;
+      f32x4 o;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        o[k] = bn_apply(v4[i][k], fm, inv, g, bt);
+        if (relu) o[k] = fmaxf(o[k], 0.0f);
+      }
+      if (!pool) {
+        *reinterpret_cast<f32x4*>(z + w.off(C, N, c)) = o;
+        continue;
+      }
+      // the float4's first maximum (the smallest point among equal values), one
+      // LDS atomic per float4: (ordered value bits, ~point) keys
+      unsigned long long best = 0ull;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const unsigned u = __float_as_uint(o[k]);
+        const unsigned key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+        const unsigned long long kk = ((unsigned long long)key << 32) | (0xFFFFFFFFu - (unsigned)(4 * w.n4 + k));
+        best = kk > best ? kk : best;
+      }
+      atomicMax(&pk[w.b], best);
+    }
+    if (!pool) return;
+    __syncthreads();
+    if (threadIdx.x < Bn) {
+      const unsigned long long k = pk[threadIdx.x];
+      const unsigned key = (unsigned)(k >> 32);
+      const unsigned u = (key & 0x80000000u) ? (key & 0x7FFFFFFFu) : ~key;
+      pool[(int64_t)threadIdx.x * C + c] = __uint_as_float(u);
+      pool_idx[(int64_t)threadIdx.x * C + c] = (int)(0xFFFFFFFFu - (unsigned)(k & 0xFFFFFFFFu));
+    }
+    return;
+  }
   float v[kCache];
   double s = 0.0;
   if (cached) {
@@ -568,6 +670,68 @@ __global__ __launch_bounds__(T) void k_tr_bn_bwd(const float* __restrict__ dz, c
   // g = dz where the forward's output was > 0 (ReLU), xhat = (y - mean) invstd;
   // pool mode: dz is [B][C], the gradient of the max over points, all of it at
   // the forward's first maximum
+  if (cached && bn_vec_ok(N, y, dy) && (pool_idx || (((uintptr_t)dz) & 15u) == 0)) {
+    constexpr int kC4 = kCache / 4;
+    const int N4 = N / 4;
+    f32x4 g4[kC4], x4[kC4];
+    {
+      ChanWalk4<T> w(N4);
+#pragma unroll
+      for (int i = 0; i < kC4; i++, w.next(N4)) {
+        f32x4 yv = {0.f, 0.f, 0.f, 0.f}, gz = {0.f, 0.f, 0.f, 0.f};
+        if (w.b < Bn) {
+          const int64_t off = w.off(C, N, c);
+          yv = *reinterpret_cast<const f32x4*>(y + off);
+          if (!pool_idx) gz = *reinterpret_cast<const f32x4*>(dz + off);
+        }
+        x4[i] = yv;  // y for now: the loads of every step issued together
+        g4[i] = gz;
+      }
+    }
+    {
+      ChanWalk4<T> w(N4);
+#pragma unroll
+      for (int i = 0; i < kC4; i++, w.next(N4)) {
+        f32x4 g = g4[i], xh;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const float yv = x4[i][k];
+          if (pool_idx) g[k] = (w.b < Bn && 4 * w.n4 + k == s_pidx[w.b]) ? s_pdz[w.b] : 0.0f;
+          if (relu && !(bn_apply(yv, mu, inv, gm, bt) > 0.0f)) g[k] = 0.0f;
+          xh[k] = (yv - mu) * inv;
+          if (w.b >= Bn) g[k] = xh[k] = 0.0f;
+        }
+        g4[i] = g;
+        x4[i] = xh;
+        sg += ((double)g[0] + (double)g[1]) + ((double)g[2] + (double)g[3]);
+        sgx += ((double)g[0] * xh[0] + (double)g[1] * xh[1]) + ((double)g[2] * xh[2] + (double)g[3] * xh[3]);
+      }
+    }
+    sg = block_sum<T>(sg, red);
+    sgx = block_sum<T>(sgx, red);
+    const float k1 = (float)(sg / (double)M), k2 = (float)(sgx / (double)M);
+    const float scale = gm * inv;
+    double sdy = 0.0;
+    {
+      ChanWalk4<T> w(N4);
+#pragma unroll
+      for (int i = 0; i < kC4; i++, w.next(N4)) {
+        if (w.b >= Bn) continue;
+        f32x4 d;
+#pragma unroll
+        for (int k = 0; k < 4; k++) d[k] = scale * (g4[i][k] - k1 - x4[i][k] * k2);
+        *reinterpret_cast<f32x4*>(dy + w.off(C, N, c)) = d;
+        sdy += ((double)d[0] + (double)d[1]) + ((double)d[2] + (double)d[3]);
+      }
+    }
+    sdy = block_sum<T>(sdy, red);
+    if (threadIdx.x == 0) {
+      if (dgamma) dgamma[c] = (float)sgx;
+      if (dbeta) dbeta[c] = (float)sg;
+      if (dbias) dbias[c] = (float)sdy;
+    }
+    return;
+  }
   auto grad_at = [&](const ChanWalk<T>& w, float& xh) {
     const int64_t off = w.off(C, N, c);
     const float yv = y[off];
