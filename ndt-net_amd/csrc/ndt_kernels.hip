@@ -3208,7 +3208,9 @@ __device__ inline void merge_runs(const KLArgs& A, const int b) {
   const uint64_t eb = (uint64_t)b * A.ecap, kb = (uint64_t)b * A.sortcap, cb = (uint64_t)b * A.nchunk;
   const uint32_t tid = threadIdx.x;
   const uint32_t lc = tid / kChunk, t = tid % kChunk;
-  const uint32_t ch = blockIdx.x * kMergeRuns + lc;
+  // chunk groups blockIdx.x, blockIdx.x + gridDim.x, ...: a plan with a CU
+  // share gives the merge fewer, longer workgroups (round 6, merge_wgs)
+  uint32_t ch = blockIdx.x * kMergeRuns + lc;
 #define MERGE_MARK(i)                                                                              \
   do {                                                                                             \
     if (A.marks && blockIdx.x == 0 && tid == 0) A.marks[(uint64_t)b * kKLMarks + (i)] = __builtin_amdgcn_s_memrealtime(); \
@@ -3272,7 +3274,6 @@ __device__ inline void merge_runs(const KLArgs& A, const int b) {
   }
   if (!kLds && tid == 0) s_nb[nch] = A.chunk_nanbase[cb + nch - 1] + (A.chunk_cnt[cb + nch - 1] & 0xffffu);  // NaN total
   const unsigned long long* gN = A.nan_key_all + eb;
-  if (ch < nch) s_own_num_slot[lc][t] = A.sort_idx_all[kb + ch * kChunk + t];
   if (kLds) {
     ulonglong2* dst = reinterpret_cast<ulonglong2*>(lK);
 #pragma unroll
@@ -3313,10 +3314,6 @@ __device__ inline void merge_runs(const KLArgs& A, const int b) {
     MERGE_MARK(17);
   }
   const uint32_t nnan_tot = s_nb[nch];
-  const uint32_t cc = ch < nch ? s_cnt[ch] : 0u;
-  const uint32_t nnum = cc >> 16, nnan = cc & 0xffffu;
-  const uint32_t nb0 = ch < nch ? s_nb[ch] : 0u;
-  if (t < nnan) s_own_nan_slot[lc][t] = kLds ? own_nan : A.nan_slot_all[eb + nb0 + t];
   // mode 1: the NaN keys (from k_kl_nan_keys) join the score runs in LDS when they fit
   const bool nan_lds = kMode == 1 && (uint64_t)nch * kChunk + nnan_tot <= A.merge_lds_keys;
   if (nan_lds) {
@@ -3338,9 +3335,20 @@ __device__ inline void merge_runs(const KLArgs& A, const int b) {
   }
   __syncthreads();
   MERGE_MARK(13);
-  if (ch >= nch) return;
+  for (uint32_t grp = blockIdx.x; grp * kMergeRuns < nch; grp += gridDim.x) {
+  ch = grp * kMergeRuns + lc;
+  if (grp != blockIdx.x) {
+    __syncthreads();  // the previous group's slot tables are read
+    if (kLds && ch < nch) own_nan = A.nan_list_all[eb + ch * kChunk + t];
+  }
+  const uint32_t cc = ch < nch ? s_cnt[ch] : 0u;
+  const uint32_t nnum = cc >> 16, nnan = cc & 0xffffu;
+  const uint32_t nb0 = ch < nch ? s_nb[ch] : 0u;
+  if (ch < nch) s_own_num_slot[lc][t] = A.sort_idx_all[kb + ch * kChunk + t];
+  if (ch < nch && t < nnan) s_own_nan_slot[lc][t] = kLds ? own_nan : A.nan_slot_all[eb + nb0 + t];
+  __syncthreads();
   const bool is_num = t < nnum;
-  if (!is_num && t >= nnum + nnan) return;
+  if (ch >= nch || (!is_num && t >= nnum + nnan)) continue;
   const uint32_t* own_num_slot = s_own_num_slot[lc];
   const uint32_t* own_nan_slot = s_own_nan_slot[lc];
   auto body = [&](auto K, auto N) {
@@ -3394,6 +3402,7 @@ __device__ inline void merge_runs(const KLArgs& A, const int b) {
     body(static_cast<const unsigned long long*>(lK), static_cast<const unsigned long long*>(lN));
   else if (kMode == 1) body(static_cast<const unsigned long long*>(lK), gN);
   else body(gK, gN);
+  }  // chunk groups
   MERGE_MARK(14);
   if (A.marks && t == 0)  // the cloud's last merge workgroup to end
     __hip_atomic_fetch_max(&A.marks[(uint64_t)b * kKLMarks + 19], (unsigned long long)__builtin_amdgcn_s_memrealtime(),
@@ -3684,12 +3693,28 @@ __global__ void __launch_bounds__(256) k_kl_chains(KLArgs A) {
 constexpr size_t kKLFusedLds = kMergeScoreChunks * kChunk * sizeof(unsigned long long);  // 144 KB
 static size_t kl_lds_bytes(const Plan* P);
 
+// Merge workgroups per cloud for chunk groups of `runs` chunks: one per group,
+// or at a CU share s > 1 (a pipeline's plan) 1 / s of that, each workgroup
+// taking several groups after one staging of the runs: the merge's workgroups
+// hold a CU each (110 KB of LDS at C2-L) and no chain workgroup fits beside
+// them, so a pipeline trades the merge's latency for its CU footprint.
+// NDNET_MERGE_SHARE (A/B, read once): 1 = one workgroup per group always.
+static uint32_t merge_grid(const Plan* P, uint32_t runs) {
+  static const int env = [] {
+    const char* e = getenv("NDNET_MERGE_SHARE");
+    return e ? atoi(e) : 0;
+  }();
+  const uint32_t groups = (P->nchunk + runs - 1) / runs;
+  const uint32_t share = env > 0 ? (uint32_t)env : (P->cu_share > 1 ? (uint32_t)P->cu_share : 1u);
+  return (groups + share - 1) / share;
+}
+
 // tail: the merge's last workgroup per cloud also prunes and emits the rows
 // (k_kl's work; the caller checked kl_fusable).
 static void launch_list_sort(Plan* P, const KLArgs& A, hipStream_t st, bool tail = false) {
   const int B = P->B;
   k_kl_rank_chunks<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
-  const uint32_t mg = (P->nchunk + kMergeRuns - 1) / kMergeRuns;
+  const uint32_t mg = merge_grid(P, kMergeRuns);
   const size_t kl = tail ? kl_lds_bytes(P) : 0;
   auto dyn = [&](size_t m) { return m > kl ? m : kl; };
   if (P->nchunk <= (uint32_t)kMergeLdsChunks) {  // the merge computes the NaN keys itself
@@ -3700,7 +3725,7 @@ static void launch_list_sort(Plan* P, const KLArgs& A, hipStream_t st, bool tail
     KLArgs A1 = A;
     const size_t keys = kMergeScoreChunks * kChunk;  // the launch's dynamic LDS, in 64-bit keys (144 KB)
     A1.merge_lds_keys = (uint32_t)keys;
-    const uint32_t mg1 = (P->nchunk + kMergeRuns1 - 1) / kMergeRuns1;
+    const uint32_t mg1 = merge_grid(P, kMergeRuns1);
     if (tail)
       k_kl_merge<1, kMergeRuns1, true><<<dim3(mg1, B), kChunk * kMergeRuns1, dyn(keys * sizeof(unsigned long long)),
                                           st>>>(A1);

@@ -609,6 +609,43 @@ def test_merge_paths_match_oracle(k):
         assert np.array_equal(p[b], pc) and np.array_equal(c[b], cov)
 
 
+@pytest.mark.parametrize("k", [1000, 2000, 2600])
+def test_merge_grid_stride_equals_one_group_per_workgroup(k):
+    """Round 6: a plan at CU share s runs k_kl_merge on ceil(groups / s)
+    workgroups per cloud, each merging several chunk groups after one staging
+    of the runs (merge_grid, csrc/ndt_kernels.hip).  All three merge forms (k =
+    1000: runs and NaN keys in LDS; 2000: runs in LDS; 2600: global memory)
+    at share 2 (two chunk groups per workgroup) against the share-1 plan (one workgroup per group): rows,
+    stats and every dumped list entry identical, on L clouds whose prune
+    removes NDs (the lists built eagerly)."""
+    import torch
+    from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
+    from ndnet.synthetic import make_batch
+    B, n = 16, 60_000
+    pts = torch.from_numpy(make_batch("L", B, n, seed0=70)).cuda()
+    res = []
+    for share in (1, 2):
+        plan = NdtPlan(B, n, k, -1)
+        plan.set_lazy_list(False)
+        if share > 1:
+            plan.set_cu_share(share)
+        out = torch.empty((B, k, 12), dtype=torch.float32, device="cuda")
+        plan.run(pts, None, out, None)
+        torch.cuda.synchronize()
+        st = plan.host_stats()
+        assert all(x.rc == 0 for x in st), (share, [x.rc for x in st])
+        dumps = [_dump(plan, b, int(st[b].num_nds), int(st[b].num_events)) for b in range(B)]
+        res.append((out.cpu().numpy(), [bytes(x) for x in st], dumps))
+        del plan
+    o0, s0, d0 = res[0]
+    assert any(x.num_nds > k for x in st)
+    for o, s_, d in res[1:]:
+        assert np.array_equal(o, o0) and s_ == s0
+        for b in range(B):
+            for key in ("ord_val", "ord_p", "ord_q", "alive"):
+                assert np.array_equal(d[b][key], d0[b][key], equal_nan=True), (b, key)
+
+
 def test_front_staged_scatter_active_at_c2():
     """The staged scatter actually runs for the C2 shape at CU share 1
     (16 x 100k points -> 1000 NDs): round 3's u16 histograms had shrunk the
