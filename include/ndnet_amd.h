@@ -266,6 +266,17 @@ int ndnet_ndt_debug_set_epoch(void *plan, uint32_t epoch);
  * turns it off) or on a k_kl launch of their own (0).  Same outputs either way. */
 int ndnet_ndt_debug_set_kl_fuse(void *plan, int on);
 
+/* The event list's sort (round 6): 1 sorts each cloud's list on one
+ * workgroup (k_kl_sort) when the plan's list fits its LDS (ecap <= 7680 slots,
+ * k <= 1065), else on k_kl_merge's workgroups per chunk group; 0 always takes
+ * k_kl_merge; 2 (the default; NDNET_KL_SORT in the environment at plan
+ * creation overrides it) takes k_kl_sort only at a CU share > 1
+ * (ndnet_ndt_set_cu_share: a pipeline's plan, where the merge's CU time
+ * matters more than its latency).  Same lists, rows and stats either way.
+ * _get_ returns 1 when the plan's runs take k_kl_sort, 0 for k_kl_merge. */
+int ndnet_ndt_debug_set_list_sort(void *plan, int on);
+int ndnet_ndt_debug_get_list_sort(void *plan);
+
 /* KL-stage phase stamps of the last run at timing level 2: marks[cloud * 32 + i],
  * 100 MHz s_memrealtime ticks.  k_kl: 0 start, 1 cloud state checked, 2 event
  * count, 5 list initialised, 6 first occurrences, 7 walk scan, 8 kills, 9 shift,

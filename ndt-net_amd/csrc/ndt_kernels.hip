@@ -188,6 +188,7 @@ struct Plan {
   uint32_t* wq_ctr;           // [8][16] k_welford_q dynamic item counters, one per XCD (re-armed by k_kl_rank_chunks)
   int eager_list;             // build every cloud's retained list in the run (ndnet_ndt_set_lazy_list(plan, 0))
   int kl_fuse;                // the run's prune rides on the merge launch (kl_fusable; NDNET_KL_FUSE=0: k_kl)
+  int list_sort;              // 2 (auto): k_kl_sort at a CU share > 1 where the list fits (sort_fits); 1: wherever it fits; 0: k_kl_merge (NDNET_KL_SORT)
   uint64_t front_sync_ticks;  // k_front's cloud-barrier timeout (ndnet_ndt_debug_set_sync_timeout)
   int lists_built;            // the deferred lists of the last run are built (no further build launches)
   int front_staged;           // k_front's scatter through LDS records (ndnet_ndt_set_front_staged; default 1)
@@ -3533,6 +3534,301 @@ __global__ void __launch_bounds__(kChunk * kMergeRuns) k_kl_merge(KLArgs A) {
   }
 }
 
+// ------------------------------------------------- the one-workgroup list sort
+// Round 6: when a cloud's whole event list fits one CU's
+// LDS twice -- 20 bytes per slot (64-bit key + 16-bit slot, two buffers):
+// ecap <= 7680, i.e. k <= 1065, C2's k = 1000 -- one workgroup per cloud
+// sorts it instead of merge_runs' workgroups per chunk group.  The total
+// order is the composite (key, slot) of merge_runs (above): k_kl_rank_chunks'
+// chunk runs are sorted by it, and so is the NaN run (keys non-decreasing in
+// slot order).  The score runs are merged pairwise in LDS, log2(chunks)
+// levels; two adjacent runs hold ordered slot ranges, so a tie against the
+// run below counts and one against the run above does not -- the key alone
+// decides, and an element's chunk (its group at every level) is its slot / 256.
+// The last level merges the score list with the NaN run comparing (key, slot).
+// Each element does ~9-13 fixed halving probes per level (6 levels at C2:
+// ~70 in all) where merge_runs does ~8 per other chunk plus three NaN-run
+// searches (~250), and the launch holds 16 CUs instead of the merge's ~110-224:
+// the L line's KL stage is CU time the chains share.
+constexpr uint32_t kSortMaxChunks = 64;          // the offsets are one wave's scan
+static_assert(kKLThreads == 1024, "k_kl_sort's item loops assume 1024 threads");
+
+// One buffer of the sort: the 64-bit keys and the slots.
+struct SortBuf {
+  unsigned long long* k;
+  uint16_t* s;
+};
+
+// pos[q]: keys of the sorted run [st[q], st[q] + n[q]) below xq[q], `rounds`
+// halving probes (2^rounds > every n).  A probe past the run reads its last
+// key instead: if that is below xq the whole run is, and pos lands on n, so
+// the bound needs no test of its own -- a probe is an add, a min, the address,
+// one 8-byte LDS read, a 64-bit compare and a select (the kernel is VALU-issue
+// bound: 4 cycles per wave64 op on a SIMD).  An empty run (n = 0) counts 0.
+template <int Q>
+__device__ inline void run_count_q(const unsigned long long* K, const uint32_t (&st)[Q], const uint32_t (&n)[Q],
+                                   const unsigned long long (&xq)[Q], int rounds, uint32_t (&pos)[Q]) {
+  const unsigned long long* base[Q];
+  unsigned long long xe[Q];
+#pragma unroll
+  for (int q = 0; q < Q; q++) {
+    pos[q] = 0;
+    base[q] = K + (n[q] ? st[q] - 1 : 0u);
+    xe[q] = n[q] ? xq[q] : 0ull;
+  }
+  for (int r = rounds - 1; r >= 0; r--) {
+    const uint32_t h = 1u << r;
+    uint32_t m[Q];
+    unsigned long long k[Q];
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+      m[q] = min(pos[q] + h, n[q]);
+      k[q] = base[q][m[q]];
+    }
+#pragma unroll
+    for (int q = 0; q < Q; q++) pos[q] = k[q] < xe[q] ? m[q] : pos[q];
+  }
+}
+
+__device__ inline int bit_len(uint32_t v) { return v ? 32 - __clz(v) : 0; }
+
+// One merge level over elements [e0, e0 + Q * 1024) of the score list: runs of
+// 2^l chunks merged pairwise from I into O (an element's group: slot / 256 >> l;
+// against the run below it counts keys <= x, i.e. < x + 1: score keys are
+// never ~0)
+template <int Q>
+__device__ inline void sort_level_items(const SortBuf& I, const SortBuf& O, const uint32_t* soff, uint32_t nch,
+                                        uint32_t l, uint32_t S, int rounds, uint32_t e0) {
+  unsigned long long x[Q], xq[Q];
+  uint32_t sl[Q], st[Q], n[Q], dst[Q], pos[Q];
+#pragma unroll
+  for (int q = 0; q < Q; q++) {
+    const uint32_t e = e0 + q * kKLThreads + threadIdx.x;
+    const uint32_t ec = e < S ? e : 0u;
+    x[q] = I.k[ec];
+    sl[q] = I.s[ec];
+    const uint32_t g = (sl[q] / kChunk) >> l, p = g ^ 1u;
+    const uint32_t lp = p << l, lm = (g < p ? g : p) << l;
+    dst[q] = soff[lm] + (e - soff[g << l]);
+    xq[q] = p < g ? x[q] + 1 : x[q];
+    st[q] = 0;
+    n[q] = 0;
+    if (e < S && lp < nch) {
+      st[q] = soff[lp];
+      n[q] = soff[lp + (1u << l) < nch ? lp + (1u << l) : nch] - st[q];
+    }
+  }
+  run_count_q<Q>(I.k, st, n, xq, rounds, pos);
+#pragma unroll
+  for (int q = 0; q < Q; q++) {
+    if (e0 + q * kKLThreads + threadIdx.x < S) {
+      O.k[dst[q] + pos[q]] = x[q];
+      O.s[dst[q] + pos[q]] = (uint16_t)sl[q];
+    }
+  }
+}
+
+// The last level over elements [e0, e0 + Q * 1024) of [0, S + NN): the score
+// list with the NaN run (a score counts the NaNs ahead of it, a NaN the
+// scores) in the composite order: keys below x, then the partner's entries of
+// key x at lower slots (its equal keys are in slot order; a NaN's key, a
+// prefix minimum, usually equals one score's), then each element's list entry
+// (ndt.c's kl_divergences row: value, p, q) at its final position
+template <int Q>
+__device__ inline void sort_final_items(const KLArgs& A, int b, const SortBuf& I, uint32_t S, uint32_t NN, int rounds,
+                                        uint32_t e0) {
+  const uint64_t eb = (uint64_t)b * A.ecap;
+  const uint32_t E = S + NN;
+  unsigned long long x[Q];
+  uint32_t xs[Q], st[Q], n[Q], pos[Q];
+#pragma unroll
+  for (int q = 0; q < Q; q++) {
+    const uint32_t e = e0 + q * kKLThreads + threadIdx.x;
+    const uint32_t ec = e < E ? e : 0u;
+    x[q] = I.k[ec];
+    xs[q] = I.s[ec];
+    st[q] = e < S ? S : 0u;
+    n[q] = e >= E ? 0u : e < S ? NN : S;
+  }
+  run_count_q<Q>(I.k, st, n, x, rounds, pos);
+#pragma unroll
+  for (int q = 0; q < Q; q++)
+    while (pos[q] < n[q] && I.k[st[q] + pos[q]] == x[q] && I.s[st[q] + pos[q]] < xs[q]) pos[q]++;
+  double ov[Q];
+  uint32_t oq[Q];
+#pragma unroll
+  for (int q = 0; q < Q; q++) {
+    const uint32_t e = e0 + q * kKLThreads + threadIdx.x;
+    pos[q] += e < S ? e : e - S;
+    if (e < E) {
+      ov[q] = A.slot_val_all[eb + xs[q]];
+      oq[q] = (uint32_t)A.nb_all[6 * (uint64_t)b * A.ndcap + xs[q]];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < Q; q++) {
+    if (e0 + q * kKLThreads + threadIdx.x < E) {
+      A.ord_val_all[eb + pos[q]] = ov[q];
+      A.ord_p_all[eb + pos[q]] = xs[q] / 6;
+      A.ord_q_all[eb + pos[q]] = oq[q];
+    }
+  }
+}
+
+// count elements in passes of up to 6 per thread (a uniform switch: count is
+// the workgroup's), f.template operator()<Q>(e0)
+template <typename F>
+__device__ inline void for_items(uint32_t count, F&& f) {
+  uint32_t nq = (count + kKLThreads - 1) / kKLThreads, e0 = 0;
+  while (nq) {
+    const uint32_t q = nq < 6 ? nq : 4;
+    switch (q) {
+      case 1: f(std::integral_constant<int, 1>{}, e0); break;
+      case 2: f(std::integral_constant<int, 2>{}, e0); break;
+      case 3: f(std::integral_constant<int, 3>{}, e0); break;
+      case 4: f(std::integral_constant<int, 4>{}, e0); break;
+      default: f(std::integral_constant<int, 5>{}, e0); break;
+    }
+    e0 += q * kKLThreads;
+    nq -= q;
+  }
+}
+
+__device__ void sort_cloud(const KLArgs& A, const int b) {
+  const CloudCtl& c = A.ctl[b];
+  const uint32_t nch = (6 * c.num_nds + kChunk - 1) / kChunk;
+  const uint64_t eb = (uint64_t)b * A.ecap, kb = (uint64_t)b * A.sortcap, cb = (uint64_t)b * A.nchunk;
+  const uint32_t tid = threadIdx.x;
+  if (A.marks && tid == 0) A.marks[(uint64_t)b * kKLMarks + 12] = __builtin_amdgcn_s_memrealtime();
+  extern __shared__ __attribute__((aligned(16))) unsigned long long dyn_sort[];
+  const uint32_t ec = A.ecap;
+  SortBuf B0{dyn_sort, reinterpret_cast<uint16_t*>(dyn_sort + 2 * ec)};
+  SortBuf B1{dyn_sort + ec, reinterpret_cast<uint16_t*>(dyn_sort + 2 * ec) + ec};
+  __shared__ uint32_t s_soff[kSortMaxChunks + 1], s_noff[kSortMaxChunks + 1], s_cnt[kSortMaxChunks];
+  __shared__ double s_pm[kSortMaxChunks];
+  __shared__ uint32_t s_maxrun[8];
+  // every slot of the chunks' runs and NaN lists loaded in one round (the
+  // counts arrive with them), placed once the offsets are known
+  constexpr int U = (kSortMaxChunks * kChunk / 2 + kKLThreads - 1) / kKLThreads;  // 7680 slots at most: 8 rounds
+  const uint32_t nslot = nch * kChunk;
+  unsigned long long key[U];
+  uint32_t sidx[U], nsl[U];
+  double emin[U];
+  uint32_t cc = 0;
+  double cm = __builtin_inf();
+  if (tid < nch) {
+    cc = A.chunk_cnt[cb + tid];
+    cm = A.chunk_min[cb + tid];
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const uint32_t i = u * kKLThreads + tid;
+    const uint32_t ie = i < ec ? i : ec - 1;
+    if (i < nslot) {
+      key[u] = A.sort_key_all[kb + i];
+      sidx[u] = A.sort_idx_all[kb + i];
+      nsl[u] = A.nan_list_all[eb + ie];
+      emin[u] = A.ev_min_all[eb + ie];
+    }
+  }
+  if (tid < 64) {  // score and NaN offsets, the min over earlier chunks (nch <= 64)
+    uint32_t nn = cc;  // (scores << 16) | NaNs, both < 2^16
+    double m = cm;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t o = __shfl_up(nn, off, 64);
+      const double om = __shfl_up(m, off, 64);
+      if ((int)tid >= off) {
+        nn += o;
+        m = MinF64()(m, om);
+      }
+    }
+    uint32_t ex = __shfl_up(nn, 1, 64);
+    double exm = __shfl_up(m, 1, 64);
+    if (tid == 0) {
+      ex = 0;
+      exm = __builtin_inf();
+    }
+    if (tid < nch) {
+      s_soff[tid] = ex >> 16;
+      s_noff[tid] = ex & 0xffffu;
+      s_pm[tid] = exm;
+      s_cnt[tid] = cc;
+    }
+    if (tid + 1 == nch) {
+      s_soff[nch] = nn >> 16;
+      s_noff[nch] = nn & 0xffffu;
+    }
+    if (tid < 8) s_maxrun[tid] = 0;
+  }
+  __syncthreads();
+  const uint32_t S = s_soff[nch], NN = s_noff[nch];
+  // each level's probe count from its longest run (not the 256 << l a run may
+  // hold): thread 64 l + g measures group g of level l (2^l chunks), read
+  // after the placement's barrier
+  if (tid < 7 * 64) {
+    const uint32_t l = tid / 64, g = tid % 64, c0 = g << l;
+    if (c0 < nch) {
+      const uint32_t c1 = c0 + (1u << l) < nch ? c0 + (1u << l) : nch;
+      atomicMax(&s_maxrun[l], s_soff[c1] - s_soff[c0]);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const uint32_t i = u * kKLThreads + tid;
+    if (i < nslot) {
+      const uint32_t ch = i / kChunk, r = i % kChunk, cn = s_cnt[ch];
+      if (r < (cn >> 16)) {
+        const uint32_t o = s_soff[ch] + r;
+        B0.k[o] = key[u];
+        B0.s[o] = (uint16_t)sidx[u];
+      }
+      if (r < (cn & 0xffffu)) {  // the NaN run sits after the scores in both buffers
+        const uint32_t o = S + s_noff[ch] + r;
+        const unsigned long long nk = score_key(MinF64()(s_pm[ch], emin[u]));
+        B0.k[o] = B1.k[o] = nk;
+        B0.s[o] = B1.s[o] = (uint16_t)nsl[u];
+      }
+    }
+  }
+  __syncthreads();
+  if (A.marks && tid == 0) A.marks[(uint64_t)b * kKLMarks + 16] = __builtin_amdgcn_s_memrealtime();
+  SortBuf I = B0, O = B1;
+  for (uint32_t l = 0; (1u << l) < nch; l++) {
+    const int rounds = bit_len(s_maxrun[l < 7 ? l : 6]);
+    for_items(S, [&](auto qc, uint32_t e0) {
+      sort_level_items<decltype(qc)::value>(I, O, s_soff, nch, l, S, rounds, e0);
+    });
+    if (A.marks && tid == 0 && l < 6) A.marks[(uint64_t)b * kKLMarks + 20 + 2 * l] = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();
+    if (A.marks && tid == 0 && l < 6) A.marks[(uint64_t)b * kKLMarks + 21 + 2 * l] = __builtin_amdgcn_s_memrealtime();
+    const SortBuf t = I;
+    I = O;
+    O = t;
+  }
+  if (A.marks && tid == 0) A.marks[(uint64_t)b * kKLMarks + 17] = __builtin_amdgcn_s_memrealtime();
+  const int rounds = bit_len(S > NN ? S : NN);
+  for_items(S + NN, [&](auto qc, uint32_t e0) { sort_final_items<decltype(qc)::value>(A, b, I, S, NN, rounds, e0); });
+  if (A.marks && tid == 0) {
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    A.marks[(uint64_t)b * kKLMarks + 13] = t1;
+    A.marks[(uint64_t)b * kKLMarks + 14] = t1;
+    A.marks[(uint64_t)b * kKLMarks + 19] = t1;
+  }
+}
+
+// One workgroup per cloud: the list sort, then (tail) the prune and the rows
+// on the same workgroup (kl_cloud; the list entries are this workgroup's own
+// stores, drained before the barrier).
+__global__ void __launch_bounds__(kKLThreads) k_kl_sort(KLArgs A, int tail) {
+  const int b = blockIdx.x;
+  const CloudCtl& c = A.ctl[b];
+  if (c.state == kAccepted && !kl_list_skipped(A, c)) sort_cloud(A, b);
+  if (!tail) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  kl_cloud<true>(A, b);
+}
+
 __global__ void __launch_bounds__(kKLThreads) k_prune(KLArgs A) {
   const int b = blockIdx.x;
   CloudCtl& c = A.ctl[b];
@@ -3711,9 +4007,28 @@ static uint32_t merge_grid(const Plan* P, uint32_t runs) {
 
 // tail: the merge's last workgroup per cloud also prunes and emits the rows
 // (k_kl's work; the caller checked kl_fusable).
+// k_kl_sort takes the list when its two key/slot buffers (20 bytes per slot)
+// fit its LDS and its offsets one wave's scan (ecap <= 7680: k <= 1065), and
+// by default only for a plan with a CU share (a pipeline's): one workgroup per
+// cloud sorts in ~23 us what k_kl_merge's ~7-14 workgroups per cloud merge in
+// ~17 us, so a plan alone on the chip keeps the merge (C2 NDT-only on L
+// clouds 87k vs 84k clouds/s), while a pipeline gains the merge's CU time
+// (its 110 KB workgroups hold ~110 CUs): the L line 66.3 / 66.0k vs 65.2 /
+// 65.5k clouds/s (profiles/r06z_list_sort_ab.txt)
+static size_t sort_lds_bytes(const Plan* P) { return 20 * (size_t)P->ecap; }
+static bool sort_fits(const Plan* P) {
+  const bool want = P->list_sort == 1 || (P->list_sort == 2 && P->cu_share > 1);
+  return want && sort_lds_bytes(P) <= (size_t)kKLLdsMax && P->nchunk <= kSortMaxChunks && P->ecap <= 65536;
+}
+
 static void launch_list_sort(Plan* P, const KLArgs& A, hipStream_t st, bool tail = false) {
   const int B = P->B;
   k_kl_rank_chunks<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
+  if (sort_fits(P)) {
+    const size_t kl = tail ? kl_lds_bytes(P) : 0, so = sort_lds_bytes(P);
+    k_kl_sort<<<B, kKLThreads, so > kl ? so : kl, st>>>(A, tail ? 1 : 0);
+    return;
+  }
   const uint32_t mg = merge_grid(P, kMergeRuns);
   const size_t kl = tail ? kl_lds_bytes(P) : 0;
   auto dyn = [&](size_t m) { return m > kl ? m : kl; };
@@ -4212,6 +4527,8 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
   }
   P->kl_fuse = 1;
   if (const char* e = getenv("NDNET_KL_FUSE")) P->kl_fuse = atoi(e) != 0;  // A/B: 0 launches k_kl
+  P->list_sort = 2;
+  if (const char* e = getenv("NDNET_KL_SORT")) P->list_sort = atoi(e);  // A/B: 0 k_kl_merge, 1 k_kl_sort wherever it fits
   if (const char* e = getenv("NDNET_WQ_FORM"))  // A/B: "light64" / "quad" for every plan (default: by CU share)
     P->wq_form = !strcmp(e, "light64") ? 1 : !strcmp(e, "quad") ? 2 : 0;
   const double upper = (double)num_desired * (1 + 0.2);
@@ -4354,6 +4671,7 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
     e = hipFuncSetAttribute((const void*)k_kl_merge<0, kMergeRuns, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)kKLFusedLds);
   if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_kl, hipFuncAttributeMaxDynamicSharedMemorySize, kKLLdsMax);
+  if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_kl_sort, hipFuncAttributeMaxDynamicSharedMemorySize, kKLLdsMax);
   if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_prune, hipFuncAttributeMaxDynamicSharedMemorySize, kKLLdsMax);
   if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_bin_count, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                (int)(16384 * sizeof(uint32_t)));
@@ -4611,6 +4929,20 @@ int ndnet_ndt_debug_set_kl_fuse(void* plan, int on) {
   if (!P) return NDNET_ERR_ARG;
   P->kl_fuse = on ? 1 : 0;
   return NDNET_OK;
+}
+
+int ndnet_ndt_debug_set_list_sort(void* plan, int on) {
+  Plan* P = (Plan*)plan;
+  if (!P) return NDNET_ERR_ARG;
+  if (on < 0 || on > 2) return NDNET_ERR_ARG;
+  P->list_sort = on;
+  return NDNET_OK;
+}
+
+int ndnet_ndt_debug_get_list_sort(void* plan) {
+  const Plan* P = (const Plan*)plan;
+  if (!P) return NDNET_ERR_ARG;
+  return sort_fits(P) ? 1 : 0;
 }
 
 int ndnet_ndt_debug_dump(void* plan, int cloud, uint32_t* nd_n, double* nd_mean, double* nd_cov_pre,

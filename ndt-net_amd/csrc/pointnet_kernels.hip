@@ -31,6 +31,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "../../include/ndnet_pointnet.h"
 
@@ -1283,39 +1284,52 @@ __global__ void __launch_bounds__(256) k_pn_fc(const float* __restrict__ in, int
 #define NDNET_PN_FC_WAVES 8
 #endif
 constexpr int kFcWaves = NDNET_PN_FC_WAVES, kFcMaxG = 64 / kFcWaves;  // K <= 16 * kFcWaves * kFcMaxG = 1024
+// CBW column blocks per workgroup (round 6): a wide, shallow layer (TNet(64)'s
+// fc3, 256 -> 4096: 256 one-block workgroups, ~5 us each, the whole chip for
+// its duration in the pipelined step) runs as 64 four-block workgroups, each
+// wave holding CBW x ng weight fragments (ng * CBW <= kFcMaxG registers'
+// worth, the host checks) -- the same per-column sums in the same order, so
+// the output is bit-identical for every CBW; only the CU-time shrinks.
+template <int CBW>
 __global__ void __launch_bounds__(kFcWaves * 64) k_pn_fc_mfma(const float* __restrict__ in, int ld_in,
                                                               const f32x4* __restrict__ wf,
                                                               const float* __restrict__ bias, float* __restrict__ out,
                                                               int ld_out, int B, int KG, int relu) {
-  __shared__ f32x4 part[kFcWaves][64];
+  constexpr int kG = kFcMaxG / CBW;
+  static_assert(CBW <= kFcWaves && kG >= 1, "one reducing wave per column block");
+  __shared__ f32x4 part[kFcWaves][CBW][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int kq = lane >> 4, cl = lane & 15;
-  const int cb = blockIdx.x;
+  const int cb0 = blockIdx.x * CBW;
   const int kg0 = KG * wave / kFcWaves, ng = KG * (wave + 1) / kFcWaves - kg0;
-  const f32x4* wp = wf + ((int64_t)cb * KG + kg0) * 64 + lane;
   const float* xr = in + (int64_t)(cl < B ? cl : 0) * ld_in + 16 * kg0 + 4 * kq;  // rows past B: discarded
-  f32x4 wv[kFcMaxG], xv[kFcMaxG];
+  f32x4 wv[CBW][kG], xv[kG];
 #pragma unroll
-  for (int i = 0; i < kFcMaxG; i++) {
+  for (int i = 0; i < kG; i++) {
     if (i < ng) {
-      wv[i] = wp[i * 64];
       xv[i] = *reinterpret_cast<const f32x4*>(xr + 16 * i);
+#pragma unroll
+      for (int j = 0; j < CBW; j++) wv[j][i] = wf[((int64_t)(cb0 + j) * KG + kg0 + i) * 64 + lane];
     }
   }
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int i = 0; i < kFcMaxG; i++)
-    if (i < ng)
+  for (int j = 0; j < CBW; j++) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < 4; s++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[i][s], wv[i][s], acc, 0, 0, 0);
-  part[wave][lane] = acc;
+    for (int i = 0; i < kG; i++)
+      if (i < ng)
+#pragma unroll
+        for (int s = 0; s < 4; s++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[i][s], wv[j][i][s], acc, 0, 0, 0);
+    part[wave][j][lane] = acc;
+  }
   __syncthreads();
-  if (wave != 0) return;
-  f32x4 t = part[0][lane];
+  if (wave >= CBW) return;
+  const int j = wave;  // wave j reduces column block cb0 + j over the waves in order
+  f32x4 t = part[0][j][lane];
 #pragma unroll
-  for (int w = 1; w < kFcWaves; w++) t += part[w][lane];
-  // lane (kq, cl): clouds 4 kq + r of column 16 cb + cl
-  const int n = 16 * cb + cl;
+  for (int w = 1; w < kFcWaves; w++) t += part[w][j][lane];
+  // lane (kq, cl): clouds 4 kq + r of column 16 (cb0 + j) + cl
+  const int n = 16 * (cb0 + j) + cl;
   const float bv = bias[n];
 #pragma unroll
   for (int r = 0; r < 4; r++) {
@@ -1599,6 +1613,18 @@ __global__ void __launch_bounds__(kFoldThreads) k_pn_fold(const ndnet_pn_fold_jo
 }
 #endif
 
+#if NDNET_PN_TILE == 64
+int fc_mfma_cbw(int nb, int ngmax) {
+  static const int cap = [] {
+    const char* e = getenv("NDNET_PN_FC_CBW");
+    return e ? atoi(e) : 4;
+  }();
+  for (int c = cap >= 4 ? 4 : cap >= 2 ? 2 : 1; c > 1; c >>= 1)
+    if (nb % c == 0 && nb / c >= 32 && ngmax * c <= kFcMaxG) return c;
+  return 1;
+}
+#endif
+
 }  // namespace
 
 extern "C" {
@@ -1609,8 +1635,18 @@ int ndnet_pn_fc_mfma_run(const float* in, int ld_in, const float* Wf, const floa
   if (!in || !Wf || !bias || !out || batch <= 0 || batch > 16 || K <= 0 || K % 16 || K > 16 * kFcWaves * kFcMaxG ||
       N <= 0 || N % 16 || ld_in % 4 || ld_in < K || ld_out < N || ((uintptr_t)in | (uintptr_t)Wf) % 16)
     return -20;
-  k_pn_fc_mfma<<<N / 16, kFcWaves * 64, 0, (hipStream_t)stream>>>(in, ld_in, reinterpret_cast<const f32x4*>(Wf), bias,
-                                                                   out, ld_out, batch, K / 16, relu);
+  const int KG = K / 16, nb = N / 16, ngmax = (KG + kFcWaves - 1) / kFcWaves;
+  // column blocks per workgroup: 4 while that keeps >= 32 workgroups and the
+  // fragments fit (fc_mfma_cbw; NDNET_PN_FC_CBW=1 restores one block each)
+  const int cbw = fc_mfma_cbw(nb, ngmax);
+  const f32x4* wf = reinterpret_cast<const f32x4*>(Wf);
+  hipStream_t st = (hipStream_t)stream;
+  if (cbw == 4)
+    k_pn_fc_mfma<4><<<nb / 4, kFcWaves * 64, 0, st>>>(in, ld_in, wf, bias, out, ld_out, batch, KG, relu);
+  else if (cbw == 2)
+    k_pn_fc_mfma<2><<<nb / 2, kFcWaves * 64, 0, st>>>(in, ld_in, wf, bias, out, ld_out, batch, KG, relu);
+  else
+    k_pn_fc_mfma<1><<<nb, kFcWaves * 64, 0, st>>>(in, ld_in, wf, bias, out, ld_out, batch, KG, relu);
   return hipGetLastError() == hipSuccess ? 0 : -21;
 }
 

@@ -85,6 +85,8 @@ EXPORTS = {
     "ndnet_ndt_debug_dump": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "ndnet_ndt_debug_set_epoch": (_I, [_P, ctypes.c_uint32]),
     "ndnet_ndt_debug_set_kl_fuse": (_I, [_P, _I]),
+    "ndnet_ndt_debug_set_list_sort": (_I, [_P, _I]),
+    "ndnet_ndt_debug_get_list_sort": (_I, [_P]),
     "ndnet_ndt_debug_kl_marks": (_I, [_P, _P]),
     "ndnet_ndt_debug_front_marks": (_I, [_P, _P]),
     "ndnet_ndt_debug_wq_marks": (_I, [_P, _P, ctypes.POINTER(ctypes.c_uint32)]),

@@ -334,6 +334,36 @@ def test_fc_mfma_matches_torch(B, K, N, relu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("B,relu", [(16, False), (7, True)])
+def test_fc_mfma_column_blocks_are_bit_identical(B, relu):
+    """A 256 -> 4096 layer (TNet(64)'s fc3) runs as four-column-block
+    workgroups (k_pn_fc_mfma<4>); the same layer issued as eight 512-column
+    slices runs one block per workgroup (k_pn_fc_mfma<1>: 32 blocks per
+    slice).  Same per-column sums in the same order: bit-identical."""
+    from ndnet import _lib
+    from ndnet.models import pointnet_hip as ph
+    K, N = 256, 4096
+    g = torch.Generator().manual_seed(40 + B)
+    x = torch.randn(B, K, generator=g).cuda()
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).cuda()
+    b = torch.randn(N, generator=g).cuda()
+    wf = ph._frag(w.t().contiguous())
+    wide = torch.empty(B, N, device="cuda")
+    ph._fc(x, w, b, wide, relu, wf)
+    sliced = torch.empty(B, N, device="cuda")
+    st = _lib.stream_ptr(x.device)
+    per = K * 512                                     # fragment-major floats per 512 columns
+    for s in range(N // 512):
+        rc = _lib.lib().ndnet_pn_fc_mfma_run(x.data_ptr(), K, wf.data_ptr() + 4 * per * s, b.data_ptr() + 4 * 512 * s,
+                                             sliced.data_ptr() + 4 * 512 * s, N, B, K, 512, 1 if relu else 0, st)
+        _lib.check(rc, "ndnet_pn_fc_mfma_run")
+    torch.cuda.synchronize()
+    assert torch.equal(wide, sliced)
+    ref = torch.addmm(b, x, w.t())
+    assert ((wide - (ref.relu() if relu else ref)).abs().max().item()) < 1e-5
+
+
+@pytest.mark.gpu
 def test_head3_in_chain_equals_head3_kernel(monkeypatch):
     """TNet(3)'s fc3 + t1 fold in chain B's prologue (default) against the
     separate k_pn_head3 launch: same log-probs within fp32 reduction order."""

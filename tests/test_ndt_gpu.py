@@ -624,9 +624,12 @@ def test_merge_grid_stride_equals_one_group_per_workgroup(k):
     B, n = 16, 60_000
     pts = torch.from_numpy(make_batch("L", B, n, seed0=70)).cuda()
     res = []
+    from ndnet import _lib
     for share in (1, 2):
         plan = NdtPlan(B, n, k, -1)
         plan.set_lazy_list(False)
+        # the merge at both shares (a plan with a share sorts k = 1000 lists on k_kl_sort by default)
+        _lib.check(_lib.lib().ndnet_ndt_debug_set_list_sort(plan.handle, 0), "set_list_sort")
         if share > 1:
             plan.set_cu_share(share)
         out = torch.empty((B, k, 12), dtype=torch.float32, device="cuda")
@@ -644,6 +647,86 @@ def test_merge_grid_stride_equals_one_group_per_workgroup(k):
         for b in range(B):
             for key in ("ord_val", "ord_p", "ord_q", "alive"):
                 assert np.array_equal(d[b][key], d0[b][key], equal_nan=True), (b, key)
+
+
+@pytest.mark.parametrize("case", ["L", "L_nofuse", "U_levels", "labelled"])
+def test_list_sort_equals_merge(case):
+    """Round 6: a plan whose event list fits one workgroup's LDS (k <= 1065)
+    sorts each cloud's list on one workgroup (k_kl_sort: the chunk runs merged
+    pairwise, then the NaN run) instead of k_kl_merge's workgroups per chunk
+    group.  Both orders are the composite (key, slot) order: rows, classes,
+    stats and every dumped list entry identical -- eager lists on L clouds
+    whose prune removes NDs (with the prune fused into the sort's workgroup,
+    and on k_kl's own launch), U clouds' deferred lists built on demand for two
+    further prune levels, and a labelled batch."""
+    import torch
+    from ndnet import _lib
+    from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
+    from ndnet.synthetic import make_batch
+    kind = "U" if case.startswith("U") else "L"
+    B, n = 12, 60_000
+    pts = torch.from_numpy(make_batch(kind, B, n, seed0=90)).cuda()
+    k = 1000 if case == "U_levels" else 800
+    ncls = 27 if case == "labelled" else -1
+    lbl = None
+    if case == "labelled":
+        lbl = torch.from_numpy(np.random.default_rng(9).integers(0, ncls + 1, size=(B, n)).astype(np.int32)).cuda()
+    res = []
+    for sort in (1, 0):
+        plan = NdtPlan(B, n, k, ncls)
+        plan.set_lazy_list(case == "U_levels")
+        _lib.check(_lib.lib().ndnet_ndt_debug_set_list_sort(plan.handle, sort), "set_list_sort")
+        assert _lib.lib().ndnet_ndt_debug_get_list_sort(plan.handle) == sort
+        if case == "L_nofuse":
+            _lib.check(_lib.lib().ndnet_ndt_debug_set_kl_fuse(plan.handle, 0), "set_kl_fuse")
+        out = torch.empty((B, k, 12), dtype=torch.float32, device="cuda")
+        oc = None if lbl is None else torch.empty((B, k, ncls + 1), dtype=torch.float32, device="cuda")
+        plan.run(pts, lbl, out, oc)
+        levels = []
+        if case == "U_levels":
+            for k2 in (700, 400):
+                o2 = torch.empty((B, k2, 12), dtype=torch.float32, device="cuda")
+                plan.prune(k2, o2)
+                levels.append(o2.cpu().numpy())
+        torch.cuda.synchronize()
+        st = plan.host_stats()
+        assert all(x.rc == 0 for x in st), (sort, [x.rc for x in st])
+        dumps = [_dump(plan, b, int(st[b].num_nds), int(st[b].num_events)) for b in range(B)]
+        res.append((out.cpu().numpy(), None if oc is None else oc.cpu().numpy(), [bytes(x) for x in st], dumps,
+                    levels))
+        del plan
+    (o1, c1, s1, d1, l1), (o0, c0, s0, d0, l0) = res
+    if case != "U_levels":
+        assert any(x.num_nds > k for x in st)
+    assert np.array_equal(o1, o0) and s1 == s0
+    if c1 is not None:
+        assert np.array_equal(c1, c0)
+    for a, b_ in zip(l1, l0):
+        assert np.array_equal(a, b_)
+    for b in range(B):
+        for key in d1[b]:
+            assert np.array_equal(d1[b][key], d0[b][key], equal_nan=True), (b, key)
+
+
+def test_list_sort_form_by_list_size_and_share():
+    """k_kl_sort takes the plans whose two key/slot buffers fit its LDS
+    (ecap = 6 * (1.2 k + 1) <= 7680 slots: k <= 1065); larger lists keep
+    k_kl_merge (test_merge_paths_match_oracle covers those).  By default
+    (form 2) only a plan with a CU share takes it."""
+    from ndnet import _lib
+    from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
+    get = lambda p: _lib.lib().ndnet_ndt_debug_get_list_sort(p.handle)  # noqa: E731
+    for k, fits in ((500, 1), (1000, 1), (1065, 1), (1070, 0), (2000, 0)):
+        plan = NdtPlan(16, 100_000, k, -1)
+        assert get(plan) == 0, k                    # share 1: the merge
+        plan.set_cu_share(2)
+        assert get(plan) == fits, k                 # a pipeline's share: the sort where it fits
+        _lib.check(_lib.lib().ndnet_ndt_debug_set_list_sort(plan.handle, 0), "set_list_sort")
+        assert get(plan) == 0, k
+        _lib.check(_lib.lib().ndnet_ndt_debug_set_list_sort(plan.handle, 1), "set_list_sort")
+        assert get(plan) == fits, k
+        del plan
+    assert _lib.lib().ndnet_ndt_debug_set_list_sort(None, 1) != 0
 
 
 def test_front_staged_scatter_active_at_c2():

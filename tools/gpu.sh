@@ -10,6 +10,7 @@
 #   bash tools/gpu.sh bench   TAG [bench args]    bench lines (args passed to bench.py)
 #   bash tools/gpu.sh final   TAG                 driver command + C5 + L lines + pipelined / isolated stats
 #   bash tools/gpu.sh ab      TAG NAME[:VAR=VAL,VAR=VAL] ...   env A/B on the bench (AB_ARGS: bench args)
+#   bash tools/gpu.sh abfull  TAG NAME[:VAR=VAL,...] ...      the same with the L (other distribution) line
 #   bash tools/gpu.sh variants TAG base NAME ...  library-variant A/B (tools/build_variant.sh NAME)
 #   bash tools/gpu.sh trace   TAG [bench args]    isolated-step kernel trace (one graph per step) + summary
 #   bash tools/gpu.sh pmc     TAG ndt|pn|chain|cache|issue|lds  PMC passes, one counter group per run
@@ -39,8 +40,10 @@ d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
 r = d.get("roofline", {})
 st = {k.split(" ")[0]: v for k, v in (d.get("stages_ms") or {}).items()}
 cl = {k: v.get("value") for k, v in (d.get("config_lines") or {}).items()}
+o = d.get("other_distribution") or {}
+ol = f"  L {o.get('value', 0):.1f} stages {o.get('stages_ms')}" if o else ""
 print(f"{sys.argv[1]:12s} {d['value']:10.1f} {d['unit']}  {d['ms_per_step']:.4f} ms/step  "
-      f"frac {r.get('frac')}  chains {r.get('all_chains', {}).get('ms')}  stages {st}  {cl}")
+      f"frac {r.get('frac')}  chains {r.get('all_chains', {}).get('ms')}  stages {st}  {cl}{ol}")
 PY
 }
 
@@ -102,6 +105,15 @@ ab)
     line $V $OUT/$V.log
   done
   ;;
+abfull)  # as ab, with the other distribution's line (the two-NDT-stream L pipeline) in the run
+  for A in "$@"; do
+    V=${A%%:*}
+    ENVS=""
+    [ "$V" != "$A" ] && ENVS=${A#*:}
+    step $V 300 $OUT/$V.log env ${ENVS//,/ } python bench.py --no-cpu-baseline --steps 100 ${AB_ARGS}
+    line $V $OUT/$V.log
+  done
+  ;;
 variants)
   for V in "$@"; do
     LIBV=""
@@ -137,6 +149,10 @@ pmc)
       pmc_passes $OUT/$K "python3 $R/bench.py --eager --kind $K --steps 3 --warmup 1 --no-cpu-baseline --no-other" \
         "SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_SCA,SQ_ACTIVE_INST_LDS,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES"
     done ;;
+  kl)  # the KL stage's kernels on L clouds (k_kl_rank_chunks, k_kl_sort / k_kl_merge): issue mix, LDS, waits
+    pmc_passes $OUT "python3 $R/tools/sort_marks.py --kind L" $SQ_MIX \
+      "SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_SCA,SQ_ACTIVE_INST_LDS,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES" \
+      $SQ_BUSY $GRBM ;;
   lds)  # the chains' LDS instruction mix and bank conflicts only (one pass)
     pmc_passes $OUT "python3 $R/tools/pn_forward.py --reps 3" $SQ_MIX ;;
   *) echo "unknown pmc kind $KIND"; exit 2 ;;

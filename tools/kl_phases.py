@@ -40,6 +40,9 @@ _lib.check(_lib.lib().ndnet_ndt_set_timing(plan.handle, 2), "set_timing")
 # (marks 12-14): staging, searches; then the gap to k_kl
 MPHASES = [(3, 4, "rank: chunk 0 scores"), (4, 15, "rank: scans, rank, writes"), (4, 18, "rank: chunk 0 scores -> last chunk end"), (18, 12, "last rank end -> merge start"),
            (12, 16, "merge: stage runs"), (16, 17, "merge: NaN bases"), (17, 13, "merge: NaN keys"), (13, 14, "merge: searches+writes"), (14, 19, "merge wg 0 end -> last merge end"), (19, 0, "last merge end -> k_kl start")]
+if _lib.lib().ndnet_ndt_debug_get_list_sort(plan.handle) == 1:  # k_kl_sort (round 6): its own marks
+    MPHASES = MPHASES[:4] + [(12, 16, "sort: load + place runs"), (16, 17, "sort: score-run levels"),
+                             (17, 13, "sort: NaN merge + list writes"), (13, 0, "sort end -> prune start")]
 acc = np.zeros(len(PHASES))
 macc = np.zeros(len(MPHASES))
 for _ in range(a.reps):
