@@ -272,8 +272,11 @@ int ndnet_ndt_debug_set_kl_fuse(void *plan, int on);
  * k_kl_merge; 2 (the default; NDNET_KL_SORT in the environment at plan
  * creation overrides it) takes k_kl_sort only at a CU share > 1
  * (ndnet_ndt_set_cu_share: a pipeline's plan, where the merge's CU time
- * matters more than its latency).  Same lists, rows and stats either way.
- * _get_ returns 1 when the plan's runs take k_kl_sort, 0 for k_kl_merge. */
+ * matters more than its latency); 3 as 1 with the chunks ranked in the
+ * sort's own launch (k_kl_rank_sort: the cloud's last ranking workgroup
+ * sorts) instead of a launch of their own (k_kl_rank_chunks, then k_kl_sort).
+ * Same lists, rows and stats every way.  _get_ returns 1 when the plan's runs sort (k_kl_rank_sort or
+ * k_kl_sort), 0 when they merge (k_kl_merge). */
 int ndnet_ndt_debug_set_list_sort(void *plan, int on);
 int ndnet_ndt_debug_get_list_sort(void *plan);
 

@@ -188,7 +188,8 @@ struct Plan {
   uint32_t* wq_ctr;           // [8][16] k_welford_q dynamic item counters, one per XCD (re-armed by k_kl_rank_chunks)
   int eager_list;             // build every cloud's retained list in the run (ndnet_ndt_set_lazy_list(plan, 0))
   int kl_fuse;                // the run's prune rides on the merge launch (kl_fusable; NDNET_KL_FUSE=0: k_kl)
-  int list_sort;              // 2 (auto): k_kl_sort at a CU share > 1 where the list fits (sort_fits); 1: wherever it fits; 0: k_kl_merge (NDNET_KL_SORT)
+  int list_sort;              // 2 (auto): k_kl_sort at a CU share > 1 where the list fits (sort_fits); 1: wherever it fits;
+                              // 3: as 1 in k_kl_rank_sort's one launch; 0: k_kl_merge (NDNET_KL_SORT)
   uint64_t front_sync_ticks;  // k_front's cloud-barrier timeout (ndnet_ndt_debug_set_sync_timeout)
   int lists_built;            // the deferred lists of the last run are built (no further build launches)
   int front_staged;           // k_front's scatter through LDS records (ndnet_ndt_set_front_staged; default 1)
@@ -3471,14 +3472,15 @@ __device__ void kl_cloud(const KLArgs& A, const int b) {
   uint32_t e_part = 0;
   if (!deferred) {
     for (uint32_t c2 = threadIdx.x; c2 < nch; c2 += blockDim.x) {
-      const uint32_t cc = A.chunk_cnt[(uint64_t)b * A.nchunk + c2];
+      const uint32_t* cp = &A.chunk_cnt[(uint64_t)b * A.nchunk + c2];
+      const uint32_t cc = kCoh ? ld_sc1(cp) : *cp;  // (kCoh: k_kl_rank_sort stored them in this launch)
       e_part += (cc >> 16) + (cc & 0xffffu);
     }
   }
   uint32_t ev[1] = {e_part};
   uint32_t E;
   block_scan_items(ev, 0u, AddU32(), s_u32, E);
-  if (deferred) E = c.flag_count;
+  if (deferred) E = kCoh ? ld_sc1(&c.flag_count) : c.flag_count;
   KL_MARK(2);
   if (!deferred) kl_poison_tail(A, eb, E);
   for (uint32_t u = threadIdx.x; u < nd; u += blockDim.x) A.alive_all[ob + u] = 1;
@@ -3634,7 +3636,7 @@ __device__ inline void sort_level_items(const SortBuf& I, const SortBuf& O, cons
 // key x at lower slots (its equal keys are in slot order; a NaN's key, a
 // prefix minimum, usually equals one score's), then each element's list entry
 // (ndt.c's kl_divergences row: value, p, q) at its final position
-template <int Q>
+template <int Q, bool kCoh>
 __device__ inline void sort_final_items(const KLArgs& A, int b, const SortBuf& I, uint32_t S, uint32_t NN, int rounds,
                                         uint32_t e0) {
   const uint64_t eb = (uint64_t)b * A.ecap;
@@ -3650,20 +3652,22 @@ __device__ inline void sort_final_items(const KLArgs& A, int b, const SortBuf& I
     st[q] = e < S ? S : 0u;
     n[q] = e >= E ? 0u : e < S ? NN : S;
   }
-  run_count_q<Q>(I.k, st, n, x, rounds, pos);
-#pragma unroll
-  for (int q = 0; q < Q; q++)
-    while (pos[q] < n[q] && I.k[st[q] + pos[q]] == x[q] && I.s[st[q] + pos[q]] < xs[q]) pos[q]++;
+  // the entry's value and neighbour depend on the slot only: loaded under the search
   double ov[Q];
   uint32_t oq[Q];
 #pragma unroll
   for (int q = 0; q < Q; q++) {
+    ov[q] = kCoh ? ld_sc1_f64(&A.slot_val_all[eb + xs[q]]) : A.slot_val_all[eb + xs[q]];
+    oq[q] = (uint32_t)A.nb_all[6 * (uint64_t)b * A.ndcap + xs[q]];
+  }
+  run_count_q<Q>(I.k, st, n, x, rounds, pos);
+#pragma unroll
+  for (int q = 0; q < Q; q++)
+    while (pos[q] < n[q] && I.k[st[q] + pos[q]] == x[q] && I.s[st[q] + pos[q]] < xs[q]) pos[q]++;
+#pragma unroll
+  for (int q = 0; q < Q; q++) {
     const uint32_t e = e0 + q * kKLThreads + threadIdx.x;
     pos[q] += e < S ? e : e - S;
-    if (e < E) {
-      ov[q] = A.slot_val_all[eb + xs[q]];
-      oq[q] = (uint32_t)A.nb_all[6 * (uint64_t)b * A.ndcap + xs[q]];
-    }
   }
 #pragma unroll
   for (int q = 0; q < Q; q++) {
@@ -3675,14 +3679,20 @@ __device__ inline void sort_final_items(const KLArgs& A, int b, const SortBuf& I
   }
 }
 
-// count elements in passes of up to 6 per thread (a uniform switch: count is
-// the workgroup's), f.template operator()<Q>(e0)
+// count elements in passes of up to 5 per thread, f(integral_constant<Q>, e0)
+// covering e0 + q * 1024 + tid, q < Q.  Q is per wave: the items none of a
+// wave's lanes holds are not searched (count = 2360: waves 5-15 run two items,
+// not three), a wave-uniform branch (no barrier inside f).
 template <typename F>
 __device__ inline void for_items(uint32_t count, F&& f) {
+  const uint32_t wb = threadIdx.x & ~63u;
   uint32_t nq = (count + kKLThreads - 1) / kKLThreads, e0 = 0;
   while (nq) {
     const uint32_t q = nq < 6 ? nq : 4;
-    switch (q) {
+    uint32_t qw = count > e0 + wb ? (count - e0 - wb + kKLThreads - 1) / kKLThreads : 0u;
+    qw = qw < q ? qw : q;
+    switch (qw) {
+      case 0: break;
       case 1: f(std::integral_constant<int, 1>{}, e0); break;
       case 2: f(std::integral_constant<int, 2>{}, e0); break;
       case 3: f(std::integral_constant<int, 3>{}, e0); break;
@@ -3694,6 +3704,9 @@ __device__ inline void for_items(uint32_t count, F&& f) {
   }
 }
 
+// kCoh: the chunks' runs were stored in this launch by workgroups on other
+// XCDs (write-through, k_kl_rank_sort): read them with sc1 loads.
+template <bool kCoh>
 __device__ void sort_cloud(const KLArgs& A, const int b) {
   const CloudCtl& c = A.ctl[b];
   const uint32_t nch = (6 * c.num_nds + kChunk - 1) / kChunk;
@@ -3717,18 +3730,25 @@ __device__ void sort_cloud(const KLArgs& A, const int b) {
   uint32_t cc = 0;
   double cm = __builtin_inf();
   if (tid < nch) {
-    cc = A.chunk_cnt[cb + tid];
-    cm = A.chunk_min[cb + tid];
+    cc = kCoh ? ld_sc1(&A.chunk_cnt[cb + tid]) : A.chunk_cnt[cb + tid];
+    cm = kCoh ? ld_sc1_f64(&A.chunk_min[cb + tid]) : A.chunk_min[cb + tid];
   }
 #pragma unroll
   for (int u = 0; u < U; u++) {
     const uint32_t i = u * kKLThreads + tid;
     const uint32_t ie = i < ec ? i : ec - 1;
     if (i < nslot) {
-      key[u] = A.sort_key_all[kb + i];
-      sidx[u] = A.sort_idx_all[kb + i];
-      nsl[u] = A.nan_list_all[eb + ie];
-      emin[u] = A.ev_min_all[eb + ie];
+      if (kCoh) {
+        key[u] = __hip_atomic_load(&A.sort_key_all[kb + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sidx[u] = ld_sc1(&A.sort_idx_all[kb + i]);
+        nsl[u] = ld_sc1(&A.nan_list_all[eb + ie]);
+        emin[u] = ld_sc1_f64(&A.ev_min_all[eb + ie]);
+      } else {
+        key[u] = A.sort_key_all[kb + i];
+        sidx[u] = A.sort_idx_all[kb + i];
+        nsl[u] = A.nan_list_all[eb + ie];
+        emin[u] = A.ev_min_all[eb + ie];
+      }
     }
   }
   if (tid < 64) {  // score and NaN offsets, the min over earlier chunks (nch <= 64)
@@ -3807,7 +3827,7 @@ __device__ void sort_cloud(const KLArgs& A, const int b) {
   }
   if (A.marks && tid == 0) A.marks[(uint64_t)b * kKLMarks + 17] = __builtin_amdgcn_s_memrealtime();
   const int rounds = bit_len(S > NN ? S : NN);
-  for_items(S + NN, [&](auto qc, uint32_t e0) { sort_final_items<decltype(qc)::value>(A, b, I, S, NN, rounds, e0); });
+  for_items(S + NN, [&](auto qc, uint32_t e0) { sort_final_items<decltype(qc)::value, kCoh>(A, b, I, S, NN, rounds, e0); });
   if (A.marks && tid == 0) {
     const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
     A.marks[(uint64_t)b * kKLMarks + 13] = t1;
@@ -3822,11 +3842,142 @@ __device__ void sort_cloud(const KLArgs& A, const int b) {
 __global__ void __launch_bounds__(kKLThreads) k_kl_sort(KLArgs A, int tail) {
   const int b = blockIdx.x;
   const CloudCtl& c = A.ctl[b];
-  if (c.state == kAccepted && !kl_list_skipped(A, c)) sort_cloud(A, b);
+  if (c.state == kAccepted && !kl_list_skipped(A, c)) sort_cloud<false>(A, b);
   if (!tail) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   kl_cloud<true>(A, b);
+}
+
+// Exclusive scan over each 256-thread quarter (four waves) of the workgroup;
+// scratch: 16 T; total: the quarter's reduction.  (min / integer add: the
+// same values as block_scan_items over a 256-thread block.)
+template <typename T, typename Op>
+__device__ inline T quarter_excl_scan(T v, T identity, Op op, T* scratch, T& total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, w0 = wid & ~3;
+  const T incl = wave_incl_scan(v, op);
+  T excl_w = __shfl_up(incl, 1, 64);
+  if (lane == 0) excl_w = identity;
+  if (lane == 63) scratch[wid] = incl;
+  __syncthreads();
+  T pre = identity;
+  for (int w = w0; w < wid; w++) pre = op(pre, scratch[w]);
+  total = op(op(op(scratch[w0], scratch[w0 + 1]), scratch[w0 + 2]), scratch[w0 + 3]);
+  __syncthreads();
+  return op(pre, excl_w);
+}
+
+// Round 6: k_kl_rank_chunks and k_kl_sort in one launch.  Four chunks per
+// 1024-thread workgroup, each quarter ranking one chunk exactly as
+// k_kl_rank_chunks does (its scans per quarter, its LDS in the dynamic
+// region the sort reuses), the outputs the sort reads stored write-through;
+// the cloud's last workgroup to finish (a ticket, as k_kl_merge's tail) then
+// sorts the list (sort_cloud, sc1 loads) and, with kTail, prunes and writes
+// the rows (kl_cloud).  The rank -> sort kernel boundary (~6 us at C2-L)
+// becomes an atomic hand-over (3.6 us: the write-through stores' drain), but
+// the ranks run 3.7 us longer on 112 one-per-CU workgroups than on 432
+// small ones (the events' FP64 scores on fewer CUs): 51 against 50 us for
+// the stage on L clouds (profiles/r06z_list_sort_ab.txt), so it is the
+// ndnet_ndt_debug_set_list_sort form 3, not a default.
+template <bool kTail>
+__global__ void __launch_bounds__(kKLThreads) k_kl_rank_sort(KLArgs A) {
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 8) A.wq_ctr[16 * threadIdx.x] = 0u;  // k_welford_q has finished
+  const int b = blockIdx.y;
+  CloudCtl& c = A.ctl[b];
+  const uint32_t tid = threadIdx.x, qtr = tid / kChunk, t = tid % kChunk;
+  const uint32_t nslots = 6 * c.num_nds;
+  const uint32_t ch = blockIdx.x * 4 + qtr;
+  // this launch scores the cloud (a build: its deferred clouds only), this quarter a chunk of it
+  const bool part = c.state == kAccepted && (A.mode != kKLBuild || c.kl_deferred);
+  const bool live = part && ch * kChunk < nslots;
+  const uint64_t eb = (uint64_t)b * A.ecap, kb = (uint64_t)b * A.sortcap + (uint64_t)ch * kChunk;
+  const uint32_t sl = ch * kChunk + t;
+  const bool deferred = kl_list_deferrable(A, c);
+  extern __shared__ __attribute__((aligned(16))) unsigned long long dyn_rank[];
+  unsigned long long* s_key = dyn_rank + qtr * kChunk;
+  unsigned long long* s_nkey = dyn_rank + 4 * kChunk + qtr * (kChunk + 4);  // 16-byte aligned rows
+  __shared__ double s_f64[16];
+  __shared__ uint32_t s_u32[16];
+  if (A.marks && ch == 0 && t == 0) A.marks[(uint64_t)b * kKLMarks + 3] = __builtin_amdgcn_s_memrealtime();
+  uint32_t fl = 0;
+  double vl = 0.0;
+  if (live) {
+    if (deferred) fl = kl_event_flag(A, b, sl < nslots ? sl : 0u);
+    else kl_event(A, b, sl < nslots ? sl : 0u, true, fl, vl);  // the clamped slot's result is dropped
+  }
+  if (deferred) {  // count the cloud's events (stats num_events / num_kl), one atomic per wave
+    const unsigned long long bal = __ballot(live && sl < nslots && fl);
+    if ((t & 63) == 0 && bal)
+      __hip_atomic_fetch_add(&c.flag_count, (uint32_t)__popcll(bal), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    if (A.marks && ch == 0 && t == 0) A.marks[(uint64_t)b * kKLMarks + 4] = __builtin_amdgcn_s_memrealtime();
+    if (live && sl < nslots) {
+      A.slot_flag_all[eb + sl] = fl;
+      st_sc1_f64(&A.slot_val_all[eb + sl], vl);
+    }
+    const bool f = live && sl < nslots && fl;
+    const double v = f ? vl : 0.0;
+    const bool isn = f && v != v;
+    const bool num = f && !isn;
+    const unsigned long long key = num ? score_key(v) : ~0ull;
+    s_key[t] = key;
+    double mtot;
+    uint32_t ctot;
+    const double pm = quarter_excl_scan(num ? v : __builtin_inf(), __builtin_inf(), MinF64(), s_f64, mtot);
+    const uint32_t cnt = quarter_excl_scan((uint32_t)isn | ((uint32_t)num << 16), 0u, AddU32(), s_u32, ctot);
+    const uint32_t nnum = ctot >> 16;
+    if (num) s_nkey[cnt >> 16] = key;
+    if (t < 2) s_nkey[nnum + t] = ~0ull;  // pad to an even count (~0 is never a score key)
+    __syncthreads();
+    // rank in the chunk (k_kl_rank_chunks): keys below, then equal keys at lower slots
+    uint32_t lt = 0, eq = 0;
+#pragma unroll 4
+    for (uint32_t j = 0; j < nnum; j += 2) {
+      const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(&s_nkey[j]);
+      lt += (kk.x < key ? 1u : 0u) + (kk.y < key ? 1u : 0u);
+      eq += (kk.x == key ? 1u : 0u) + (kk.y == key ? 1u : 0u);
+    }
+    uint32_t r;
+    if (num) {
+      r = lt;
+      if (eq > 1)
+        for (uint32_t j = 0; j < t; j++) r += s_key[j] == key ? 1u : 0u;
+    } else {
+      r = nnum + (t - (cnt >> 16));
+    }
+    if (live) {
+      __hip_atomic_store(&A.sort_key_all[kb + r], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      st_sc1(&A.sort_idx_all[kb + r], sl);
+      if (isn) {
+        const uint32_t j = cnt & 0xffffu;
+        st_sc1(&A.nan_list_all[eb + ch * kChunk + j], sl);
+        st_sc1_f64(&A.ev_min_all[eb + ch * kChunk + j], pm);
+      }
+      if (t == 0) {
+        st_sc1(&A.chunk_cnt[(uint64_t)b * A.nchunk + ch], ctot);
+        st_sc1_f64(&A.chunk_min[(uint64_t)b * A.nchunk + ch], mtot);
+      }
+    }
+    if (A.marks && ch == 0 && t == 0) A.marks[(uint64_t)b * kKLMarks + 15] = __builtin_amdgcn_s_memrealtime();
+  }
+  if (A.marks && t == 0 && live)
+    __hip_atomic_fetch_max(&A.marks[(uint64_t)b * kKLMarks + 18], (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the cloud's last workgroup sorts (and prunes)
+  __shared__ uint32_t s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores are done
+  __syncthreads();
+  if (tid == 0)
+    s_last = __hip_atomic_fetch_add(&c.kl_arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  if (tid == 0) __hip_atomic_store(&c.kl_arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (part && !kl_list_skipped(A, c)) sort_cloud<true>(A, b);
+  if constexpr (kTail) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    kl_cloud<true>(A, b);
+  }
 }
 
 __global__ void __launch_bounds__(kKLThreads) k_prune(KLArgs A) {
@@ -4017,18 +4168,28 @@ static uint32_t merge_grid(const Plan* P, uint32_t runs) {
 // 65.5k clouds/s (profiles/r06z_list_sort_ab.txt)
 static size_t sort_lds_bytes(const Plan* P) { return 20 * (size_t)P->ecap; }
 static bool sort_fits(const Plan* P) {
-  const bool want = P->list_sort == 1 || (P->list_sort == 2 && P->cu_share > 1);
+  const bool want = P->list_sort == 1 || P->list_sort == 3 || (P->list_sort == 2 && P->cu_share > 1);
   return want && sort_lds_bytes(P) <= (size_t)kKLLdsMax && P->nchunk <= kSortMaxChunks && P->ecap <= 65536;
 }
 
 static void launch_list_sort(Plan* P, const KLArgs& A, hipStream_t st, bool tail = false) {
   const int B = P->B;
-  k_kl_rank_chunks<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
   if (sort_fits(P)) {
     const size_t kl = tail ? kl_lds_bytes(P) : 0, so = sort_lds_bytes(P);
-    k_kl_sort<<<B, kKLThreads, so > kl ? so : kl, st>>>(A, tail ? 1 : 0);
+    size_t dyn = so > kl ? so : kl;
+    if (P->list_sort == 3) {  // one launch: the ranks, then the cloud's last workgroup sorts (and prunes)
+      const size_t rk = (size_t)(8 * kChunk + 16) * sizeof(unsigned long long);
+      dyn = dyn > rk ? dyn : rk;
+      const dim3 grid((P->nchunk + 3) / 4, B);
+      if (tail) k_kl_rank_sort<true><<<grid, kKLThreads, dyn, st>>>(A);
+      else k_kl_rank_sort<false><<<grid, kKLThreads, dyn, st>>>(A);
+      return;
+    }
+    k_kl_rank_chunks<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
+    k_kl_sort<<<B, kKLThreads, dyn, st>>>(A, tail ? 1 : 0);
     return;
   }
+  k_kl_rank_chunks<<<dim3(P->nchunk, B), kChunk, 0, st>>>(A);
   const uint32_t mg = merge_grid(P, kMergeRuns);
   const size_t kl = tail ? kl_lds_bytes(P) : 0;
   auto dyn = [&](size_t m) { return m > kl ? m : kl; };
@@ -4672,6 +4833,10 @@ int ndnet_ndt_plan_create(int batch, uint64_t num_points, uint64_t num_desired, 
                             (int)kKLFusedLds);
   if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_kl, hipFuncAttributeMaxDynamicSharedMemorySize, kKLLdsMax);
   if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_kl_sort, hipFuncAttributeMaxDynamicSharedMemorySize, kKLLdsMax);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_kl_rank_sort<true>, hipFuncAttributeMaxDynamicSharedMemorySize, kKLLdsMax);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_kl_rank_sort<false>, hipFuncAttributeMaxDynamicSharedMemorySize, kKLLdsMax);
   if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_prune, hipFuncAttributeMaxDynamicSharedMemorySize, kKLLdsMax);
   if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_bin_count, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                (int)(16384 * sizeof(uint32_t)));
@@ -4934,7 +5099,7 @@ int ndnet_ndt_debug_set_kl_fuse(void* plan, int on) {
 int ndnet_ndt_debug_set_list_sort(void* plan, int on) {
   Plan* P = (Plan*)plan;
   if (!P) return NDNET_ERR_ARG;
-  if (on < 0 || on > 2) return NDNET_ERR_ARG;
+  if (on < 0 || on > 3) return NDNET_ERR_ARG;
   P->list_sort = on;
   return NDNET_OK;
 }

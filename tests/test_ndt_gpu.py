@@ -649,7 +649,7 @@ def test_merge_grid_stride_equals_one_group_per_workgroup(k):
                 assert np.array_equal(d[b][key], d0[b][key], equal_nan=True), (b, key)
 
 
-@pytest.mark.parametrize("case", ["L", "L_nofuse", "U_levels", "labelled"])
+@pytest.mark.parametrize("case", ["L", "L_nofuse", "L_rank_sort", "L_rank_sort_nofuse", "U_levels", "labelled"])
 def test_list_sort_equals_merge(case):
     """Round 6: a plan whose event list fits one workgroup's LDS (k <= 1065)
     sorts each cloud's list on one workgroup (k_kl_sort: the chunk runs merged
@@ -657,8 +657,10 @@ def test_list_sort_equals_merge(case):
     group.  Both orders are the composite (key, slot) order: rows, classes,
     stats and every dumped list entry identical -- eager lists on L clouds
     whose prune removes NDs (with the prune fused into the sort's workgroup,
-    and on k_kl's own launch), U clouds' deferred lists built on demand for two
-    further prune levels, and a labelled batch."""
+    and on k_kl's own launch), with the chunks ranked by a launch of their
+    own (the default) and in the sort's launch (form 3: k_kl_rank_sort), U
+    clouds' deferred lists built on demand for two further prune levels, and
+    a labelled batch."""
     import torch
     from ndnet import _lib
     from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
@@ -675,9 +677,10 @@ def test_list_sort_equals_merge(case):
     for sort in (1, 0):
         plan = NdtPlan(B, n, k, ncls)
         plan.set_lazy_list(case == "U_levels")
-        _lib.check(_lib.lib().ndnet_ndt_debug_set_list_sort(plan.handle, sort), "set_list_sort")
+        form = 3 if sort and case.startswith("L_rank_sort") else sort
+        _lib.check(_lib.lib().ndnet_ndt_debug_set_list_sort(plan.handle, form), "set_list_sort")
         assert _lib.lib().ndnet_ndt_debug_get_list_sort(plan.handle) == sort
-        if case == "L_nofuse":
+        if case.endswith("nofuse"):
             _lib.check(_lib.lib().ndnet_ndt_debug_set_kl_fuse(plan.handle, 0), "set_kl_fuse")
         out = torch.empty((B, k, 12), dtype=torch.float32, device="cuda")
         oc = None if lbl is None else torch.empty((B, k, ncls + 1), dtype=torch.float32, device="cuda")
@@ -727,6 +730,8 @@ def test_list_sort_form_by_list_size_and_share():
         assert get(plan) == fits, k
         del plan
     assert _lib.lib().ndnet_ndt_debug_set_list_sort(None, 1) != 0
+    plan = NdtPlan(2, 20_000, 500, -1)
+    assert _lib.lib().ndnet_ndt_debug_set_list_sort(plan.handle, 4) != 0
 
 
 def test_front_staged_scatter_active_at_c2():

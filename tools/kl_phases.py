@@ -30,11 +30,14 @@ ap.add_argument("--points", type=int, default=100_000)
 ap.add_argument("--nds", type=int, default=1000)
 ap.add_argument("--kind", default="U")
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--list-sort", type=int, default=-1, help="ndnet_ndt_debug_set_list_sort form (default: the plan's)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 pts = torch.from_numpy(make_batch(a.kind, a.batch, a.points, seed0=0)).to(dev)
 ndt_preprocessing(a.nds, pts)
 plan = get_plan(a.batch, a.points, a.nds, -1, dev)
+if a.list_sort >= 0:
+    _lib.check(_lib.lib().ndnet_ndt_debug_set_list_sort(plan.handle, a.list_sort), "set_list_sort")
 _lib.check(_lib.lib().ndnet_ndt_set_timing(plan.handle, 2), "set_timing")
 # k_kl_rank_chunks, chunk 0 of each cloud (marks 3, 4, 15); k_kl_merge, workgroup 0 of each cloud
 # (marks 12-14): staging, searches; then the gap to k_kl

@@ -27,6 +27,7 @@ B, n, k = 16, 100_000, 1000
 pts = torch.from_numpy(make_batch(a.kind, B, n, seed0=0)).to(dev)
 ndt_preprocessing(k, pts)
 plan = get_plan(B, n, k, -1, dev)
+_lib.check(_lib.lib().ndnet_ndt_debug_set_list_sort(plan.handle, 1), "set_list_sort")  # k_kl_sort at any share
 _lib.check(_lib.lib().ndnet_ndt_set_timing(plan.handle, 2), "set_timing")
 acc = []
 for _ in range(a.reps):
