@@ -4161,11 +4161,11 @@ static uint32_t merge_grid(const Plan* P, uint32_t runs) {
 // k_kl_sort takes the list when its two key/slot buffers (20 bytes per slot)
 // fit its LDS and its offsets one wave's scan (ecap <= 7680: k <= 1065), and
 // by default only for a plan with a CU share (a pipeline's): one workgroup per
-// cloud sorts in ~23 us what k_kl_merge's ~7-14 workgroups per cloud merge in
-// ~17 us, so a plan alone on the chip keeps the merge (C2 NDT-only on L
-// clouds 87k vs 84k clouds/s), while a pipeline gains the merge's CU time
-// (its 110 KB workgroups hold ~110 CUs): the L line 66.3 / 66.0k vs 65.2 /
-// 65.5k clouds/s (profiles/r06z_list_sort_ab.txt)
+// cloud sorts in ~19 us what k_kl_merge's ~7-14 workgroups per cloud merge in
+// ~17-18 us (the KL stage 49.8 vs 47.7 us on L clouds), so a plan alone on
+// the chip keeps the merge, while a pipeline gains the merge's CU time (its
+// 110 KB workgroups hold ~110 CUs): the L line 66.2 / 66.6k vs 65.2 / 64.8k
+// clouds/s (profiles/r06z_list_sort_ab.txt)
 static size_t sort_lds_bytes(const Plan* P) { return 20 * (size_t)P->ecap; }
 static bool sort_fits(const Plan* P) {
   const bool want = P->list_sort == 1 || P->list_sort == 3 || (P->list_sort == 2 && P->cu_share > 1);
