@@ -191,10 +191,11 @@ def main() -> None:
     # want more k_front workgroups than the chip holds.  Each rank's k_front
     # then takes CUs / (ranks per card x its NDT streams) (pipe_share); the
     # cached plan of the stage lines takes CUs / ranks per card.
-    from ndnet.pipeline import PIPE_CU_SHARE
+    from ndnet.pipeline import PIPE_CU_SHARE, PIPE_CU_SHARE_MULTI
 
     def pipe_share(ndt_streams: int = 1):
-        return None if per_dev == 1 else max(PIPE_CU_SHARE, ndt_streams) * per_dev
+        base = PIPE_CU_SHARE if ndt_streams == 1 else PIPE_CU_SHARE_MULTI
+        return None if per_dev == 1 else max(base, ndt_streams) * per_dev
     if per_dev > 1:
         get_plan(B, n, k, -1, dev).set_cu_share(per_dev)
     torch.manual_seed(1234)

@@ -37,6 +37,11 @@ PIPE_CU_SHARE = int(os.environ.get("NDNET_PIPE_CU_SHARE", "2"))
 # k_welford_q keeps every CU: front 2 / welford 1 measured 70.5k clouds/s
 # against 68.8-70.2k for 2 / 2 and 62.8k for 2 / 4 (profiles/r03n_cu_share.txt)
 PIPE_WQ_SHARE = int(os.environ.get("NDNET_PIPE_WQ_SHARE", "1"))
+# ... and of a pipeline with more than one NDT stream (the L clouds' two):
+# share 3 measured 67.8 / 68.0k against 67.3 / 67.2k clouds/s at 2 and 67.4k
+# at 4 (profiles/r06sl_cu_share_ab.txt), where the U line keeps 2 (88.3k; 3:
+# 87.7-89.1k, 4: 87.4k)
+PIPE_CU_SHARE_MULTI = int(os.environ.get("NDNET_PIPE_CU_SHARE_MULTI", "3"))
 # Forward streams of PipelinedSegmentation: more than one lets consecutive
 # forwards overlap (each in its own workspace slot), one's TNet heads and
 # chain prologues beside the other's chains.  C2: 1 stream 74.9-75.0k, 2
@@ -240,7 +245,7 @@ class PipelinedSegmentation:
         self.plans = [NdtPlan(batch, num_points, self.num_nds, -1, device=dev) for _ in range(N)]
         self.plan = self.plans[0]
         if cu_share is None:
-            cu_share = PIPE_CU_SHARE
+            cu_share = PIPE_CU_SHARE if N == 1 else PIPE_CU_SHARE_MULTI
         # k_front's workgroups of a cloud meet at cloud barriers, so all of them
         # must be resident at once.  One NDT stream: k_front alone spans at most
         # the chip (the other kernels never wait on anything, so they drain).
