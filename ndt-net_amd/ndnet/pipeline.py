@@ -39,8 +39,9 @@ PIPE_CU_SHARE = int(os.environ.get("NDNET_PIPE_CU_SHARE", "2"))
 PIPE_WQ_SHARE = int(os.environ.get("NDNET_PIPE_WQ_SHARE", "1"))
 # ... and of a pipeline with more than one NDT stream (the L clouds' two):
 # share 3 measured 67.8 / 68.0k against 67.3 / 67.2k clouds/s at 2 and 67.4k
-# at 4 (profiles/r06sl_cu_share_ab.txt), where the U line keeps 2 (88.3k; 3:
-# 87.7-89.1k, 4: 87.4k)
+# at 4 on one box, 66.3 / 66.1k against 66.1 / 66.3k on another (+0.5% over
+# both, within the spread; profiles/r06sl_cu_share_ab.txt), where the U line
+# keeps 2 (88.3k; 3: 87.7-89.1k, 4: 87.4k)
 PIPE_CU_SHARE_MULTI = int(os.environ.get("NDNET_PIPE_CU_SHARE_MULTI", "3"))
 # Forward streams of PipelinedSegmentation: more than one lets consecutive
 # forwards overlap (each in its own workspace slot), one's TNet heads and
