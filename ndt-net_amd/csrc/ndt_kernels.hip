@@ -3710,6 +3710,7 @@ template <bool kCoh>
 __device__ void sort_cloud(const KLArgs& A, const int b) {
   const CloudCtl& c = A.ctl[b];
   const uint32_t nch = (6 * c.num_nds + kChunk - 1) / kChunk;
+  if (nch == 0) return;  // no slots, no list (uniform: before any barrier)
   const uint64_t eb = (uint64_t)b * A.ecap, kb = (uint64_t)b * A.sortcap, cb = (uint64_t)b * A.nchunk;
   const uint32_t tid = threadIdx.x;
   if (A.marks && tid == 0) A.marks[(uint64_t)b * kKLMarks + 12] = __builtin_amdgcn_s_memrealtime();
