@@ -127,6 +127,8 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-stream-lines", action="store_true",
+                    help="skip the C2 / C3 lines over consecutive batches on several streams")
     ap.add_argument("--settle-ms", type=float, default=300.0,
                     help="untimed replays of the step before the warmup steps (GPU clocks to steady state)")
     ap.add_argument("--batch", type=int, default=16)
@@ -423,6 +425,76 @@ def main() -> None:
                                 "ms_per_step": round(1e3 * t_fwd / args.steps, 4),
                                 "workload": f"batch {B} x {k} x 12-D NDs, NDTNetSegmentation F={F} C={C} eval forward alone"},
         }
+        # the same two stages over a stream of batches (round 6: C2 201k vs
+        # 167k sequential at CU share 2, 146-158k at share 1; C3 127-130k vs
+        # 100-102k, profiles/r06su_stream_lines.txt): consecutive batches on
+        # S streams, each stream its own workspace and graph (the NDT stage: a
+        # plan per stream; the forward: a pointnet_hip workspace slot per
+        # stream), so one batch's latency-bound phases overlap the next one's
+        # (the way the headline pipeline overlaps them).  Every step is one
+        # whole batch; the lines above replay one graph after another.
+        if not args.no_stream_lines and per_dev == 1:
+            from ndnet.preprocessing.ndtnet_preprocessing import NdtPlan
+            from ndnet.models import pointnet_hip
+
+            def streams_rate(S, body):
+                sts = [torch.cuda.Stream(device=dev) for _ in range(S)]
+                cur = torch.cuda.current_stream(dev)
+                graphs = []
+                for i, st in enumerate(sts):
+                    st.wait_stream(cur)
+                    with torch.no_grad(), torch.cuda.stream(st):
+                        body(i)
+                        body(i)
+                torch.cuda.synchronize()
+                for i, st in enumerate(sts):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.no_grad(), torch.cuda.graph(g, stream=st):
+                        body(i)
+                    graphs.append(g)
+                torch.cuda.synchronize()
+
+                def run(m):
+                    for st in sts:
+                        st.wait_stream(cur)
+                    for s_ in range(m):
+                        with torch.cuda.stream(sts[s_ % S]):
+                            graphs[s_ % S].replay()
+                    for st in sts:
+                        cur.wait_stream(st)
+                run(3 * S)
+                torch.cuda.synchronize()
+                D.barrier()
+                t0_ = time.perf_counter()
+                run(args.steps)
+                torch.cuda.synchronize()
+                D.barrier()
+                return D.max_over_ranks(time.perf_counter() - t0_)
+
+            S_ndt, S_fwd = 2, 3
+            splans = [NdtPlan(B, n, k, -1, device=dev) for _ in range(S_ndt)]
+            ndt_share = int(os.environ.get("NDNET_STREAMS_NDT_SHARE", "2"))
+            if ndt_share > 1:
+                for pl in splans:
+                    pl.set_cu_share(ndt_share)
+            souts = [torch.zeros((B, k, 12), dtype=torch.float32, device=dev) for _ in range(S_ndt)]
+            t_ndt_s = streams_rate(S_ndt, lambda i: splans[i].run(pts, None, souts[i], None))
+            assert all(st.rc == 0 for pl in splans for st in pl.host_stats())
+            assert all(torch.equal(o, rows) for o in souts), "stream-line NDT rows differ from ndt_preprocessing's"
+
+            def fwd_slot(i):
+                with pointnet_hip.workspace_slot(i):
+                    return model(rows[..., :3], rows[..., 3:])
+            t_fwd_s = streams_rate(S_fwd, fwd_slot)
+            del splans, souts
+            config_lines["C2_ndt_only_streams"] = {
+                "value": round(total_clouds / t_ndt_s, 2), "unit": "clouds/s",
+                "ms_per_step": round(1e3 * t_ndt_s / args.steps, 4),
+                "workload": f"as C2_ndt_only, consecutive batches on {S_ndt} streams (a plan each, CU share {ndt_share})"}
+            config_lines["C3_forward_only_streams"] = {
+                "value": round(total_clouds / t_fwd_s, 2), "unit": "clouds/s",
+                "ms_per_step": round(1e3 * t_fwd_s / args.steps, 4),
+                "workload": f"as C3_forward_only, consecutive batches on {S_fwd} streams (a workspace slot each)"}
 
         # ---- config C5 (BASELINE configs[4], tools/train_multiscale.py): the
         # multiscale step -- downsample to 2000, prune to 1000 and 500, a
