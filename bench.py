@@ -519,6 +519,7 @@ def main() -> None:
         assert all(st.rc == 0 for pl in p5.plans for st in pl.host_stats())
         config_lines["C5_multiscale"] = {
             "value": round(total_clouds / t5, 2), "unit": "clouds/s", "ms_per_step": round(1e3 * t5 / args.steps, 4),
+            "front_share": list(p5.front_share),
             "workload": f"batch {B} x {n} pts ({args.kind}) -> downsample {c5[0]} -> prune {c5[1]} -> prune {c5[2]}, "
                         f"NDTNetSegmentation F={F} C={C} eval per level (3 forwards per step), stream pipeline"}
         del p5
@@ -790,6 +791,7 @@ def main() -> None:
             "settle": {"ms": args.settle_ms, "steps": n_settle},
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
+            "pipeline_front_share": list(getattr(graphed, "front_share", [])) if not args.eager else None,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
